@@ -1,0 +1,200 @@
+"""ctypes view of the CPU restatement (oracle/nh_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py, always as the checker / timed CPU baseline, never
+by the product package (nano-hevc_amd/nano_hevc).  Parity pinned against the
+reference's outputs in tests/golden/ (see tests/test_oracle_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnh_oracle.so")
+
+ERRORS = {-1: ValueError, -2: IndexError, -3: OverflowError, -4: ZeroDivisionError}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        i64, i32 = C.c_int64, C.c_int
+        sig = {
+            "oh_intra_dc": [P, i64, P, i64, i64, i32, P],
+            "oh_intra_planar": [P, i64, P, i64, i64, i64, i64, i64, P],
+            "oh_intra_angular": [P, i64, P, i64, i64, i32, i32, i64, P],
+            "oh_mode_to_angle": [i32, P, P],
+            "oh_residual": [P, P, i64, P],
+            "oh_reconstruct": [P, P, i64, P],
+            "oh_clip": [P, i64, i64, P],
+            "oh_forward_transform": [P, i64, i32, P],
+            "oh_inverse_transform": [P, i64, i32, P],
+            "oh_get_matrix": [i64, i32, P],
+            "oh_quantize": [P, i64, i32, i64, i32, i32, P],
+            "oh_dequantize": [P, i64, i32, P],
+            "oh_fwd8x8_quant_plane": [P, P, i32, i32, i32, i32, i32],
+            "oh_intra_rdo_plane": [P, i32, i32, i32, i32, P, P, P, P],
+            "oh_tu_pipeline_plane": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P],
+            "oh_tu_split": [C.c_uint32, i32, i32, i32, i32],
+        }
+        for name, args in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = None if name in ("oh_residual", "oh_reconstruct", "oh_clip", "oh_fwd8x8_quant_plane",
+                                         "oh_intra_rdo_plane", "oh_tu_pipeline_plane") else C.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def _check(rc):
+    if rc != 0:
+        raise ERRORS.get(rc, RuntimeError)(f"oracle rc={rc}")
+
+
+def matrix(size, use_dst=False):
+    out = np.zeros((size, size), np.int32)
+    _check(lib().oh_get_matrix(size, int(use_dst), _p(out)))
+    return out
+
+
+def forward_transform(block, use_dst=False):
+    n = block.shape[0]
+    x = np.ascontiguousarray(block.astype(np.int32)[:n, :n])
+    out = np.zeros((n, n), np.int32)
+    _check(lib().oh_forward_transform(_p(x), n, int(use_dst), _p(out)))
+    return out
+
+
+def inverse_transform(block, use_dst=False):
+    n = block.shape[0]
+    x = np.ascontiguousarray(block.astype(np.int32)[:n, :n])
+    out = np.zeros((n, n), np.int32)
+    _check(lib().oh_inverse_transform(_p(x), n, int(use_dst), _p(out)))
+    return out
+
+
+def _abs_bits(dt):
+    dt = np.dtype(dt)
+    return dt.itemsize * 8 if dt.kind == "i" else 64
+
+
+def quantize(c, qp, size, is_intra=True):
+    c = np.asarray(c)
+    ab = _abs_bits(c.dtype)
+    x = np.ascontiguousarray(c.astype(np.int64))
+    out = np.zeros(c.shape, np.int32)
+    _check(lib().oh_quantize(_p(x), x.size, int(qp), int(np.log2(size)), int(bool(is_intra)), ab, _p(out)))
+    return out
+
+
+def dequantize(l, qp, size=None):
+    x = np.ascontiguousarray(np.asarray(l).astype(np.int64))
+    out = np.zeros(x.shape, np.int32)
+    _check(lib().oh_dequantize(_p(x), x.size, int(qp), _p(out)))
+    return out
+
+
+def intra_dc(top, left, size, variant4x4=False):
+    t = np.ascontiguousarray(np.asarray(top, np.int64))
+    l = np.ascontiguousarray(np.asarray(left, np.int64))
+    n = 4 if variant4x4 else size
+    out = np.zeros((n, n), np.int16)
+    _check(lib().oh_intra_dc(_p(t), t.size, _p(l), l.size, int(size), int(variant4x4), _p(out)))
+    return out
+
+
+def intra_planar(top, left, tr, bl, size):
+    t = np.ascontiguousarray(np.asarray(top, np.int64))
+    l = np.ascontiguousarray(np.asarray(left, np.int64))
+    out = np.zeros((size, size), np.int16)
+    _check(lib().oh_intra_planar(_p(t), t.size, _p(l), l.size, int(tr), int(bl), size, int(np.log2(size)), _p(out)))
+    return out
+
+
+def mode_to_angle(mode):
+    a, v = C.c_int(), C.c_int()
+    _check(lib().oh_mode_to_angle(int(mode), C.byref(a), C.byref(v)))
+    return a.value, bool(v.value)
+
+
+def intra_angular(top, left, corner, mode, size):
+    angle, vert = mode_to_angle(mode)
+    t = np.ascontiguousarray(np.asarray(top, np.int64))
+    l = np.ascontiguousarray(np.asarray(left, np.int64))
+    out = np.zeros((size, size), np.int16)
+    _check(lib().oh_intra_angular(_p(t), t.size, _p(l), l.size, int(corner), angle, int(vert), size, _p(out)))
+    return out
+
+
+def residual(a, b):
+    a = np.ascontiguousarray(a, np.int16); b = np.ascontiguousarray(b, np.int16)
+    out = np.zeros(a.shape, np.int16)
+    lib().oh_residual(_p(a), _p(b), a.size, _p(out))
+    return out
+
+
+def reconstruct(a, b):
+    a = np.ascontiguousarray(a, np.int16); b = np.ascontiguousarray(b, np.int16)
+    out = np.zeros(a.shape, np.int16)
+    lib().oh_reconstruct(_p(a), _p(b), a.size, _p(out))
+    return out
+
+
+def clip(x, bit_depth=8):
+    x = np.ascontiguousarray(np.asarray(x).astype(np.int64))
+    mv = min((1 << bit_depth) - 1, 2**63 - 1)
+    out = np.zeros(x.shape, np.int16)
+    lib().oh_clip(_p(x), x.size, mv, _p(out))
+    return out
+
+
+def fwd8x8_quant_plane(res, qp=32, is_intra=True):
+    res = np.ascontiguousarray(res, np.int16)
+    h, w = res.shape
+    out = np.zeros_like(res)
+    lib().oh_fwd8x8_quant_plane(_p(res), _p(out), w, h, w, int(qp), int(is_intra))
+    return out
+
+
+def intra_rdo_plane(src, qp=32):
+    src = np.ascontiguousarray(src, np.int16)
+    h, w = src.shape
+    modes = np.zeros((h // 8, w // 8), np.uint8)
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    sse = np.zeros(1, np.int64)
+    lib().oh_intra_rdo_plane(_p(src), w, h, w, int(qp), _p(modes), _p(lvl), _p(rec), _p(sse))
+    return modes, lvl, rec, int(sse[0])
+
+
+def tu_pipeline_plane(src, ctb, plane_id, seed, qp, is_luma, row0=0, row1=1 << 30):
+    src = np.ascontiguousarray(src, np.int16)
+    h, w = src.shape
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    tul = np.zeros((h // 4, w // 4), np.uint8)
+    lib().oh_tu_pipeline_plane(_p(src), w, h, w, ctb, plane_id, seed, qp, int(is_luma), row0, row1,
+                               _p(lvl), _p(rec), _p(tul))
+    return lvl, rec, tul
+
+
+def tu_split(seed, plane_id, x, y, size):
+    return bool(lib().oh_tu_split(seed, plane_id, x, y, size))

@@ -1,0 +1,361 @@
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE.
+
+Run in the build container only (the reference never travels to the GPU box):
+
+    python tests/golden/make_golden.py [/root/reference]
+
+It imports the reference ``nano_hevc`` package (pure Python + numpy) and records
+inputs and reference outputs as data (.npz) plus a manifest with the numpy
+version (NEP 50 promotion matters: SURVEY.md §0.1 D8).  Fixture plan: SURVEY.md
+§8(c) C4.  Frame-level fixtures (cfg 3 / cfg 4) compose the reference
+functions exactly as DESIGN.md §3.3/§3.4 define the drivers.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _import_reference(path):
+    sys.path.insert(0, path)
+    import nano_hevc  # noqa: F401  (the reference package)
+    from nano_hevc import intra, transform, quant
+    assert os.path.abspath(intra.__file__).startswith(os.path.abspath(path)), intra.__file__
+    return intra, transform, quant
+
+
+def _err(fn):
+    try:
+        return ("ok", fn())
+    except Exception as e:  # record the reference's exception type
+        return ("err", type(e).__name__)
+
+
+def gen_matrices(T):
+    return {"DST4": T.DST4, "DCT4": T.DCT4, "DCT8": T.DCT8, "DCT16": T.DCT16, "DCT32": T.DCT32}
+
+
+def gen_transform(T, rng):
+    out = {}
+    for n, dst in [(4, True), (4, False), (8, False), (16, False), (32, False)]:
+        key = f"n{n}_{'dst' if dst else 'dct'}"
+        blocks = [rng.integers(-255, 256, size=(n, n)) for _ in range(48)]
+        cb = np.indices((n, n)).sum(0) % 2
+        blocks += [255 * (2 * cb - 1), -255 * (2 * cb - 1), np.zeros((n, n), int),
+                   np.full((n, n), 32767), np.full((n, n), -32768),
+                   32767 * (2 * cb - 1), rng.integers(-32768, 32768, size=(n, n)),
+                   rng.integers(-32768, 32768, size=(n, n))]
+        fin = np.stack(blocks).astype(np.int16)
+        fout = np.stack([T.forward_transform(b, use_dst=dst) for b in fin])
+        # inverse inputs: forward outputs + raw int32 coefficients (wrap cases)
+        raw = [rng.integers(-2000, 2001, size=(n, n)) for _ in range(16)]
+        raw += [rng.integers(-2**31, 2**31, size=(n, n), dtype=np.int64) for _ in range(8)]
+        raw += [np.full((n, n), 2**31 - 1), np.full((n, n), -2**31)]
+        iin = np.concatenate([fout, np.stack(raw).astype(np.int32)])
+        iout = np.stack([T.inverse_transform(b, use_dst=dst) for b in iin])
+        out[key + "_fwd_in"] = fin
+        out[key + "_fwd_out"] = fout.astype(np.int32)
+        out[key + "_inv_in"] = iin
+        out[key + "_inv_out"] = iout.astype(np.int32)
+    return out
+
+
+def gen_quant(Q, rng):
+    vec32 = np.concatenate([
+        np.array([0, 1, -1, 2, -2, 5, -5, 1020, -1020, 32767, -32768, 2**31 - 1, -2**31,
+                  131072, -131072, 1 << 20, -(1 << 20)]),
+        rng.integers(-2000, 2001, size=200), rng.integers(-2**31, 2**31, size=39, dtype=np.int64),
+    ]).astype(np.int32)
+    vec16 = np.concatenate([np.array([0, 1, -1, 32767, -32768, -32767]),
+                            rng.integers(-32768, 32768, size=58)]).astype(np.int16)
+    qps = list(range(0, 52)) + [-5, 60]
+    out = {"q_vec32": vec32, "q_vec16": vec16, "q_qps": np.array(qps)}
+    q32 = np.zeros((len(qps), 4, 2, vec32.size), np.int32)
+    q16 = np.zeros((len(qps), 4, 2, vec16.size), np.int32)
+    for a, qp in enumerate(qps):
+        for b, size in enumerate([4, 8, 16, 32]):
+            for c, intra in enumerate([True, False]):
+                q32[a, b, c] = Q.quantize(vec32, qp, size, intra)
+                q16[a, b, c] = Q.quantize(vec16, qp, size, intra)
+    out["q_out32"], out["q_out16"] = q32, q16
+    lv = np.concatenate([np.array([0, 1, -1, 100, -100, 32767, -32768, 2**31 - 1, -2**31]),
+                         rng.integers(-3000, 3001, size=100),
+                         rng.integers(-2**31, 2**31, size=19, dtype=np.int64)]).astype(np.int32)
+    out["dq_in"] = lv
+    out["dq_out"] = np.stack([Q.dequantize(lv, qp, 4) for qp in qps]).astype(np.int32)
+    out["qp_params"] = np.array([Q.get_qp_params(q) for q in range(-3, 56)])
+    return out
+
+
+def gen_intra(I, rng):
+    """Predictions for modes 0..34 x N in {4,8,16,32} x 8 reference sets."""
+    out = {}
+    for n in [4, 8, 16, 32]:
+        sets = []
+        for s in range(8):
+            if s < 4:
+                top = rng.integers(0, 256, size=2 * n + 1)
+                left = rng.integers(0, 256, size=2 * n + 1)
+            elif s == 4:   # short refs (D6): replicate-last and secondary gating
+                top = rng.integers(0, 256, size=n + 1)
+                left = rng.integers(0, 256, size=max(2, n // 2))
+            elif s == 5:   # 2000-valued refs: int16 wrap in interpolation (D8)
+                top = rng.integers(1800, 2200, size=2 * n + 1)
+                left = rng.integers(1800, 2200, size=2 * n + 1)
+            elif s == 6:   # 10-bit content
+                top = rng.integers(0, 1024, size=2 * n + 1)
+                left = rng.integers(0, 1024, size=2 * n + 1)
+            else:          # near int16 extremes
+                top = rng.integers(-32768, 32768, size=2 * n + 1)
+                left = rng.integers(-32768, 32768, size=2 * n + 1)
+            corner = int(rng.integers(0, 256)) if s != 7 else int(rng.integers(-32768, 32768))
+            sets.append((top.astype(np.int16), left.astype(np.int16), corner))
+        tops = np.full((8, 2 * n + 1), -1, np.int16)
+        lefts = np.full((8, 2 * n + 1), -1, np.int16)
+        ntop = np.zeros(8, np.int64)
+        nleft = np.zeros(8, np.int64)
+        corners = np.zeros(8, np.int64)
+        pred = np.zeros((8, 35, n, n), np.int16)
+        status = np.zeros((8, 35), np.int8)       # 0 ok, 1 OverflowError
+        for s, (top, left, corner) in enumerate(sets):
+            tops[s, :top.size], lefts[s, :left.size] = top, left
+            ntop[s], nleft[s], corners[s] = top.size, left.size, corner
+            for m in range(35):
+                if m == 0:
+                    r = _err(lambda: I.intra_planar_predict(top[:n] if top.size >= n else top, left[:n] if left.size >= n else left,
+                                                            int(top[min(n, top.size) - 1]), int(left[min(n, left.size) - 1]), n))
+                elif m == 1:
+                    r = _err(lambda: I.intra_dc_predict(top, left, n))
+                else:
+                    r = _err(lambda: I.intra_angular_predict(top, left, corner, m, n))
+                if r[0] == "ok":
+                    pred[s, m] = r[1]
+                else:
+                    status[s, m] = {"OverflowError": 1, "IndexError": 2}.get(r[1], 9)
+        out[f"n{n}_top"], out[f"n{n}_left"] = tops, lefts
+        out[f"n{n}_ntop"], out[f"n{n}_nleft"], out[f"n{n}_corner"] = ntop, nleft, corners
+        out[f"n{n}_pred"], out[f"n{n}_status"] = pred, status
+    # quirk modes 0/1 through the angular entry (D10) and the 4x4 DC variant
+    top = rng.integers(0, 256, size=9).astype(np.int16)
+    left = rng.integers(0, 256, size=9).astype(np.int16)
+    out["quirk_top"], out["quirk_left"] = top, left
+    out["quirk_ang0"] = I.intra_angular_predict(top, left, 77, 0, 4)
+    out["quirk_ang1"] = I.intra_angular_predict(top, left, 77, 1, 4)
+    out["quirk_angm5"] = I.intra_angular_predict(top, left, 77, -5, 4)
+    out["quirk_dc4"] = I.intra_dc_predict_4x4(top, left)
+    out["quirk_dc4_len9"] = I.intra_dc_predict(top, left, 4)
+    # residual / reconstruct / clip vectors
+    a = rng.integers(-32768, 32768, size=300).astype(np.int16)
+    b = rng.integers(-32768, 32768, size=300).astype(np.int16)
+    out["rr_a"], out["rr_b"] = a, b
+    out["rr_res"], out["rr_rec"] = I.residual_block(a, b), I.reconstruct_block(a, b)
+    cv = np.concatenate([np.array([-2**40, -1, 0, 1, 255, 256, 1023, 1024, 32767, 65535, 70000, 2**40]),
+                         rng.integers(-5000, 70000, size=100)]).astype(np.int64)
+    out["clip_in"] = cv
+    for bd in [1, 8, 10, 12, 16, 40, 63]:
+        out[f"clip_bd{bd}"] = I.clip_to_pixel_range(cv, bd)
+    return out
+
+
+def gen_chain(I, T, Q):
+    """Config-1 chain (README.md:44-71, test_quant.py:283-322)."""
+    top = np.array([102, 98, 100, 101], dtype=np.int16)
+    left = np.array([103, 102, 101, 99], dtype=np.int16)
+    orig = np.array([[102, 101, 100, 100], [103, 102, 101, 100], [103, 102, 100, 99], [104, 101, 99, 98]], dtype=np.int16)
+    out = {"c1_top": top, "c1_left": left, "c1_orig": orig}
+    pred = I.intra_dc_predict(top, left, 4)
+    res = I.residual_block(orig, pred)
+    for qp in [20, 22]:
+        coeff = T.forward_transform(res, use_dst=True)
+        lvl = Q.quantize_block(coeff, qp)
+        deq = Q.dequantize_block(lvl, qp)
+        rres = T.inverse_transform(deq, use_dst=True)
+        recon = I.clip_to_pixel_range(I.reconstruct_block(pred, rres.astype(np.int16)))
+        out.update({f"c1_pred": pred, f"c1_res": res, f"c1_coeff": coeff, f"c1_lvl_qp{qp}": lvl,
+                    f"c1_deq_qp{qp}": deq, f"c1_rres_qp{qp}": rres, f"c1_recon_qp{qp}": recon})
+    return out
+
+
+def ref_plane_cfg2(T, Q, plane, qp=32):
+    h, w = plane.shape
+    lvl = np.zeros_like(plane)
+    for by in range(0, h - 7, 8):
+        for bx in range(0, w - 7, 8):
+            c = T.forward_transform(plane[by:by + 8, bx:bx + 8])
+            lvl[by:by + 8, bx:bx + 8] = Q.quantize_block(c, qp)
+    return lvl
+
+
+def _neighbors(src, x, y, count):
+    """block.py:38-55 with count (numpy slices truncate at the plane edge)."""
+    top = np.full(count, 128, src.dtype) if y == 0 else src[y - 1, x:x + count].copy()
+    left = np.full(count, 128, src.dtype) if x == 0 else src[y:y + count, x - 1].copy()
+    tl = 128 if (y == 0 or x == 0) else int(src[y - 1, x - 1])
+    return top, left, tl
+
+
+def _chain(I, T, Q, orig, pred, qp, use_dst):
+    res = I.residual_block(orig, pred)
+    lvl = Q.quantize_block(T.forward_transform(res, use_dst=use_dst), qp)
+    rres = T.inverse_transform(Q.dequantize_block(lvl, qp), use_dst=use_dst)
+    rec = I.clip_to_pixel_range(I.reconstruct_block(pred, rres.astype(np.int16)), 8)
+    sse = int(np.sum(I.residual_block(orig, rec).astype(np.int64) ** 2))
+    return lvl, rec, sse
+
+
+def ref_plane_cfg3(I, T, Q, src, qp):
+    h, w = src.shape
+    n = 8
+    modes = np.zeros((h // n, w // n), np.uint8)
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    total = 0
+    for by in range(0, h - n + 1, n):
+        for bx in range(0, w - n + 1, n):
+            orig = src[by:by + n, bx:bx + n]
+            top, left, tl = _neighbors(src, bx, by, n)
+            top2, left2, _ = _neighbors(src, bx, by, 2 * n)
+            topa = np.concatenate([[tl], top2]).astype(np.int16)
+            lefta = np.concatenate([[tl], left2]).astype(np.int16)
+            best = None
+            for m in range(35):
+                if m == 0:
+                    pred = I.intra_planar_predict(top, left, int(top[-1]), int(left[-1]), n)
+                elif m == 1:
+                    pred = I.intra_dc_predict(top, left, n)
+                else:
+                    pred = I.intra_angular_predict(topa, lefta, tl, m, n)
+                l, r, sse = _chain(I, T, Q, orig, pred, qp, False)
+                if best is None or sse < best[0]:
+                    best = (sse, m, l, r)
+            total += best[0]
+            modes[by // n, bx // n] = best[1]
+            lvl[by:by + n, bx:bx + n] = best[2]
+            rec[by:by + n, bx:bx + n] = best[3]
+    return modes, lvl, rec, total
+
+
+def _mix32(x):
+    x &= 0xFFFFFFFF
+    x ^= x >> 16; x = (x * 0x7feb352d) & 0xFFFFFFFF
+    x ^= x >> 15; x = (x * 0x846ca68b) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def tu_split(seed, plane_id, x, y, size):
+    k = _mix32(seed ^ ((0x9E3779B9 * (plane_id + 1)) & 0xFFFFFFFF))
+    k = _mix32(k ^ x)
+    k = _mix32(k ^ ((y * 0x85ebca6b) & 0xFFFFFFFF))
+    k = _mix32(k ^ size)
+    return (k & 3) < 2
+
+
+def ref_plane_cfg4(I, T, Q, src, ctb, plane_id, seed, qp, is_luma):
+    h, w = src.shape
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    tul = np.zeros((h // 4, w // 4), np.uint8)
+
+    def one(x, y, n):
+        orig = src[y:y + n, x:x + n]
+        top, left, _ = _neighbors(src, x, y, n)
+        dc = I.intra_dc_predict(top, left, n)
+        pl = I.intra_planar_predict(top, left, int(top[-1]), int(left[-1]), n)
+        edc = int(np.sum(I.residual_block(orig, dc).astype(np.int64) ** 2))
+        epl = int(np.sum(I.residual_block(orig, pl).astype(np.int64) ** 2))
+        pred = dc if edc <= epl else pl
+        l, r, _ = _chain(I, T, Q, orig, pred, qp, bool(is_luma and n == 4))
+        lvl[y:y + n, x:x + n] = l
+        rec[y:y + n, x:x + n] = r
+        tul[y // 4:(y + n) // 4, x // 4:(x + n) // 4] = int(np.log2(n))
+
+    def tree(x, y, s):
+        if x >= w or y >= h:
+            return
+        over = (x + s > w) or (y + s > h)
+        if s > 4 and (over or tu_split(seed, plane_id, x, y, s)):
+            hs = s // 2
+            for dy in (0, hs):
+                for dx in (0, hs):
+                    tree(x + dx, y + dy, hs)
+            return
+        if not over:
+            one(x, y, s)
+
+    for cy in range((h + ctb - 1) // ctb):
+        for cx in range((w + ctb - 1) // ctb):
+            tree(cx * ctb, cy * ctb, ctb)
+    return lvl, rec, tul
+
+
+def gen_planes(I, T, Q, rng):
+    out = {}
+    # cfg 2: full 1080p residual plane -> sha256 of levels; plus a small plane in full
+    small = rng.integers(-255, 256, size=(72, 136)).astype(np.int16)   # 136 % 8 == 0, 72 rows
+    out["p2_small_in"] = small
+    out["p2_small_lvl"] = ref_plane_cfg2(T, Q, small)
+    edge = rng.integers(-32768, 32768, size=(16, 24)).astype(np.int16)
+    out["p2_edge_in"], out["p2_edge_lvl"] = edge, ref_plane_cfg2(T, Q, edge, qp=0)
+    # cfg 3: small YUV-like source plane with gradients + noise, and an edge-case plane
+    yy, xx = np.mgrid[0:40, 0:56]
+    src = np.clip(60 + 2 * xx + yy + rng.integers(-12, 13, size=xx.shape), 0, 255).astype(np.int16)
+    m, l, r, tot = ref_plane_cfg3(I, T, Q, src, 32)
+    out.update(p3_src=src, p3_modes=m, p3_lvl=l, p3_rec=r, p3_sse=np.int64(tot))
+    src2 = rng.integers(0, 256, size=(20, 28)).astype(np.int16)        # partial edge blocks skipped
+    m, l, r, tot = ref_plane_cfg3(I, T, Q, src2, 22)
+    out.update(p3b_src=src2, p3b_modes=m, p3b_lvl=l, p3b_rec=r, p3b_sse=np.int64(tot))
+    # cfg 4: small luma (ctb 32) and chroma (ctb 16) planes with partial CTUs
+    yy, xx = np.mgrid[0:80, 0:104]
+    lum = np.clip(100 + xx - yy + rng.integers(-20, 21, size=xx.shape), 0, 255).astype(np.int16)
+    l, r, t = ref_plane_cfg4(I, T, Q, lum, 32, 0, 1234, 32, True)
+    out.update(p4y_src=lum, p4y_lvl=l, p4y_rec=r, p4y_tu=t)
+    chro = rng.integers(90, 170, size=(40, 52)).astype(np.int16)
+    l, r, t = ref_plane_cfg4(I, T, Q, chro, 16, 1, 1234, 32, False)
+    out.update(p4u_src=chro, p4u_lvl=l, p4u_rec=r, p4u_tu=t)
+    return out
+
+
+def plane_hash_1080p(T, Q):
+    rng = np.random.default_rng(20260)
+    plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
+    lvl = ref_plane_cfg2(T, Q, plane, 32)
+    return hashlib.sha256(lvl.tobytes()).hexdigest()
+
+
+def main():
+    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    warnings.simplefilter("ignore")
+    I, T, Q = _import_reference(ref)
+    rng = np.random.default_rng(1234)
+    files = {
+        "matrices.npz": gen_matrices(T),
+        "transform.npz": gen_transform(T, rng),
+        "quant.npz": gen_quant(Q, rng),
+        "intra.npz": gen_intra(I, rng),
+        "chain.npz": gen_chain(I, T, Q),
+        "planes.npz": gen_planes(I, T, Q, rng),
+    }
+    manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
+                "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",
+                "files": {}}
+    for name, arrays in files.items():
+        p = os.path.join(HERE, name)
+        np.savez_compressed(p, **arrays)
+        manifest["files"][name] = hashlib.sha256(open(p, "rb").read()).hexdigest()
+    if "--skip-1080p" not in sys.argv:
+        manifest["cfg2_1080p_qp32_seed20260_levels_sha256"] = plane_hash_1080p(T, Q)
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    print(json.dumps(manifest, indent=1))
+
+
+if __name__ == "__main__":
+    main()

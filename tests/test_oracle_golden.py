@@ -1,0 +1,188 @@
+"""Pin the CPU restatement (oracle/) to the reference.
+
+Two sources of truth, both data:
+  * tests/golden/*.npz -- reference outputs recorded by tests/golden/make_golden.py;
+  * the known answers the reference's own tests hold, restated
+    here as literal vectors with the reference test file:line they come from.
+CPU only (no GPU needed).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def test_matrices(golden):
+    g = golden("matrices.npz")
+    assert np.array_equal(O.matrix(4, True), g["DST4"])
+    for n in (4, 8, 16, 32):
+        assert np.array_equal(O.matrix(n), g[f"DCT{n}"]), n
+    with pytest.raises(ValueError):
+        O.matrix(6)
+
+
+@pytest.mark.parametrize("key,n,dst", [("n4_dst", 4, True), ("n4_dct", 4, False), ("n8_dct", 8, False),
+                                       ("n16_dct", 16, False), ("n32_dct", 32, False)])
+def test_transforms(golden, key, n, dst):
+    g = golden("transform.npz")
+    for x, y in zip(g[key + "_fwd_in"], g[key + "_fwd_out"]):
+        assert np.array_equal(O.forward_transform(x, dst), y)
+    for x, y in zip(g[key + "_inv_in"], g[key + "_inv_out"]):
+        assert np.array_equal(O.inverse_transform(x, dst), y)
+
+
+def test_quant(golden):
+    g = golden("quant.npz")
+    for a, qp in enumerate(g["q_qps"]):
+        for b, size in enumerate([4, 8, 16, 32]):
+            for c, intra in enumerate([True, False]):
+                assert np.array_equal(O.quantize(g["q_vec32"], qp, size, intra), g["q_out32"][a, b, c]), (qp, size, intra)
+                assert np.array_equal(O.quantize(g["q_vec16"], qp, size, intra), g["q_out16"][a, b, c]), (qp, size, intra)
+        assert np.array_equal(O.dequantize(g["dq_in"], qp), g["dq_out"][a]), qp
+
+
+@pytest.mark.parametrize("n", [4, 8, 16, 32])
+def test_intra(golden, n):
+    g = golden("intra.npz")
+    for s in range(8):
+        top = g[f"n{n}_top"][s, :g[f"n{n}_ntop"][s]]
+        left = g[f"n{n}_left"][s, :g[f"n{n}_nleft"][s]]
+        corner = int(g[f"n{n}_corner"][s])
+        for m in range(35):
+            st = g[f"n{n}_status"][s, m]
+            exp = g[f"n{n}_pred"][s, m]
+            if m == 0:
+                t = top[:n] if top.size >= n else top
+                l = left[:n] if left.size >= n else left
+                fn = lambda: O.intra_planar(t, l, int(top[min(n, top.size) - 1]), int(left[min(n, left.size) - 1]), n)
+            elif m == 1:
+                fn = lambda: O.intra_dc(top, left, n)
+            else:
+                fn = lambda: O.intra_angular(top, left, corner, m, n)
+            if st == 0:
+                assert np.array_equal(fn(), exp), (n, s, m)
+            else:
+                with pytest.raises({1: OverflowError, 2: IndexError}[int(st)]):
+                    fn()
+
+
+def test_intra_quirks(golden):
+    g = golden("intra.npz")
+    t, l = g["quirk_top"], g["quirk_left"]
+    assert np.array_equal(O.intra_angular(t, l, 77, 0, 4), g["quirk_ang0"])      # D10 modes 0/1
+    assert np.array_equal(O.intra_angular(t, l, 77, 1, 4), g["quirk_ang1"])
+    assert np.array_equal(O.intra_angular(t, l, 77, -5, 4), g["quirk_angm5"])
+    assert np.array_equal(O.intra_dc(t, l, 4, variant4x4=True), g["quirk_dc4"])  # D7 whole-array sum
+    assert np.array_equal(O.intra_dc(t, l, 4), g["quirk_dc4_len9"])
+    with pytest.raises(IndexError):
+        O.intra_angular(t, l, 77, 35, 4)
+    assert np.array_equal(O.residual(g["rr_a"], g["rr_b"]), g["rr_res"])
+    assert np.array_equal(O.reconstruct(g["rr_a"], g["rr_b"]), g["rr_rec"])
+    for bd in [1, 8, 10, 12, 16, 40, 63]:
+        assert np.array_equal(O.clip(g["clip_in"], bd), g[f"clip_bd{bd}"]), bd
+
+
+def test_chain(golden):
+    g = golden("chain.npz")
+    pred = O.intra_dc(g["c1_top"], g["c1_left"], 4)
+    assert np.array_equal(pred, g["c1_pred"])
+    res = O.residual(g["c1_orig"], pred)
+    assert np.array_equal(res, g["c1_res"])
+    coeff = O.forward_transform(res, True)
+    assert np.array_equal(coeff, g["c1_coeff"])
+    for qp in (20, 22):
+        lvl = O.quantize(coeff, qp, 4)
+        assert np.array_equal(lvl, g[f"c1_lvl_qp{qp}"])
+        deq = O.dequantize(lvl, qp)
+        assert np.array_equal(deq, g[f"c1_deq_qp{qp}"])
+        rres = O.inverse_transform(deq, True)
+        assert np.array_equal(rres, g[f"c1_rres_qp{qp}"])
+        rec = O.clip(O.reconstruct(pred, rres.astype(np.int16)), 8)
+        assert np.array_equal(rec, g[f"c1_recon_qp{qp}"])
+
+
+# ---- known answers from the reference's own tests (restated as data) ----
+
+def test_reference_known_answers():
+    # test_intra_dc.py:23-43 (DC = 101) and :45-56 variants
+    assert np.all(O.intra_dc([102, 98, 100, 101], [103, 102, 101, 99], 4, variant4x4=True) == 101)
+    assert np.all(O.intra_dc([1, 1, 1, 1], [1, 1, 1, 0], 4, variant4x4=True) == 1)
+    assert np.all(O.intra_dc([100] * 8, [100] * 8, 8) == 100)                 # :62-70
+    assert np.all(O.intra_dc([50] * 16, [50] * 16, 16) == 50)                 # :72-80
+    # test_intra_dc.py:86-127 residual example
+    orig = np.array([[102, 101, 100, 100], [103, 102, 101, 100], [103, 102, 100, 99], [104, 101, 99, 98]], np.int16)
+    exp = np.array([[1, 0, -1, -1], [2, 1, 0, -1], [2, 1, -1, -2], [3, 0, -2, -3]], np.int16)
+    assert np.array_equal(O.residual(orig, np.full((4, 4), 101, np.int16)), exp)
+    # test_intra_dc.py:163-177 clip
+    assert np.array_equal(O.clip([[-10, 0, 128, 255, 300]], 8), [[0, 0, 128, 255, 255]])
+    assert np.array_equal(O.clip([[-10, 0, 512, 1023, 2000]], 10), [[0, 0, 512, 1023, 1023]])
+    # test_intra_planar.py:56-76 corners
+    p = O.intra_planar([0] * 4, [0] * 4, 255, 255, 4)
+    assert p[0, 0] == 64 and p[3, 3] == 255
+    for n, v in [(4, 100), (8, 128), (16, 200), (32, 50)]:                    # :78-86
+        assert np.all(O.intra_planar([v] * n, [v] * n, v, v, n) == v)
+    # test_intra_angular.py:69-85 mode 18 full matrix (pins D5)
+    top = [0, 10, 20, 30, 40, 50, 60, 70, 80]
+    left = [0, 5, 5, 5, 5, 5, 5, 5, 5]
+    exp18 = np.array([[0, 10, 20, 30], [0, 0, 10, 20], [5, 0, 0, 10], [5, 5, 0, 0]])
+    assert np.array_equal(O.intra_angular(top, left, 0, 18, 4), exp18)
+    # :25-43 mode 26 with len-9 refs at sizes 4 and 8 (D6)
+    t9 = [99, 100, 110, 120, 130, 0, 0, 0, 0]
+    l9 = [99, 50, 50, 50, 50, 0, 0, 0, 0]
+    for n in (4, 8):
+        p = O.intra_angular(t9, l9, 99, 26, n)
+        assert list(p[:, 0]) == [100] * n and list(p[:, 3]) == [130] * n
+    # :45-67 mode 34, :111-133 mode 2
+    p = O.intra_angular(top, [0] * 9, 0, 34, 4)
+    assert (p[0, 0], p[0, 3], p[1, 0], p[3, 3]) == (20, 50, 30, 80)
+    p = O.intra_angular([0] * 9, top, 0, 2, 4)
+    assert (p[0, 0], p[3, 0], p[0, 1], p[3, 3]) == (20, 50, 30, 80)
+    # :91-109 mode 10 rows
+    p = O.intra_angular(l9, t9, 99, 10, 4)
+    assert [int(p[i, 0]) for i in range(4)] == [100, 110, 120, 130]
+    # :175-188 every mode on a flat reference
+    for m in range(2, 35):
+        assert np.all(O.intra_angular([128] * 9, [128] * 9, 128, m, 4) == 128)
+    # test_quant.py:25-56 qp params via quantize's clamp: QP -5 == QP 0, QP 100 == QP 51
+    v = np.array([1000, -1000, 77])
+    assert np.array_equal(O.quantize(v, -5, 4), O.quantize(v, 0, 4))
+    assert np.array_equal(O.quantize(v, 100, 4), O.quantize(v, 51, 4))
+    # test_transform.py:57-64 zeros in, zeros out
+    for n, d in [(4, False), (8, False), (4, True)]:
+        assert not O.forward_transform(np.zeros((n, n), np.int16), d).any()
+
+
+def test_planes(golden):
+    g = golden("planes.npz")
+    assert np.array_equal(O.fwd8x8_quant_plane(g["p2_small_in"]), g["p2_small_lvl"])
+    assert np.array_equal(O.fwd8x8_quant_plane(g["p2_edge_in"], qp=0), g["p2_edge_lvl"])
+    for k, qp in (("p3", 32), ("p3b", 22)):
+        m, l, r, sse = O.intra_rdo_plane(g[f"{k}_src"], qp)
+        assert np.array_equal(m, g[f"{k}_modes"]) and np.array_equal(l, g[f"{k}_lvl"])
+        assert np.array_equal(r, g[f"{k}_rec"]) and sse == int(g[f"{k}_sse"])
+    l, r, t = O.tu_pipeline_plane(g["p4y_src"], 32, 0, 1234, 32, True)
+    assert np.array_equal(t, g["p4y_tu"]) and np.array_equal(l, g["p4y_lvl"]) and np.array_equal(r, g["p4y_rec"])
+    l, r, t = O.tu_pipeline_plane(g["p4u_src"], 16, 1, 1234, 32, False)
+    assert np.array_equal(t, g["p4u_tu"]) and np.array_equal(l, g["p4u_lvl"]) and np.array_equal(r, g["p4u_rec"])
+
+
+def test_plane_hash_1080p():
+    """sha256 of the reference's levels for a seeded 1080p plane."""
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    rng = np.random.default_rng(20260)
+    plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
+    lvl = O.fwd8x8_quant_plane(plane, 32)
+    assert hashlib.sha256(lvl.tobytes()).hexdigest() == man["cfg2_1080p_qp32_seed20260_levels_sha256"]
+
+
+def test_manifest_integrity():
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    assert man["numpy"].split(".")[0] == "2"      # NEP 50 semantics (D8)
+    for name, h in man["files"].items():
+        assert hashlib.sha256(open(os.path.join(GOLDEN, name), "rb").read()).hexdigest() == h, name
