@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Headline benchmark: transform-blocks/sec (8x8 DCT+quant, 4K YUV420) on 1..N MI355X.
+
+A "step" = one launch of the fused 8x8 forward DCT + quant (QP 32, intra
+offset) over this rank's share of a batch of synthetic 4K YUV420 int16 residual
+frames already resident in HBM (BASELINE.json configs[1] kernel on the
+metric's 4K YUV420 stream).  Multi-GPU: every frame is cut into
+CTU-row bands (32 luma / 16 chroma rows), rank r owns band r of every frame of
+a global batch of N x frames_per_gpu frames -- no data-path collective, weak
+scaling.  Timing: W warmup steps, then K steps between barrier +
+synchronize; the max over ranks is reported.  Rank 0 prints one JSON line.
+
+Roofline: algorithmic bytes per 8x8 block = 128 B int16 in + 128 B int16 out
+ x blocks per launch / average launch duration (HIP events
+on the launch stream), against 8.0 TB/s.  ``traffic`` comes from the rocprofv3
+PMC pass committed under profiles/ (tools/pmc_traffic.py) when one matches this
+configuration, else null.
+
+cpu_baseline (rank 0, N=1 only): the CPU restatement oracle/ ("port", 1
+thread) timed on a bounded sample of the same workload; the same sample's GPU
+levels are checked bit-exact against it.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "nano-hevc_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "transform-blocks/sec (8×8 DCT+quant, 4K YUV420) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_BLOCK = 256          # 64 x int16 in + 64 x int16 out
+W4K, H4K, CTU = 3840, 2160, 32
+
+
+def band_rows(rank: int, world: int, height: int, ctu: int):
+    """CTU-row band [r0, r1) of a plane for this rank (the last band may be short)."""
+    rows = (height + ctu - 1) // ctu
+    per = (rows + world - 1) // world
+    r0 = min(rank * per, rows) * ctu
+    r1 = min((rank + 1) * per * ctu, height)
+    return r0, max(r0, r1)
+
+
+def build_sets(gpu, frames: int, y_rows: int, c_rows: int):
+    """Plane sets of this rank's local buffer: per frame [Y band][U band][V band]."""
+    cw = W4K // 2
+    fe = W4K * y_rows + 2 * cw * c_rows
+    sets = []
+    if y_rows:
+        sets.append(gpu.plane_set(0, W4K, y_rows, W4K, 1, frames, 0, fe))
+    if c_rows:
+        sets.append(gpu.plane_set(W4K * y_rows, cw, c_rows, cw, 2, frames, cw * c_rows, fe))
+    return sets, fe
+
+
+def load_traffic(cfg_key: str):
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+    except Exception:
+        return None
+    e = d.get(cfg_key)
+    return None if e is None else e.get("hbm_bytes_per_launch")
+
+
+def cpu_baseline(gpu_out: torch.Tensor, res: torch.Tensor, fe: int, frames: int, qp: int, budget_s: float):
+    """Time the oracle (CPU restatement, 1 thread) on whole 4K YUV420 frames until
+    ~budget_s elapsed; check the GPU levels of those frames bit-exact."""
+    from oracle import oracle as O   # checker + CPU baseline only
+    O.lib()
+    cw, ch = W4K // 2, H4K // 2
+    done_blocks, t_cpu, exact, f = 0, 0.0, True, 0
+    while f < frames and (t_cpu < budget_s or f == 0):
+        r = res[f * fe:(f + 1) * fe].cpu().numpy()
+        g = gpu_out[f * fe:(f + 1) * fe].cpu().numpy()
+        planes = [(0, H4K, W4K), (W4K * H4K, ch, cw), (W4K * H4K + cw * ch, ch, cw)]
+        for off, h, w in planes:
+            p = r[off:off + h * w].reshape(h, w)
+            t0 = time.perf_counter()
+            lv = O.fwd8x8_quant_plane(p, qp, True)
+            t_cpu += time.perf_counter() - t0
+            done_blocks += (h // 8) * (w // 8)
+            exact &= bool(np.array_equal(lv, g[off:off + h * w].reshape(h, w)))
+        f += 1
+    return {"value": done_blocks / t_cpu, "unit": "blocks/s", "cores": 1, "kind": "port",
+            "sample": f"{f} whole 4K YUV420 frames ({done_blocks} 8x8 blocks, QP {qp}) through "
+                      f"oracle/nh_oracle.c fwd8x8_quant_plane, 1 thread, {t_cpu:.1f} s",
+            "gpu_levels_bit_exact_on_sample": exact}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--frames", type=int, default=128, help="4K YUV420 frames per GPU per step")
+    ap.add_argument("--qp", type=int, default=32)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from nano_hevc import gpu, _lib
+    _lib.load()
+
+    y0, y1 = band_rows(rank, world, H4K, CTU)
+    c0, c1 = band_rows(rank, world, H4K // 2, CTU // 2)
+    frames_global = args.frames * world
+    sets, fe = build_sets(gpu, frames_global, y1 - y0, c1 - c0)
+    nblk = gpu.blocks_in(sets)
+    # synthetic residual: U[-255,255] (worst-case 8-bit residual magnitude), seeded per rank
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234 + rank)
+    res = torch.randint(-255, 256, (frames_global * fe,), dtype=torch.int16, device=dev, generator=gen)
+    out = torch.zeros_like(res)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        gpu.fwd8x8_quant(res, sets, args.qp, True, out=out, variant=args.variant, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    blocks_t = torch.tensor([nblk], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(blocks_t, op=dist.ReduceOp.SUM)
+    elapsed, kern_ms = float(t[0]), float(t[1])
+    total_blocks = float(blocks_t[0]) * args.steps
+    value = total_blocks / elapsed
+
+    if rank == 0:
+        achieved = nblk * BYTES_PER_BLOCK / (kern_ms * 1e-3) / 1e9
+        cfg_key = f"fwd8x8_qp{args.qp}_4k_yuv420_f{args.frames}_v{args.variant}_n{world}"
+        traffic = load_traffic(cfg_key)
+        line = {
+            "metric": METRIC, "value": value, "unit": "blocks/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32",
+            "data": "synthetic (seeded U[-255,255] int16 residual frames, resident in HBM)",
+            "config": {"workload": "4K YUV420 residual frame stream, fused fwd 8x8 int-DCT + quant QP32 intra "
+                                   "(cfg 2 kernel on the metric's 4K stream), CTU-row band sharding",
+                       "frames_per_gpu": args.frames, "blocks_per_launch": nblk, "qp": args.qp,
+                       "resolution": "3840x2160 YUV420 int16 in / int16 levels out",
+                       "parallelism": f"band{world}", "kernel_variant": args.variant},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "bytes_per_block": BYTES_PER_BLOCK, "kernel_ms_avg": kern_ms},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(out, res, fe, frames_global, args.qp, args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+/*
+ * nanohevc.h -- C ABI of the MI355X-native HEVC intra-block hot path.
+ *
+ * The reference (Luodian/nano-hevc) is pure Python + numpy and has no FFI; its
+ * drop-in boundary is the set of Python functions re-exported by
+ * nano_hevc/__init__.py:50-91.  This header is what a binding of that boundary
+ * calls (ctypes shim: nano-hevc_amd/nano_hevc/_lib.py).
+ *
+ * Two groups of entry points:
+ *   (i)  per-block, host pointers, synchronous -- one reference call each
+ *        (inputs already converted by the shim exactly as the reference
+ *        converts them: .astype(np.int32) for transforms, int64 for sums);
+ *   (ii) batched, device pointers, asynchronous on a caller hipStream_t
+ *        (passed as void*; NULL = the null stream) -- the frame-level path.
+ * No entry point allocates caller-visible memory; no C++ exception crosses the
+ * ABI.  Every function returns NH_OK (0) or a negative NH_E* code; the shim
+ * maps codes to the exception the reference raises in the same situation.
+ */
+#ifndef NANOHEVC_H
+#define NANOHEVC_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NH_OK 0
+#define NH_EVALUE (-1)    /* ValueError("Unsupported transform size: N") transform.py:150-151 */
+#define NH_EINDEX (-2)    /* IndexError (mode >= 35, short refs) intra.py:142, :177 */
+#define NH_EOVERFLOW (-3) /* OverflowError: int16 store out of range (numpy 2) intra.py:62,111,173 */
+#define NH_EZERODIV (-4)  /* ZeroDivisionError: intra_dc_predict size 0, intra.py:61 */
+#define NH_EARG (-5)      /* bad argument (null pointer, misaligned plane, negative count) */
+#define NH_ENODEV (-10)   /* no HIP device visible */
+#define NH_EHIP (-11)     /* HIP runtime error (message: nh_last_error()) */
+
+/* ---------------- library / device ---------------- */
+const char* nh_version(void);
+const char* nh_last_error(void);
+int nh_device_count(int* count);
+
+/* ---------------- (i) per-block entry points (host pointers) ---------------- */
+
+/* intra.py:37-43 intra_dc_predict_4x4 (variant4x4=1, size ignored) and
+ * intra.py:46-62 intra_dc_predict: dc over the WHOLE top/left arrays (D7). out: size*size */
+int nh_intra_dc(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft,
+                int64_t size, int variant4x4, int16_t* out);
+/* intra.py:81-113 intra_planar_predict; log2size = int(np.log2(size)) */
+int nh_intra_planar(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft,
+                    int64_t top_right, int64_t bottom_left, int64_t size, int64_t log2size,
+                    int16_t* out);
+/* intra.py:116-207 intra_angular_predict (+ _build_ref_array, _project_sample_at);
+ * mode uses Python list indexing into INTRA_PRED_ANGLE (D10) */
+int nh_intra_angular(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft,
+                     int64_t corner, int mode, int64_t size, int16_t* out);
+/* intra.py:65-67 residual_block / :70-72 reconstruct_block on int16 (wrap) */
+int nh_residual(const int16_t* orig, const int16_t* pred, int64_t n, int16_t* out);
+int nh_reconstruct(const int16_t* pred, const int16_t* res, int64_t n, int16_t* out);
+/* intra.py:75-78 clip_to_pixel_range: clamp to [0, maxval] then wrap to int16 */
+int nh_clip(const int64_t* x, int64_t n, int64_t maxval, int16_t* out);
+/* transform.py:154-196 forward_transform / :199-238 inverse_transform on an
+ * int32 size x size block (row-major) */
+int nh_forward_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out);
+int nh_inverse_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out);
+/* quant.py:41-79 quantize: abs_bits = bit width in which np.abs wraps (8/16/32/64) */
+int nh_quantize(const int64_t* coeff, int64_t n, int qp, int64_t log2size, int is_intra,
+                int abs_bits, int32_t* out);
+/* quant.py:82-123 dequantize (size unused, D4) */
+int nh_dequantize(const int64_t* level, int64_t n, int qp, int32_t* out);
+/* quant.py:171-173 count_nonzero */
+int nh_count_nonzero(const int64_t* level, int64_t n, int64_t* count);
+/* quant.py:153-168 estimate_bits: the float64 sum (numpy pairwise order) of
+ * log2(|l|+1) + 2*(|l|>0), |l|+1 wrapping in an abs_bits (32/64) dtype; the
+ * caller applies int() (which raises on NaN/inf exactly as the reference). */
+int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits);
+
+/* ---------------- (ii) batched device entry points ---------------- */
+
+/* A set of equally shaped raster planes inside one buffer (e.g. the Y planes,
+ * or the U+V planes, of a stream of YUV420 frames).  Offsets/pitches are in
+ * elements.  Plane p = g*planes_per_group + c lives at
+ *   base + g*group_stride + c*plane_stride.
+ * Only full 8x8 blocks are processed (block.py:68-74 skips partial blocks). */
+typedef struct nh_plane_set {
+    int64_t base;
+    int64_t plane_stride;
+    int64_t group_stride;
+    int32_t width, height, pitch;
+    int32_t planes_per_group;
+    int32_t num_groups;
+    int32_t reserved;
+} nh_plane_set;
+
+#define NH_MAX_PLANE_SETS 4
+
+/* THE HOT PATH (config 2 / north-star metric): forward 8x8 integer DCT
+ * (transform.py:154-196) fused with quantize_block (quant.py:126-137) over
+ * every full 8x8 block of int16 residual planes.  Levels are written as int16
+ * at the block's raster position in d_lvl (same layout as d_res).  Exact for
+ * every int16 input: |level| <= 26214 always fits int16 for N=8.
+ * Requires base/pitch/strides to be multiples of 8 elements (16-B rows). */
+int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
+                           int nsets, int qp, int is_intra, void* stream);
+/* Same computation, one wave-cooperative variant kept for A/B measurement. */
+int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
+                                   int nsets, int qp, int is_intra, int variant, void* stream);
+
+/* nblocks contiguous size x size int32 blocks (row-major) */
+int nh_fwd_transform_batch(const int32_t* d_in, int32_t* d_out, int64_t nblocks, int size,
+                           int use_dst, void* stream);
+int nh_inv_transform_batch(const int32_t* d_in, int32_t* d_out, int64_t nblocks, int size,
+                           int use_dst, void* stream);
+/* elementwise over n int32 values (abs wraps at 32 bits, as for int32 input) */
+int nh_quant_batch(const int32_t* d_coeff, int32_t* d_level, int64_t n, int qp, int log2size,
+                   int is_intra, void* stream);
+int nh_dequant_batch(const int32_t* d_level, int32_t* d_coeff, int64_t n, int qp, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,198 @@
+// nh_fused8x8.hip -- THE HOT PATH (config 2 / north-star metric):
+// forward 8x8 integer DCT (transform.py:154-196) fused with quantize_block
+// (quant.py:126-137, :41-79) over every full 8x8 block (block.py:68-74) of
+// int16 residual planes, int16 levels written back at the block's raster
+// position.
+//
+// Design:
+//   * one thread = one 8x8 block, entirely in VGPRs -- no LDS round trip.
+//     Lane l of a wave owns block bx0+l of a block row, so each of the 8 row
+//     loads is one 16-B dwordx4 per lane = one contiguous 1 KiB segment per
+//     wave instruction (and the same for the 8 row stores);
+//   * both 1-D passes are the recursive even/odd butterfly of nh_common.hpp
+//     (E/O adds + 24-bit mads, v_mad_i32_i24, full rate).  Exactness: int16
+//     input => pass-1 operands |O| <= 2^16, pass-2 operands <= 2^18, all
+//     within the signed 24-bit multiply; sums stay < 2^31 so the int32 ring of
+//     the reference (D1/D2) is reproduced exactly;
+//   * quantizer in 4 ops (quant_s in nh_common.hpp: signed v_mad_i32_i24 with a
+//     sign-selected offset, exact for |c| <= 2^17 which int16 input guarantees);
+//     |level| <= 26214 always fits int16;
+//   * workgroups never straddle two plane sets, so the set lookup is scalar.
+// Roofline: 128 B in + 128 B out per block (HBM-bound; ~1.2k VALU ops/block).
+#include <hip/hip_runtime.h>
+#include "nh_common.hpp"
+#include "nh_internal.hpp"
+
+namespace nh {
+
+struct SetDev {
+    int64_t base, plane_stride, group_stride;
+    int32_t pitch;
+    uint32_t nblocks;
+    uint32_t wg_start;  // first workgroup of this set
+    FastDiv bpp, bpr, ppg;
+};
+
+struct Fused8Args {
+    const int16_t* in;
+    int16_t* out;
+    SetDev set[NH_MAX_PLANE_SETS];
+    int32_t nsets;
+    QuantS q;
+};
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+template <int VARIANT>
+__device__ __forceinline__ v4i ld16(const int16_t* p) {
+    if constexpr (VARIANT == 1) return __builtin_nontemporal_load((const v4i*)p);
+    else return *(const v4i*)p;
+}
+template <int VARIANT>
+__device__ __forceinline__ void st16(int16_t* p, v4i v) {
+    if constexpr (VARIANT == 1) __builtin_nontemporal_store(v, (v4i*)p);
+    else *(v4i*)p = v;
+}
+
+template <int VARIANT>
+__global__ void __launch_bounds__(256) k_fwd8x8_quant(Fused8Args a) {
+    // scalar (wave-uniform) set selection
+    int s = 0;
+#pragma unroll
+    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
+        if (k < a.nsets && blockIdx.x >= a.set[k].wg_start) s = k;
+    SetDev S = a.set[0];
+#pragma unroll
+    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
+        if (s == k) S = a.set[k];
+
+    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    if (b >= S.nblocks) return;
+    const uint32_t p = fdiv(b, S.bpp), r = b - p * S.bpp.d;
+    const uint32_t by = fdiv(r, S.bpr), bx = r - by * S.bpr.d;
+    const uint32_t g = fdiv(p, S.ppg), c = p - g * S.ppg.d;
+    const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride +
+                        (int64_t)by * 8 * S.pitch + (int64_t)bx * 8;
+    const int16_t* src = a.in + off;
+    int16_t* dst = a.out + off;
+
+    // ---- load 8 rows x 16 B, unpack int16 -> int32 ----
+    v4i raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) raw[i] = ld16<VARIANT>(src + (int64_t)i * S.pitch);
+    uint32_t X[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            X[i][2 * m] = (uint32_t)(int32_t)(int16_t)(w[m] & 0xffff);
+            X[i][2 * m + 1] = (uint32_t)(w[m] >> 16);
+        }
+    }
+
+    // ---- pass 1: columns, temp = T.X, (acc+128)>>8  (transform.py:179-185) ----
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = X[k][j];
+        fwd_dct<8, Mul24>(x, y, 128u);   // rounding constant folded into the accumulators
+#pragma unroll
+        for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)y[i] >> 8);
+    }
+
+    // ---- pass 2: rows, coeff = temp.T^T  (transform.py:188-194) + quant + pack ----
+    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
+    asm volatile("" : "+v"(h_v), "+v"(hneg_v));  // pin the two offsets in VGPRs
+    v4i outv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t y[8];
+        fwd_dct<8, Mul24>(X[i], y, 128u);
+        int32_t L[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) L[j] = quant_s((int32_t)y[j] >> 8, a.q, h_v, hneg_v);
+        int w[4];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) w[m] = (int)__builtin_amdgcn_perm((uint32_t)L[2 * m + 1], (uint32_t)L[2 * m], 0x05040100u);
+        outv[i] = v4i{w[0], w[1], w[2], w[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<VARIANT>(dst + (int64_t)i * S.pitch, outv[i]);
+}
+
+static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
+                      int is_intra, Fused8Args& a, uint32_t& total_wg) {
+    if (!d_res || !d_lvl || !sets || nsets < 1 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
+    if (((uintptr_t)d_res & 15) || ((uintptr_t)d_lvl & 15)) {
+        set_error("fwd8x8: buffers must be 16-byte aligned");
+        return NH_EARG;
+    }
+    a = Fused8Args{};
+    a.in = d_res;
+    a.out = d_lvl;
+    a.nsets = nsets;
+    int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);  // quant.py:35
+    const int per = q / 6, rem = q % 6;
+    const int shift = 14 + per + 3;             // quant.py:77, log2(8) = 3
+    QuantParams qp0;
+    qp0.mf = quant_scale(rem);
+    qp0.off = is_intra ? (1u << shift) / 3 : (1u << shift) / 6;
+    qp0.shift = shift;
+    a.q = make_quants(qp0);
+    uint64_t wg = 0;
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& p = sets[k];
+        if (p.width < 0 || p.height < 0 || p.pitch < p.width || p.planes_per_group < 1 || p.num_groups < 0 ||
+            (p.base | p.plane_stride | p.group_stride | p.pitch) & 7) {
+            set_error("fwd8x8: plane set must have pitch>=width and 8-element aligned base/pitch/strides");
+            return NH_EARG;
+        }
+        const uint64_t bpr = p.width / 8, rows = p.height / 8;
+        const uint64_t bpp = bpr * rows, planes = (uint64_t)p.planes_per_group * p.num_groups;
+        const uint64_t nb = bpp * planes;
+        if (nb >= (1ull << 31)) { set_error("fwd8x8: > 2^31 blocks per set"); return NH_EARG; }
+        SetDev& d = a.set[k];
+        d.base = p.base;
+        d.plane_stride = p.plane_stride;
+        d.group_stride = p.group_stride;
+        d.pitch = p.pitch;
+        d.nblocks = (uint32_t)nb;
+        d.wg_start = (uint32_t)wg;
+        d.bpp = make_fastdiv(bpp ? (uint32_t)bpp : 1);
+        d.bpr = make_fastdiv(bpr ? (uint32_t)bpr : 1);
+        d.ppg = make_fastdiv((uint32_t)p.planes_per_group);
+        wg += (nb + 255) / 256;
+    }
+    for (int k = nsets; k < NH_MAX_PLANE_SETS; ++k) a.set[k].wg_start = 0xffffffffu;
+    if (wg >= (1ull << 31)) return NH_EARG;
+    total_wg = (uint32_t)wg;
+    return NH_OK;
+}
+
+}  // namespace nh
+
+using namespace nh;
+
+extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
+                                              int nsets, int qp, int is_intra, int variant, void* stream) {
+    Fused8Args a;
+    uint32_t wg = 0;
+    int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+    if (rc) return rc;
+    if (!wg) return NH_OK;
+    hipStream_t s = as_stream(stream);
+    switch (variant) {
+        case 0: k_fwd8x8_quant<0><<<wg, 256, 0, s>>>(a); break;
+        case 1: k_fwd8x8_quant<1><<<wg, 256, 0, s>>>(a); break;
+        default: return NH_EARG;
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,
+                                      int qp, int is_intra, void* stream) {
+    return nh_fwd8x8_quant_planes_variant(d_res, d_lvl, sets, nsets, qp, is_intra, 0, stream);
+}

@@ -1,0 +1,112 @@
+"""ctypes binding of include/nanohevc.h (libnanohevc.so, built in-tree for gfx950).
+
+There is no CPU fallback: if the library or a HIP device is missing, every
+compute call raises ``NanoHevcUnavailable`` (a RuntimeError) -- loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnanohevc.so")
+
+NH_OK, NH_EVALUE, NH_EINDEX, NH_EOVERFLOW, NH_EZERODIV, NH_EARG = 0, -1, -2, -3, -4, -5
+NH_ENODEV, NH_EHIP = -10, -11
+
+
+class NanoHevcUnavailable(RuntimeError):
+    """The HIP library or an MI355X is not available (no CPU fallback exists)."""
+
+
+class PlaneSet(C.Structure):
+    """nh_plane_set (include/nanohevc.h)."""
+    _fields_ = [("base", C.c_int64), ("plane_stride", C.c_int64), ("group_stride", C.c_int64),
+                ("width", C.c_int32), ("height", C.c_int32), ("pitch", C.c_int32),
+                ("planes_per_group", C.c_int32), ("num_groups", C.c_int32), ("reserved", C.c_int32)]
+
+
+P, I64, I32, U32, VP = C.c_void_p, C.c_int64, C.c_int, C.c_uint32, C.c_void_p
+
+# every symbol declared in include/nanohevc.h, with its argument types
+SIGNATURES = {
+    "nh_version": ([], C.c_char_p),
+    "nh_last_error": ([], C.c_char_p),
+    "nh_device_count": ([P], I32),
+    "nh_intra_dc": ([P, I64, P, I64, I64, I32, P], I32),
+    "nh_intra_planar": ([P, I64, P, I64, I64, I64, I64, I64, P], I32),
+    "nh_intra_angular": ([P, I64, P, I64, I64, I32, I64, P], I32),
+    "nh_residual": ([P, P, I64, P], I32),
+    "nh_reconstruct": ([P, P, I64, P], I32),
+    "nh_clip": ([P, I64, I64, P], I32),
+    "nh_forward_transform": ([P, I64, I32, P], I32),
+    "nh_inverse_transform": ([P, I64, I32, P], I32),
+    "nh_quantize": ([P, I64, I32, I64, I32, I32, P], I32),
+    "nh_dequantize": ([P, I64, I32, P], I32),
+    "nh_count_nonzero": ([P, I64, P], I32),
+    "nh_estimate_bits": ([P, I64, I32, P], I32),
+    "nh_fwd8x8_quant_planes": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, VP], I32),
+    "nh_fwd8x8_quant_planes_variant": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, I32, VP], I32),
+    "nh_fwd_transform_batch": ([P, P, I64, I32, I32, VP], I32),
+    "nh_inv_transform_batch": ([P, P, I64, I32, I32, VP], I32),
+    "nh_quant_batch": ([P, P, I64, I32, I32, I32, VP], I32),
+    "nh_dequant_batch": ([P, P, I64, I32, VP], I32),
+}
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load libnanohevc.so (raises NanoHevcUnavailable if it was not built)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NanoHevcUnavailable(
+            f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950); nano_hevc has no CPU fallback")
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        _load_error = e
+        raise NanoHevcUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    for name, (args, res) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    load().nh_device_count(C.byref(n))
+    return n.value
+
+
+def check(rc: int, what: str = ""):
+    """Map an NH_E* code to the exception the reference raises in that case."""
+    if rc == NH_OK:
+        return
+    msg = f"{what}: " if what else ""
+    if rc == NH_EVALUE:
+        raise ValueError(msg + "unsupported value")
+    if rc == NH_EINDEX:
+        raise IndexError(msg + "index out of range")
+    if rc == NH_EOVERFLOW:
+        raise OverflowError(msg + "Python integer out of bounds for int16")
+    if rc == NH_EZERODIV:
+        raise ZeroDivisionError(msg + "integer division or modulo by zero")
+    if rc == NH_ENODEV:
+        raise NanoHevcUnavailable(msg + "no HIP device visible: nano_hevc (MI355X) has no CPU fallback")
+    err = load().nh_last_error().decode(errors="replace")
+    if rc == NH_EARG:
+        raise ValueError(msg + "bad argument: " + err)
+    raise RuntimeError(msg + f"HIP error {rc}: {err}")
+
+
+def ptr(a: np.ndarray):
+    return a.ctypes.data_as(C.c_void_p)

@@ -1,0 +1,131 @@
+"""Batched, device-resident entry points (the frame-level path).
+
+The reference functions are one block per call; these take whole device
+buffers (torch tensors on an MI355X, used only as device memory + stream) and
+launch the gfx950 kernels through the C ABI on the tensor's current stream.
+
+  fwd8x8_quant        -- the hot path: fused 8x8 DCT + quant over plane sets
+  yuv420_plane_sets   -- nh_plane_set descriptors for a stream of YUV420 frames
+  fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Sequence
+
+from . import _lib
+from ._lib import PlaneSet, check
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _stream(stream=None) -> int:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _need(t, dtype, what):
+    torch = _torch()
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError(f"{what}: expected a CUDA/HIP torch tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{what}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+
+
+def plane_set(base: int, width: int, height: int, pitch: int | None = None, planes_per_group: int = 1,
+              num_groups: int = 1, plane_stride: int = 0, group_stride: int = 0) -> PlaneSet:
+    return PlaneSet(base, plane_stride, group_stride, width, height, pitch or width, planes_per_group, num_groups, 0)
+
+
+def yuv420_frame_elems(width: int, height: int) -> int:
+    return width * height + 2 * (width // 2) * (height // 2)
+
+
+def yuv420_plane_sets(num_frames: int, width: int, height: int, frame_stride: int | None = None,
+                      base: int = 0) -> List[PlaneSet]:
+    """Descriptors for frames laid out [Y][U][V] back to back (PackedFrame layout):
+    one set for the Y planes, one for the U+V planes."""
+    fs = frame_stride or yuv420_frame_elems(width, height)
+    cw, ch = width // 2, height // 2
+    ys = width * height
+    return [plane_set(base, width, height, width, 1, num_frames, 0, fs),
+            plane_set(base + ys, cw, ch, cw, 2, num_frames, cw * ch, fs)]
+
+
+def blocks_in(sets: Sequence[PlaneSet]) -> int:
+    return sum((s.width // 8) * (s.height // 8) * s.planes_per_group * s.num_groups for s in sets)
+
+
+def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = True, out=None,
+                 variant: int = 0, stream=None):
+    """Forward 8x8 DCT (transform.py:154-196) + quantize_block (quant.py:126-137) on
+    every full 8x8 block of the int16 planes described by ``sets`` inside ``res``.
+    Levels land at the same raster positions of ``out`` (int16)."""
+    torch = _torch()
+    _need(res, torch.int16, "fwd8x8_quant(res)")
+    if out is None:
+        out = torch.zeros_like(res)
+    _need(out, torch.int16, "fwd8x8_quant(out)")
+    arr = (PlaneSet * len(sets))(*sets)
+    check(_lib.load().nh_fwd8x8_quant_planes_variant(res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp),
+                                                     int(bool(is_intra)), int(variant), C.c_void_p(_stream(stream))),
+          "fwd8x8_quant")
+    return out
+
+
+def fwd8x8_quant_plane(res2d, qp: int = 32, is_intra: bool = True, out=None, stream=None):
+    """One raster int16 plane (H, W); W must be a multiple of 8 (row pitch = W)."""
+    h, w = res2d.shape
+    return fwd8x8_quant(res2d, [plane_set(0, w, h, w)], qp, is_intra, out, stream=stream)
+
+
+def _blocks(x, what):
+    torch = _torch()
+    _need(x, torch.int32, what)
+    if x.dim() != 3 or x.shape[1] != x.shape[2]:
+        raise ValueError(f"{what}: expected (B, N, N) int32")
+    return x.shape[0], x.shape[1]
+
+
+def fwd_transform_batch(x, use_dst: bool = False, out=None, stream=None):
+    """(B, N, N) int32 -> forward_transform of every block (transform.py:154-196)."""
+    b, n = _blocks(x, "fwd_transform_batch")
+    out = _torch().empty_like(x) if out is None else out
+    check(_lib.load().nh_fwd_transform_batch(x.data_ptr(), out.data_ptr(), b, n, int(bool(use_dst)),
+                                             C.c_void_p(_stream(stream))), "fwd_transform_batch")
+    return out
+
+
+def inv_transform_batch(x, use_dst: bool = False, out=None, stream=None):
+    """(B, N, N) int32 -> inverse_transform of every block (transform.py:199-238)."""
+    b, n = _blocks(x, "inv_transform_batch")
+    out = _torch().empty_like(x) if out is None else out
+    check(_lib.load().nh_inv_transform_batch(x.data_ptr(), out.data_ptr(), b, n, int(bool(use_dst)),
+                                             C.c_void_p(_stream(stream))), "inv_transform_batch")
+    return out
+
+
+def quant_batch(c, qp: int, log2size: int, is_intra: bool = True, out=None, stream=None):
+    """Elementwise quantize (quant.py:41-79) of an int32 tensor."""
+    torch = _torch()
+    _need(c, torch.int32, "quant_batch")
+    out = torch.empty_like(c) if out is None else out
+    check(_lib.load().nh_quant_batch(c.data_ptr(), out.data_ptr(), c.numel(), int(qp), int(log2size),
+                                     int(bool(is_intra)), C.c_void_p(_stream(stream))), "quant_batch")
+    return out
+
+
+def dequant_batch(l, qp: int, out=None, stream=None):
+    """Elementwise dequantize (quant.py:82-123) of an int32 tensor."""
+    torch = _torch()
+    _need(l, torch.int32, "dequant_batch")
+    out = torch.empty_like(l) if out is None else out
+    check(_lib.load().nh_dequant_batch(l.data_ptr(), out.data_ptr(), l.numel(), int(qp),
+                                       C.c_void_p(_stream(stream))), "dequant_batch")
+    return out

@@ -1,0 +1,98 @@
+"""Quantization -- drop-in for the reference ``nano_hevc.quant`` (quant.py:1-178).
+
+Parameters (qp clamp, qp/6, qp%6, shift, offset) are computed with the
+reference's own Python expressions; the per-coefficient arithmetic runs on the
+gfx950 kernels (k_quant_i64 / k_dequant_i64 / k_count_nonzero /
+k_estimate_bits in csrc/nh_blocks.hip).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, ptr
+
+# quant.py:21-22 (spec Table 8-10)
+QUANT_SCALE = [26214, 23302, 20560, 18396, 16384, 14564]
+DEQUANT_SCALE = [40, 45, 51, 57, 64, 72]
+
+
+def get_qp_params(qp: int) -> tuple[int, int]:
+    """quant.py:25-38."""
+    qp = max(0, min(51, qp))
+    return qp // 6, qp % 6
+
+
+def _abs_bits(dt) -> int:
+    """Width in which np.abs wraps for this dtype (quant.py:75)."""
+    dt = np.dtype(dt)
+    if dt.kind == "i":
+        return dt.itemsize * 8
+    if dt.kind in "ub" and dt.itemsize < 8:
+        return 64
+    raise NotImplementedError(f"quantize: integer coefficients only (got {dt})")
+
+
+def quantize(coeff, qp: int, size: int, is_intra: bool = True) -> np.ndarray:
+    """quant.py:41-79: level = sign(c) * ((|c|*MF + offset) >> shift), int32."""
+    qp_per, qp_rem = get_qp_params(qp)
+    mf = QUANT_SCALE[qp_rem]                                  # noqa: F841 (same lookup/errors)
+    log2_size = int(np.log2(size))
+    shift = 14 + qp_per + log2_size
+    offset = (1 << shift) // 3 if is_intra else (1 << shift) // 6   # noqa: F841
+    c = np.asarray(coeff)
+    ab = _abs_bits(c.dtype)
+    x = np.ascontiguousarray(c, dtype=np.int64)
+    out = np.empty(c.shape, np.int32)
+    check(_lib.load().nh_quantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), log2_size, int(bool(is_intra)),
+                                  ab, ptr(out)), "quantize")
+    return out
+
+
+def dequantize(level, qp: int, size: int) -> np.ndarray:
+    """quant.py:82-123 (size unused, D4)."""
+    qp_per, qp_rem = get_qp_params(qp)
+    DEQUANT_SCALE[qp_rem]
+    x = np.ascontiguousarray(np.asarray(level).astype(np.int64))   # quant.py:113 cast
+    out = np.empty(x.shape, np.int32)
+    check(_lib.load().nh_dequantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), ptr(out)), "dequantize")
+    return out
+
+
+def quantize_block(coeff, qp: int, is_intra: bool = True) -> np.ndarray:
+    """quant.py:126-137."""
+    size = coeff.shape[0]
+    return quantize(coeff, qp, size, is_intra)
+
+
+def dequantize_block(level, qp: int) -> np.ndarray:
+    """quant.py:140-150."""
+    size = level.shape[0]
+    return dequantize(level, qp, size)
+
+
+def estimate_bits(level) -> int:
+    """quant.py:153-168: int(sum(log2(|l|+1) + (|l|>0)*2)) (float64, numpy summation order)."""
+    a = np.asarray(level)
+    if a.dtype not in (np.int32, np.int64):
+        raise NotImplementedError(f"estimate_bits: int32/int64 levels only (got {a.dtype})")
+    x = np.ascontiguousarray(a, dtype=np.int64)
+    bits = np.zeros(1, np.float64)
+    check(_lib.load().nh_estimate_bits(ptr(x), x.size, a.dtype.itemsize * 8, ptr(bits)), "estimate_bits")
+    return int(bits[0])
+
+
+def count_nonzero(level) -> int:
+    """quant.py:171-173."""
+    a = np.asarray(level)
+    if a.dtype.kind not in "iub":
+        raise NotImplementedError(f"count_nonzero: integer levels only (got {a.dtype})")
+    x = np.ascontiguousarray(a, dtype=np.int64)
+    cnt = np.zeros(1, np.int64)
+    check(_lib.load().nh_count_nonzero(ptr(x), x.size, ptr(cnt)), "count_nonzero")
+    return int(cnt[0])
+
+
+def is_all_zero(level) -> bool:
+    """quant.py:176-178 (returns numpy.bool like np.all)."""
+    return np.bool_(count_nonzero(level) == 0)

@@ -1,0 +1,252 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's recorded
+outputs (tests/golden) and the CPU restatement (oracle/) on seeded inputs.
+Bar: bit-exact (integer work).  Run with ``pytest -m gpu`` on an MI355X."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402  (checker only)
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def nh():
+    import nano_hevc
+    from nano_hevc import _lib
+    assert _lib.device_count() > 0, "no HIP device: the gpu tests need an MI355X"
+    return nano_hevc
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available()
+    return torch
+
+
+# ------------------------------------------------------------------ per-block drop-in path
+
+@pytest.mark.parametrize("key,n,dst", [("n4_dst", 4, True), ("n4_dct", 4, False), ("n8_dct", 8, False),
+                                       ("n16_dct", 16, False), ("n32_dct", 32, False)])
+def test_shim_transforms_golden(nh, golden, key, n, dst):
+    g = golden("transform.npz")
+    for x, y in zip(g[key + "_fwd_in"], g[key + "_fwd_out"]):
+        out = nh.forward_transform(x, use_dst=dst)
+        assert out.dtype == np.int32 and np.array_equal(out, y)
+    for x, y in zip(g[key + "_inv_in"], g[key + "_inv_out"]):
+        assert np.array_equal(nh.inverse_transform(x, use_dst=dst), y)
+
+
+def test_shim_quant_golden(nh, golden):
+    g = golden("quant.npz")
+    for a, qp in enumerate(g["q_qps"]):
+        qp = int(qp)
+        for b, size in enumerate([4, 8, 16, 32]):
+            for c, intra in enumerate([True, False]):
+                out = nh.quantize(g["q_vec32"], qp, size, intra)
+                assert out.dtype == np.int32 and np.array_equal(out, g["q_out32"][a, b, c]), (qp, size, intra)
+                assert np.array_equal(nh.quantize(g["q_vec16"], qp, size, intra), g["q_out16"][a, b, c])
+        assert np.array_equal(nh.dequantize(g["dq_in"], qp, 4), g["dq_out"][a]), qp
+
+
+@pytest.mark.parametrize("n", [4, 8, 16, 32])
+def test_shim_intra_golden(nh, golden, n):
+    g = golden("intra.npz")
+    for s in range(8):
+        top = g[f"n{n}_top"][s, :g[f"n{n}_ntop"][s]]
+        left = g[f"n{n}_left"][s, :g[f"n{n}_nleft"][s]]
+        corner = int(g[f"n{n}_corner"][s])
+        for m in range(35):
+            st = int(g[f"n{n}_status"][s, m])
+            if m == 0:
+                t = top[:n] if top.size >= n else top
+                l = left[:n] if left.size >= n else left
+                fn = lambda: nh.intra_planar_predict(t, l, int(top[min(n, top.size) - 1]),
+                                                     int(left[min(n, left.size) - 1]), n)
+            elif m == 1:
+                fn = lambda: nh.intra_dc_predict(top, left, n)
+            else:
+                fn = lambda: nh.intra_angular_predict(top, left, corner, m, n)
+            if st == 0:
+                out = fn()
+                assert out.dtype == np.int16 and np.array_equal(out, g[f"n{n}_pred"][s, m]), (n, s, m)
+            else:
+                with pytest.raises({1: OverflowError, 2: IndexError}[st]):
+                    fn()
+
+
+def test_shim_quirks_and_elementwise(nh, golden):
+    g = golden("intra.npz")
+    t, l = g["quirk_top"], g["quirk_left"]
+    assert np.array_equal(nh.intra_angular_predict(t, l, 77, 0, 4), g["quirk_ang0"])
+    assert np.array_equal(nh.intra_angular_predict(t, l, 77, 1, 4), g["quirk_ang1"])
+    assert np.array_equal(nh.intra_angular_predict(t, l, 77, -5, 4), g["quirk_angm5"])
+    assert np.array_equal(nh.intra_dc_predict_4x4(t, l), g["quirk_dc4"])
+    assert np.array_equal(nh.intra_dc_predict(t, l, 4), g["quirk_dc4_len9"])
+    assert np.array_equal(nh.residual_block(g["rr_a"], g["rr_b"]), g["rr_res"])
+    assert np.array_equal(nh.reconstruct_block(g["rr_a"], g["rr_b"]), g["rr_rec"])
+    for bd in [1, 8, 10, 12, 16, 40, 63]:
+        assert np.array_equal(nh.clip_to_pixel_range(g["clip_in"], bd), g[f"clip_bd{bd}"]), bd
+    # broadcasting + dtype casts of residual_block (intra.py:65-67)
+    assert np.array_equal(nh.residual_block(np.array([[1, 2]], np.uint8), np.array([[300]], np.int32)), [[-299, -298]])
+
+
+def test_shim_chain_config1(nh, golden):
+    """Config 1: the README / test_quant.py:283-322 chain, bit-exact per stage."""
+    g = golden("chain.npz")
+    pred = nh.intra_dc_predict(g["c1_top"], g["c1_left"], 4)
+    res = nh.residual_block(g["c1_orig"], pred)
+    coeff = nh.forward_transform(res, use_dst=True)
+    assert np.array_equal(pred, g["c1_pred"]) and np.array_equal(res, g["c1_res"]) and np.array_equal(coeff, g["c1_coeff"])
+    for qp in (20, 22):
+        lvl = nh.quantize_block(coeff, qp)
+        deq = nh.dequantize_block(lvl, qp)
+        rres = nh.inverse_transform(deq, use_dst=True)
+        rec = nh.clip_to_pixel_range(nh.reconstruct_block(pred, rres.astype(np.int16)))
+        for k, v in (("lvl", lvl), ("deq", deq), ("rres", rres), ("recon", rec)):
+            assert np.array_equal(v, g[f"c1_{k}_qp{qp}"]), (k, qp)
+
+
+def test_shim_reference_known_answers(nh):
+    """Known answers held by the reference's own tests, via the drop-in."""
+    assert np.all(nh.intra_dc_predict_4x4(np.array([102, 98, 100, 101]), np.array([103, 102, 101, 99])) == 101)
+    p = nh.intra_planar_predict(np.zeros(4, np.int16), np.zeros(4, np.int16), 255, 255, 4)
+    assert p[0, 0] == 64 and p[3, 3] == 255                                    # test_intra_planar.py:56-76
+    top = np.array([0, 10, 20, 30, 40, 50, 60, 70, 80], np.int16)
+    left = np.array([0, 5, 5, 5, 5, 5, 5, 5, 5], np.int16)
+    exp18 = np.array([[0, 10, 20, 30], [0, 0, 10, 20], [5, 0, 0, 10], [5, 5, 0, 0]])
+    assert np.array_equal(nh.intra_angular_predict(top, left, 0, 18, 4), exp18)   # test_intra_angular.py:69-85
+    for m in range(2, 35):
+        assert np.all(nh.intra_angular_predict(np.full(9, 128, np.int16), np.full(9, 128, np.int16), 128, m, 4) == 128)
+    assert np.array_equal(nh.clip_to_pixel_range(np.array([[-10, 0, 128, 255, 300]], np.int16)), [[0, 0, 128, 255, 255]])
+    lv = np.array([[10, 0, 0, 0], [0, 5, 0, 0], [0, 0, 0, 0], [0, 0, 0, 1]], np.int32)
+    assert nh.quant.count_nonzero(lv) == 3 and nh.quant.is_all_zero(np.zeros((4, 4), np.int32))
+    assert not nh.quant.is_all_zero(np.array([[1, 0], [0, 0]], np.int32))
+    assert nh.quant.quantize(np.array([-32768], np.int16), 0, 4)[0] == 13107       # np.abs int16 wrap
+
+
+def test_shim_estimate_bits(nh):
+    rng = np.random.default_rng(5)
+    for n in [1, 7, 8, 16, 64, 129, 1024, 4096]:
+        lv = rng.integers(-3000, 3000, size=n).astype(np.int32)
+        lv[rng.random(n) < 0.5] = 0
+        a = np.abs(lv)
+        exp = int(np.sum(np.log2(a + 1) + (a > 0) * 2))     # quant.py:166-167 (numpy as checker)
+        assert nh.quant.estimate_bits(lv) == exp, n
+        assert nh.quant.count_nonzero(lv) == int(np.count_nonzero(lv))
+
+
+# ------------------------------------------------------------------ batched device path
+
+@pytest.mark.parametrize("n,dst", [(4, True), (4, False), (8, False), (16, False), (32, False)])
+def test_batch_transforms_vs_oracle(nh, torch_dev, n, dst):
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(n + dst)
+    x = rng.integers(-2**31, 2**31, size=(97, n, n), dtype=np.int64).astype(np.int32)
+    x[:40] = rng.integers(-255, 256, size=(40, n, n))
+    d = torch.from_numpy(x).cuda()
+    f = gpu.fwd_transform_batch(d, dst).cpu().numpy()
+    i = gpu.inv_transform_batch(d, dst).cpu().numpy()
+    for b in range(x.shape[0]):
+        assert np.array_equal(f[b], O.forward_transform(x[b], dst)), b
+        assert np.array_equal(i[b], O.inverse_transform(x[b], dst)), b
+
+
+def test_batch_quant_vs_oracle(nh, torch_dev):
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(3)
+    c = rng.integers(-2**31, 2**31, size=5000, dtype=np.int64).astype(np.int32)
+    c[:2000] = rng.integers(-3000, 3000, size=2000)
+    c[:3] = [-2**31, 2**31 - 1, 0]
+    d = torch.from_numpy(c).cuda()
+    for qp in [0, 7, 22, 32, 45, 51]:
+        for lg in [2, 3, 4, 5]:
+            for intra in (True, False):
+                got = gpu.quant_batch(d, qp, lg, intra).cpu().numpy()
+                assert np.array_equal(got, O.quantize(c, qp, 1 << lg, intra)), (qp, lg, intra)
+        assert np.array_equal(gpu.dequant_batch(d, qp).cpu().numpy(), O.dequantize(c, qp)), qp
+
+
+def _plane_gpu(torch, plane, qp=32, intra=True, variant=0):
+    from nano_hevc import gpu
+    h, w = plane.shape
+    d = torch.from_numpy(np.ascontiguousarray(plane)).cuda()
+    out = torch.full_like(d, 0x5555)
+    gpu.fwd8x8_quant(d, [gpu.plane_set(0, w, h, w)], qp, intra, out=out, variant=variant)
+    return out.cpu().numpy()
+
+
+def test_fused8x8_golden_planes(nh, torch_dev, golden):
+    g = golden("planes.npz")
+    out = _plane_gpu(torch_dev, g["p2_small_in"])
+    assert np.array_equal(out, g["p2_small_lvl"])
+    out = _plane_gpu(torch_dev, g["p2_edge_in"], qp=0)
+    assert np.array_equal(out, g["p2_edge_lvl"])
+
+
+def test_fused8x8_1080p_hash(nh, torch_dev):
+    """reference levels of a seeded 1080p plane, by sha256."""
+    man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+    rng = np.random.default_rng(20260)
+    plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
+    out = _plane_gpu(torch_dev, plane, 32)
+    assert hashlib.sha256(out.tobytes()).hexdigest() == man["cfg2_1080p_qp32_seed20260_levels_sha256"]
+
+
+@pytest.mark.parametrize("qp,intra", [(0, True), (22, True), (32, True), (32, False), (51, True), (-4, True), (70, False)])
+def test_fused8x8_full_int16_range_vs_oracle(nh, torch_dev, qp, intra):
+    """Every int16 input (incl. +-32767/-32768 blocks) is exact: the 24-bit mads
+    and the single-mad quantizer are proved for the whole int16 range."""
+    rng = np.random.default_rng(qp + 100)
+    plane = rng.integers(-32768, 32768, size=(136, 264)).astype(np.int16)
+    plane[:8, :8] = 32767
+    plane[:8, 8:16] = -32768
+    plane[8:16, :8] = np.where(np.indices((8, 8)).sum(0) % 2, 32767, -32768)
+    plane[8:16, 8:16] = np.where(np.indices((8, 8))[0] < 4, -32768, 32767)
+    exp = O.fwd8x8_quant_plane(plane, qp, intra)
+    got = _plane_gpu(torch_dev, plane, qp, intra)
+    assert np.array_equal(got, exp)
+    assert np.array_equal(_plane_gpu(torch_dev, plane, qp, intra, variant=1), got)
+
+
+def test_fused8x8_partial_blocks_untouched(nh, torch_dev):
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(9)
+    plane = rng.integers(-255, 256, size=(21, 40)).astype(np.int16)   # 21 rows: last 5 rows partial
+    d = torch.from_numpy(plane).cuda()
+    out = torch.full_like(d, 1234)
+    gpu.fwd8x8_quant(d, [gpu.plane_set(0, 40, 21, 40)], 32, True, out=out)
+    o = out.cpu().numpy()
+    assert np.all(o[16:] == 1234)
+    assert np.array_equal(o[:16], O.fwd8x8_quant_plane(plane[:16], 32))
+
+
+def test_fused8x8_4k_yuv420_stream_vs_oracle(nh, torch_dev):
+    """The metric's workload shape: 4K YUV420 frames back to back, one launch
+    over both plane sets (Y, U+V), every block compared with the oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H = 3, 3840, 2160
+    fe = gpu.yuv420_frame_elems(W, H)
+    rng = np.random.default_rng(77)
+    buf = rng.integers(-255, 256, size=F * fe).astype(np.int16)
+    d = torch.from_numpy(buf).cuda()
+    sets = gpu.yuv420_plane_sets(F, W, H)
+    out = gpu.fwd8x8_quant(d, sets, 32, True).cpu().numpy()
+    for f in range(F):
+        base = f * fe
+        y = buf[base:base + W * H].reshape(H, W)
+        assert np.array_equal(out[base:base + W * H].reshape(H, W), O.fwd8x8_quant_plane(y, 32)), f
+        for c in range(2):
+            o = base + W * H + c * (W // 2) * (H // 2)
+            p = buf[o:o + (W // 2) * (H // 2)].reshape(H // 2, W // 2)
+            assert np.array_equal(out[o:o + p.size].reshape(p.shape), O.fwd8x8_quant_plane(p, 32)), (f, c)

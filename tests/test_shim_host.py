@@ -1,0 +1,73 @@
+"""Host-side logic of the drop-in shim (no GPU): constants, parameter
+computation and the exceptions raised before any device work, all compared
+with the reference's recorded values in tests/golden/."""
+import numpy as np
+import pytest
+
+import nano_hevc as nh
+from nano_hevc import gpu, quant, transform
+
+
+def test_constants_match_reference(golden):
+    g = golden("matrices.npz")
+    for name in ("DST4", "DCT4", "DCT8", "DCT16", "DCT32"):
+        assert np.array_equal(getattr(nh, name), g[name]) and getattr(nh, name).dtype == np.int32
+    assert nh.INTRA_PRED_ANGLE[10 - 2] == 0 and nh.INTRA_PRED_ANGLE[18 - 2] == -32   # test_intra_angular.py:190-197
+    assert len(nh.INTRA_PRED_ANGLE) == 33
+    assert nh.QUANT_SCALE == [26214, 23302, 20560, 18396, 16384, 14564]
+    assert nh.DEQUANT_SCALE == [40, 45, 51, 57, 64, 72]
+
+
+def test_qp_params(golden):
+    g = golden("quant.npz")
+    got = np.array([quant.get_qp_params(q) for q in range(-3, 56)])
+    assert np.array_equal(got, g["qp_params"])
+
+
+def test_errors_raised_before_device_work():
+    with pytest.raises(ValueError):
+        nh.forward_transform(np.zeros((6, 6), np.int16))              # transform.py:150-151
+    with pytest.raises(ValueError):
+        transform._get_transform_matrix(64)
+    with pytest.raises(IndexError):
+        nh.intra_angular_predict(np.zeros(9, np.int16), np.zeros(9, np.int16), 0, 35, 4)   # intra.py:142
+    with pytest.raises(ZeroDivisionError):
+        nh.intra_dc_predict(np.zeros(4, np.int16), np.zeros(4, np.int16), 0)
+    with pytest.raises(OverflowError):
+        nh.quantize(np.zeros(4, np.int32), 22, 0)                   # int(np.log2(0))
+    with pytest.raises(ValueError):
+        nh.clip_to_pixel_range(np.zeros(3, np.int16), -1)           # 1 << -1
+
+
+def test_yuv420_plane_sets():
+    sets = gpu.yuv420_plane_sets(3, 3840, 2160)
+    assert gpu.blocks_in(sets) == 3 * (480 * 270 + 2 * 240 * 135)   # 194,400 8x8 blocks per 4K frame
+    y, uv = sets
+    fs = gpu.yuv420_frame_elems(3840, 2160)
+    assert (y.group_stride, uv.base, uv.plane_stride, uv.planes_per_group) == (fs, 3840 * 2160, 1920 * 1080, 2)
+    # 1080p chroma (540 rows) has a partial bottom block row: skipped like block.py:72-74
+    assert gpu.blocks_in(gpu.yuv420_plane_sets(1, 1920, 1080)) == 240 * 135 + 2 * 120 * 67
+
+
+def test_block_iteration_rules():
+    p = nh.Plane(np.arange(20 * 28, dtype=np.int16).reshape(20, 28))
+    blocks = list(nh.iterate_blocks(p, 8))
+    assert [(b.x, b.y) for b in blocks] == [(0, 0), (8, 0), (16, 0), (0, 8), (8, 8), (16, 8)]
+    b = nh.BlockView(p, 24, 8, 8)                      # right-edge block: slice truncation
+    assert b.get_top_neighbors(16).size == 4 and b.get_top_left_neighbor() == int(p.data[7, 23])
+    assert np.all(nh.BlockView(p, 0, 0, 4).get_top_neighbors() == 128)
+
+
+def test_frame_containers_roundtrip():
+    raw = bytes(range(256)) * ((16 * 8 * 3 // 2) // 256 + 1)
+    raw = raw[:16 * 8 * 3 // 2]
+    f = nh.Frame.from_yuv420p(raw, 8, 16)
+    assert f.to_yuv420p() == raw
+    pf = nh.PackedFrame.from_frame(f)
+    assert pf.to_yuv420p() == raw and pf.to_frame().u.data.shape == (4, 8)
+    pool = nh.FrameBufferPool(8, 16, pool_size=2)
+    i, _ = pool.acquire()
+    assert pool.in_use_count == 1
+    pool.release(i)
+    with pytest.raises(ValueError):
+        pool.release(i)
