@@ -115,6 +115,29 @@ int nh_quant_batch(const int32_t* d_coeff, int32_t* d_level, int64_t n, int qp, 
                    int is_intra, void* stream);
 int nh_dequant_batch(const int32_t* d_level, int32_t* d_coeff, int64_t n, int qp, void* stream);
 
+/* Config 3: 35-mode open-loop RDO over every full 8x8 block of an int16
+ * source plane: per block and mode, the README chain
+ * pred -> residual_block -> forward_transform -> quantize_block ->
+ * dequantize_block -> inverse_transform -> reconstruct_block ->
+ * clip_to_pixel_range(.,8); cost = SSE(orig, recon), ties -> lowest mode.
+ * d_modes: (h/8)*(w/8) u8 (mode 0 planar, 1 DC, 2..34 angular);
+ * d_lvl (int32) / d_recon (int16): raster with the given pitch;
+ * d_sse (optional, one int64): the chosen SSEs are added to it. */
+int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch, int qp,
+                       uint8_t* d_modes, int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse,
+                       void* stream);
+
+/* Config 4: mixed 4/8/16/32 TU pipeline on one plane over CTU rows
+ * [row0, row1): seeded quadtree per CTB (ctb 32 luma / 16
+ * chroma), per TU the __main__.py:165-178 DC-vs-planar choice then the full
+ * reconstruction chain (DST for 4x4 luma).  d_tu: (h/4)*(w/4) u8 log2 TU size;
+ * d_work: nh_tu_workspace_bytes(w, h, ctb) bytes of device scratch. */
+int64_t nh_tu_workspace_bytes(int w, int h, int ctb);
+int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb, int plane_id,
+                         uint32_t seed, int qp, int is_luma, int row0, int row1,
+                         int32_t* d_lvl, int16_t* d_recon, uint8_t* d_tu, void* d_work,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

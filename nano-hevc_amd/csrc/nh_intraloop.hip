@@ -1,0 +1,486 @@
+// nh_intraloop.hip -- frame-level intra drivers on device (configs 3 and 4).
+//
+// Both compose the reference's per-block functions exactly as DESIGN.md §3.3 /
+// §3.4 define them (the reference has no frame-level transform driver; the
+// composition follows __main__.py:142-189 and the README chain README.md:55-71),
+// with the neighbour rules of block.py:38-55 (source plane = open loop, D12).
+// Every per-block step keeps the reference's integer semantics; the oracle
+// (the test-side CPU restatement, oh_intra_rdo_plane / oh_tu_pipeline_plane) and the golden
+// planes generated from the reference functions pin them.
+#include <hip/hip_runtime.h>
+#include <climits>
+#include "nh_common.hpp"
+#include "nh_internal.hpp"
+
+namespace nh {
+
+// ===========================================================================
+// Config 3: 35-mode open-loop RDO per full 8x8 block.
+// Workgroup = 7 blocks x 35 modes (245 of 256 lanes): lane = (block slot, mode).
+// Each lane runs pred -> residual -> fwd DCT -> quant -> dequant -> inv DCT ->
+// recon -> SSE for its mode; an LDS atomicMin on (sse<<6 | mode) picks the
+// lowest SSE, lowest mode on ties; the winning lane writes levels/recon/mode.
+// Exactness of the 24-bit mads for any int16 plane: DESIGN.md §4.3.
+// ===========================================================================
+constexpr int kRdoSlots = 7;
+constexpr int kModes = 35;
+
+struct RdoSlotLds {
+    int16_t orig[64];
+    int16_t topA[17], leftA[17];   // [tl] + up to 16 samples (numpy slice truncation)
+    int16_t topN[8], leftN[8];
+    int32_t ntA, nlA;              // lengths of topA / leftA (9..17)
+    int32_t valid;
+    unsigned long long best;
+};
+
+__device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+
+__global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
+                                                    QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
+                                                    int32_t* lvl, int16_t* recon, unsigned long long* sse_out) {
+    __shared__ RdoSlotLds S[kRdoSlots];
+    __shared__ int16_t refs[kRdoSlots * kModes][26];
+    const int bw = w / 8, bh = h / 8;
+    const int nblk = bw * bh;
+    const int t = threadIdx.x;
+    const int slot = t / kModes, mode = t - slot * kModes;
+    const bool lane_on = slot < kRdoSlots;
+
+    // ---- cooperative load of the 7 blocks' samples and neighbours ----
+    for (int e = t; e < kRdoSlots * 64; e += 256) {
+        int sl = e / 64, k = e % 64;
+        int b = blockIdx.x * kRdoSlots + sl;
+        if (b < nblk) {
+            int by = b / bw, bx = b - by * bw;
+            S[sl].orig[k] = src[(int64_t)(by * 8 + k / 8) * pitch + bx * 8 + (k % 8)];
+        }
+    }
+    for (int e = t; e < kRdoSlots * 32; e += 256) {
+        int sl = e / 32, k = e % 32;
+        int b = blockIdx.x * kRdoSlots + sl;
+        if (b >= nblk) continue;
+        int by = b / bw, bx = b - by * bw, x = bx * 8, y = by * 8;
+        if (k < 16) {   // top row samples x..x+15 (block.py:38-43)
+            int16_t v = 128;
+            if (y > 0 && x + k < w) v = src[(int64_t)(y - 1) * pitch + x + k];
+            S[sl].topA[1 + k] = v;
+            if (k < 8) S[sl].topN[k] = v;
+        } else {        // left column samples y..y+15 (block.py:45-50)
+            int kk = k - 16;
+            int16_t v = 128;
+            if (x > 0 && y + kk < h) v = src[(int64_t)(y + kk) * pitch + x - 1];
+            S[sl].leftA[1 + kk] = v;
+            if (kk < 8) S[sl].leftN[kk] = v;
+        }
+    }
+    if (t < kRdoSlots) {
+        int b = blockIdx.x * kRdoSlots + t;
+        S[t].valid = b < nblk;
+        if (b < nblk) {
+            int by = b / bw, bx = b - by * bw, x = bx * 8, y = by * 8;
+            int16_t tl = (y == 0 || x == 0) ? (int16_t)128 : src[(int64_t)(y - 1) * pitch + x - 1];
+            S[t].topA[0] = tl;
+            S[t].leftA[0] = tl;
+            S[t].ntA = 1 + (y == 0 ? 16 : min(16, w - x));
+            S[t].nlA = 1 + (x == 0 ? 16 : min(16, h - y));
+        }
+        S[t].best = ULLONG_MAX;
+    }
+    __syncthreads();
+    const bool active = lane_on && S[lane_on ? slot : 0].valid;
+    RdoSlotLds& L = S[lane_on ? slot : 0];
+
+    // ---- prediction (int32 registers holding int16 values) ----
+    int32_t P[64];
+    if (active) {
+        if (mode == 0) {            // planar, intra.py:81-113, tr=top[-1], bl=left[-1] (__main__.py:168-169)
+            const int32_t tr = L.topN[7], bl = L.leftN[7];
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+#pragma unroll
+                for (int x = 0; x < 8; ++x)
+                    P[y * 8 + x] = ((7 - x) * L.leftN[y] + (x + 1) * tr + (7 - y) * L.topN[x] + (y + 1) * bl + 8) >> 4;
+        } else if (mode == 1) {     // DC, intra.py:46-62
+            int32_t s = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s += L.topN[k] + L.leftN[k];
+            const int32_t dc = (s + 8) >> 4;   // floor division by 16
+#pragma unroll
+            for (int k = 0; k < 64; ++k) P[k] = dc;
+        } else {                    // angular, intra.py:116-207
+            const int angle = intra_angle(mode - 2);
+            const bool vert = mode >= 18;
+            const int16_t* pri = vert ? L.topA : L.leftA;
+            const int16_t* sec = vert ? L.leftA : L.topA;
+            const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
+            int16_t* ref = refs[t];
+            // _build_ref_array (intra.py:159-188): ref[8+i], i in [-8, 16]
+            for (int i = 0; i < 26; ++i) ref[i] = 0;
+            ref[8] = pri[0];
+            for (int i = 1; i <= 16; ++i) ref[8 + i] = pri[i < np ? i : np - 1];
+            if (angle < 0) {
+                const int inv = inv_angle(angle), next = (8 * angle) >> 5;
+                for (int i = -1; i > next - 1; --i) {
+                    int proj = ((i + 1) * inv + 128) >> 8;
+                    if (proj < ns) ref[8 + i] = sec[proj];
+                }
+            }
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+#pragma unroll
+                for (int x = 0; x < 8; ++x) {
+                    const int base = vert ? x : y, scan = vert ? y : x;
+                    const int proj = (scan + 1) * angle;
+                    const int idx = 8 + base + 1 + (proj >> 5);
+                    const int f = proj & 31;
+                    const int32_t a = ref[idx];
+                    int32_t v;
+                    if (f == 0) v = a;
+                    else {
+                        const int32_t b = ref[idx + 1];
+                        v = wrap16((32 - f) * a + f * b + 16) >> 5;   // int16 arithmetic (D8)
+                    }
+                    P[y * 8 + x] = v;
+                }
+        }
+    }
+
+    // ---- residual -> fwd DCT -> quant -> dequant -> inv DCT -> recon -> SSE ----
+    unsigned long long key = ULLONG_MAX;
+    uint32_t X[8][8];
+    int32_t Lv[64];
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < 64; ++k) X[k / 8][k % 8] = (uint32_t)(int32_t)wrap16((int32_t)L.orig[k] - P[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {           // pass 1: columns
+            uint32_t x[8], y[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) x[k] = X[k][j];
+            fwd_dct<8, Mul24>(x, y, 128u);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)y[i] >> 8);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {           // pass 2: rows, then quant / dequant
+            uint32_t y[8];
+            fwd_dct<8, Mul24>(X[i], y, 128u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int32_t c = (int32_t)y[j] >> 8;
+                const int32_t l = quant_i32(c, qp);
+                Lv[i * 8 + j] = l;
+                X[i][j] = (uint32_t)dequant_i32(l, dq_scale, dq_per);
+            }
+        }
+        // inverse pass 1: columns (transform.py:221-227)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t yv[8], x[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) yv[k] = X[k][j];
+            inv_dct<8, Mul24>(yv, x, 128u);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)x[i] >> 8);
+        }
+        unsigned long long sse = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {           // inverse pass 2: rows, recon, SSE
+            uint32_t x[8];
+            inv_dct<8, Mul24>(X[i], x, 128u);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int32_t rr = wrap16((int32_t)x[j] >> 8);               // rres.astype(int16)
+                int32_t rc = wrap16(P[i * 8 + j] + rr);                       // reconstruct_block (int16 wrap)
+                rc = rc < 0 ? 0 : (rc > 255 ? 255 : rc);                      // clip_to_pixel_range(., 8)
+                P[i * 8 + j] = rc;
+                const int32_t d = wrap16((int32_t)L.orig[i * 8 + j] - rc);   // residual_block(orig, recon)
+                sse += (unsigned long long)(d * d);
+            }
+        }
+        key = (sse << 6) | (unsigned long long)mode;
+        atomicMin(&L.best, key);
+    }
+    __syncthreads();
+    if (active && key == L.best) {
+        const int b = blockIdx.x * kRdoSlots + slot;
+        const int by = b / bw, bx = b - by * bw;
+        modes[b] = (uint8_t)mode;
+        if (sse_out) atomicAdd(sse_out, key >> 6);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
+            int16_t* rrow = recon + (int64_t)(by * 8 + i) * pitch + bx * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { lrow[j] = Lv[i * 8 + j]; rrow[j] = (int16_t)P[i * 8 + j]; }
+        }
+    }
+}
+
+// ===========================================================================
+// Config 4: mixed 4/8/16/32 TU pipeline.
+//   k_tu_plan    : one thread per CTB walks the seeded quadtree and appends its
+//                  leaves to one list per TU size (order irrelevant: every TU
+//                  writes only its own samples).
+//   k_tu_process : N threads per TU (thread t = column t, then row t), LDS tiles;
+//                  DC-vs-planar open-loop choice (__main__.py:165-178), then the
+//                  full residual -> transform -> quant -> dequant -> inverse ->
+//                  recon chain with exact int32/int64 arithmetic.
+// ===========================================================================
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ bool tu_split(uint32_t seed, int plane_id, int x, int y, int size) {
+    uint32_t k = mix32(seed ^ (0x9E3779B9U * (uint32_t)(plane_id + 1)));
+    k = mix32(k ^ (uint32_t)x);
+    k = mix32(k ^ ((uint32_t)y * 0x85ebca6bU));
+    k = mix32(k ^ (uint32_t)size);
+    return (k & 3u) < 2u;
+}
+
+struct TuLists {
+    uint32_t* count;     // [4] for sizes 4, 8, 16, 32
+    uint32_t* list[4];   // packed (y << 16) | x
+    uint32_t cap[4];
+};
+
+__global__ void k_tu_plan(int w, int h, int ctb, int plane_id, uint32_t seed, int row0, int row1, TuLists tl) {
+    const int ctb_w = (w + ctb - 1) / ctb;
+    const int n = (row1 - row0) * ctb_w;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int cy = row0 + i / ctb_w, cx = i % ctb_w;
+    int sx[16], sy[16], ss[16], sp = 0;
+    sx[0] = cx * ctb; sy[0] = cy * ctb; ss[0] = ctb; sp = 1;
+    while (sp) {
+        --sp;
+        const int x = sx[sp], y = sy[sp], s = ss[sp];
+        if (x >= w || y >= h) continue;
+        const bool over = (x + s > w) || (y + s > h);
+        if (s > 4 && (over || tu_split(seed, plane_id, x, y, s))) {
+            const int hs = s / 2;   // push in reverse so pops follow Z order (order is irrelevant)
+            sx[sp] = x + hs; sy[sp] = y + hs; ss[sp++] = hs;
+            sx[sp] = x;      sy[sp] = y + hs; ss[sp++] = hs;
+            sx[sp] = x + hs; sy[sp] = y;      ss[sp++] = hs;
+            sx[sp] = x;      sy[sp] = y;      ss[sp++] = hs;
+            continue;
+        }
+        if (over) continue;
+        const int c = s == 4 ? 0 : s == 8 ? 1 : s == 16 ? 2 : 3;
+        const uint32_t slot = atomicAdd(&tl.count[c], 1u);
+        if (slot < tl.cap[c]) tl.list[c][slot] = ((uint32_t)y << 16) | (uint32_t)x;
+    }
+}
+
+template <int N, bool DST>
+__global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ src, int w, int h, int pitch,
+                                                    const uint32_t* __restrict__ list, const uint32_t* count,
+                                                    QuantParams qp, int dq_scale, int dq_per, int32_t* lvl,
+                                                    int16_t* recon, uint8_t* tu_log2) {
+    constexpr int G = 256 / N;            // TUs per workgroup
+    constexpr int P = N + 1;              // padded LDS row
+    constexpr int S = Log2<N>::v + 5;
+    __shared__ int32_t tile[G][N][P];
+    __shared__ int16_t orig[G][N][N];
+    __shared__ int16_t topv[G][N], leftv[G][N];
+    __shared__ long long e_dc[G][N], e_pl[G][N];
+    const int g = threadIdx.x / N, t = threadIdx.x % N;
+    const uint32_t idx = blockIdx.x * G + g;
+    const bool active = idx < *count;
+    int x0 = 0, y0 = 0;
+    if (active) {
+        const uint32_t e = list[idx];
+        x0 = e & 0xffff;
+        y0 = e >> 16;
+        // neighbours (block.py:38-50): count N, 128 outside the plane (full TUs: no truncation)
+        topv[g][t] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + t];
+        leftv[g][t] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + t) * pitch + x0 - 1];
+#pragma unroll
+        for (int i = 0; i < N; ++i) orig[g][i][t] = src[(int64_t)(y0 + i) * pitch + x0 + t];
+    }
+    __syncthreads();
+    // DC (intra.py:46-62) and planar (intra.py:81-113) for column t
+    int32_t dc = 0, tr = 0, bl = 0;
+    if (active) {
+        long long s = 0;
+        for (int k = 0; k < N; ++k) s += topv[g][k] + leftv[g][k];
+        dc = (int32_t)((s + N) >> (Log2<N>::v + 1));   // floor((s+N)/(2N)), 2N a power of two
+        tr = topv[g][N - 1];
+        bl = leftv[g][N - 1];
+        long long ed = 0, ep = 0;
+        for (int y = 0; y < N; ++y) {
+            const int32_t o = orig[g][y][t];
+            const int32_t pl = ((N - 1 - t) * leftv[g][y] + (t + 1) * tr + (N - 1 - y) * topv[g][t] + (y + 1) * bl + N) >>
+                               (Log2<N>::v + 1);
+            const int32_t d1 = wrap16(o - dc), d2 = wrap16(o - pl);
+            ed += (long long)d1 * d1;
+            ep += (long long)d2 * d2;
+        }
+        e_dc[g][t] = ed;
+        e_pl[g][t] = ep;
+    }
+    __syncthreads();
+    bool use_dc = true;
+    if (active) {
+        long long ed = 0, ep = 0;
+        for (int k = 0; k < N; ++k) { ed += e_dc[g][k]; ep += e_pl[g][k]; }
+        use_dc = ed <= ep;                               // __main__.py:173: DC wins ties
+    }
+    auto pred_at = [&](int y, int x) -> int32_t {
+        if (use_dc) return dc;
+        return ((N - 1 - x) * leftv[g][y] + (x + 1) * tr + (N - 1 - y) * topv[g][x] + (y + 1) * bl + N) >> (Log2<N>::v + 1);
+    };
+    uint32_t v[N], r[N];
+    // forward pass 1 on column t of the residual
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)(int32_t)wrap16((int32_t)orig[g][k][t] - pred_at(k, t));
+        fwd1d<N, DST, MulWrap>(v, r);
+#pragma unroll
+        for (int i = 0; i < N; ++i) tile[g][i][t] = rshift_round<S>(r[i]);
+    }
+    __syncthreads();
+    // forward pass 2 on row t, quant, dequant
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][t][k];
+        fwd1d<N, DST, MulWrap>(v, r);
+        int32_t* lrow = lvl + (int64_t)(y0 + t) * pitch + x0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int32_t l = quant_i32(rshift_round<S>(r[j]), qp);
+            lrow[j] = l;
+            v[j] = (uint32_t)dequant_i32(l, dq_scale, dq_per);
+        }
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) tile[g][t][j] = (int32_t)v[j];
+    }
+    __syncthreads();
+    // inverse pass 1 on column t
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][k][t];
+        inv1d<N, DST, MulWrap>(v, r);
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tile[g][i][t] = rshift_round<S>(r[i]);
+    }
+    __syncthreads();
+    // inverse pass 2 on row t, reconstruct + clip
+    if (active) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][t][k];
+        inv1d<N, DST, MulWrap>(v, r);
+        int16_t* rrow = recon + (int64_t)(y0 + t) * pitch + x0;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int32_t rr = wrap16(rshift_round<S>(r[j]));
+            int32_t rc = wrap16(pred_at(t, j) + rr);
+            rrow[j] = (int16_t)(rc < 0 ? 0 : (rc > 255 ? 255 : rc));
+        }
+        if (t < N / 4) {
+            const int w4 = w / 4;
+            for (int j = 0; j < N / 4; ++j) tu_log2[(int64_t)(y0 / 4 + t) * w4 + x0 / 4 + j] = (uint8_t)Log2<N>::v;
+        }
+    }
+}
+
+static void qp_split(int qp, int* per, int* rem) {
+    qp = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
+    *per = qp / 6;
+    *rem = qp % 6;
+}
+static QuantParams qparams(int qp, int log2n, bool intra) {
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    QuantParams q;
+    q.shift = 14 + per + log2n;
+    q.mf = quant_scale(rem);
+    q.off = (uint32_t)(intra ? (1ull << q.shift) / 3 : (1ull << q.shift) / 6);
+    return q;
+}
+
+static int64_t tu_cap(int w, int h, int s) { return (int64_t)((w + s - 1) / s) * ((h + s - 1) / s); }
+
+}  // namespace nh
+
+using namespace nh;
+
+extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch, int qp, uint8_t* d_modes,
+                                  int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse, void* stream) {
+    if (!d_src || !d_modes || !d_lvl || !d_recon || w < 0 || h < 0 || pitch < w) return NH_EARG;
+    const int nblk = (w / 8) * (h / 8);
+    if (!nblk) return NH_OK;
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    const unsigned grid = (unsigned)((nblk + kRdoSlots - 1) / kRdoSlots);
+    k_intra_rdo8<<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
+                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int64_t nh_tu_workspace_bytes(int w, int h, int ctb) {
+    (void)ctb;
+    int64_t b = 256;
+    for (int s = 4; s <= 32; s *= 2) b += align_up((size_t)tu_cap(w, h, s) * 4, 256);
+    return b;
+}
+
+extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb, int plane_id,
+                                    uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
+                                    int16_t* d_recon, uint8_t* d_tu, void* d_work, void* stream) {
+    if (!d_src || !d_lvl || !d_recon || !d_tu || !d_work || pitch < w || w <= 0 || h <= 0) return NH_EARG;
+    if (ctb != 4 && ctb != 8 && ctb != 16 && ctb != 32) return NH_EVALUE;
+    if ((w & 3) || (h & 3) || w > 65535 || h > 65535) return NH_EARG;
+    hipStream_t s = as_stream(stream);
+    const int rows = (h + ctb - 1) / ctb;
+    if (row0 < 0) row0 = 0;
+    if (row1 > rows) row1 = rows;
+    if (row1 <= row0) return NH_OK;
+    TuLists tl;
+    char* p = (char*)d_work;
+    tl.count = (uint32_t*)p;
+    p += 256;
+    for (int c = 0; c < 4; ++c) {
+        tl.cap[c] = (uint32_t)tu_cap(w, h, 4 << c);
+        tl.list[c] = (uint32_t*)p;
+        p += align_up((size_t)tl.cap[c] * 4, 256);
+    }
+    NH_HIP(hipMemsetAsync(tl.count, 0, 16, s));
+    const int nctb = (row1 - row0) * ((w + ctb - 1) / ctb);
+    k_tu_plan<<<(nctb + 63) / 64, 64, 0, s>>>(w, h, ctb, plane_id, seed, row0, row1, tl);
+    NH_HIP(hipGetLastError());
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    const int dqs = dequant_scale(rem);
+    // grids sized by the capacity bound; surplus workgroups see idx >= count and idle
+    const int64_t band = (int64_t)(row1 - row0) * ctb;  // rows covered
+    auto grid = [&](int size, int cap) {
+        int64_t bound = (int64_t)((w + size - 1) / size) * ((band + size - 1) / size + 1);
+        if (bound > cap) bound = cap;
+        const int G = 256 / size;
+        return (unsigned)((bound + G - 1) / G);
+    };
+    if (is_luma)
+        k_tu_process<4, true><<<grid(4, tl.cap[0]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[0], tl.count + 0,
+                                                                qparams(qp, 2, true), dqs, per, d_lvl, d_recon, d_tu);
+    else
+        k_tu_process<4, false><<<grid(4, tl.cap[0]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[0], tl.count + 0,
+                                                                 qparams(qp, 2, true), dqs, per, d_lvl, d_recon, d_tu);
+    k_tu_process<8, false><<<grid(8, tl.cap[1]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[1], tl.count + 1,
+                                                             qparams(qp, 3, true), dqs, per, d_lvl, d_recon, d_tu);
+    k_tu_process<16, false><<<grid(16, tl.cap[2]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[2], tl.count + 2,
+                                                               qparams(qp, 4, true), dqs, per, d_lvl, d_recon, d_tu);
+    k_tu_process<32, false><<<grid(32, tl.cap[3]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[3], tl.count + 3,
+                                                               qparams(qp, 5, true), dqs, per, d_lvl, d_recon, d_tu);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}

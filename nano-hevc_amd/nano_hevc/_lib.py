@@ -53,6 +53,9 @@ SIGNATURES = {
     "nh_inv_transform_batch": ([P, P, I64, I32, I32, VP], I32),
     "nh_quant_batch": ([P, P, I64, I32, I32, I32, VP], I32),
     "nh_dequant_batch": ([P, P, I64, I32, VP], I32),
+    "nh_intra_rdo_plane": ([P, I32, I32, I32, I32, P, P, P, P, VP], I32),
+    "nh_tu_workspace_bytes": ([I32, I32, I32], I64),
+    "nh_tu_pipeline_plane": ([P, I32, I32, I32, I32, I32, U32, I32, I32, I32, I32, P, P, P, P, VP], I32),
 }
 
 _lib = None
@@ -64,6 +67,15 @@ def load():
     global _lib, _load_error
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch wheels bundle their own libamdhip64
+    # (SONAME libamdhip64.so.7).  Importing torch first makes that copy the
+    # process's runtime, and our DT_NEEDED libamdhip64.so.7 then binds to it
+    # (loading /opt/rocm's copy first would leave torch with a second runtime
+    # that cannot see the device).  Without torch, /opt/rocm's runtime is used.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the C-ABI path
+        pass
     if not os.path.exists(LIB_PATH):
         raise NanoHevcUnavailable(
             f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -7,6 +7,8 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   fwd8x8_quant        -- the hot path: fused 8x8 DCT + quant over plane sets
   yuv420_plane_sets   -- nh_plane_set descriptors for a stream of YUV420 frames
   fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
+  intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
+  tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
 """
 from __future__ import annotations
 
@@ -129,3 +131,39 @@ def dequant_batch(l, qp: int, out=None, stream=None):
     check(_lib.load().nh_dequant_batch(l.data_ptr(), out.data_ptr(), l.numel(), int(qp),
                                        C.c_void_p(_stream(stream))), "dequant_batch")
     return out
+
+
+def intra_rdo_plane(src, qp: int = 32, pitch: int | None = None, stream=None):
+    """Config 3 on one int16 plane (H, W): returns
+    (modes u8 (H/8, W/8), levels int32 (H, W), recon int16 (H, W), sse int64 (1,))."""
+    torch = _torch()
+    _need(src, torch.int16, "intra_rdo_plane")
+    h, w = src.shape
+    dev = src.device
+    modes = torch.zeros((h // 8, w // 8), dtype=torch.uint8, device=dev)
+    lvl = torch.zeros((h, w), dtype=torch.int32, device=dev)
+    rec = torch.zeros((h, w), dtype=torch.int16, device=dev)
+    sse = torch.zeros(1, dtype=torch.int64, device=dev)
+    check(_lib.load().nh_intra_rdo_plane(src.data_ptr(), w, h, pitch or w, int(qp), modes.data_ptr(), lvl.data_ptr(),
+                                         rec.data_ptr(), sse.data_ptr(), C.c_void_p(_stream(stream))), "intra_rdo_plane")
+    return modes, lvl, rec, sse
+
+
+def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
+                      row0: int = 0, row1: int = 1 << 30, lvl=None, rec=None, tu=None, work=None, stream=None):
+    """Config 4 on one int16 plane (H, W), CTU rows [row0, row1).
+    Returns (levels int32 (H, W), recon int16 (H, W), tu_log2 u8 (H/4, W/4))."""
+    torch = _torch()
+    _need(src, torch.int16, "tu_pipeline_plane")
+    h, w = src.shape
+    dev = src.device
+    L = _lib.load()
+    lvl = torch.zeros((h, w), dtype=torch.int32, device=dev) if lvl is None else lvl
+    rec = torch.zeros((h, w), dtype=torch.int16, device=dev) if rec is None else rec
+    tu = torch.zeros((h // 4, w // 4), dtype=torch.uint8, device=dev) if tu is None else tu
+    if work is None:
+        work = torch.empty(int(L.nh_tu_workspace_bytes(w, h, ctb)), dtype=torch.uint8, device=dev)
+    check(L.nh_tu_pipeline_plane(src.data_ptr(), w, h, w, int(ctb), int(plane_id), int(seed) & 0xFFFFFFFF, int(qp),
+                                 int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)), lvl.data_ptr(), rec.data_ptr(),
+                                 tu.data_ptr(), work.data_ptr(), C.c_void_p(_stream(stream))), "tu_pipeline_plane")
+    return lvl, rec, tu

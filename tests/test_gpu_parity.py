@@ -250,3 +250,76 @@ def test_fused8x8_4k_yuv420_stream_vs_oracle(nh, torch_dev):
             o = base + W * H + c * (W // 2) * (H // 2)
             p = buf[o:o + (W // 2) * (H // 2)].reshape(H // 2, W // 2)
             assert np.array_equal(out[o:o + p.size].reshape(p.shape), O.fwd8x8_quant_plane(p, 32)), (f, c)
+
+
+# ------------------------------------------------------------------ config 3 / config 4 drivers
+
+def test_intra_rdo_golden(nh, torch_dev, golden):
+    """Config 3 vs planes recorded from the reference functions (make_golden.py)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    g = golden("planes.npz")
+    for k, qp in (("p3", 32), ("p3b", 22)):
+        m, l, r, sse = gpu.intra_rdo_plane(torch.from_numpy(g[f"{k}_src"]).cuda(), qp)
+        h8, w8 = g[f"{k}_modes"].shape
+        assert np.array_equal(m.cpu().numpy(), g[f"{k}_modes"]), k
+        assert np.array_equal(l.cpu().numpy()[:h8 * 8, :w8 * 8], g[f"{k}_lvl"][:h8 * 8, :w8 * 8]), k
+        assert np.array_equal(r.cpu().numpy()[:h8 * 8, :w8 * 8], g[f"{k}_rec"][:h8 * 8, :w8 * 8]), k
+        assert int(sse.item()) == int(g[f"{k}_sse"]), k
+
+
+@pytest.mark.parametrize("h,w,kind", [(64, 96, "natural"), (48, 40, "noise"), (72, 64, "int16")])
+def test_intra_rdo_vs_oracle(nh, torch_dev, h, w, kind):
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(h * w)
+    if kind == "natural":
+        yy, xx = np.mgrid[0:h, 0:w]
+        src = np.clip(40 + 3 * xx - yy + rng.integers(-10, 11, size=xx.shape), 0, 255).astype(np.int16)
+    elif kind == "noise":
+        src = rng.integers(0, 256, size=(h, w)).astype(np.int16)
+    else:   # arbitrary int16 samples: exercises the int16 wraps of residual/recon (D8-like) and 24-bit bounds
+        src = rng.integers(-32768, 32768, size=(h, w)).astype(np.int16)
+    for qp in (0, 32, 51):
+        m, l, r, sse = gpu.intra_rdo_plane(torch.from_numpy(src).cuda(), qp)
+        em, el, er, esse = O.intra_rdo_plane(src, qp)
+        assert np.array_equal(m.cpu().numpy(), em), (kind, qp)
+        assert np.array_equal(l.cpu().numpy(), el), (kind, qp)
+        assert np.array_equal(r.cpu().numpy(), er), (kind, qp)
+        assert int(sse.item()) == esse
+
+
+def test_tu_pipeline_golden(nh, torch_dev, golden):
+    torch = torch_dev
+    from nano_hevc import gpu
+    g = golden("planes.npz")
+    l, r, t = gpu.tu_pipeline_plane(torch.from_numpy(g["p4y_src"]).cuda(), 32, 0, 1234, 32, True)
+    assert np.array_equal(t.cpu().numpy(), g["p4y_tu"])
+    assert np.array_equal(l.cpu().numpy(), g["p4y_lvl"]) and np.array_equal(r.cpu().numpy(), g["p4y_rec"])
+    l, r, t = gpu.tu_pipeline_plane(torch.from_numpy(g["p4u_src"]).cuda(), 16, 1, 1234, 32, False)
+    assert np.array_equal(t.cpu().numpy(), g["p4u_tu"])
+    assert np.array_equal(l.cpu().numpy(), g["p4u_lvl"]) and np.array_equal(r.cpu().numpy(), g["p4u_rec"])
+
+
+@pytest.mark.parametrize("h,w,ctb,luma,seed", [(136, 200, 32, True, 7), (68, 100, 16, False, 7), (64, 64, 32, True, 99)])
+def test_tu_pipeline_vs_oracle_and_bands(nh, torch_dev, h, w, ctb, luma, seed):
+    """Whole plane, then the same plane as CTU-row bands (the multi-GPU shard
+    unit): bands must tile the plane and agree with the oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(seed + h)
+    yy, xx = np.mgrid[0:h, 0:w]
+    src = np.clip(120 + xx - 2 * yy + rng.integers(-25, 26, size=xx.shape), 0, 255).astype(np.int16)
+    d = torch.from_numpy(src).cuda()
+    for qp in (22, 37):
+        l, r, t = gpu.tu_pipeline_plane(d, ctb, 0 if luma else 1, seed, qp, luma)
+        el, er, et = O.tu_pipeline_plane(src, ctb, 0 if luma else 1, seed, qp, luma)
+        assert np.array_equal(t.cpu().numpy(), et) and np.array_equal(l.cpu().numpy(), el)
+        assert np.array_equal(r.cpu().numpy(), er)
+        rows = (h + ctb - 1) // ctb
+        lb = torch.zeros((h, w), dtype=torch.int32, device="cuda")
+        rb = torch.zeros((h, w), dtype=torch.int16, device="cuda")
+        tb = torch.zeros((h // 4, w // 4), dtype=torch.uint8, device="cuda")
+        for r0 in range(0, rows, 2):
+            gpu.tu_pipeline_plane(d, ctb, 0 if luma else 1, seed, qp, luma, r0, r0 + 2, lvl=lb, rec=rb, tu=tb)
+        assert np.array_equal(lb.cpu().numpy(), el) and np.array_equal(rb.cpu().numpy(), er)
