@@ -106,7 +106,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--frames", type=int, default=128, help="4K YUV420 frames per GPU per step")
     ap.add_argument("--qp", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=5, help="launch variant (nanohevc.h); 5 = default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

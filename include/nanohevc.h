@@ -101,9 +101,17 @@ typedef struct nh_plane_set {
  * Requires base/pitch/strides to be multiples of 8 elements (16-B rows). */
 int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                            int nsets, int qp, int is_intra, void* stream);
-/* Same computation, one wave-cooperative variant kept for A/B measurement. */
+/* Same computation, launch variants kept for A/B measurement (identical
+ * output): variant = cache policy (0 default, 1 nontemporal loads+stores,
+ * 2 nontemporal loads, 3 nontemporal stores) + 4 * occupancy class
+ * (0 compiler choice, 1 >= 5 waves/SIMD). */
 int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                    int nsets, int qp, int is_intra, int variant, void* stream);
+/* Measurement helper (not a product path): copies d_in to d_out over the same
+ * blocks with the hot kernel's exact access pattern -- the achievable-bandwidth
+ * ceiling for that pattern.  policy: as the variant's cache policy (0..3). */
+int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, const nh_plane_set* sets, int nsets,
+                            int policy, void* stream);
 
 /* nblocks contiguous size x size int32 blocks (row-major) */
 int nh_fwd_transform_batch(const int32_t* d_in, int32_t* d_out, int64_t nblocks, int size,

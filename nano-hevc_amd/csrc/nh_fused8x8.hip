@@ -43,43 +43,37 @@ struct Fused8Args {
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
-template <int VARIANT>
+// Cache policy of the streaming accesses: 0 default, 1 nontemporal loads and
+// stores, 2 nontemporal loads only, 3 nontemporal stores only.
+template <int POLICY>
 __device__ __forceinline__ v4i ld16(const int16_t* p) {
-    if constexpr (VARIANT == 1) return __builtin_nontemporal_load((const v4i*)p);
+    if constexpr (POLICY == 1 || POLICY == 2) return __builtin_nontemporal_load((const v4i*)p);
     else return *(const v4i*)p;
 }
-template <int VARIANT>
+template <int POLICY>
 __device__ __forceinline__ void st16(int16_t* p, v4i v) {
-    if constexpr (VARIANT == 1) __builtin_nontemporal_store(v, (v4i*)p);
+    if constexpr (POLICY == 1 || POLICY == 3) __builtin_nontemporal_store(v, (v4i*)p);
     else *(v4i*)p = v;
 }
 
-template <int VARIANT>
-__global__ void __launch_bounds__(256) k_fwd8x8_quant(Fused8Args a) {
-    // scalar (wave-uniform) set selection
-    int s = 0;
-#pragma unroll
-    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
-        if (k < a.nsets && blockIdx.x >= a.set[k].wg_start) s = k;
-    SetDev S = a.set[0];
-#pragma unroll
-    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
-        if (s == k) S = a.set[k];
-
-    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
-    if (b >= S.nblocks) return;
+// Locate block b of set S: element offset of its top-left sample.
+__device__ __forceinline__ int64_t block_offset(const SetDev& S, uint32_t b) {
     const uint32_t p = fdiv(b, S.bpp), r = b - p * S.bpp.d;
     const uint32_t by = fdiv(r, S.bpr), bx = r - by * S.bpr.d;
     const uint32_t g = fdiv(p, S.ppg), c = p - g * S.ppg.d;
-    const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride +
-                        (int64_t)by * 8 * S.pitch + (int64_t)bx * 8;
-    const int16_t* src = a.in + off;
-    int16_t* dst = a.out + off;
+    return S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride + (int64_t)by * 8 * S.pitch +
+           (int64_t)bx * 8;
+}
 
-    // ---- load 8 rows x 16 B, unpack int16 -> int32 ----
-    v4i raw[8];
+template <int POLICY>
+__device__ __forceinline__ void load_block(const int16_t* src, int32_t pitch, v4i (&raw)[8]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) raw[i] = ld16<VARIANT>(src + (int64_t)i * S.pitch);
+    for (int i = 0; i < 8; ++i) raw[i] = ld16<POLICY>(src + (int64_t)i * pitch);
+}
+
+// One 8x8 block: raw int16 rows -> int16 level rows (the whole fused computation).
+__device__ __forceinline__ void dct8_quant_block(const v4i (&raw)[8], v4i (&outv)[8], const QuantS& q,
+                                                 uint32_t h_v, uint32_t hneg_v) {
     uint32_t X[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -90,7 +84,6 @@ __global__ void __launch_bounds__(256) k_fwd8x8_quant(Fused8Args a) {
             X[i][2 * m + 1] = (uint32_t)(w[m] >> 16);
         }
     }
-
     // ---- pass 1: columns, temp = T.X, (acc+128)>>8  (transform.py:179-185) ----
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -101,25 +94,65 @@ __global__ void __launch_bounds__(256) k_fwd8x8_quant(Fused8Args a) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)y[i] >> 8);
     }
-
     // ---- pass 2: rows, coeff = temp.T^T  (transform.py:188-194) + quant + pack ----
-    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
-    asm volatile("" : "+v"(h_v), "+v"(hneg_v));  // pin the two offsets in VGPRs
-    v4i outv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         uint32_t y[8];
         fwd_dct<8, Mul24>(X[i], y, 128u);
         int32_t L[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) L[j] = quant_s((int32_t)y[j] >> 8, a.q, h_v, hneg_v);
+        for (int j = 0; j < 8; ++j) L[j] = quant_s((int32_t)y[j] >> 8, q, h_v, hneg_v);
         int w[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) w[m] = (int)__builtin_amdgcn_perm((uint32_t)L[2 * m + 1], (uint32_t)L[2 * m], 0x05040100u);
         outv[i] = v4i{w[0], w[1], w[2], w[3]};
     }
+}
+
+__device__ __forceinline__ int select_set(const Fused8Args& a, SetDev& S) {
+    int s = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) st16<VARIANT>(dst + (int64_t)i * S.pitch, outv[i]);
+    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
+        if (k < a.nsets && blockIdx.x >= a.set[k].wg_start) s = k;
+    S = a.set[0];
+#pragma unroll
+    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
+        if (s == k) S = a.set[k];
+    return s;
+}
+
+// One thread = one block.  POLICY: cache policy (ld16/st16); WAVES: minimum
+// waves per SIMD requested from the register allocator (1 = compiler choice).
+template <int POLICY, int WAVES>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant(Fused8Args a) {
+    SetDev S;
+    select_set(a, S);
+    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
+    asm volatile("" : "+v"(h_v), "+v"(hneg_v));  // pin the two offsets in VGPRs
+    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    if (b >= S.nblocks) return;
+    const int64_t off = block_offset(S, b);
+    v4i raw[8], outv[8];
+    load_block<POLICY>(a.in + off, S.pitch, raw);
+    dct8_quant_block(raw, outv, a.q, h_v, hneg_v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
+}
+
+// Memory-only probe with the kernel's exact access pattern (8 rows x 16 B per
+// thread, same block walk): copies input to output.  Measurement helper for the
+// achievable-bandwidth ceiling of this pattern; not a product path.
+template <int POLICY>
+__global__ void __launch_bounds__(256) k_probe_copy8x8(Fused8Args a) {
+    SetDev S;
+    select_set(a, S);
+    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    if (b >= S.nblocks) return;
+    const int64_t off = block_offset(S, b);
+    v4i raw[8];
+    load_block<POLICY>(a.in + off, S.pitch, raw);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, raw[i]);
 }
 
 static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
@@ -175,24 +208,54 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
 
 using namespace nh;
 
+static constexpr int kDefaultVariant = 5;
+
 extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                               int nsets, int qp, int is_intra, int variant, void* stream) {
+    // variant = cache policy (0..3, see ld16/st16) + 4 * occupancy class (0 compiler, 1 >= 5 waves/SIMD)
+    const int policy = variant & 3, occ = variant >> 2;
+    if (variant < 0 || occ > 1) return NH_EARG;
     Fused8Args a;
     uint32_t wg = 0;
     int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
     if (rc) return rc;
     if (!wg) return NH_OK;
     hipStream_t s = as_stream(stream);
-    switch (variant) {
-        case 0: k_fwd8x8_quant<0><<<wg, 256, 0, s>>>(a); break;
-        case 1: k_fwd8x8_quant<1><<<wg, 256, 0, s>>>(a); break;
-        default: return NH_EARG;
+#define NH_L(P) do { if (occ) k_fwd8x8_quant<P, 5><<<wg, 256, 0, s>>>(a); else k_fwd8x8_quant<P, 1><<<wg, 256, 0, s>>>(a); } while (0)
+    switch (policy) {
+        case 0: NH_L(0); break;
+        case 1: NH_L(1); break;
+        case 2: NH_L(2); break;
+        default: NH_L(3); break;
     }
+#undef NH_L
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
 
 extern "C" int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,
                                       int qp, int is_intra, void* stream) {
-    return nh_fwd8x8_quant_planes_variant(d_res, d_lvl, sets, nsets, qp, is_intra, 0, stream);
+    // default launch = variant 5: nontemporal loads+stores (streamed once, keep
+    // them out of L2/MALL) and >= 5 waves/SIMD (74 VGPRs -> 6 waves); fastest
+    // in the interleaved A/B (profiles/r01/ab_variants.json).
+    return nh_fwd8x8_quant_planes_variant(d_res, d_lvl, sets, nsets, qp, is_intra, kDefaultVariant, stream);
+}
+
+extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, const nh_plane_set* sets, int nsets,
+                                       int policy, void* stream) {
+    if (policy < 0 || policy > 3) return NH_EARG;
+    Fused8Args a;
+    uint32_t wg = 0;
+    int rc = build_args(d_in, d_out, sets, nsets, 32, 1, a, wg);
+    if (rc) return rc;
+    if (!wg) return NH_OK;
+    hipStream_t s = as_stream(stream);
+    switch (policy) {
+        case 0: k_probe_copy8x8<0><<<wg, 256, 0, s>>>(a); break;
+        case 1: k_probe_copy8x8<1><<<wg, 256, 0, s>>>(a); break;
+        case 2: k_probe_copy8x8<2><<<wg, 256, 0, s>>>(a); break;
+        default: k_probe_copy8x8<3><<<wg, 256, 0, s>>>(a); break;
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
 }

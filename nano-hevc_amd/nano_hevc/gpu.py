@@ -64,8 +64,11 @@ def blocks_in(sets: Sequence[PlaneSet]) -> int:
     return sum((s.width // 8) * (s.height // 8) * s.planes_per_group * s.num_groups for s in sets)
 
 
+DEFAULT_VARIANT = 5   # nontemporal loads+stores, >= 5 waves/SIMD (see nh_fused8x8.hip)
+
+
 def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = True, out=None,
-                 variant: int = 0, stream=None):
+                 variant: int = DEFAULT_VARIANT, stream=None):
     """Forward 8x8 DCT (transform.py:154-196) + quantize_block (quant.py:126-137) on
     every full 8x8 block of the int16 planes described by ``sets`` inside ``res``.
     Levels land at the same raster positions of ``out`` (int16)."""
