@@ -4,10 +4,13 @@
 A "step" = one launch of the fused 8x8 forward DCT + quant (QP 32, intra
 offset) over this rank's share of a batch of synthetic 4K YUV420 int16 residual
 frames already resident in HBM (BASELINE.json configs[1] kernel on the
-metric's 4K YUV420 stream).  Multi-GPU: every frame is cut into
-CTU-row bands (32 luma / 16 chroma rows), rank r owns band r of every frame of
-a global batch of N x frames_per_gpu frames -- no data-path collective, weak
-scaling.  Timing: W warmup steps, then K steps between barrier +
+metric's 4K YUV420 stream).  Multi-GPU (nano_hevc/shard.py):
+every frame is cut into N balanced CTU-row bands, band b of frame f goes to
+rank (b - f) mod N, over a global batch of N x frames_per_gpu frames -- every
+rank carries exactly frames_per_gpu frames of blocks, no data-path collective,
+weak scaling.  With N > 1 a separate, shorter phase also times the path's one
+exchange step (RCCL gather of the levels to rank 0) and reports it as
+``gather_inclusive``.  Timing: W warmup steps, then K steps between barrier +
 synchronize; the max over ranks is reported.  Rank 0 prints one JSON line.
 
 Roofline: algorithmic bytes per 8x8 block = 128 B int16 in + 128 B int16 out
@@ -38,28 +41,7 @@ import torch  # noqa: E402
 METRIC = "transform-blocks/sec (8×8 DCT+quant, 4K YUV420) at 1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_BLOCK = 256          # 64 x int16 in + 64 x int16 out
-W4K, H4K, CTU = 3840, 2160, 32
-
-
-def band_rows(rank: int, world: int, height: int, ctu: int):
-    """CTU-row band [r0, r1) of a plane for this rank (the last band may be short)."""
-    rows = (height + ctu - 1) // ctu
-    per = (rows + world - 1) // world
-    r0 = min(rank * per, rows) * ctu
-    r1 = min((rank + 1) * per * ctu, height)
-    return r0, max(r0, r1)
-
-
-def build_sets(gpu, frames: int, y_rows: int, c_rows: int):
-    """Plane sets of this rank's local buffer: per frame [Y band][U band][V band]."""
-    cw = W4K // 2
-    fe = W4K * y_rows + 2 * cw * c_rows
-    sets = []
-    if y_rows:
-        sets.append(gpu.plane_set(0, W4K, y_rows, W4K, 1, frames, 0, fe))
-    if c_rows:
-        sets.append(gpu.plane_set(W4K * y_rows, cw, c_rows, cw, 2, frames, cw * c_rows, fe))
-    return sets, fe
+W4K, H4K = 3840, 2160
 
 
 def load_traffic(cfg_key: str):
@@ -108,6 +90,7 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--variant", type=int, default=5, help="launch variant (nanohevc.h); 5 = default")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--gather-steps", type=int, default=3, help="N>1: steps of the gather-inclusive phase")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -127,15 +110,17 @@ def main():
     from nano_hevc import gpu, _lib
     _lib.load()
 
-    y0, y1 = band_rows(rank, world, H4K, CTU)
-    c0, c1 = band_rows(rank, world, H4K // 2, CTU // 2)
+    from nano_hevc import shard
     frames_global = args.frames * world
-    sets, fe = build_sets(gpu, frames_global, y1 - y0, c1 - c0)
+    layout = shard.rank_layout(rank, world, frames_global, W4K, H4K)
+    sets = layout.plane_sets(gpu)
     nblk = gpu.blocks_in(sets)
+    assert nblk == layout.blocks() == args.frames * 194400, (nblk, layout.blocks())
+    fe = gpu.yuv420_frame_elems(W4K, H4K)
     # synthetic residual: U[-255,255] (worst-case 8-bit residual magnitude), seeded per rank
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234 + rank)
-    res = torch.randint(-255, 256, (frames_global * fe,), dtype=torch.int16, device=dev, generator=gen)
+    res = torch.randint(-255, 256, (layout.total_elems,), dtype=torch.int16, device=dev, generator=gen)
     out = torch.zeros_like(res)
     stream = torch.cuda.current_stream()
 
@@ -169,6 +154,26 @@ def main():
     total_blocks = float(blocks_t[0]) * args.steps
     value = total_blocks / elapsed
 
+    gather = None
+    if dist and args.gather_steps > 0:
+        # the path's one exchange step: levels of every rank -> rank 0 (RCCL gather over xGMI)
+        sizes = [shard.rank_layout(r, world, frames_global, W4K, H4K).total_elems for r in range(world)]
+        dist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(args.gather_steps):
+            step()
+            shard.gather_to_root(out, sizes, dist)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gt = torch.tensor([time.perf_counter() - g0], dtype=torch.float64, device=dev)
+        dist.all_reduce(gt, op=dist.ReduceOp.MAX)
+        gv = float(blocks_t[0]) * args.gather_steps / float(gt[0])
+        gather = {"value": gv, "unit": "blocks/s", "steps": args.gather_steps,
+                  "ms_per_step": float(gt[0]) / args.gather_steps * 1e3,
+                  "bytes_gathered_per_step": 2 * sum(sizes[1:]),
+                  "note": "compute + torch.distributed.gather (RCCL) of int16 levels to rank 0"}
+
     if rank == 0:
         achieved = nblk * BYTES_PER_BLOCK / (kern_ms * 1e-3) / 1e9
         cfg_key = f"fwd8x8_qp{args.qp}_4k_yuv420_f{args.frames}_v{args.variant}_n{world}"
@@ -182,14 +187,16 @@ def main():
                                    "(cfg 2 kernel on the metric's 4K stream), CTU-row band sharding",
                        "frames_per_gpu": args.frames, "blocks_per_launch": nblk, "qp": args.qp,
                        "resolution": "3840x2160 YUV420 int16 in / int16 levels out",
-                       "parallelism": f"band{world}", "kernel_variant": args.variant},
+                       "parallelism": f"ctu-band{world} (rotated)", "kernel_variant": args.variant},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "bytes_per_block": BYTES_PER_BLOCK, "kernel_ms_avg": kern_ms},
             "cpu_baseline": None,
         }
+        if gather:
+            line["gather_inclusive"] = gather
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(out, res, fe, frames_global, args.qp, args.cpu_seconds)
+            line["cpu_baseline"] = cpu_baseline(out, res, fe, frames_global, args.qp, args.cpu_seconds)  # N=1: whole frames
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

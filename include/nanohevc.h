@@ -91,7 +91,7 @@ typedef struct nh_plane_set {
     int32_t reserved;
 } nh_plane_set;
 
-#define NH_MAX_PLANE_SETS 4
+#define NH_MAX_PLANE_SETS 8
 
 /* THE HOT PATH (config 2 / north-star metric): forward 8x8 integer DCT
  * (transform.py:154-196) fused with quantize_block (quant.py:126-137) over

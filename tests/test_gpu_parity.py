@@ -323,3 +323,30 @@ def test_tu_pipeline_vs_oracle_and_bands(nh, torch_dev, h, w, ctb, luma, seed):
         for r0 in range(0, rows, 2):
             gpu.tu_pipeline_plane(d, ctb, 0 if luma else 1, seed, qp, luma, r0, r0 + 2, lvl=lb, rec=rb, tu=tb)
         assert np.array_equal(lb.cpu().numpy(), el) and np.array_equal(rb.cpu().numpy(), er)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_fused8x8_rank_layouts_vs_oracle(nh, torch_dev, world):
+    """The multi-GPU shard layout (nano_hevc/shard.py): every rank's local buffer
+    (up to 6 plane sets of different band heights) through one launch; the
+    scattered-back levels equal the oracle on the full frames."""
+    torch = torch_dev
+    from nano_hevc import gpu, shard
+    w, h, n = 256, 416, 2 * world            # 13 CTU rows -> uneven bands
+    fe = gpu.yuv420_frame_elems(w, h)
+    rng = np.random.default_rng(world)
+    frames = [rng.integers(-255, 256, size=fe).astype(np.int16) for _ in range(n)]
+    back = [np.zeros_like(f) for f in frames]
+    for r in range(world):
+        L = shard.rank_layout(r, world, n, w, h)
+        loc = np.zeros(L.total_elems, np.int16)
+        shard.fill_from_frames(L, frames, loc)
+        d = torch.from_numpy(loc).cuda()
+        out = gpu.fwd8x8_quant(d, L.plane_sets(gpu), 32, True)
+        shard.scatter_to_frames(L, out.cpu().numpy(), back)
+    cw, ch = w // 2, h // 2
+    for f, fr in enumerate(frames):
+        exp = np.concatenate([O.fwd8x8_quant_plane(fr[:w * h].reshape(h, w), 32).ravel(),
+                              O.fwd8x8_quant_plane(fr[w * h:w * h + cw * ch].reshape(ch, cw), 32).ravel(),
+                              O.fwd8x8_quant_plane(fr[w * h + cw * ch:].reshape(ch, cw), 32).ravel()])
+        assert np.array_equal(back[f], exp), f
