@@ -100,8 +100,15 @@ def main():
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # NH_DIST_BACKEND / NH_FORCE_DEVICE: rehearsal knobs only (e.g. 2 gloo ranks
+        # sharing the one GPU of a test box); the driver's runs use RCCL, 1 GPU/rank.
+        backend = os.environ.get("NH_DIST_BACKEND", "nccl")
+        local = int(os.environ.get("NH_FORCE_DEVICE", local))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         dist = None
         torch.cuda.set_device(0)

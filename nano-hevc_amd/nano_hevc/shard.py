@@ -141,6 +141,9 @@ def gather_to_root(local, layouts_total_elems: List[int], dist, group=None):
     has an int16 type), padded to the largest rank's size."""
     import torch
     n = max(layouts_total_elems) * local.element_size()
+    if local.is_cuda and dist.get_backend(group) == "gloo":   # gloo gathers host tensors only
+        out = gather_to_root(local.cpu(), layouts_total_elems, dist, group)
+        return None if out is None else [o.to(local.device) for o in out]
     raw = local.contiguous().view(torch.uint8)
     send = raw if raw.numel() == n else torch.nn.functional.pad(raw, (0, n - raw.numel()))
     rank = dist.get_rank(group)
