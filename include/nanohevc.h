@@ -74,7 +74,21 @@ int nh_count_nonzero(const int64_t* level, int64_t n, int64_t* count);
  * caller applies int() (which raises on NaN/inf exactly as the reference). */
 int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits);
 
+/* metrics.py:7-48 as device reductions.
+ * nh_sum_sq_diff: exact int64 sum((a-b)^2) (mse = sum / n; psnr from mse);
+ * nh_sad: int32 difference/abs (wrapping like the int32 arrays of metrics.py:26);
+ * nh_satd_4x4: H.diff.H^T in int32, sum |.| (metrics.py:29-43), 16 samples;
+ * nh_residual_energy: sum(int64(r)^2) mod 2^64 (metrics.py:46-48). */
+int nh_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, int64_t* out);
+int nh_sad(const int32_t* a, const int32_t* b, int64_t n, int64_t* out);
+int nh_satd_4x4(const int32_t* a, const int32_t* b, int64_t* out);
+int nh_residual_energy(const int64_t* r, int64_t n, int64_t* out);
+
 /* ---------------- (ii) batched device entry points ---------------- */
+
+/* SSE between two int16 device buffers, added into *d_out (one int64): frame
+ * PSNR / RDO distortion without a host round trip. */
+int nh_sse_i16(const int16_t* d_a, const int16_t* d_b, int64_t n, int64_t* d_out, void* stream);
 
 /* A set of equally shaped raster planes inside one buffer (e.g. the Y planes,
  * or the U+V planes, of a stream of YUV420 frames).  Offsets/pitches are in

@@ -402,6 +402,73 @@ __global__ void k_estimate_bits(const int64_t* l, int64_t n, int bits, double* o
     *out = n > 0 ? pw_sum(l, n, bits) : 0.0;   // the shim applies int() (quant.py:168)
 }
 
+// ---------------------------------------------------------------------------
+// quality metrics (metrics.py:7-48) as device reductions
+// ---------------------------------------------------------------------------
+template <class T, class F>
+__device__ __forceinline__ void block_reduce_add(T v, unsigned long long* out, F) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, (unsigned long long)v);
+}
+struct NoOp {};
+// sum((a-b)^2) exactly in int64 (inputs are <= 16-bit samples widened by the shim)
+__global__ void k_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, unsigned long long* out) {
+    unsigned long long s = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t d = a[i] - b[i];
+        s += (unsigned long long)(d * d);
+    }
+    block_reduce_add(s, out, NoOp{});
+}
+// metrics.py:24-26: int32 difference (wraps), np.abs (wraps at INT32_MIN), int64 sum
+__global__ void k_sad_i32(const int32_t* a, const int32_t* b, int64_t n, unsigned long long* out) {
+    unsigned long long s = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int32_t d = (int32_t)((uint32_t)a[i] - (uint32_t)b[i]);
+        int32_t ad = d == INT32_MIN ? d : (d < 0 ? -d : d);
+        s += (unsigned long long)(long long)ad;
+    }
+    block_reduce_add(s, out, NoOp{});
+}
+// metrics.py:29-43: H . diff . H^T in int32 (wrap), sum |.| in int64
+__global__ void k_satd_4x4(const int32_t* a, const int32_t* b, long long* out) {
+    if (threadIdx.x || blockIdx.x) return;
+    constexpr int H[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
+    uint32_t d[4][4], t[4][4];
+    for (int i = 0; i < 16; ++i) d[i / 4][i % 4] = (uint32_t)a[i] - (uint32_t)b[i];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            uint32_t acc = 0;
+            for (int k = 0; k < 4; ++k) acc += (uint32_t)H[i][k] * d[k][j];
+            t[i][j] = acc;
+        }
+    long long s = 0;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            uint32_t acc = 0;
+            for (int k = 0; k < 4; ++k) acc += t[i][k] * (uint32_t)H[j][k];
+            int32_t v = (int32_t)acc;
+            s += (v == INT32_MIN) ? (long long)v : (v < 0 ? -(long long)v : (long long)v);
+        }
+    *out = s;
+}
+// metrics.py:46-48: sum(r.astype(int64)**2), int64 wrap
+__global__ void k_residual_energy(const int64_t* r, int64_t n, unsigned long long* out) {
+    unsigned long long s = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        s += (unsigned long long)r[i] * (unsigned long long)r[i];
+    block_reduce_add(s, out, NoOp{});
+}
+// batched: SSE between two int16 device buffers (frame PSNR without a host round trip)
+__global__ void k_sse_i16(const int16_t* a, const int16_t* b, int64_t n, unsigned long long* out) {
+    unsigned long long s = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int32_t d = (int32_t)a[i] - (int32_t)b[i];
+        s += (unsigned long long)(uint32_t)(d * d);
+    }
+    block_reduce_add(s, out, NoOp{});
+}
+
 static unsigned grid_for(int64_t n, int64_t cap = 8192) {
     int64_t g = (n + 255) / 256;
     if (g < 1) g = 1;
@@ -655,4 +722,41 @@ int nh_dequant_batch(const int32_t* d_level, int32_t* d_coeff, int64_t n, int qp
     return NH_OK;
 }
 
+// ----- metrics (metrics.py:7-48) -----
+static int reduce_call(const void* a, size_t abytes, const void* b, size_t bbytes, int64_t* out, int which, int64_t n) {
+    Layout L;
+    size_t oa = L.take(abytes + 8), ob = L.take(bbytes + 8), oc = L.take(8);
+    NH_STAGE_BEGIN(L.off);
+    NH_TRY(staging_upload(S, oa, a, abytes));
+    if (b) NH_TRY(staging_upload(S, ob, b, bbytes));
+    char* d = (char*)S.dbuf;
+    NH_HIP(hipMemsetAsync(d + oc, 0, 8, S.stream));
+    unsigned long long* o = (unsigned long long*)(d + oc);
+    if (which == 0 && n) k_sum_sq_diff<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oa), (int64_t*)(d + ob), n, o);
+    if (which == 1 && n) k_sad_i32<<<grid_for(n), 256, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), n, o);
+    if (which == 2) k_satd_4x4<<<1, 64, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), (long long*)o);
+    if (which == 3 && n) k_residual_energy<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oa), n, o);
+    return finish_copy(S, out, oc, 8);
+}
+int nh_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, int64_t* out) {
+    if (n < 0) return NH_EARG;
+    return reduce_call(a, n * 8, b, n * 8, out, 0, n);
+}
+int nh_sad(const int32_t* a, const int32_t* b, int64_t n, int64_t* out) {
+    if (n < 0) return NH_EARG;
+    return reduce_call(a, n * 4, b, n * 4, out, 1, n);
+}
+int nh_satd_4x4(const int32_t* a, const int32_t* b, int64_t* out) { return reduce_call(a, 64, b, 64, out, 2, 16); }
+int nh_residual_energy(const int64_t* r, int64_t n, int64_t* out) {
+    if (n < 0) return NH_EARG;
+    return reduce_call(r, n * 8, nullptr, 0, out, 3, n);
+}
+int nh_sse_i16(const int16_t* d_a, const int16_t* d_b, int64_t n, int64_t* d_out, void* stream) {
+    if (!d_a || !d_b || !d_out || n < 0) return NH_EARG;
+    if (n) k_sse_i16<<<grid_for(n), 256, 0, as_stream(stream)>>>(d_a, d_b, n, (unsigned long long*)d_out);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
 }  // extern "C"
+

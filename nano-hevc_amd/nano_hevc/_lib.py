@@ -47,6 +47,11 @@ SIGNATURES = {
     "nh_dequantize": ([P, I64, I32, P], I32),
     "nh_count_nonzero": ([P, I64, P], I32),
     "nh_estimate_bits": ([P, I64, I32, P], I32),
+    "nh_sum_sq_diff": ([P, P, I64, P], I32),
+    "nh_sad": ([P, P, I64, P], I32),
+    "nh_satd_4x4": ([P, P, P], I32),
+    "nh_residual_energy": ([P, I64, P], I32),
+    "nh_sse_i16": ([P, P, I64, P, VP], I32),
     "nh_fwd8x8_quant_planes": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, VP], I32),
     "nh_fwd8x8_quant_planes_variant": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, I32, VP], I32),
     "nh_probe_copy8x8_planes": ([P, P, C.POINTER(PlaneSet), I32, I32, VP], I32),

@@ -26,9 +26,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def _import_reference(path):
     sys.path.insert(0, path)
     import nano_hevc  # noqa: F401  (the reference package)
-    from nano_hevc import intra, transform, quant
+    from nano_hevc import intra, transform, quant, metrics
     assert os.path.abspath(intra.__file__).startswith(os.path.abspath(path)), intra.__file__
-    return intra, transform, quant
+    return intra, transform, quant, metrics
 
 
 def _err(fn):
@@ -323,6 +323,37 @@ def gen_planes(I, T, Q, rng):
     return out
 
 
+def gen_metrics(M):
+    """metrics.py:7-48 on seeded integer samples (its own rng: other fixtures unchanged)."""
+    rng = np.random.default_rng(4321)
+    out = {}
+    a8 = rng.integers(0, 256, size=(6, 64, 64)).astype(np.uint8)
+    b8 = np.clip(a8.astype(np.int16) + rng.integers(-20, 21, size=a8.shape), 0, 255).astype(np.uint8)
+    out["m_a8"], out["m_b8"] = a8, b8
+    out["m_mse"] = np.array([M.mse(x, y) for x, y in zip(a8, b8)])
+    out["m_psnr"] = np.array([M.psnr(x, y) for x, y in zip(a8, b8)])
+    out["m_psnr1023"] = np.array([M.psnr(x, y, peak=1023) for x, y in zip(a8, b8)])
+    a16 = rng.integers(-32768, 32768, size=(4, 100)).astype(np.int16)
+    b16 = rng.integers(-32768, 32768, size=(4, 100)).astype(np.int16)
+    out["m_a16"], out["m_b16"] = a16, b16
+    out["m_mse16"] = np.array([M.mse(x, y) for x, y in zip(a16, b16)])
+    out["m_sad16"] = np.array([M.sad(x, y) for x, y in zip(a16, b16)])
+    out["m_energy16"] = np.array([M.residual_energy(x) for x in a16])
+    a32 = rng.integers(-2**31, 2**31, size=(4, 16), dtype=np.int64).astype(np.int32)
+    b32 = rng.integers(-2**31, 2**31, size=(4, 16), dtype=np.int64).astype(np.int32)
+    out["m_a32"], out["m_b32"] = a32, b32
+    out["m_sad32"] = np.array([M.sad(x, y) for x, y in zip(a32, b32)])            # int32 wrap
+    out["m_satd32"] = np.array([M.satd_4x4(x, y) for x, y in zip(a32, b32)])
+    s4a = rng.integers(0, 256, size=(8, 4, 4))
+    s4b = rng.integers(0, 256, size=(8, 4, 4))
+    out["m_s4a"], out["m_s4b"] = s4a, s4b
+    out["m_satd"] = np.array([M.satd_4x4(x, y) for x, y in zip(s4a, s4b)])
+    e64 = rng.integers(-2**40, 2**40, size=(3, 50), dtype=np.int64)
+    out["m_e64"] = e64
+    out["m_energy64"] = np.array([M.residual_energy(x) for x in e64])              # int64 wrap
+    return out
+
+
 def plane_hash_1080p(T, Q):
     rng = np.random.default_rng(20260)
     plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
@@ -333,7 +364,7 @@ def plane_hash_1080p(T, Q):
 def main():
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     warnings.simplefilter("ignore")
-    I, T, Q = _import_reference(ref)
+    I, T, Q, M = _import_reference(ref)
     rng = np.random.default_rng(1234)
     files = {
         "matrices.npz": gen_matrices(T),
@@ -342,6 +373,7 @@ def main():
         "intra.npz": gen_intra(I, rng),
         "chain.npz": gen_chain(I, T, Q),
         "planes.npz": gen_planes(I, T, Q, rng),
+        "metrics.npz": gen_metrics(M),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

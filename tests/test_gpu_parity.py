@@ -350,3 +350,40 @@ def test_fused8x8_rank_layouts_vs_oracle(nh, torch_dev, world):
                               O.fwd8x8_quant_plane(fr[w * h:w * h + cw * ch].reshape(ch, cw), 32).ravel(),
                               O.fwd8x8_quant_plane(fr[w * h + cw * ch:].reshape(ch, cw), 32).ravel()])
         assert np.array_equal(back[f], exp), f
+
+
+def test_metrics_golden(nh, golden):
+    """metrics.py:7-48 through the device reductions vs the reference's values."""
+    g = golden("metrics.npz")
+    for i, (a, b) in enumerate(zip(g["m_a8"], g["m_b8"])):
+        assert nh.mse(a, b) == g["m_mse"][i]
+        assert nh.psnr(a, b) == g["m_psnr"][i]
+        assert nh.psnr(a, b, peak=1023) == g["m_psnr1023"][i]
+    assert nh.psnr(g["m_a8"][0], g["m_a8"][0]) == float("inf")
+    for i, (a, b) in enumerate(zip(g["m_a16"], g["m_b16"])):
+        assert nh.mse(a, b) == g["m_mse16"][i]
+        assert nh.sad(a, b) == g["m_sad16"][i]
+        assert nh.residual_energy(a) == g["m_energy16"][i]
+    for i, (a, b) in enumerate(zip(g["m_a32"], g["m_b32"])):
+        assert nh.sad(a, b) == g["m_sad32"][i]
+        assert nh.satd_4x4(a, b) == g["m_satd32"][i]
+    for i, (a, b) in enumerate(zip(g["m_s4a"], g["m_s4b"])):
+        assert nh.satd_4x4(a, b) == g["m_satd"][i]
+    for i, e in enumerate(g["m_e64"]):
+        assert nh.residual_energy(e) == g["m_energy64"][i]
+    with pytest.raises(ValueError):
+        nh.satd_4x4(np.arange(8), np.arange(8))
+
+
+def test_sse_i16_device(nh, torch_dev):
+    torch = torch_dev
+    from nano_hevc import _lib
+    import ctypes as C
+    rng = np.random.default_rng(2)
+    a = rng.integers(-32768, 32768, size=1 << 20).astype(np.int16)
+    b = rng.integers(-32768, 32768, size=1 << 20).astype(np.int16)
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _lib.check(_lib.load().nh_sse_i16(da.data_ptr(), db.data_ptr(), a.size, out.data_ptr(),
+                                      C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    assert int(out.item()) == int(np.sum((a.astype(np.int64) - b) ** 2))

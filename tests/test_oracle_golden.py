@@ -184,5 +184,6 @@ def test_plane_hash_1080p():
 def test_manifest_integrity():
     man = json.load(open(os.path.join(GOLDEN, "manifest.json")))
     assert man["numpy"].split(".")[0] == "2"      # NEP 50 semantics (D8)
+    assert "metrics.npz" in man["files"]
     for name, h in man["files"].items():
         assert hashlib.sha256(open(os.path.join(GOLDEN, name), "rb").read()).hexdigest() == h, name
