@@ -160,6 +160,16 @@ int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb,
                          int32_t* d_lvl, int16_t* d_recon, uint8_t* d_tu, void* d_work,
                          void* stream);
 
+/* Config 5: every full 32x32 block of an int16 source plane through the
+ * config-4 chain at N=32.  variant 0 = butterfly
+ * (k_tu_process<32>), 1 = int8 matrix cores (v_mfma_i32_32x32x32_i8 with
+ * exact int8 part splitting).  Identical outputs.  pitch % 8 == 0. */
+int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl,
+                  int16_t* d_recon, int variant, void* stream);
+/* Measurement / validation helper: D = A.B for row-major int8 32x32 A, B
+ * (int32 D) with the lane maps the config-5 MFMA kernel assumes. */
+int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -274,11 +274,18 @@ __global__ void k_tu_plan(int w, int h, int ctb, int plane_id, uint32_t seed, in
     }
 }
 
-template <int N, bool DST>
+// GRID mode (config 5): TU idx is the idx-th full NxN block of the plane in
+// raster order (grid_bw blocks per row, grid_n blocks), no list, no TU map.
+// Multiplies are 24-bit (v_mad_i32_i24): exact for the whole chain because the
+// residual is int16 (forward operands < 2^21), dequantized coefficients are
+// ~|c|*2^20/2^(17+log2N) < 2^19, and inverse pass-2 operands are a >> S of an
+// int32 sum bounded by 2^27 -> < 2^21.
+template <int N, bool DST, bool GRID = false>
 __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     const uint32_t* __restrict__ list, const uint32_t* count,
                                                     QuantParams qp, int dq_scale, int dq_per, int32_t* lvl,
-                                                    int16_t* recon, uint8_t* tu_log2) {
+                                                    int16_t* recon, uint8_t* tu_log2, int grid_bw = 0,
+                                                    int grid_n = 0) {
     constexpr int G = 256 / N;            // TUs per workgroup
     constexpr int P = N + 1;              // padded LDS row
     constexpr int S = Log2<N>::v + 5;
@@ -288,12 +295,17 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     __shared__ long long e_dc[G][N], e_pl[G][N];
     const int g = threadIdx.x / N, t = threadIdx.x % N;
     const uint32_t idx = blockIdx.x * G + g;
-    const bool active = idx < *count;
+    const bool active = GRID ? idx < (uint32_t)grid_n : idx < *count;
     int x0 = 0, y0 = 0;
     if (active) {
-        const uint32_t e = list[idx];
-        x0 = e & 0xffff;
-        y0 = e >> 16;
+        if constexpr (GRID) {
+            x0 = (idx % grid_bw) * N;
+            y0 = (idx / grid_bw) * N;
+        } else {
+            const uint32_t e = list[idx];
+            x0 = e & 0xffff;
+            y0 = e >> 16;
+        }
         // neighbours (block.py:38-50): count N, 128 outside the plane (full TUs: no truncation)
         topv[g][t] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + t];
         leftv[g][t] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + t) * pitch + x0 - 1];
@@ -337,7 +349,7 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     if (active) {
 #pragma unroll
         for (int k = 0; k < N; ++k) v[k] = (uint32_t)(int32_t)wrap16((int32_t)orig[g][k][t] - pred_at(k, t));
-        fwd1d<N, DST, MulWrap>(v, r);
+        fwd1d<N, DST, Mul24>(v, r);
 #pragma unroll
         for (int i = 0; i < N; ++i) tile[g][i][t] = rshift_round<S>(r[i]);
     }
@@ -346,7 +358,7 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     if (active) {
 #pragma unroll
         for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][t][k];
-        fwd1d<N, DST, MulWrap>(v, r);
+        fwd1d<N, DST, Mul24>(v, r);
         int32_t* lrow = lvl + (int64_t)(y0 + t) * pitch + x0;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -365,7 +377,7 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     if (active) {
 #pragma unroll
         for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][k][t];
-        inv1d<N, DST, MulWrap>(v, r);
+        inv1d<N, DST, Mul24>(v, r);
     }
     __syncthreads();
     if (active) {
@@ -377,7 +389,7 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     if (active) {
 #pragma unroll
         for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][t][k];
-        inv1d<N, DST, MulWrap>(v, r);
+        inv1d<N, DST, Mul24>(v, r);
         int16_t* rrow = recon + (int64_t)(y0 + t) * pitch + x0;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
@@ -385,7 +397,7 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
             int32_t rc = wrap16(pred_at(t, j) + rr);
             rrow[j] = (int16_t)(rc < 0 ? 0 : (rc > 255 ? 255 : rc));
         }
-        if (t < N / 4) {
+        if (!GRID && t < N / 4) {
             const int w4 = w / 4;
             for (int j = 0; j < N / 4; ++j) tu_log2[(int64_t)(y0 / 4 + t) * w4 + x0 / 4 + j] = (uint8_t)Log2<N>::v;
         }
@@ -408,6 +420,18 @@ static QuantParams qparams(int qp, int log2n, bool intra) {
 }
 
 static int64_t tu_cap(int w, int h, int s) { return (int64_t)((w + s - 1) / s) * ((h + s - 1) / s); }
+
+int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
+                   hipStream_t s) {
+    const int bw = w / 32, n = bw * (h / 32);
+    if (!n) return NH_OK;
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    k_tu_process<32, false, true><<<(n + 7) / 8, 256, 0, s>>>(d_src, w, h, pitch, nullptr, nullptr, qparams(qp, 5, true),
+                                                             dequant_scale(rem), per, d_lvl, d_recon, nullptr, bw, n);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
 
 }  // namespace nh
 

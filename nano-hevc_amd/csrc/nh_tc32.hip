@@ -1,0 +1,304 @@
+// nh_tc32.hip -- config 5: the 32x32 transform-coding chain, MFMA variant.
+//
+// Semantics: every full 32x32 block of a plane goes through
+// the config-4 TU chain at N=32 (DC-vs-planar by residual energy,
+// __main__.py:165-178; residual -> forward_transform (transform.py:154-196) ->
+// quantize_block -> dequantize_block (quant.py:126-150) -> inverse_transform
+// (transform.py:199-238) -> reconstruct + clip (intra.py:70-78)).  The
+// butterfly variant is k_tu_process<32> (nh_intraloop.hip, grid mode); this
+// file holds the matrix-core variant and the dispatcher.
+//
+// MFMA formulation (one wave = one block, v_mfma_i32_32x32x32_i8):
+//   int8 operands, int32 accumulation: every data operand v is split into
+//   int8 parts v = sum_p 128^p * part_p (2 parts when |v| < 2^14, else 3;
+//   wave-uniform choice), each part multiplied by the int8 basis (|T| <= 90),
+//   partial products recombined with shifts.  All of it is ring arithmetic
+//   mod 2^32, so results equal the reference's int32 matrix products exactly.
+//   Data never needs an explicit transpose between the two passes of a
+//   transform: the accumulator (column on the lane, rows in registers) feeds
+//   the next MFMA as its B operand with the basis' k index permuted to the
+//   accumulator's row order; one LDS transpose sits between quantization and
+//   the inverse transform.
+// Lane maps (gfx950, i8 32x32x32, checked by nh_probe_mfma_i8 in the tests):
+//   A: lane l holds A[l&31][16(l>>5) + j], j = 0..15 (bytes of a 16-B operand)
+//   B: lane l holds B[16(l>>5) + j][l&31]
+//   C/D: register g of lane l is D[(g&3) + 8(g>>2) + 4(l>>5)][l&31]
+#include <hip/hip_runtime.h>
+#include "nh_common.hpp"
+#include "nh_internal.hpp"
+
+namespace nh {
+
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int crow(int g, int h) { return (g & 3) + 8 * (g >> 2) + 4 * h; }
+
+__device__ __forceinline__ v16i_t mfma(v4i_t a, v4i_t b) {
+    v16i_t z = {};
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, z, 0, 0, 0);
+}
+
+// Pack the low bytes of 16 int32 values into a 16-byte operand (byte j = v[j]).
+__device__ __forceinline__ v4i_t pack16(const int32_t* v) {
+    v4i_t r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        uint32_t lo = __builtin_amdgcn_perm((uint32_t)v[4 * q + 1], (uint32_t)v[4 * q], 0x0c0c0400u);
+        uint32_t hi = __builtin_amdgcn_perm((uint32_t)v[4 * q + 3], (uint32_t)v[4 * q + 2], 0x0c0c0400u);
+        r[q] = (int)(lo | (hi << 16));
+    }
+    return r;
+}
+
+// Split 16 values into int8 parts (NP = 2 or 3) and pack each part.
+template <int NP>
+__device__ __forceinline__ void split_pack(const int32_t* v, v4i_t* parts) {
+    int32_t t[16];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int32_t s = v[j] >> (7 * p);
+            t[j] = (p == NP - 1) ? s : (s & 127);
+        }
+        parts[p] = pack16(t);
+    }
+}
+
+// D = sum_p 128^p * (A_p . B)   (A from data parts)  or  (A . B_p)  (B from data parts)
+template <int NP, bool DATA_IS_A>
+__device__ __forceinline__ v16i_t mfma_parts(const v4i_t* parts, v4i_t c) {
+    v16i_t acc = DATA_IS_A ? mfma(parts[0], c) : mfma(c, parts[0]);
+#pragma unroll
+    for (int p = 1; p < NP; ++p) {
+        v16i_t x = DATA_IS_A ? mfma(parts[p], c) : mfma(c, parts[p]);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) acc[g] = (int)((uint32_t)acc[g] + ((uint32_t)x[g] << (7 * p)));
+    }
+    return acc;
+}
+
+template <bool DATA_IS_A>
+__device__ __forceinline__ v16i_t mfma_auto(const int32_t* v, v4i_t c) {
+    int32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) m = max(m, abs(v[j]));
+    v4i_t parts[3];
+    if (__any(m >= (1 << 14))) {   // wave-uniform: 3 parts only if some |v| >= 2^14
+        split_pack<3>(v, parts);
+        return mfma_parts<3, DATA_IS_A>(parts, c);
+    }
+    split_pack<2>(v, parts);
+    return mfma_parts<2, DATA_IS_A>(parts, c);
+}
+
+// int8 basis tables: T[k][n] = DCT32[k][n] and its transpose
+struct Basis {
+    int8_t t[32][32];
+    int8_t tt[32][32];
+};
+__constant__ Basis c_basis;
+
+static Basis make_basis() {
+    Basis b;
+    for (int k = 0; k < 32; ++k)
+        for (int n = 0; n < 32; ++n) {
+            b.t[k][n] = (int8_t)dct32(k, n);
+            b.tt[n][k] = (int8_t)dct32(k, n);
+        }
+    return b;
+}
+
+__device__ __forceinline__ v4i_t load_row16(const int8_t* row, int off) {
+    return *(const v4i_t*)(row + off);
+}
+__device__ __forceinline__ v4i_t load_perm16(const int8_t* row, int h) {
+    // bytes j = 0..15 of row[crow(j, h)]: four runs of 4 contiguous bytes
+    v4i_t r;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r[q] = *(const int*)(row + 8 * q + 4 * h);
+    return r;
+}
+
+__device__ __forceinline__ int32_t wrap16i(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+
+constexpr int kOP = 40;  // LDS row pitch (elements) of the per-wave tiles: 16-B aligned rows
+
+__global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ src, int w, int h, int pitch,
+                                                   int nbx, int nblk, QuantParams qp, int dq_scale, int dq_per,
+                                                   int32_t* lvl, int16_t* recon) {
+    __shared__ int16_t s_orig[4][32][kOP];
+    __shared__ int32_t s_dq[4][32][kOP];
+    __shared__ int16_t s_top[4][32], s_left[4][32];
+    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+    const int b = blockIdx.x * 4 + wv;
+    if (b >= nblk) return;                       // whole wave exits together
+    const int x0 = (b % nbx) * 32, y0 = (b / nbx) * 32;
+
+    // ---- load the block (2 x 16 B per lane) and its neighbours (block.py:38-50) ----
+    {
+        const int row = l >> 1, half = l & 1;
+        const int16_t* g = src + (int64_t)(y0 + row) * pitch + x0 + half * 16;
+        v4i_t a0 = *(const v4i_t*)g, a1 = *(const v4i_t*)(g + 8);
+        *(v4i_t*)&s_orig[wv][row][half * 16] = a0;
+        *(v4i_t*)&s_orig[wv][row][half * 16 + 8] = a1;
+        if (hh == 0) s_top[wv][r] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + r];
+        else s_left[wv][r] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + r) * pitch + x0 - 1];
+    }
+    // Each wave touches only its own LDS slices, and LDS executes one wave's
+    // instructions in order: a wave barrier (no s_barrier) orders write -> read.
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- DC (intra.py:46-62) and planar (intra.py:81-113) ----
+    const int32_t my_nb = hh == 0 ? s_top[wv][r] : s_left[wv][r];
+    int32_t s = my_nb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const int32_t dc = (s + 32) >> 6;
+    const int32_t tr = s_top[wv][31], bl = s_left[wv][31];
+    auto planar = [&](int y, int x) -> int32_t {
+        return ((31 - x) * s_left[wv][y] + (x + 1) * tr + (31 - y) * s_top[wv][x] + (y + 1) * bl + 32) >> 6;
+    };
+    // this lane's operand slice of the block: column j = r, rows k = 16hh .. 16hh+15
+    long long e_dc = 0, e_pl = 0;
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+        const int k = 16 * hh + jj;
+        const int32_t o = s_orig[wv][k][r];
+        const int32_t d1 = wrap16i(o - dc), d2 = wrap16i(o - planar(k, r));
+        e_dc += (long long)d1 * d1;
+        e_pl += (long long)d2 * d2;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        e_dc += __shfl_xor(e_dc, o, 64);
+        e_pl += __shfl_xor(e_pl, o, 64);
+    }
+    const bool use_dc = e_dc <= e_pl;                      // DC wins ties (__main__.py:173)
+    int32_t X[16];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+        const int k = 16 * hh + jj;
+        X[jj] = wrap16i((int32_t)s_orig[wv][k][r] - (use_dc ? dc : planar(k, r)));
+    }
+
+    // ---- forward pass 1: tempPre^T = X^T . T^T   (lane = i, registers = j) ----
+    const v4i_t F1 = load_row16(&c_basis.t[r][0], 16 * hh);     // B[k][i] = T[i][k]
+    v16i_t acc = mfma_auto<true>(X, F1);
+    int32_t V[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) V[g] = rshift_round<10>((uint32_t)acc[g]);   // transform.py:185
+    // ---- forward pass 2: coeff^T = T . temp^T  (B from the accumulator, k permuted) ----
+    const v4i_t F2 = load_perm16(&c_basis.t[r][0], hh);         // A[j][k] = T[j][k]
+    acc = mfma_auto<false>(V, F2);
+    // ---- quant / dequant, levels out (lane = row i, registers = columns crow(g)) ----
+    int32_t* lrow = lvl + (int64_t)(y0 + r) * pitch + x0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int32_t L4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int g = 4 * q + e;
+            L4[e] = quant_i32(rshift_round<10>((uint32_t)acc[g]), qp);
+            s_dq[wv][r][crow(g, hh)] = dequant_i32(L4[e], dq_scale, dq_per);
+        }
+        *(v4i_t*)(lrow + 8 * q + 4 * hh) = v4i_t{L4[0], L4[1], L4[2], L4[3]};
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- inverse pass 1: temp2^T = dq^T . T   (A = dq^T via the LDS transpose) ----
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) X[jj] = s_dq[wv][16 * hh + jj][r];
+    const v4i_t F3 = load_row16(&c_basis.tt[r][0], 16 * hh);    // B[k][i] = T[k][i]
+    acc = mfma_auto<true>(X, F3);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) V[g] = rshift_round<10>((uint32_t)acc[g]);   // transform.py:227
+    // ---- inverse pass 2: res^T = T^T . temp2^T ----
+    const v4i_t F4 = load_perm16(&c_basis.tt[r][0], hh);        // A[j][k] = T[k][j]
+    acc = mfma_auto<false>(V, F4);
+    // ---- reconstruct + clip (intra.py:70-78), recon out ----
+    int16_t* rrow = recon + (int64_t)(y0 + r) * pitch + x0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int16_t R4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int g = 4 * q + e, j = crow(g, hh);
+            const int32_t rr = wrap16i(rshift_round<10>((uint32_t)acc[g]));
+            int32_t rc = wrap16i((use_dc ? dc : planar(r, j)) + rr);
+            R4[e] = (int16_t)(rc < 0 ? 0 : (rc > 255 ? 255 : rc));
+        }
+        *(uint2*)(rrow + 8 * q + 4 * hh) =
+            make_uint2((uint16_t)R4[0] | ((uint32_t)(uint16_t)R4[1] << 16), (uint16_t)R4[2] | ((uint32_t)(uint16_t)R4[3] << 16));
+    }
+}
+
+// Probe: D = A . B for row-major int8 32x32 A, B using the assumed lane maps.
+__global__ void k_probe_mfma_i8(const int8_t* A, const int8_t* B, int32_t* D) {
+    const int l = threadIdx.x, r = l & 31, hh = l >> 5;
+    int32_t a[16], bb[16];
+    for (int j = 0; j < 16; ++j) {
+        a[j] = A[r * 32 + 16 * hh + j];
+        bb[j] = B[(16 * hh + j) * 32 + r];
+    }
+    v16i_t d = mfma(pack16(a), pack16(bb));
+    for (int g = 0; g < 16; ++g) D[crow(g, hh) * 32 + r] = d[g];
+}
+
+static bool g_basis_ready = false;
+static int ensure_basis(hipStream_t s) {
+    (void)s;
+    int dev = 0;
+    static int ready_dev = -1;
+    NH_HIP(hipGetDevice(&dev));
+    if (!g_basis_ready || ready_dev != dev) {
+        Basis b = make_basis();
+        NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis), &b, sizeof(b)));
+        g_basis_ready = true;
+        ready_dev = dev;
+    }
+    return NH_OK;
+}
+
+}  // namespace nh
+
+using namespace nh;
+
+// butterfly variant lives in nh_intraloop.hip
+namespace nh {
+int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
+                   hipStream_t s);
+}
+
+extern "C" int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl,
+                             int16_t* d_recon, int variant, void* stream) {
+    if (!d_src || !d_lvl || !d_recon || w < 0 || h < 0 || pitch < w) return NH_EARG;
+    if ((pitch & 7) || ((uintptr_t)d_src & 15) || ((uintptr_t)d_lvl & 15) || ((uintptr_t)d_recon & 15)) {
+        set_error("tc32: pitch must be a multiple of 8 and buffers 16-byte aligned");
+        return NH_EARG;
+    }
+    hipStream_t s = as_stream(stream);
+    const int nbx = w / 32, nblk = nbx * (h / 32);
+    if (!nblk) return NH_OK;
+    if (variant == 0) return tc32_butterfly(d_src, w, h, pitch, qp, d_lvl, d_recon, s);
+    if (variant != 1) return NH_EARG;
+    int rc = ensure_basis(s);
+    if (rc) return rc;
+    int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
+    const int per = q / 6, rem = q % 6;
+    QuantParams p;
+    p.shift = 14 + per + 5;
+    p.mf = quant_scale(rem);
+    p.off = (uint32_t)((1ull << p.shift) / 3);
+    k_tc32_mfma<<<(nblk + 3) / 4, 256, 0, s>>>(d_src, w, h, pitch, nbx, nblk, p, dequant_scale(rem), per, d_lvl,
+                                               d_recon);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream) {
+    if (!d_a || !d_b || !d_d) return NH_EARG;
+    k_probe_mfma_i8<<<1, 64, 0, as_stream(stream)>>>(d_a, d_b, d_d);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}

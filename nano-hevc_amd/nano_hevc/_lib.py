@@ -62,6 +62,8 @@ SIGNATURES = {
     "nh_intra_rdo_plane": ([P, I32, I32, I32, I32, P, P, P, P, VP], I32),
     "nh_tu_workspace_bytes": ([I32, I32, I32], I64),
     "nh_tu_pipeline_plane": ([P, I32, I32, I32, I32, I32, U32, I32, I32, I32, I32, P, P, P, P, VP], I32),
+    "nh_tc32_plane": ([P, I32, I32, I32, I32, P, P, I32, VP], I32),
+    "nh_probe_mfma_i8": ([P, P, P, VP], I32),
 }
 
 _lib = None

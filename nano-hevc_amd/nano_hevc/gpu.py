@@ -9,6 +9,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
   intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
+  tc32_plane          -- config 5: 32x32 chain, butterfly or int8-MFMA variant
 """
 from __future__ import annotations
 
@@ -170,3 +171,17 @@ def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_
                                  int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)), lvl.data_ptr(), rec.data_ptr(),
                                  tu.data_ptr(), work.data_ptr(), C.c_void_p(_stream(stream))), "tu_pipeline_plane")
     return lvl, rec, tu
+
+
+def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=None):
+    """Config 5 on one int16 plane (H, W), W % 8 == 0: every full
+    32x32 block through the chain.  variant 0 = butterfly, 1 = int8 MFMA.
+    Returns (levels int32 (H, W), recon int16 (H, W))."""
+    torch = _torch()
+    _need(src, torch.int16, "tc32_plane")
+    h, w = src.shape
+    lvl = torch.zeros((h, w), dtype=torch.int32, device=src.device) if lvl is None else lvl
+    rec = torch.zeros((h, w), dtype=torch.int16, device=src.device) if rec is None else rec
+    check(_lib.load().nh_tc32_plane(src.data_ptr(), w, h, w, int(qp), lvl.data_ptr(), rec.data_ptr(), int(variant),
+                                    C.c_void_p(_stream(stream))), "tc32_plane")
+    return lvl, rec

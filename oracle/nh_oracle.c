@@ -474,3 +474,13 @@ void oh_tu_pipeline_plane(const int16_t* src, int w, int h, int pitch, int ctb,
             tu_tree(src, w, h, pitch, cx * ctb, cy * ctb, ctb, plane_id, seed, qp, is_luma,
                     lvl, recon, tu_log2);
 }
+
+/* cfg 5: every full 32x32 block of a plane (block.py:68-74
+ * raster walk, partial blocks skipped) through the cfg-4 TU chain at N=32. */
+void oh_tc32_plane(const int16_t* src, int w, int h, int pitch, int qp, int32_t* lvl, int16_t* recon) {
+    int w4 = w / 4;
+    uint8_t* tmap = (uint8_t*)calloc((size_t)(h / 4 + 1) * (w4 + 1), 1);
+    for (int by = 0; by + 32 <= h; by += 32)
+        for (int bx = 0; bx + 32 <= w; bx += 32) tu_one(src, w, h, pitch, bx, by, 32, qp, 1, lvl, recon, tmap);
+    free(tmap);
+}

@@ -50,12 +50,13 @@ def lib():
             "oh_intra_rdo_plane": [P, i32, i32, i32, i32, P, P, P, P],
             "oh_tu_pipeline_plane": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P],
             "oh_tu_split": [C.c_uint32, i32, i32, i32, i32],
+            "oh_tc32_plane": [P, i32, i32, i32, i32, P, P],
         }
         for name, args in sig.items():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = None if name in ("oh_residual", "oh_reconstruct", "oh_clip", "oh_fwd8x8_quant_plane",
-                                         "oh_intra_rdo_plane", "oh_tu_pipeline_plane") else C.c_int
+                                         "oh_intra_rdo_plane", "oh_tu_pipeline_plane", "oh_tc32_plane") else C.c_int
         _lib = L
     return _lib
 
@@ -198,3 +199,12 @@ def tu_pipeline_plane(src, ctb, plane_id, seed, qp, is_luma, row0=0, row1=1 << 3
 
 def tu_split(seed, plane_id, x, y, size):
     return bool(lib().oh_tu_split(seed, plane_id, x, y, size))
+
+
+def tc32_plane(src, qp=32):
+    src = np.ascontiguousarray(src, np.int16)
+    h, w = src.shape
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    lib().oh_tc32_plane(_p(src), w, h, w, int(qp), _p(lvl), _p(rec))
+    return lvl, rec

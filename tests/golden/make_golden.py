@@ -323,6 +323,33 @@ def gen_planes(I, T, Q, rng):
     return out
 
 
+def gen_cfg5(I, T, Q, M):
+    """cfg 5: every full 32x32 block through the cfg-4 chain,
+    plus the reference's Y-PSNR of the reconstruction (metrics.psnr)."""
+    rng = np.random.default_rng(555)
+    yy, xx = np.mgrid[0:72, 0:104]
+    src = np.clip(110 + 2 * xx - yy + rng.integers(-30, 31, size=xx.shape), 0, 255).astype(np.int16)
+    out = {"p5_src": src}
+    for qp in (22, 37):
+        lvl = np.zeros(src.shape, np.int32)
+        rec = np.zeros(src.shape, np.int16)
+        for by in range(0, src.shape[0] - 31, 32):
+            for bx in range(0, src.shape[1] - 31, 32):
+                orig = src[by:by + 32, bx:bx + 32]
+                top, left, _ = _neighbors(src, bx, by, 32)
+                dc = I.intra_dc_predict(top, left, 32)
+                pl = I.intra_planar_predict(top, left, int(top[-1]), int(left[-1]), 32)
+                edc = int(np.sum(I.residual_block(orig, dc).astype(np.int64) ** 2))
+                epl = int(np.sum(I.residual_block(orig, pl).astype(np.int64) ** 2))
+                l, r, _ = _chain(I, T, Q, orig, dc if edc <= epl else pl, qp, False)
+                lvl[by:by + 32, bx:bx + 32] = l
+                rec[by:by + 32, bx:bx + 32] = r
+        h32, w32 = 64, 96
+        out[f"p5_lvl_qp{qp}"], out[f"p5_rec_qp{qp}"] = lvl, rec
+        out[f"p5_psnr_qp{qp}"] = np.float64(M.psnr(src[:h32, :w32].astype(np.uint8), rec[:h32, :w32].astype(np.uint8)))
+    return out
+
+
 def gen_metrics(M):
     """metrics.py:7-48 on seeded integer samples (its own rng: other fixtures unchanged)."""
     rng = np.random.default_rng(4321)
@@ -374,6 +401,7 @@ def main():
         "chain.npz": gen_chain(I, T, Q),
         "planes.npz": gen_planes(I, T, Q, rng),
         "metrics.npz": gen_metrics(M),
+        "cfg5.npz": gen_cfg5(I, T, Q, M),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

@@ -387,3 +387,71 @@ def test_sse_i16_device(nh, torch_dev):
     _lib.check(_lib.load().nh_sse_i16(da.data_ptr(), db.data_ptr(), a.size, out.data_ptr(),
                                       C.c_void_p(torch.cuda.current_stream().cuda_stream)))
     assert int(out.item()) == int(np.sum((a.astype(np.int64) - b) ** 2))
+
+
+# ------------------------------------------------------------------ config 5 (32x32, MFMA vs butterfly)
+
+def test_probe_mfma_i8_lane_maps(nh, torch_dev):
+    """The i8 32x32x32 operand/accumulator lane maps the config-5 kernel relies on,
+    checked with exact integer data and an asymmetric B."""
+    torch = torch_dev
+    from nano_hevc import _lib
+    import ctypes as C
+    rng = np.random.default_rng(8)
+    a = rng.integers(-128, 128, size=(32, 32)).astype(np.int8)
+    b = rng.integers(-128, 128, size=(32, 32)).astype(np.int8)
+    b[0, :] = np.arange(32)          # asymmetric rows/cols
+    da, db = torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()
+    dd = torch.zeros((32, 32), dtype=torch.int32, device="cuda")
+    _lib.check(_lib.load().nh_probe_mfma_i8(da.data_ptr(), db.data_ptr(), dd.data_ptr(),
+                                            C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    assert np.array_equal(dd.cpu().numpy(), a.astype(np.int32) @ b.astype(np.int32))
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_tc32_golden(nh, torch_dev, golden, variant):
+    """Config 5 vs the reference-composed golden plane, incl. the reference's Y-PSNR."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    g = golden("cfg5.npz")
+    src = g["p5_src"]
+    for qp in (22, 37):
+        l, r = gpu.tc32_plane(torch.from_numpy(src).cuda(), qp, variant)
+        l, r = l.cpu().numpy(), r.cpu().numpy()
+        assert np.array_equal(l, g[f"p5_lvl_qp{qp}"]) and np.array_equal(r, g[f"p5_rec_qp{qp}"]), qp
+        assert nh.psnr(src[:64, :96].astype(np.uint8), r[:64, :96].astype(np.uint8)) == g[f"p5_psnr_qp{qp}"]
+
+
+@pytest.mark.parametrize("kind", ["natural", "noise", "int16"])
+def test_tc32_mfma_equals_butterfly_and_oracle(nh, torch_dev, kind):
+    """int16-extreme planes force the 3-part int8 split in every MFMA stage."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(len(kind))
+    h, w = 96, 160
+    if kind == "natural":
+        yy, xx = np.mgrid[0:h, 0:w]
+        src = np.clip(60 + xx + yy // 2 + rng.integers(-15, 16, size=xx.shape), 0, 255).astype(np.int16)
+    elif kind == "noise":
+        src = rng.integers(0, 256, size=(h, w)).astype(np.int16)
+    else:
+        src = rng.integers(-32768, 32768, size=(h, w)).astype(np.int16)
+    d = torch.from_numpy(src).cuda()
+    for qp in (0, 30, 51):
+        el, er = O.tc32_plane(src, qp)
+        for v in (0, 1):
+            l, r = gpu.tc32_plane(d, qp, v)
+            assert np.array_equal(l.cpu().numpy(), el), (kind, qp, v)
+            assert np.array_equal(r.cpu().numpy(), er), (kind, qp, v)
+
+
+def test_tu_pipeline_int16_extremes(nh, torch_dev):
+    """Config 4 on arbitrary int16 samples: the 24-bit mad bounds hold at every TU size."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(31)
+    src = rng.integers(-32768, 32768, size=(96, 128)).astype(np.int16)
+    for luma, ctb in ((True, 32), (False, 16)):
+        l, r, t = gpu.tu_pipeline_plane(torch.from_numpy(src).cuda(), ctb, int(not luma), 5, 3, luma)
+        el, er, et = O.tu_pipeline_plane(src, ctb, int(not luma), 5, 3, luma)
+        assert np.array_equal(l.cpu().numpy(), el) and np.array_equal(r.cpu().numpy(), er)

@@ -187,3 +187,10 @@ def test_manifest_integrity():
     assert "metrics.npz" in man["files"]
     for name, h in man["files"].items():
         assert hashlib.sha256(open(os.path.join(GOLDEN, name), "rb").read()).hexdigest() == h, name
+
+
+def test_cfg5_plane(golden):
+    g = golden("cfg5.npz")
+    for qp in (22, 37):
+        l, r = O.tc32_plane(g["p5_src"], qp)
+        assert np.array_equal(l, g[f"p5_lvl_qp{qp}"]) and np.array_equal(r, g[f"p5_rec_qp{qp}"]), qp
