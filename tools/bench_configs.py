@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Throughput of the non-headline configs (BASELINE.json configs[2..4]) on one MI355X.
+
+  cfg3  1080p YUV420, 35-mode RDO per 8x8 block (pred+residual+DCT+quant+recon)
+  cfg4  4K YUV420, mixed 4/8/16/32 TUs per CTU (plan + per-size chains)
+  cfg5  8K YUV420, every 32x32 block through the chain: butterfly vs int8-MFMA,
+        plus the frame's Y-PSNR (metrics.psnr semantics) for both variants and,
+        with --check, the oracle's PSNR on the same frame.
+
+Synthetic 8-bit content (gradient + seeded noise) resident in HBM; HIP events
+on the launch stream; one JSON line per config.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "nano-hevc_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def synth_plane(h, w, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    yy = torch.arange(h, device="cuda").view(h, 1)
+    xx = torch.arange(w, device="cuda").view(1, w)
+    base = (40 + (xx * 3 + yy * 2) % 160 + (xx // 97) * 7) % 256
+    noise = torch.randint(-12, 13, (h, w), device="cuda", generator=g)
+    return torch.clamp(base + noise, 0, 255).to(torch.int16).contiguous()
+
+
+def timed(fn, reps):
+    st = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in evs:
+        a.record(st)
+        fn()
+        b.record(st)
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in evs)
+    return ts[len(ts) // 2]
+
+
+def psnr_dev(a, b, peak=255):
+    from nano_hevc import _lib
+    import ctypes as C
+    out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    _lib.check(_lib.load().nh_sse_i16(a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(),
+                                      C.c_void_p(torch.cuda.current_stream().cuda_stream)))
+    mse = float(np.float64(int(out.item())) / np.float64(a.numel()))
+    return float("inf") if mse == 0 else float(10 * np.log10(peak ** 2 / mse))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--qp", type=int, default=32)
+    ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
+    ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
+    ap.add_argument("--configs", default="3,4,5")
+    args = ap.parse_args()
+    from nano_hevc import gpu, _lib
+    _lib.load()
+    torch.cuda.set_device(0)
+    cfgs = {int(c) for c in args.configs.split(",")}
+
+    if 3 in cfgs:
+        W, H = 1920, 1080
+        planes = [synth_plane(H, W, 1), synth_plane(H // 2, W // 2, 2), synth_plane(H // 2, W // 2, 3)]
+        nblk = sum((p.shape[0] // 8) * (p.shape[1] // 8) for p in planes)
+        ms = timed(lambda: [gpu.intra_rdo_plane(p, args.qp) for p in planes], args.reps)
+        print(json.dumps({"config": "cfg3 1080p YUV420 35-mode RDO per 8x8 (pred+res+DCT+Q+DQ+IDCT+recon+SSE)",
+                          "ms_per_frame": ms, "frames_per_s": 1e3 / ms, "blocks_per_frame": nblk,
+                          "blocks_per_s": nblk / ms * 1e3, "mode_evals_per_s": 35 * nblk / ms * 1e3,
+                          "bound": "valu (~3.3k int ops per block-mode)"}), flush=True)
+
+    if 4 in cfgs:
+        W, H = 3840, 2160
+        planes = [(synth_plane(H, W, 4), 32, 0, True), (synth_plane(H // 2, W // 2, 5), 16, 1, False),
+                  (synth_plane(H // 2, W // 2, 6), 16, 2, False)]
+        bufs = []
+        L = _lib.load()
+        for p, ctb, pid, luma in planes:
+            h, w = p.shape
+            bufs.append((torch.zeros((h, w), dtype=torch.int32, device="cuda"),
+                         torch.zeros((h, w), dtype=torch.int16, device="cuda"),
+                         torch.zeros((h // 4, w // 4), dtype=torch.uint8, device="cuda"),
+                         torch.empty(int(L.nh_tu_workspace_bytes(w, h, ctb)), dtype=torch.uint8, device="cuda")))
+
+        def run4():
+            for (p, ctb, pid, luma), (lv, rc, tu, wk) in zip(planes, bufs):
+                gpu.tu_pipeline_plane(p, ctb, pid, 1234, args.qp, luma, lvl=lv, rec=rc, tu=tu, work=wk)
+        ms = timed(run4, args.reps)
+        samples = sum(p.numel() for p, *_ in planes)
+        hist = {}
+        for (p, *_), (lv, rc, tu, wk) in zip(planes, bufs):
+            for lg in (2, 3, 4, 5):
+                hist[1 << lg] = hist.get(1 << lg, 0) + int((tu == lg).sum().item()) * 16
+        print(json.dumps({"config": "cfg4 4K YUV420 mixed 4/8/16/32 TUs per CTU (DC/planar + full chain)",
+                          "ms_per_frame": ms, "frames_per_s": 1e3 / ms, "samples_per_s": samples / ms * 1e3,
+                          "samples_by_tu_size": hist, "psnr_y": psnr_dev(planes[0][0], bufs[0][1])}), flush=True)
+
+    if 5 in cfgs:
+        W, H = 7680, 4320
+        planes = [synth_plane(H, W, 7), synth_plane(H // 2, W // 2, 8), synth_plane(H // 2, W // 2, 9)]
+        nblk = sum((p.shape[0] // 32) * (p.shape[1] // 32) for p in planes)
+        outs = [(torch.zeros(p.shape, dtype=torch.int32, device="cuda"),
+                 torch.zeros(p.shape, dtype=torch.int16, device="cuda")) for p in planes]
+        res = {}
+        for v, name in ((0, "butterfly"), (1, "mfma_i8")):
+            ms = timed(lambda: [gpu.tc32_plane(p, args.qp5, v, lvl=o[0], rec=o[1]) for p, o in zip(planes, outs)],
+                       args.reps)
+            res[name] = {"ms_per_frame": ms, "blocks_per_s": nblk / ms * 1e3,
+                         "samples_per_s": sum(p.numel() for p in planes) / ms * 1e3,
+                         "psnr_y": psnr_dev(planes[0], outs[0][1])}
+            lv = outs[0][0].to(torch.int64).flatten()
+            wts = torch.arange(1, lv.numel() + 1, device="cuda", dtype=torch.int64) % 1000003
+            res[name]["levels_checksum"] = int(torch.sum(lv * wts).item())
+            res[name]["nonzero_levels_y"] = int(torch.count_nonzero(lv).item())
+        line = {"config": "cfg5 8K YUV420, every 32x32 block through the chain: butterfly vs int8 MFMA",
+                "blocks_per_frame": nblk, **res,
+                "qp": args.qp5,
+                "variants_identical": res["butterfly"]["levels_checksum"] == res["mfma_i8"]["levels_checksum"]
+                and res["butterfly"]["psnr_y"] == res["mfma_i8"]["psnr_y"]}
+        if args.check:
+            from oracle import oracle as O   # checker only
+            y = planes[0].cpu().numpy()
+            t0 = time.perf_counter()
+            _, er = O.tc32_plane(y, args.qp5)
+            line["oracle_seconds_luma"] = time.perf_counter() - t0
+            d = y.astype(np.float64) - er.astype(np.float64)
+            mse = float(np.mean(d ** 2))
+            line["psnr_y_oracle"] = float(10 * np.log10(255 ** 2 / mse))
+            line["psnr_matches_oracle"] = line["psnr_y_oracle"] == res["mfma_i8"]["psnr_y"]
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
