@@ -126,6 +126,10 @@ int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const n
  * ceiling for that pattern.  policy: as the variant's cache policy (0..3). */
 int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, const nh_plane_set* sets, int nsets,
                             int policy, void* stream);
+/* Measurement helper: plain linear 16-B-per-lane streaming copy of nelems
+ * (multiple of 8) int16 (grid <= 0: one chunk per thread, else grid-stride). */
+int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t nelems, int policy, int grid,
+                         void* stream);
 
 /* nblocks contiguous size x size int32 blocks (row-major) */
 int nh_fwd_transform_batch(const int32_t* d_in, int32_t* d_out, int64_t nblocks, int size,

@@ -405,10 +405,19 @@ __global__ void k_estimate_bits(const int64_t* l, int64_t n, int bits, double* o
 // ---------------------------------------------------------------------------
 // quality metrics (metrics.py:7-48) as device reductions
 // ---------------------------------------------------------------------------
+// Workgroup reduction (256 threads) then ONE atomic per workgroup: an atomic
+// per wave on one word serialises (~90 adds/us per address).
 template <class T, class F>
 __device__ __forceinline__ void block_reduce_add(T v, unsigned long long* out, F) {
+    __shared__ unsigned long long part[4];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
-    if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, (unsigned long long)v);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = (unsigned long long)v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long s = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); ++k) s += part[k];
+        if (s) atomicAdd(out, s);
+    }
 }
 struct NoOp {};
 // sum((a-b)^2) exactly in int64 (inputs are <= 16-bit samples widened by the shim)
@@ -469,7 +478,9 @@ __global__ void k_sse_i16(const int16_t* a, const int16_t* b, int64_t n, unsigne
     block_reduce_add(s, out, NoOp{});
 }
 
-static unsigned grid_for(int64_t n, int64_t cap = 8192) {
+static unsigned grid_for(int64_t n, int64_t cap = 8192);
+static unsigned grid_red(int64_t n) { return grid_for(n, 1024); }
+static unsigned grid_for(int64_t n, int64_t cap) {
     int64_t g = (n + 255) / 256;
     if (g < 1) g = 1;
     if (g > cap) g = cap;
@@ -671,7 +682,7 @@ int nh_count_nonzero(const int64_t* level, int64_t n, int64_t* count) {
     NH_TRY(staging_upload(S, oi, level, n * 8));
     char* d = (char*)S.dbuf;
     NH_HIP(hipMemsetAsync(d + oc, 0, 8, S.stream));
-    if (n) k_count_nonzero<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oi), n, (unsigned long long*)(d + oc));
+    if (n) k_count_nonzero<<<grid_red(n), 256, 0, S.stream>>>((int64_t*)(d + oi), n, (unsigned long long*)(d + oc));
     return finish_copy(S, count, oc, 8);
 }
 
@@ -732,10 +743,10 @@ static int reduce_call(const void* a, size_t abytes, const void* b, size_t bbyte
     char* d = (char*)S.dbuf;
     NH_HIP(hipMemsetAsync(d + oc, 0, 8, S.stream));
     unsigned long long* o = (unsigned long long*)(d + oc);
-    if (which == 0 && n) k_sum_sq_diff<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oa), (int64_t*)(d + ob), n, o);
-    if (which == 1 && n) k_sad_i32<<<grid_for(n), 256, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), n, o);
+    if (which == 0 && n) k_sum_sq_diff<<<grid_red(n), 256, 0, S.stream>>>((int64_t*)(d + oa), (int64_t*)(d + ob), n, o);
+    if (which == 1 && n) k_sad_i32<<<grid_red(n), 256, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), n, o);
     if (which == 2) k_satd_4x4<<<1, 64, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), (long long*)o);
-    if (which == 3 && n) k_residual_energy<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oa), n, o);
+    if (which == 3 && n) k_residual_energy<<<grid_red(n), 256, 0, S.stream>>>((int64_t*)(d + oa), n, o);
     return finish_copy(S, out, oc, 8);
 }
 int nh_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, int64_t* out) {
@@ -753,7 +764,7 @@ int nh_residual_energy(const int64_t* r, int64_t n, int64_t* out) {
 }
 int nh_sse_i16(const int16_t* d_a, const int16_t* d_b, int64_t n, int64_t* d_out, void* stream) {
     if (!d_a || !d_b || !d_out || n < 0) return NH_EARG;
-    if (n) k_sse_i16<<<grid_for(n), 256, 0, as_stream(stream)>>>(d_a, d_b, n, (unsigned long long*)d_out);
+    if (n) k_sse_i16<<<grid_red(n), 256, 0, as_stream(stream)>>>(d_a, d_b, n, (unsigned long long*)d_out);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

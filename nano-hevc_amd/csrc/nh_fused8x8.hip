@@ -155,6 +155,16 @@ __global__ void __launch_bounds__(256) k_probe_copy8x8(Fused8Args a) {
     for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, raw[i]);
 }
 
+// Memory-only probe: plain linear streaming copy of n 16-B chunks (grid-stride),
+// the HBM ceiling this device reaches with the simplest possible pattern.
+template <int POLICY>
+__global__ void __launch_bounds__(256) k_probe_linear(const int16_t* __restrict__ in, int16_t* __restrict__ out,
+                                                     int64_t nchunks) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks; i += stride)
+        st16<POLICY>(out + i * 8, ld16<POLICY>(in + i * 8));
+}
+
 static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
                       int is_intra, Fused8Args& a, uint32_t& total_wg) {
     if (!d_res || !d_lvl || !sets || nsets < 1 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
@@ -255,6 +265,24 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
         case 1: k_probe_copy8x8<1><<<wg, 256, 0, s>>>(a); break;
         case 2: k_probe_copy8x8<2><<<wg, 256, 0, s>>>(a); break;
         default: k_probe_copy8x8<3><<<wg, 256, 0, s>>>(a); break;
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t nelems, int policy, int grid,
+                                    void* stream) {
+    if (!d_in || !d_out || nelems < 0 || (nelems & 7) || policy < 0 || policy > 3) return NH_EARG;
+    hipStream_t s = as_stream(stream);
+    const int64_t chunks = nelems / 8;
+    int64_t g = grid > 0 ? grid : (chunks + 255) / 256;
+    if (g > (1 << 30)) g = 1 << 30;
+    if (!chunks) return NH_OK;
+    switch (policy) {
+        case 0: k_probe_linear<0><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
+        case 1: k_probe_linear<1><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
+        case 2: k_probe_linear<2><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
+        default: k_probe_linear<3><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
     }
     NH_HIP(hipGetLastError());
     return NH_OK;

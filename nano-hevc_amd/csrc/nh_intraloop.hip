@@ -246,31 +246,45 @@ struct TuLists {
     uint32_t cap[4];
 };
 
-__global__ void k_tu_plan(int w, int h, int ctb, int plane_id, uint32_t seed, int row0, int row1, TuLists tl) {
-    const int ctb_w = (w + ctb - 1) / ctb;
-    const int n = (row1 - row0) * ctb_w;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int cy = row0 + i / ctb_w, cx = i % ctb_w;
-    int sx[16], sy[16], ss[16], sp = 0;
-    sx[0] = cx * ctb; sy[0] = cy * ctb; ss[0] = ctb; sp = 1;
-    while (sp) {
-        --sp;
-        const int x = sx[sp], y = sy[sp], s = ss[sp];
-        if (x >= w || y >= h) continue;
-        const bool over = (x + s > w) || (y + s > h);
-        if (s > 4 && (over || tu_split(seed, plane_id, x, y, s))) {
-            const int hs = s / 2;   // push in reverse so pops follow Z order (order is irrelevant)
-            sx[sp] = x + hs; sy[sp] = y + hs; ss[sp++] = hs;
-            sx[sp] = x;      sy[sp] = y + hs; ss[sp++] = hs;
-            sx[sp] = x + hs; sy[sp] = y;      ss[sp++] = hs;
-            sx[sp] = x;      sy[sp] = y;      ss[sp++] = hs;
-            continue;
+// One thread per 4x4 unit of the band: descend the seeded quadtree of the unit's
+// CTB (<= 3 hash evaluations) to the leaf that contains the unit; the unit at the
+// leaf's top-left emits the TU, every unit writes its entry of the TU-size map.
+// Emission: per size a wave ballot + ONE atomic per wave (a per-TU atomic on 4
+// shared counters serialises at ~90 adds/us per word).  List order is
+// irrelevant: every TU writes only its own samples.
+__global__ void __launch_bounds__(256) k_tu_plan(int w, int h, int ctb, int plane_id, uint32_t seed, int row0,
+                                                 int row1, TuLists tl, uint8_t* tu_log2) {
+    const int w4 = w / 4;
+    const int y4_0 = row0 * ctb / 4, y4_1 = min(row1 * ctb, h) / 4;
+    const int64_t n = (int64_t)(y4_1 - y4_0) * w4;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = i < n;
+    int ux = 0, uy = 0, c = -1;
+    if (act) {
+        ux = (int)(i % w4) * 4;
+        uy = (y4_0 + (int)(i / w4)) * 4;
+        int s = ctb, x = (ux / ctb) * ctb, y = (uy / ctb) * ctb;
+        while (s > 4 && ((x + s > w) || (y + s > h) || tu_split(seed, plane_id, x, y, s))) {
+            s >>= 1;
+            x += (ux >= x + s) ? s : 0;
+            y += (uy >= y + s) ? s : 0;
         }
-        if (over) continue;
-        const int c = s == 4 ? 0 : s == 8 ? 1 : s == 16 ? 2 : 3;
-        const uint32_t slot = atomicAdd(&tl.count[c], 1u);
-        if (slot < tl.cap[c]) tl.list[c][slot] = ((uint32_t)y << 16) | (uint32_t)x;
+        const int lg = s == 4 ? 2 : s == 8 ? 3 : s == 16 ? 4 : 5;
+        tu_log2[(int64_t)(uy / 4) * w4 + ux / 4] = (uint8_t)lg;
+        if (ux == x && uy == y) c = lg - 2;
+    }
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const unsigned long long m = __ballot(c == k);
+        if (!m) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&tl.count[k], (uint32_t)__popcll(m));
+        base = __shfl(base, 0, 64);
+        if (c == k) {
+            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+            if (slot < tl.cap[k]) tl.list[k][slot] = ((uint32_t)uy << 16) | (uint32_t)ux;
+        }
     }
 }
 
@@ -397,10 +411,6 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
             int32_t rc = wrap16(pred_at(t, j) + rr);
             rrow[j] = (int16_t)(rc < 0 ? 0 : (rc > 255 ? 255 : rc));
         }
-        if (!GRID && t < N / 4) {
-            const int w4 = w / 4;
-            for (int j = 0; j < N / 4; ++j) tu_log2[(int64_t)(y0 / 4 + t) * w4 + x0 / 4 + j] = (uint8_t)Log2<N>::v;
-        }
     }
 }
 
@@ -479,8 +489,8 @@ extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitc
         p += align_up((size_t)tl.cap[c] * 4, 256);
     }
     NH_HIP(hipMemsetAsync(tl.count, 0, 16, s));
-    const int nctb = (row1 - row0) * ((w + ctb - 1) / ctb);
-    k_tu_plan<<<(nctb + 63) / 64, 64, 0, s>>>(w, h, ctb, plane_id, seed, row0, row1, tl);
+    const int64_t nunits = (int64_t)((min(row1 * ctb, h) - row0 * ctb) / 4) * (w / 4);
+    k_tu_plan<<<(unsigned)((nunits + 255) / 256), 256, 0, s>>>(w, h, ctb, plane_id, seed, row0, row1, tl, d_tu);
     NH_HIP(hipGetLastError());
     int per, rem;
     qp_split(qp, &per, &rem);

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="0,1,2,3,4,5,6,7")
+    ap.add_argument("--variants", default="1,5")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     L = _lib.load()
@@ -48,13 +48,18 @@ def main():
         o = outs[name]   # preallocated: nothing but the measured kernel runs in the timed region
         if name == "torch_copy":
             o.copy_(res)
+        elif name.startswith("linear"):
+            pol, grid = name[6:].split("g")
+            _lib.check(L.nh_probe_copy_linear(res.data_ptr(), o.data_ptr(), res.numel() // 8 * 8, int(pol), int(grid),
+                                              C.c_void_p(st.cuda_stream)))
         elif name.startswith("probe"):
             _lib.check(L.nh_probe_copy8x8_planes(res.data_ptr(), o.data_ptr(), arr, len(sets), int(name[5:]),
                                                  C.c_void_p(st.cuda_stream)))
         else:
             gpu.fwd8x8_quant(res, sets, 32, True, out=o, variant=int(name[1:]), stream=st)
 
-    names = ["torch_copy"] + [f"probe{p}" for p in range(4)] + [f"v{v}" for v in variants]
+    names = (["torch_copy"] + [f"probe{p}" for p in range(4)] + [f"linear{p}g{g}" for p in (0, 1) for g in (0, 4096)]
+             + [f"v{v}" for v in variants])
     for n in names:
         outs[n] = torch.zeros_like(res)
     times = {n: [] for n in names}
