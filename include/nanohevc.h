@@ -157,7 +157,8 @@ int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch, int qp,
  * [row0, row1): seeded quadtree per CTB (ctb 32 luma / 16
  * chroma), per TU the __main__.py:165-178 DC-vs-planar choice then the full
  * reconstruction chain (DST for 4x4 luma).  d_tu: (h/4)*(w/4) u8 log2 TU size;
- * d_work: nh_tu_workspace_bytes(w, h, ctb) bytes of device scratch. */
+ * d_work: nh_tu_workspace_bytes(w, h, ctb) bytes of device scratch (currently
+ * 0: TUs are found by per-size grid walks; NULL accepted). */
 int64_t nh_tu_workspace_bytes(int w, int h, int ctb);
 int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb, int plane_id,
                          uint32_t seed, int qp, int is_luma, int row0, int row1,

@@ -220,10 +220,10 @@ __global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ 
 
 // ===========================================================================
 // Config 4: mixed 4/8/16/32 TU pipeline.
-//   k_tu_plan    : one thread per CTB walks the seeded quadtree and appends its
-//                  leaves to one list per TU size (order irrelevant: every TU
-//                  writes only its own samples).
-//   k_tu_process : N threads per TU (thread t = column t, then row t), LDS tiles;
+//   tu_leaf      : the seeded quadtree's leaf containing a sample (<= 3 hashes);
+//   k_tu_process : one launch per TU size over the N-aligned positions of the
+//                  band, keeping the positions whose leaf is NxN; N threads per
+//                  TU (thread t = column t, then row t), LDS tiles;
 //                  DC-vs-planar open-loop choice (__main__.py:165-178), then the
 //                  full residual -> transform -> quant -> dequant -> inverse ->
 //                  recon chain with exact int32/int64 arithmetic.
@@ -240,66 +240,38 @@ __device__ __forceinline__ bool tu_split(uint32_t seed, int plane_id, int x, int
     return (k & 3u) < 2u;
 }
 
-struct TuLists {
-    uint32_t* count;     // [4] for sizes 4, 8, 16, 32
-    uint32_t* list[4];   // packed (y << 16) | x
-    uint32_t cap[4];
-};
-
-// One thread per 4x4 unit of the band: descend the seeded quadtree of the unit's
-// CTB (<= 3 hash evaluations) to the leaf that contains the unit; the unit at the
-// leaf's top-left emits the TU, every unit writes its entry of the TU-size map.
-// Emission: per size a wave ballot + ONE atomic per wave (a per-TU atomic on 4
-// shared counters serialises at ~90 adds/us per word).  List order is
-// irrelevant: every TU writes only its own samples.
-__global__ void __launch_bounds__(256) k_tu_plan(int w, int h, int ctb, int plane_id, uint32_t seed, int row0,
-                                                 int row1, TuLists tl, uint8_t* tu_log2) {
-    const int w4 = w / 4;
-    const int y4_0 = row0 * ctb / 4, y4_1 = min(row1 * ctb, h) / 4;
-    const int64_t n = (int64_t)(y4_1 - y4_0) * w4;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool act = i < n;
-    int ux = 0, uy = 0, c = -1;
-    if (act) {
-        ux = (int)(i % w4) * 4;
-        uy = (y4_0 + (int)(i / w4)) * 4;
-        int s = ctb, x = (ux / ctb) * ctb, y = (uy / ctb) * ctb;
-        while (s > 4 && ((x + s > w) || (y + s > h) || tu_split(seed, plane_id, x, y, s))) {
-            s >>= 1;
-            x += (ux >= x + s) ? s : 0;
-            y += (uy >= y + s) ? s : 0;
-        }
-        const int lg = s == 4 ? 2 : s == 8 ? 3 : s == 16 ? 4 : 5;
-        tu_log2[(int64_t)(uy / 4) * w4 + ux / 4] = (uint8_t)lg;
-        if (ux == x && uy == y) c = lg - 2;
+// Leaf of the seeded quadtree containing sample (ux, uy):
+// descend from the CTB root, at most 3 hash evaluations.  Returns its size.
+__device__ __forceinline__ int tu_leaf(int w, int h, int ctb, int plane_id, uint32_t seed, int ux, int uy) {
+    int s = ctb, x = (ux / ctb) * ctb, y = (uy / ctb) * ctb;
+    while (s > 4 && ((x + s > w) || (y + s > h) || tu_split(seed, plane_id, x, y, s))) {
+        s >>= 1;
+        x += (ux >= x + s) ? s : 0;
+        y += (uy >= y + s) ? s : 0;
     }
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const unsigned long long m = __ballot(c == k);
-        if (!m) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&tl.count[k], (uint32_t)__popcll(m));
-        base = __shfl(base, 0, 64);
-        if (c == k) {
-            const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-            if (slot < tl.cap[k]) tl.list[k][slot] = ((uint32_t)uy << 16) | (uint32_t)ux;
-        }
-    }
+    return s;
 }
 
-// GRID mode (config 5): TU idx is the idx-th full NxN block of the plane in
-// raster order (grid_bw blocks per row, grid_n blocks), no list, no TU map.
+// MODE kAll (config 5): TU idx is the idx-th full NxN block of the plane in
+// raster order (grid_bw blocks per row, grid_n blocks), no TU map.
+// MODE kTree (config 4): idx walks the N-aligned positions of CTU rows
+// [row0, row1); a position is a TU iff its quadtree leaf is exactly NxN
+// (tu_leaf) -- no lists, no atomics, deterministic; the TU writes its map.
 // Multiplies are 24-bit (v_mad_i32_i24): exact for the whole chain because the
 // residual is int16 (forward operands < 2^21), dequantized coefficients are
 // ~|c|*2^20/2^(17+log2N) < 2^19, and inverse pass-2 operands are a >> S of an
 // int32 sum bounded by 2^27 -> < 2^21.
-template <int N, bool DST, bool GRID = false>
+enum { kAll = 0, kTree = 1 };
+struct TreeArgs {
+    int ctb, plane_id, y_base;   // y_base: first sample row of the band
+    uint32_t seed;
+};
+
+template <int N, bool DST, int MODE>
 __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ src, int w, int h, int pitch,
-                                                    const uint32_t* __restrict__ list, const uint32_t* count,
                                                     QuantParams qp, int dq_scale, int dq_per, int32_t* lvl,
-                                                    int16_t* recon, uint8_t* tu_log2, int grid_bw = 0,
-                                                    int grid_n = 0) {
+                                                    int16_t* recon, uint8_t* tu_log2, int grid_bw, int grid_n,
+                                                    TreeArgs ta) {
     constexpr int G = 256 / N;            // TUs per workgroup
     constexpr int P = N + 1;              // padded LDS row
     constexpr int S = Log2<N>::v + 5;
@@ -309,17 +281,15 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     __shared__ long long e_dc[G][N], e_pl[G][N];
     const int g = threadIdx.x / N, t = threadIdx.x % N;
     const uint32_t idx = blockIdx.x * G + g;
-    const bool active = GRID ? idx < (uint32_t)grid_n : idx < *count;
+    bool active = idx < (uint32_t)grid_n;
     int x0 = 0, y0 = 0;
     if (active) {
-        if constexpr (GRID) {
-            x0 = (idx % grid_bw) * N;
-            y0 = (idx / grid_bw) * N;
-        } else {
-            const uint32_t e = list[idx];
-            x0 = e & 0xffff;
-            y0 = e >> 16;
-        }
+        x0 = (idx % grid_bw) * N;
+        y0 = (idx / grid_bw) * N + (MODE == kTree ? ta.y_base : 0);
+        if constexpr (MODE == kTree)
+            active = (x0 + N <= w) && (y0 + N <= h) && tu_leaf(w, h, ta.ctb, ta.plane_id, ta.seed, x0, y0) == N;
+    }
+    if (active) {
         // neighbours (block.py:38-50): count N, 128 outside the plane (full TUs: no truncation)
         topv[g][t] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + t];
         leftv[g][t] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + t) * pitch + x0 - 1];
@@ -411,6 +381,10 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
             int32_t rc = wrap16(pred_at(t, j) + rr);
             rrow[j] = (int16_t)(rc < 0 ? 0 : (rc > 255 ? 255 : rc));
         }
+        if (MODE == kTree && t < N / 4) {
+            const int w4 = w / 4;
+            for (int j = 0; j < N / 4; ++j) tu_log2[(int64_t)(y0 / 4 + t) * w4 + x0 / 4 + j] = (uint8_t)Log2<N>::v;
+        }
     }
 }
 
@@ -429,7 +403,6 @@ static QuantParams qparams(int qp, int log2n, bool intra) {
     return q;
 }
 
-static int64_t tu_cap(int w, int h, int s) { return (int64_t)((w + s - 1) / s) * ((h + s - 1) / s); }
 
 int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
                    hipStream_t s) {
@@ -437,8 +410,9 @@ int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_
     if (!n) return NH_OK;
     int per, rem;
     qp_split(qp, &per, &rem);
-    k_tu_process<32, false, true><<<(n + 7) / 8, 256, 0, s>>>(d_src, w, h, pitch, nullptr, nullptr, qparams(qp, 5, true),
-                                                             dequant_scale(rem), per, d_lvl, d_recon, nullptr, bw, n);
+    k_tu_process<32, false, kAll><<<(n + 7) / 8, 256, 0, s>>>(d_src, w, h, pitch, qparams(qp, 5, true),
+                                                             dequant_scale(rem), per, d_lvl, d_recon, nullptr, bw, n,
+                                                             TreeArgs{});
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
@@ -462,16 +436,15 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
 }
 
 extern "C" int64_t nh_tu_workspace_bytes(int w, int h, int ctb) {
-    (void)ctb;
-    int64_t b = 256;
-    for (int s = 4; s <= 32; s *= 2) b += align_up((size_t)tu_cap(w, h, s) * 4, 256);
-    return b;
+    (void)w; (void)h; (void)ctb;
+    return 0;   // no scratch: TUs are found by per-size grid walks (k_tu_process kTree)
 }
 
 extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb, int plane_id,
                                     uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
                                     int16_t* d_recon, uint8_t* d_tu, void* d_work, void* stream) {
-    if (!d_src || !d_lvl || !d_recon || !d_tu || !d_work || pitch < w || w <= 0 || h <= 0) return NH_EARG;
+    (void)d_work;
+    if (!d_src || !d_lvl || !d_recon || !d_tu || pitch < w || w <= 0 || h <= 0) return NH_EARG;
     if (ctb != 4 && ctb != 8 && ctb != 16 && ctb != 32) return NH_EVALUE;
     if ((w & 3) || (h & 3) || w > 65535 || h > 65535) return NH_EARG;
     hipStream_t s = as_stream(stream);
@@ -479,42 +452,23 @@ extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitc
     if (row0 < 0) row0 = 0;
     if (row1 > rows) row1 = rows;
     if (row1 <= row0) return NH_OK;
-    TuLists tl;
-    char* p = (char*)d_work;
-    tl.count = (uint32_t*)p;
-    p += 256;
-    for (int c = 0; c < 4; ++c) {
-        tl.cap[c] = (uint32_t)tu_cap(w, h, 4 << c);
-        tl.list[c] = (uint32_t*)p;
-        p += align_up((size_t)tl.cap[c] * 4, 256);
-    }
-    NH_HIP(hipMemsetAsync(tl.count, 0, 16, s));
-    const int64_t nunits = (int64_t)((min(row1 * ctb, h) - row0 * ctb) / 4) * (w / 4);
-    k_tu_plan<<<(unsigned)((nunits + 255) / 256), 256, 0, s>>>(w, h, ctb, plane_id, seed, row0, row1, tl, d_tu);
-    NH_HIP(hipGetLastError());
     int per, rem;
     qp_split(qp, &per, &rem);
     const int dqs = dequant_scale(rem);
-    // grids sized by the capacity bound; surplus workgroups see idx >= count and idle
-    const int64_t band = (int64_t)(row1 - row0) * ctb;  // rows covered
-    auto grid = [&](int size, int cap) {
-        int64_t bound = (int64_t)((w + size - 1) / size) * ((band + size - 1) / size + 1);
-        if (bound > cap) bound = cap;
-        const int G = 256 / size;
-        return (unsigned)((bound + G - 1) / G);
-    };
-    if (is_luma)
-        k_tu_process<4, true><<<grid(4, tl.cap[0]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[0], tl.count + 0,
-                                                                qparams(qp, 2, true), dqs, per, d_lvl, d_recon, d_tu);
-    else
-        k_tu_process<4, false><<<grid(4, tl.cap[0]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[0], tl.count + 0,
-                                                                 qparams(qp, 2, true), dqs, per, d_lvl, d_recon, d_tu);
-    k_tu_process<8, false><<<grid(8, tl.cap[1]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[1], tl.count + 1,
-                                                             qparams(qp, 3, true), dqs, per, d_lvl, d_recon, d_tu);
-    k_tu_process<16, false><<<grid(16, tl.cap[2]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[2], tl.count + 2,
-                                                               qparams(qp, 4, true), dqs, per, d_lvl, d_recon, d_tu);
-    k_tu_process<32, false><<<grid(32, tl.cap[3]), 256, 0, s>>>(d_src, w, h, pitch, tl.list[3], tl.count + 3,
-                                                               qparams(qp, 5, true), dqs, per, d_lvl, d_recon, d_tu);
+    const int yb = row0 * ctb, ye = row1 * ctb < h ? row1 * ctb : h;
+    TreeArgs ta{ctb, plane_id, yb, seed};
+#define NH_TU(NN, DST)                                                                                       \
+    do {                                                                                                     \
+        const int bw = w / NN, bh = (ye - yb + NN - 1) / NN, n = bw * bh;                                   \
+        if (NN <= ctb && n > 0)                                                                              \
+            k_tu_process<NN, DST, kTree><<<(n + 256 / NN - 1) / (256 / NN), 256, 0, s>>>(                    \
+                d_src, w, h, pitch, qparams(qp, Log2<NN>::v, true), dqs, per, d_lvl, d_recon, d_tu, bw, n, ta); \
+    } while (0)
+    if (is_luma) NH_TU(4, true); else NH_TU(4, false);
+    NH_TU(8, false);
+    NH_TU(16, false);
+    NH_TU(32, false);
+#undef NH_TU
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

@@ -165,11 +165,13 @@ def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_
     lvl = torch.zeros((h, w), dtype=torch.int32, device=dev) if lvl is None else lvl
     rec = torch.zeros((h, w), dtype=torch.int16, device=dev) if rec is None else rec
     tu = torch.zeros((h // 4, w // 4), dtype=torch.uint8, device=dev) if tu is None else tu
-    if work is None:
-        work = torch.empty(int(L.nh_tu_workspace_bytes(w, h, ctb)), dtype=torch.uint8, device=dev)
+    nwork = int(L.nh_tu_workspace_bytes(w, h, ctb))
+    if work is None and nwork > 0:
+        work = torch.empty(nwork, dtype=torch.uint8, device=dev)
     check(L.nh_tu_pipeline_plane(src.data_ptr(), w, h, w, int(ctb), int(plane_id), int(seed) & 0xFFFFFFFF, int(qp),
                                  int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)), lvl.data_ptr(), rec.data_ptr(),
-                                 tu.data_ptr(), work.data_ptr(), C.c_void_p(_stream(stream))), "tu_pipeline_plane")
+                                 tu.data_ptr(), work.data_ptr() if work is not None else None,
+                                 C.c_void_p(_stream(stream))), "tu_pipeline_plane")
     return lvl, rec, tu
 
 

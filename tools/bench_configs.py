@@ -92,7 +92,7 @@ def main():
             bufs.append((torch.zeros((h, w), dtype=torch.int32, device="cuda"),
                          torch.zeros((h, w), dtype=torch.int16, device="cuda"),
                          torch.zeros((h // 4, w // 4), dtype=torch.uint8, device="cuda"),
-                         torch.empty(int(L.nh_tu_workspace_bytes(w, h, ctb)), dtype=torch.uint8, device="cuda")))
+                         torch.empty(max(1, int(L.nh_tu_workspace_bytes(w, h, ctb))), dtype=torch.uint8, device="cuda")))
 
         def run4():
             for (p, ctb, pid, luma), (lv, rc, tu, wk) in zip(planes, bufs):
