@@ -137,19 +137,23 @@ def scatter_to_frames(layout: RankLayout, local, frames_yuv):
 
 def gather_to_root(local, layouts_total_elems: List[int], dist, group=None):
     """RCCL/gloo gather of every rank's local buffer to rank 0 (the path's one
-    exchange step).  Buffers travel as raw bytes (neither NCCL/RCCL nor gloo
-    has an int16 type), padded to the largest rank's size."""
+    exchange step).  Buffers travel as raw 8-byte words (neither NCCL/RCCL nor
+    gloo has an int16 type, and 8-byte words keep element counts < 2^31 for
+    multi-GB buffers), padded to the largest rank's size."""
     import torch
-    n = max(layouts_total_elems) * local.element_size()
+    es = local.element_size()
     if local.is_cuda and dist.get_backend(group) == "gloo":   # gloo gathers host tensors only
         out = gather_to_root(local.cpu(), layouts_total_elems, dist, group)
         return None if out is None else [o.to(local.device) for o in out]
+    nbytes = -(-max(layouts_total_elems) * es // 8) * 8
     raw = local.contiguous().view(torch.uint8)
-    send = raw if raw.numel() == n else torch.nn.functional.pad(raw, (0, n - raw.numel()))
+    if raw.numel() != nbytes:
+        raw = torch.nn.functional.pad(raw, (0, nbytes - raw.numel()))
+    send = raw.view(torch.int64)
     rank = dist.get_rank(group)
     if rank == 0:
-        bufs = [torch.empty(n, dtype=torch.uint8, device=local.device) for _ in layouts_total_elems]
+        bufs = [torch.empty(nbytes // 8, dtype=torch.int64, device=local.device) for _ in layouts_total_elems]
         dist.gather(send, gather_list=bufs, dst=0, group=group)
-        return [b[:m * local.element_size()].view(local.dtype) for b, m in zip(bufs, layouts_total_elems)]
+        return [b.view(torch.uint8)[:m * es].view(local.dtype) for b, m in zip(bufs, layouts_total_elems)]
     dist.gather(send, dst=0, group=group)
     return None
