@@ -118,7 +118,9 @@ int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_
 /* Same computation, launch variants kept for A/B measurement (identical
  * output): variant = cache policy (0 default, 1 nontemporal loads+stores,
  * 2 nontemporal loads, 3 nontemporal stores) + 4 * occupancy class
- * (0 compiler choice, 1 >= 5 waves/SIMD). */
+ * (0 compiler choice, 1 >= 5 waves/SIMD; 4 for the pipelined form) + 8 *
+ * persistent software-pipelined form (next tile's loads under this tile's
+ * compute). */
 int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                    int nsets, int qp, int is_intra, int variant, void* stream);
 /* Measurement helper (not a product path): copies d_in to d_out over the same

@@ -139,6 +139,65 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
 }
 
+// Persistent, software-pipelined form: a fixed grid of workgroups walks the
+// 256-block tiles with stride gridDim.x; each thread prefetches its block of
+// the NEXT tile (8 x 16 B) before computing the current one, so every wave
+// keeps a tile of loads in flight under its own compute.
+// Set descriptor of a tile, read from the kernarg segment with a wave-uniform
+// index (scalar loads; indexing the by-value argument struct dynamically would
+// make the compiler copy it to scratch).
+__device__ __forceinline__ bool tile_set(const Fused8Args& a, uint32_t tile, SetDev& S) {
+    int s = 0;
+#pragma unroll
+    for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
+        if (k < a.nsets && tile >= a.set[k].wg_start) s = k;
+    s = __builtin_amdgcn_readfirstlane(s);
+    const Fused8Args* ka = (const Fused8Args*)__builtin_amdgcn_kernarg_segment_ptr();
+    S = ka->set[s];
+    return true;
+}
+
+template <int POLICY, int WAVES>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)))
+k_fwd8x8_quant_pipe(Fused8Args a, uint32_t ntiles) {
+    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
+    asm volatile("" : "+v"(h_v), "+v"(hneg_v));
+    uint32_t tile = blockIdx.x;
+    if (tile >= ntiles) return;
+    SetDev S;
+    tile_set(a, tile, S);
+    uint32_t b = (tile - S.wg_start) * 256u + threadIdx.x;
+    int64_t off = b < S.nblocks ? block_offset(S, b) : -1;
+    v4i raw[8];
+    if (off >= 0) load_block<POLICY>(a.in + off, S.pitch, raw);
+    for (;;) {
+        const uint32_t nt = tile + gridDim.x;
+        SetDev Sn = S;
+        int64_t noff = -1;
+        v4i nraw[8];
+        if (nt < ntiles) {
+            tile_set(a, nt, Sn);
+            const uint32_t nb = (nt - Sn.wg_start) * 256u + threadIdx.x;
+            if (nb < Sn.nblocks) {
+                noff = block_offset(Sn, nb);
+                load_block<POLICY>(a.in + noff, Sn.pitch, nraw);
+            }
+        }
+        if (off >= 0) {
+            v4i outv[8];
+            dct8_quant_block(raw, outv, a.q, h_v, hneg_v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
+        }
+        if (nt >= ntiles) break;
+        tile = nt;
+        S = Sn;
+        off = noff;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) raw[i] = nraw[i];
+    }
+}
+
 // Memory-only probe with the kernel's exact access pattern (8 rows x 16 B per
 // thread, same block walk): copies input to output.  Measurement helper for the
 // achievable-bandwidth ceiling of this pattern; not a product path.
@@ -223,14 +282,28 @@ static constexpr int kDefaultVariant = 5;
 extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                               int nsets, int qp, int is_intra, int variant, void* stream) {
     // variant = cache policy (0..3, see ld16/st16) + 4 * occupancy class (0 compiler, 1 >= 5 waves/SIMD)
-    const int policy = variant & 3, occ = variant >> 2;
-    if (variant < 0 || occ > 1) return NH_EARG;
+    //           + 8 * persistent software-pipelined form (grid = min(tiles, 256 CUs x 8))
+    const int policy = variant & 3, occ = (variant >> 2) & 1, pipe = variant >> 3;
+    if (variant < 0 || pipe > 1) return NH_EARG;
     Fused8Args a;
     uint32_t wg = 0;
     int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
     if (rc) return rc;
     if (!wg) return NH_OK;
     hipStream_t s = as_stream(stream);
+    if (pipe) {
+        const uint32_t g = wg < 2048u ? wg : 2048u;
+#define NH_P(P) do { if (occ) k_fwd8x8_quant_pipe<P, 4><<<g, 256, 0, s>>>(a, wg); else k_fwd8x8_quant_pipe<P, 1><<<g, 256, 0, s>>>(a, wg); } while (0)
+        switch (policy) {
+            case 0: NH_P(0); break;
+            case 1: NH_P(1); break;
+            case 2: NH_P(2); break;
+            default: NH_P(3); break;
+        }
+#undef NH_P
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
 #define NH_L(P) do { if (occ) k_fwd8x8_quant<P, 5><<<wg, 256, 0, s>>>(a); else k_fwd8x8_quant<P, 1><<<wg, 256, 0, s>>>(a); } while (0)
     switch (policy) {
         case 0: NH_L(0); break;

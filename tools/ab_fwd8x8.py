@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--frames", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--variants", default="1,5")
+    ap.add_argument("--variants", default="1,5,9,13")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     L = _lib.load()
