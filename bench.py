@@ -19,8 +19,9 @@ on the launch stream), against 8.0 TB/s.  ``traffic`` comes from the rocprofv3
 PMC pass committed under profiles/ (tools/pmc_traffic.py) when one matches this
 configuration, else null.
 
-cpu_baseline (rank 0, N=1 only): the CPU restatement oracle/ ("port", 1
-thread) timed on a bounded sample of the same workload; the same sample's GPU
+cpu_baseline (rank 0, N=1 only): the CPU restatement oracle/ ("port") timed on
+a bounded sample of the same workload, on all of the job's host threads
+("value", "cores") and on one thread ("value_1thread"); the same sample's GPU
 levels are checked bit-exact against it.
 """
 from __future__ import annotations
@@ -56,28 +57,62 @@ def load_traffic(cfg_key: str):
     return None if e is None else e.get("hbm_bytes_per_launch")
 
 
+def cpu_threads() -> int:
+    """Host threads for the all-cores leg: the job's CPU share (OMP_NUM_THREADS
+    on the GPU box = 16), else the affinity mask; nproc there shows the whole
+    machine, not this job's share."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(gpu_out: torch.Tensor, res: torch.Tensor, fe: int, frames: int, qp: int, budget_s: float):
-    """Time the oracle (CPU restatement, 1 thread) on whole 4K YUV420 frames until
-    ~budget_s elapsed; check the GPU levels of those frames bit-exact."""
+    """Time the oracle (CPU restatement) on whole 4K YUV420 frames: first 1
+    thread, then all of the job's host threads, each for
+    ~budget_s/2; the GPU levels of every sampled frame are checked bit-exact
+    against the single-thread output, and the threaded output against that."""
     from oracle import oracle as O   # checker + CPU baseline only
     O.lib()
+    nthr = cpu_threads()
     cw, ch = W4K // 2, H4K // 2
-    done_blocks, t_cpu, exact, f = 0, 0.0, True, 0
-    while f < frames and (t_cpu < budget_s or f == 0):
-        r = res[f * fe:(f + 1) * fe].cpu().numpy()
-        g = gpu_out[f * fe:(f + 1) * fe].cpu().numpy()
-        planes = [(0, H4K, W4K), (W4K * H4K, ch, cw), (W4K * H4K + cw * ch, ch, cw)]
-        for off, h, w in planes:
-            p = r[off:off + h * w].reshape(h, w)
-            t0 = time.perf_counter()
-            lv = O.fwd8x8_quant_plane(p, qp, True)
-            t_cpu += time.perf_counter() - t0
-            done_blocks += (h // 8) * (w // 8)
-            exact &= bool(np.array_equal(lv, g[off:off + h * w].reshape(h, w)))
-        f += 1
-    return {"value": done_blocks / t_cpu, "unit": "blocks/s", "cores": 1, "kind": "port",
-            "sample": f"{f} whole 4K YUV420 frames ({done_blocks} 8x8 blocks, QP {qp}) through "
-                      f"oracle/nh_oracle.c fwd8x8_quant_plane, 1 thread, {t_cpu:.1f} s",
+    planes = [(0, H4K, W4K), (W4K * H4K, ch, cw), (W4K * H4K + cw * ch, ch, cw)]
+    legs = {}
+    exact = True
+    for threads in (1, nthr):
+        done_blocks, t_cpu, f = 0, 0.0, 0
+        while f < frames and (t_cpu < budget_s / 2 or f == 0):
+            r = res[f * fe:(f + 1) * fe].cpu().numpy()
+            g = gpu_out[f * fe:(f + 1) * fe].cpu().numpy()
+            for off, h, w in planes:
+                p = r[off:off + h * w].reshape(h, w)
+                t0 = time.perf_counter()
+                if threads == 1:
+                    lv = O.fwd8x8_quant_plane(p, qp, True)
+                else:
+                    lv = O.fwd8x8_quant_plane_mt(p, qp, True, threads)
+                t_cpu += time.perf_counter() - t0
+                done_blocks += (h // 8) * (w // 8)
+                exact &= bool(np.array_equal(lv, g[off:off + h * w].reshape(h, w)))
+            f += 1
+        legs[threads] = (done_blocks / t_cpu, f, done_blocks, t_cpu)
+    v1, f1, b1, t1 = legs[1]
+    vn, fn, bn, tn = legs[nthr]
+    return {"value": vn, "unit": "blocks/s", "cores": nthr, "kind": "port",
+            "sample": f"{fn} whole 4K YUV420 frames ({bn} 8x8 blocks, QP {qp}) through oracle/nh_oracle.c "
+                      f"fwd8x8_quant_plane_mt on {nthr} threads ({tn:.1f} s); single thread: {f1} frames, "
+                      f"{b1} blocks, {t1:.1f} s",
+            "value_1thread": v1, "cpu_model": cpu_model(), "nproc_machine": os.cpu_count(),
             "gpu_levels_bit_exact_on_sample": exact}
 
 
@@ -89,7 +124,7 @@ def main():
     ap.add_argument("--frames", type=int, default=128, help="4K YUV420 frames per GPU per step")
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--variant", type=int, default=5, help="launch variant (nanohevc.h); 5 = default")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget, split between the 1-thread and all-threads legs")
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: steps of the gather-inclusive phase")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

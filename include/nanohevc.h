@@ -177,6 +177,35 @@ int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t
  * (int32 D) with the lane maps the config-5 MFMA kernel assumes. */
 int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream);
 
+/* ---- Frame I/O and the frame-level intra driver ----
+ * Frame.from_yuv420p / Plane.from_buffer + .astype(np.int16) (frame.py:44-54,
+ * :87-110) and Frame.to_yuv420p / PackedFrame.to_yuv420p's .astype(np.uint8)
+ * (frame.py:112-115, :176-183) as device-to-device element casts over n
+ * samples (any frame count: YUV420p frames are contiguous Y, U, V planes). */
+int nh_widen_u8_i16(const uint8_t* d_in, int16_t* d_out, int64_t n, void* stream);
+/* int16 -> uint8 keeps the low byte (numpy's wrapping astype) */
+int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* stream);
+
+/* encode_frame_intra (__main__.py:142-189) over every plane of the given plane
+ * sets: per full block_sizes[s] block (raster order, partial blocks skipped:
+ * block.py:68-74), DC (intra.py:46-62) vs planar with tr=top[-1], bl=left[-1]
+ * (__main__.py:165-168), neighbours from the SOURCE plane with 128 at the
+ * border (block.py:38-50), energies = residual_energy(residual_block(..))
+ * (metrics.py:46-48, int16 residual wrap), DC wins ties (__main__.py:171),
+ * recon = clip_to_pixel_range(best pred) (intra.py:75-78); samples outside
+ * full blocks get recon 0 (Frame.zeros, frame.py:81-88).
+ * d_src: uint8 (src_is_u8 = 1) or int16 samples.  block_sizes[s] in
+ * {4, 8, 16, 32, 64}.  d_recon (int16) and d_recon_u8 (the recon's
+ * .astype(np.uint8), i.e. to_yuv420p bytes) are optional and use the source
+ * layout.  d_stats (NH_ENC_STATS int64 per plane, planes numbered set by set
+ * in plane order g * planes_per_group + c) is ACCUMULATED into (zero it first):
+ *   blocks, dc wins, planar wins, sum of DC energies, sum of planar energies,
+ *   SSE of (uint8)src vs (uint8)recon over the whole plane (metrics.psnr). */
+#define NH_ENC_STATS 6
+int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set* sets, int nsets,
+                           const int32_t* block_sizes, int16_t* d_recon, uint8_t* d_recon_u8,
+                           int64_t* d_stats, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,505 @@
+// nh_frame.hip -- frame I/O casts and the frame-level intra driver
+// (DESIGN.md §3.6, §4.7).
+//
+//   k_widen / k_narrow      frame.py:44-54, :87-115, :176-183 (astype casts)
+//   k_encode_dcpl<T, N>     __main__.py:142-189 encode_frame_intra (and the
+//                           demo's per-block decision, __main__.py:75-100)
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <type_traits>
+#include "nh_common.hpp"
+#include "nh_internal.hpp"
+
+namespace nh {
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------
+// uint8 <-> int16 casts: nontemporal streaming (the best policy of the
+// linear-copy probe), a scalar tail, a scalar kernel for
+// unaligned views.
+// ---------------------------------------------------------------------------
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+// 8 samples per thread: an 8-B load and ONE 16-B store, so every store
+// instruction of a wave covers 1 KB contiguously.
+__global__ void __launch_bounds__(256) k_widen(const uint8_t* __restrict__ in, int16_t* __restrict__ out,
+                                               int64_t nchunks, int64_t n) {
+    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+    if (i < nchunks) {
+        const v2u b = __builtin_nontemporal_load((const v2u*)in + i);
+        v4u o;   // 8 bytes -> 8 int16, zero-extended (uint8 values are non-negative)
+        o[0] = __builtin_amdgcn_perm(0u, b[0], 0x0c010c00u);
+        o[1] = __builtin_amdgcn_perm(0u, b[0], 0x0c030c02u);
+        o[2] = __builtin_amdgcn_perm(0u, b[1], 0x0c010c00u);
+        o[3] = __builtin_amdgcn_perm(0u, b[1], 0x0c030c02u);
+        __builtin_nontemporal_store(o, (v4u*)out + i);
+    } else {
+        const int64_t j = nchunks * 8 + (i - nchunks);
+        if (j < n) out[j] = in[j];
+    }
+}
+
+// 8 samples per thread: ONE 16-B load and an 8-B store.
+__global__ void __launch_bounds__(256) k_narrow(const int16_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                int64_t nchunks, int64_t n) {
+    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+    if (i < nchunks) {
+        const v4u a = __builtin_nontemporal_load((const v4u*)in + i);
+        v2u o;   // low byte of each int16 (numpy's wrapping astype(np.uint8))
+        o[0] = __builtin_amdgcn_perm(a[1], a[0], 0x06040200u);
+        o[1] = __builtin_amdgcn_perm(a[3], a[2], 0x06040200u);
+        __builtin_nontemporal_store(o, (v2u*)out + i);
+    } else {
+        const int64_t j = nchunks * 8 + (i - nchunks);
+        if (j < n) out[j] = (uint8_t)in[j];
+    }
+}
+
+// Unaligned views: one sample per thread.
+__global__ void k_widen_scalar(const uint8_t* in, int16_t* out, int64_t n) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = in[i];
+}
+__global__ void k_narrow_scalar(const int16_t* in, uint8_t* out, int64_t n) {
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) out[i] = (uint8_t)in[i];
+}
+
+// ---------------------------------------------------------------------------
+// encode_frame_intra.  N lanes per block, lane r owns block row r: it loads its
+// source row and the block's top row (one vector load each when the layout is
+// 16-element aligned: AL), left[r] and bl = left[N-1]; the segment (N lanes,
+// 64 % N == 0) sums left[] for DC; both residual energies are segment-reduced
+// and the winner's clipped prediction row is stored.  A workgroup walks one
+// plane with a stride of gridDim.x (<= 512 workgroups per plane), so each
+// stats word takes <= 512 atomics.
+// ---------------------------------------------------------------------------
+struct EncArgs {
+    const void* src;
+    int16_t* rec;
+    uint8_t* rec8;
+    int64_t* stats;          // stats of this set's plane 0
+    int64_t base, plane_stride, group_stride;
+    int32_t w, h, pitch, ppg;
+    FastDiv nbx;             // blocks per row (partial included)
+    uint32_t nblk;
+};
+
+template <int N, class V>
+__device__ __forceinline__ V seg_sum(V v) {
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+// N samples of T at p into v[] (AL: p is aligned to min(16, N*sizeof(T)) bytes).
+template <class T, int N, bool AL>
+__device__ __forceinline__ void load_row(const T* p, int (&v)[N]) {
+    if constexpr (AL) {
+        constexpr int B = N * (int)sizeof(T), A = B < 16 ? B : 16;
+        T t[N];
+        __builtin_memcpy(t, __builtin_assume_aligned(p, A), B);
+#pragma unroll
+        for (int x = 0; x < N; ++x) v[x] = t[x];
+    } else {
+#pragma unroll
+        for (int x = 0; x < N; ++x) v[x] = p[x];
+    }
+}
+template <class T, int N, bool AL>
+__device__ __forceinline__ void store_row(T* p, const int (&v)[N]) {
+    T t[N];
+#pragma unroll
+    for (int x = 0; x < N; ++x) t[x] = (T)v[x];
+    if constexpr (AL) {
+        constexpr int B = N * (int)sizeof(T), A = B < 16 ? B : 16;
+        __builtin_memcpy(__builtin_assume_aligned(p, A), t, B);
+    } else {
+#pragma unroll
+        for (int x = 0; x < N; ++x) p[x] = t[x];
+    }
+}
+
+template <class T, int N, bool AL>
+__global__ void __launch_bounds__(256) k_encode_dcpl(EncArgs a) {
+    constexpr int L2 = N == 4 ? 2 : N == 8 ? 3 : N == 16 ? 4 : N == 32 ? 5 : 6;
+    // uint8 sources: every energy of a block (<= 64*64*255^2) fits int32
+    using Acc = typename std::conditional<std::is_same<T, uint8_t>::value, int32_t, int64_t>::type;
+    const int p = blockIdx.y;
+    const int g = p / a.ppg, c = p - g * a.ppg;
+    const int64_t off = a.base + (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
+    const T* src = static_cast<const T*>(a.src) + off;
+    const int lane = threadIdx.x & 63, r = lane & (N - 1);
+    constexpr uint32_t kPerWG = 256 / N;
+    int64_t st_blocks = 0, st_dc = 0, st_edc = 0, st_epl = 0, st_sse = 0;
+
+    for (uint32_t b0 = blockIdx.x * kPerWG; b0 < a.nblk; b0 += gridDim.x * kPerWG) {
+        const uint32_t b = b0 + threadIdx.x / N;
+        const bool act = b < a.nblk;
+        const uint32_t by = act ? fdiv(b, a.nbx) : 0, bx = act ? b - by * a.nbx.d : 0;
+        const int x0 = bx * N, y0 = by * N, y = y0 + r;
+        const bool full = act && x0 + N <= a.w && y0 + N <= a.h;   // uniform per segment
+        int o[N], top[N], lt = 128, bl = 128;
+#pragma unroll
+        for (int x = 0; x < N; ++x) o[x] = top[x] = 128;
+        if (full) {
+            load_row<T, N, AL>(src + (int64_t)y * a.pitch + x0, o);
+            if (y0 > 0) load_row<T, N, AL>(src + (int64_t)(y0 - 1) * a.pitch + x0, top);
+            if (x0 > 0) {
+                lt = src[(int64_t)y * a.pitch + x0 - 1];
+                bl = src[(int64_t)(y0 + N - 1) * a.pitch + x0 - 1];
+            }
+        }
+        int tsum = 0;
+#pragma unroll
+        for (int x = 0; x < N; ++x) tsum += top[x];
+        const int dc = (int16_t)((tsum + seg_sum<N>(lt) + N) >> (L2 + 1));   // floor division by 2N
+        const int tr = top[N - 1];
+        int pl[N];
+        Acc edc = 0, epl = 0;
+#pragma unroll
+        for (int x = 0; x < N; ++x) {
+            pl[x] = (int16_t)(((N - 1 - x) * lt + (x + 1) * tr + (N - 1 - r) * top[x] + (r + 1) * bl + N) >> (L2 + 1));
+            const Acc rd = (int16_t)(o[x] - dc), rp = (int16_t)(o[x] - pl[x]);
+            edc += rd * rd;
+            epl += rp * rp;
+        }
+        const Acc sdc = seg_sum<N>(edc), spl = seg_sum<N>(epl);
+        if (full) {
+            const bool use_dc = sdc <= spl;
+            Acc sse = 0;
+#pragma unroll
+            for (int x = 0; x < N; ++x) {
+                const int v = use_dc ? dc : pl[x];
+                pl[x] = v < 0 ? 0 : v > 255 ? 255 : v;
+                const int d = (int)(uint8_t)o[x] - pl[x];
+                sse += d * d;
+            }
+            const int64_t i = off + (int64_t)y * a.pitch + x0;
+            if (a.rec) store_row<int16_t, N, AL>(a.rec + i, pl);
+            if (a.rec8) store_row<uint8_t, N, AL>(a.rec8 + i, pl);
+            st_sse += sse;
+            if (r == 0) {
+                st_blocks += 1;
+                st_dc += use_dc;
+                st_edc += sdc;
+                st_epl += spl;
+            }
+        } else if (act && y < a.h) {   // samples outside full blocks: recon stays 0
+            for (int x = 0; x < N && x0 + x < a.w; ++x) {
+                const int64_t i = (int64_t)y * a.pitch + x0 + x;
+                if (a.rec) a.rec[off + i] = 0;
+                if (a.rec8) a.rec8[off + i] = 0;
+                const int d = (uint8_t)src[i];
+                st_sse += d * d;
+            }
+        }
+    }
+    // workgroup reduction, then one atomic per stats word
+    __shared__ int64_t part[4][5];
+    int64_t v[5] = {st_blocks, st_dc, st_edc, st_epl, st_sse};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        for (int m = 32; m > 0; m >>= 1) v[k] += __shfl_xor(v[k], m, 64);
+        if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t[5];
+        for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+        int64_t* s = a.stats + (int64_t)p * NH_ENC_STATS;
+        const int64_t add[NH_ENC_STATS] = {t[0], t[1], t[0] - t[1], t[2], t[3], t[4]};
+        for (int k = 0; k < NH_ENC_STATS; ++k)
+            if (add[k]) atomicAdd((unsigned long long*)(s + k), (unsigned long long)add[k]);
+    }
+}
+
+// Lane-per-block form for N in {4, 8} (the CLI default: 8x8 luma, 4x4
+// chroma).  Each lane takes U blocks (b, b + 256, ...), issues all their row
+// loads first (U * (N + 1) rows in flight per lane), then decides each block.
+// A wave covers 64 consecutive blocks, so every row access of a wave is one
+// contiguous 64 * N-sample run; the left column is the previous lane's last
+// column (lane shuffle), loaded only by lane 0 of a wave.
+template <class T, int N>
+struct RowT;   // one block row of N samples of T, packed in dwords
+template <> struct RowT<uint8_t, 4> { typedef unsigned int type; };
+template <> struct RowT<uint8_t, 8> { typedef v2u type; };
+template <> struct RowT<int16_t, 4> { typedef v2u type; };
+template <> struct RowT<int16_t, 8> { typedef v4u type; };
+
+template <class T, class R>
+__device__ __forceinline__ unsigned word(const R& r, int k) {
+    if constexpr (sizeof(R) == 4) return r;
+    else return r[k];
+}
+template <class T, class R>
+__device__ __forceinline__ int elem(const R& r, int x) {
+    if constexpr (sizeof(T) == 1) return (word<T>(r, x >> 2) >> (8 * (x & 3))) & 0xff;
+    else return (int16_t)(word<T>(r, x >> 1) >> (16 * (x & 1)));
+}
+template <class T, int N, bool AL>
+__device__ __forceinline__ typename RowT<T, N>::type load_rowv(const T* p) {
+    typedef typename RowT<T, N>::type R;
+    if constexpr (AL) {
+        return *(const R*)p;
+    } else {
+        T t[N];
+#pragma unroll
+        for (int x = 0; x < N; ++x) t[x] = p[x];
+        R r;
+        __builtin_memcpy(&r, t, sizeof(R));
+        return r;
+    }
+}
+
+template <class T, int N, int U, bool AL>
+__global__ void __launch_bounds__(256) k_encode_small(EncArgs a) {
+    constexpr int L2 = N == 4 ? 2 : 3;
+    typedef typename RowT<T, N>::type R;
+    using Acc = typename std::conditional<std::is_same<T, uint8_t>::value, int32_t, int64_t>::type;
+    const int p = blockIdx.y;
+    const int g = p / a.ppg, c = p - g * a.ppg;
+    const int64_t off = a.base + (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
+    const T* src = static_cast<const T*>(a.src) + off;
+    const int lane = threadIdx.x & 63;
+    int64_t st_blocks = 0, st_dc = 0, st_edc = 0, st_epl = 0, st_sse = 0;
+
+    for (uint32_t b0 = blockIdx.x * 256u * U; b0 < a.nblk; b0 += gridDim.x * 256u * U) {
+        R o[U][N], top[U];
+        int x0[U], y0[U];
+        bool act[U], full[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {   // load phase
+            const uint32_t b = b0 + u * 256u + threadIdx.x;
+            act[u] = b < a.nblk;
+            const uint32_t by = act[u] ? fdiv(b, a.nbx) : 0, bx = act[u] ? b - by * a.nbx.d : 0;
+            x0[u] = bx * N;
+            y0[u] = by * N;
+            full[u] = act[u] && x0[u] + N <= a.w && y0[u] + N <= a.h;
+            const T* blk = src + (int64_t)y0[u] * a.pitch + x0[u];
+#pragma unroll
+            for (int i = 0; i < N; ++i) o[u][i] = full[u] ? load_rowv<T, N, AL>(blk + (int64_t)i * a.pitch) : R{};
+            top[u] = full[u] && y0[u] > 0 ? load_rowv<T, N, AL>(blk - a.pitch) : R{};
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {   // decide + store phase
+            int left[N];
+#pragma unroll
+            for (int i = 0; i < N; ++i) {
+                // previous lane = block b-1 = (bx-1, by) whenever bx > 0
+                const unsigned last = word<T>(o[u][i], (int)(sizeof(R) / 4) - 1);
+                const unsigned prev = __shfl_up(last, 1, 64);
+                left[i] = sizeof(T) == 1 ? (int)(prev >> 24) : (int)(int16_t)(prev >> 16);
+            }
+            if (x0[u] == 0) {
+#pragma unroll
+                for (int i = 0; i < N; ++i) left[i] = 128;
+            } else if (lane == 0 && full[u]) {
+#pragma unroll
+                for (int i = 0; i < N; ++i) left[i] = src[(int64_t)(y0[u] + i) * a.pitch + x0[u] - 1];
+            }
+            int tp[N], tsum = 0, lsum = 0;
+#pragma unroll
+            for (int x = 0; x < N; ++x) {
+                tp[x] = y0[u] > 0 ? elem<T>(top[u], x) : 128;
+                tsum += tp[x];
+                lsum += left[x];
+            }
+            const int dc = (int16_t)((tsum + lsum + N) >> (L2 + 1));   // floor division by 2N
+            const int tr = tp[N - 1], bl = left[N - 1];
+            Acc edc = 0, epl = 0;
+#pragma unroll
+            for (int y = 0; y < N; ++y)
+#pragma unroll
+                for (int x = 0; x < N; ++x) {
+                    const int ov = elem<T>(o[u][y], x);
+                    const int pl = (int16_t)(((N - 1 - x) * left[y] + (x + 1) * tr + (N - 1 - y) * tp[x] +
+                                              (y + 1) * bl + N) >> (L2 + 1));
+                    const Acc rd = (int16_t)(ov - dc), rp = (int16_t)(ov - pl);
+                    edc += rd * rd;
+                    epl += rp * rp;
+                }
+            if (full[u]) {
+                const bool use_dc = edc <= epl;
+                Acc sse = 0;
+#pragma unroll
+                for (int y = 0; y < N; ++y) {
+                    int rv[N];
+#pragma unroll
+                    for (int x = 0; x < N; ++x) {
+                        const int v = use_dc ? dc : (int16_t)(((N - 1 - x) * left[y] + (x + 1) * tr +
+                                                               (N - 1 - y) * tp[x] + (y + 1) * bl + N) >> (L2 + 1));
+                        rv[x] = v < 0 ? 0 : v > 255 ? 255 : v;
+                        const int d = (elem<T>(o[u][y], x) & 0xff) - rv[x];
+                        sse += d * d;
+                    }
+                    const int64_t i = off + (int64_t)(y0[u] + y) * a.pitch + x0[u];
+                    if (a.rec) store_row<int16_t, N, AL>(a.rec + i, rv);
+                    if (a.rec8) store_row<uint8_t, N, AL>(a.rec8 + i, rv);
+                }
+                st_sse += sse;
+                st_blocks += 1;
+                st_dc += use_dc;
+                st_edc += edc;
+                st_epl += epl;
+            } else if (act[u]) {   // samples outside full blocks: recon stays 0
+                for (int y = y0[u]; y < y0[u] + N && y < a.h; ++y)
+                    for (int x = x0[u]; x < x0[u] + N && x < a.w; ++x) {
+                        const int64_t i = (int64_t)y * a.pitch + x;
+                        if (a.rec) a.rec[off + i] = 0;
+                        if (a.rec8) a.rec8[off + i] = 0;
+                        const int d = (uint8_t)src[i];
+                        st_sse += d * d;
+                    }
+            }
+        }
+    }
+    __shared__ int64_t part[4][5];
+    int64_t v[5] = {st_blocks, st_dc, st_edc, st_epl, st_sse};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        for (int m = 32; m > 0; m >>= 1) v[k] += __shfl_xor(v[k], m, 64);
+        if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t[5];
+        for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+        int64_t* s = a.stats + (int64_t)p * NH_ENC_STATS;
+        const int64_t add[NH_ENC_STATS] = {t[0], t[1], t[0] - t[1], t[2], t[3], t[4]};
+        for (int k = 0; k < NH_ENC_STATS; ++k)
+            if (add[k]) atomicAdd((unsigned long long*)(s + k), (unsigned long long)add[k]);
+    }
+}
+
+// Blocks per lane for N = 4 / 8 (loads in flight vs registers).  Tuning knob
+// for measurement: NH_ENC_UNROLL="u4,u8" (each 1, 2 or 4), read once.
+static void small_unroll(int& u4, int& u8) {
+    static int c4 = 0, c8 = 0;
+    if (!c4) {
+        int a = 4, b = 2;
+        if (const char* e = getenv("NH_ENC_UNROLL")) sscanf(e, "%d,%d", &a, &b);
+        c4 = (a == 1 || a == 2 || a == 4) ? a : 4;
+        c8 = (b == 1 || b == 2 || b == 4) ? b : 2;
+    }
+    u4 = c4;
+    u8 = c8;
+}
+
+template <class T, int N, bool AL>
+static void launch_small(int u, const EncArgs& a, dim3 grid, hipStream_t s) {
+    if (u == 1) k_encode_small<T, N, 1, AL><<<grid, 256, 0, s>>>(a);
+    else if (u == 2) k_encode_small<T, N, 2, AL><<<grid, 256, 0, s>>>(a);
+    else k_encode_small<T, N, 4, AL><<<grid, 256, 0, s>>>(a);
+}
+
+template <class T, bool AL>
+static int launch_encode_al(int n, const EncArgs& a, dim3 grid, hipStream_t s) {
+    int u4, u8;
+    small_unroll(u4, u8);
+    switch (n) {
+        case 4: launch_small<T, 4, AL>(u4, a, grid, s); break;
+        case 8: launch_small<T, 8, AL>(u8, a, grid, s); break;
+        case 16: k_encode_dcpl<T, 16, AL><<<grid, 256, 0, s>>>(a); break;
+        case 32: k_encode_dcpl<T, 32, AL><<<grid, 256, 0, s>>>(a); break;
+        case 64: k_encode_dcpl<T, 64, AL><<<grid, 256, 0, s>>>(a); break;
+        default: return NH_EARG;
+    }
+    return NH_OK;
+}
+template <class T>
+static int launch_encode(int n, bool al, const EncArgs& a, dim3 grid, hipStream_t s) {
+    return al ? launch_encode_al<T, true>(n, a, grid, s) : launch_encode_al<T, false>(n, a, grid, s);
+}
+
+}  // namespace nh
+
+using namespace nh;
+
+extern "C" {
+
+int nh_widen_u8_i16(const uint8_t* d_in, int16_t* d_out, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!d_in || !d_out))) { set_error("nh_widen_u8_i16: bad arguments"); return NH_EARG; }
+    if (n == 0) return NH_OK;
+    const hipStream_t s = as_stream(stream);
+    if (((uintptr_t)d_in & 7) == 0 && ((uintptr_t)d_out & 15) == 0) {
+        const int64_t chunks = n / 8, threads = chunks + (n - chunks * 8);
+        k_widen<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n);
+    } else {
+        k_widen_scalar<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(d_in, d_out, n);
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* stream) {
+    if (n < 0 || (n > 0 && (!d_in || !d_out))) { set_error("nh_narrow_i16_u8: bad arguments"); return NH_EARG; }
+    if (n == 0) return NH_OK;
+    const hipStream_t s = as_stream(stream);
+    if (((uintptr_t)d_in & 15) == 0 && ((uintptr_t)d_out & 7) == 0) {
+        const int64_t chunks = n / 8, threads = chunks + (n - chunks * 8);
+        k_narrow<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n);
+    } else {
+        k_narrow_scalar<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(d_in, d_out, n);
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set* sets, int nsets,
+                           const int32_t* block_sizes, int16_t* d_recon, uint8_t* d_recon_u8,
+                           int64_t* d_stats, void* stream) {
+    if (!d_src || !sets || !block_sizes || !d_stats || nsets < 0 || nsets > NH_MAX_PLANE_SETS) {
+        set_error("nh_encode_intra_planes: bad arguments");
+        return NH_EARG;
+    }
+    const hipStream_t s = as_stream(stream);
+    int64_t plane0 = 0;
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& S = sets[k];
+        const int n = block_sizes[k];
+        const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
+        if (S.width < 0 || S.height < 0 || S.pitch < S.width || S.planes_per_group < 1 || S.num_groups < 0 ||
+            planes > 65535 || !(n == 4 || n == 8 || n == 16 || n == 32 || n == 64)) {
+            set_error("nh_encode_intra_planes: bad plane set or block size (4, 8, 16, 32 or 64)");
+            return NH_EARG;
+        }
+        if (planes == 0 || S.width == 0 || S.height == 0) continue;
+        EncArgs a;
+        a.src = d_src;
+        a.rec = d_recon;
+        a.rec8 = d_recon_u8;
+        a.stats = d_stats + plane0 * NH_ENC_STATS;
+        a.base = S.base;
+        a.plane_stride = S.plane_stride;
+        a.group_stride = S.group_stride;
+        a.w = S.width;
+        a.h = S.height;
+        a.pitch = S.pitch;
+        a.ppg = S.planes_per_group;
+        const int64_t nbx = (S.width + n - 1) / n, nblk = nbx * ((S.height + n - 1) / n);
+        if (nblk * n >= (1ll << 31)) {
+            set_error("nh_encode_intra_planes: plane too large");
+            return NH_EARG;
+        }
+        a.nbx = make_fastdiv((uint32_t)nbx);
+        a.nblk = (uint32_t)nblk;
+        // vector row access when every row start is 16-element aligned
+        const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+        const bool al = al16(d_src) && (!d_recon || al16(d_recon)) && (!d_recon_u8 || al16(d_recon_u8)) &&
+                        S.base % 16 == 0 && S.plane_stride % 16 == 0 && S.group_stride % 16 == 0 && S.pitch % 16 == 0;
+        int u4, u8;
+        small_unroll(u4, u8);
+        const int64_t per_wg = n == 4 ? 256 * u4 : n == 8 ? 256 * u8 : 256 / n;   // blocks per workgroup pass
+        const int64_t wgs = (nblk + per_wg - 1) / per_wg;
+        const dim3 grid((unsigned)std::min<int64_t>(wgs, 512), (unsigned)planes);
+        const int rc = src_is_u8 ? launch_encode<uint8_t>(n, al, a, grid, s) : launch_encode<int16_t>(n, al, a, grid, s);
+        if (rc) return rc;
+        NH_HIP(hipGetLastError());
+        plane0 += planes;
+    }
+    return NH_OK;
+}
+
+}  // extern "C"

@@ -10,6 +10,8 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
   tc32_plane          -- config 5: 32x32 chain, butterfly or int8-MFMA variant
+  widen_u8 / narrow_u8 -- frame I/O casts (YUV420p bytes <-> int16 planes)
+  encode_intra_yuv420 -- encode_frame_intra (DC vs planar per block) over a frame stream
 """
 from __future__ import annotations
 
@@ -187,3 +189,105 @@ def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=N
     check(_lib.load().nh_tc32_plane(src.data_ptr(), w, h, w, int(qp), lvl.data_ptr(), rec.data_ptr(), int(variant),
                                     C.c_void_p(_stream(stream))), "tc32_plane")
     return lvl, rec
+
+
+# ---------------------------------------------------------------------------
+# Frame I/O (frame.py:44-54, :87-115, :176-183) and the frame-level intra
+# driver (__main__.py:142-189) -- SURVEY.md §8(f) f-3 / f-1.
+# ---------------------------------------------------------------------------
+ENC_STATS = 6   # blocks, dc wins, planar wins, dc energy, planar energy, uint8 SSE
+
+
+def widen_u8(src, out=None, stream=None):
+    """uint8 samples (e.g. YUV420p bytes uploaded as-is) -> int16, i.e.
+    Plane.from_buffer(..).data.astype(np.int16) for every plane at once."""
+    torch = _torch()
+    _need(src, torch.uint8, "widen_u8(src)")
+    if out is None:
+        out = torch.empty(src.shape, dtype=torch.int16, device=src.device)
+    _need(out, torch.int16, "widen_u8(out)")
+    if out.numel() != src.numel():
+        raise ValueError("widen_u8: size mismatch")
+    check(_lib.load().nh_widen_u8_i16(src.data_ptr(), out.data_ptr(), src.numel(), C.c_void_p(_stream(stream))))
+    return out
+
+
+def narrow_u8(src, out=None, stream=None):
+    """int16 -> uint8 keeping the low byte: numpy's .astype(np.uint8) as used by
+    Frame.to_yuv420p / PackedFrame.to_yuv420p."""
+    torch = _torch()
+    _need(src, torch.int16, "narrow_u8(src)")
+    if out is None:
+        out = torch.empty(src.shape, dtype=torch.uint8, device=src.device)
+    _need(out, torch.uint8, "narrow_u8(out)")
+    if out.numel() != src.numel():
+        raise ValueError("narrow_u8: size mismatch")
+    check(_lib.load().nh_narrow_i16_u8(src.data_ptr(), out.data_ptr(), src.numel(), C.c_void_p(_stream(stream))))
+    return out
+
+
+def chroma_block_size(block_size: int) -> int:
+    """encode_frame_intra's chroma block: block_size // 2, at least 4 (__main__.py:155-157)."""
+    return max(4, block_size // 2)
+
+
+def _check_block_size(bs: int):
+    if bs not in (4, 8, 16, 32, 64):
+        raise NotImplementedError(f"block size {bs}: the device driver handles 4, 8, 16, 32 and 64")
+
+
+def encode_intra_planes(src, sets: Sequence[PlaneSet], block_sizes: Sequence[int], recon=None, recon_u8=None,
+                        stats=None, stream=None):
+    """The per-block decision of encode_frame_intra over every plane of ``sets``
+    inside ``src`` (uint8 or int16).  Returns the (accumulated) int64 stats
+    tensor, one ENC_STATS row per plane, planes numbered set by set."""
+    torch = _torch()
+    if not isinstance(src, torch.Tensor) or not src.is_cuda or src.dtype not in (torch.uint8, torch.int16):
+        raise TypeError("encode_intra_planes(src): expected a uint8 or int16 device tensor")
+    if not src.is_contiguous():
+        raise ValueError("encode_intra_planes(src): tensor must be contiguous")
+    for bs in block_sizes:
+        _check_block_size(int(bs))
+    if len(block_sizes) != len(sets):
+        raise ValueError("encode_intra_planes: one block size per plane set")
+    nplanes = sum(s.planes_per_group * s.num_groups for s in sets)
+    for s in sets:
+        last = s.base + (s.num_groups - 1) * s.group_stride + (s.planes_per_group - 1) * s.plane_stride + \
+            (s.height - 1) * s.pitch + s.width
+        if s.num_groups and s.width and s.height and last > src.numel():
+            raise ValueError("encode_intra_planes: a plane set reaches past the end of src")
+    if stats is None:
+        stats = torch.zeros((nplanes, ENC_STATS), dtype=torch.int64, device=src.device)
+    _need(stats, torch.int64, "encode_intra_planes(stats)")
+    if stats.numel() < nplanes * ENC_STATS:
+        raise ValueError("encode_intra_planes: stats too small")
+    for t, dt, nm in ((recon, torch.int16, "recon"), (recon_u8, torch.uint8, "recon_u8")):
+        if t is not None:
+            _need(t, dt, f"encode_intra_planes({nm})")
+            if t.numel() < src.numel():
+                raise ValueError(f"encode_intra_planes: {nm} smaller than src")
+    arr = (PlaneSet * len(sets))(*sets)
+    bsz = (C.c_int32 * len(sets))(*[int(b) for b in block_sizes])
+    check(_lib.load().nh_encode_intra_planes(
+        src.data_ptr(), int(src.dtype == torch.uint8), arr, len(sets), bsz,
+        recon.data_ptr() if recon is not None else None, recon_u8.data_ptr() if recon_u8 is not None else None,
+        stats.data_ptr(), C.c_void_p(_stream(stream))))
+    return stats
+
+
+def encode_intra_yuv420(frames, width: int, height: int, block_size: int, recon=None, recon_u8=None,
+                        stream=None):
+    """encode_frame_intra (__main__.py:142-189) on a stream of YUV420p frames laid
+    out back to back in ``frames`` (uint8 bytes straight from a .yuv file, or
+    int16 samples).  Returns stats as an int64 tensor (F, 3, ENC_STATS) for
+    the Y, U and V planes of every frame; ``recon`` (int16) / ``recon_u8``
+    (to_yuv420p bytes) receive the reconstruction when given."""
+    fe = yuv420_frame_elems(width, height)
+    if frames.numel() % fe:
+        raise ValueError("encode_intra_yuv420: size is not a whole number of frames")
+    nf = frames.numel() // fe
+    sets = yuv420_plane_sets(nf, width, height)
+    st = encode_intra_planes(frames, sets, [block_size, chroma_block_size(block_size)], recon, recon_u8,
+                             stream=stream)
+    y, uv = st[:nf], st[nf:].view(nf, 2, ENC_STATS)
+    return _torch().cat([y.view(nf, 1, ENC_STATS), uv], 1)

@@ -16,6 +16,7 @@
  * tests/test_oracle_golden.py.
  */
 #include "nh_oracle.h"
+#include <pthread.h>
 #include <string.h>
 #include <stdlib.h>
 
@@ -310,6 +311,43 @@ void oh_fwd8x8_quant_plane(const int16_t* res, int16_t* lvl, int w, int h, int p
         }
 }
 
+/* Same walk split over nthreads POSIX threads by block row (SURVEY.md §8(d)
+ * D-4: the all-cores CPU baseline).  Block rows are independent (D12), so the
+ * output equals oh_fwd8x8_quant_plane's. */
+typedef struct {
+    const int16_t* res; int16_t* lvl; int w, h, pitch, qp, is_intra, row0, row1;
+} oh_band;
+
+static void* oh_band_run(void* p) {
+    const oh_band* b = (const oh_band*)p;
+    oh_fwd8x8_quant_plane(b->res + (int64_t)b->row0 * 8 * b->pitch, b->lvl + (int64_t)b->row0 * 8 * b->pitch,
+                          b->w, (b->row1 - b->row0) * 8, b->pitch, b->qp, b->is_intra);
+    return NULL;
+}
+
+int oh_fwd8x8_quant_plane_mt(const int16_t* res, int16_t* lvl, int w, int h, int pitch,
+                             int qp, int is_intra, int nthreads) {
+    enum { kMaxThreads = 256 };
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > kMaxThreads) nthreads = kMaxThreads;
+    int rows = h / 8;
+    if (nthreads > rows) nthreads = rows > 0 ? rows : 1;
+    if (!g_dct_init) dct_init();   /* lazy table init stays single-threaded */
+    pthread_t tid[kMaxThreads];
+    oh_band band[kMaxThreads];
+    int spawned[kMaxThreads];
+    for (int t = 0; t < nthreads; ++t) {
+        oh_band b = {res, lvl, w, h, pitch, qp, is_intra, rows * t / nthreads, rows * (t + 1) / nthreads};
+        band[t] = b;
+        /* the last band runs on the caller; a failed spawn runs inline too */
+        spawned[t] = t < nthreads - 1 && pthread_create(&tid[t], NULL, oh_band_run, &band[t]) == 0;
+        if (!spawned[t]) oh_band_run(&band[t]);
+    }
+    for (int t = 0; t < nthreads; ++t)
+        if (spawned[t]) pthread_join(tid[t], NULL);
+    return 0;
+}
+
 /* block.py:38-55 neighbour rules, source plane (open loop, D12). */
 static void get_top(const int16_t* src, int w, int pitch, int x, int y, int count,
                     int64_t* out, int64_t* n) {
@@ -483,4 +521,62 @@ void oh_tc32_plane(const int16_t* src, int w, int h, int pitch, int qp, int32_t*
     for (int by = 0; by + 32 <= h; by += 32)
         for (int bx = 0; bx + 32 <= w; bx += 32) tu_one(src, w, h, pitch, bx, by, 32, qp, 1, lvl, recon, tmap);
     free(tmap);
+}
+
+/* Frame-level intra driver, one plane (__main__.py:142-189 encode_frame_intra;
+ * the demo's per-block loop __main__.py:75-100 is the same decision on luma).
+ * Blocks in raster order (block.py:68-74; partial blocks skipped, their
+ * samples stay 0 in the zero-initialised recon, frame.py:81-88).  Per block:
+ * top/left from the SOURCE plane with 128 at the frame border (block.py:38-50),
+ * DC (intra.py:46-62) and planar with tr=top[-1], bl=left[-1]
+ * (__main__.py:165-168, intra.py:81-113); energies = residual_energy of
+ * residual_block (metrics.py:46-48, intra.py:65-67: int16 wrap); DC wins ties
+ * (__main__.py:171); recon = clip_to_pixel_range(best) (intra.py:75-78).
+ * stats[6] += {blocks, dc wins, planar wins, sum dc energy, sum planar energy,
+ *             SSE of (uint8)src vs (uint8)recon over the whole plane}. */
+void oh_encode_intra_plane(const int16_t* src, int w, int h, int pitch, int N, int16_t* recon,
+                           int64_t* stats) {
+    int l2 = 0;
+    while ((2 << l2) <= N) ++l2;                       /* int(np.log2(size)) */
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) recon[(int64_t)y * pitch + x] = 0;
+    for (int by = 0; by + N <= h; by += N)
+        for (int bx = 0; bx + N <= w; bx += N) {
+            int64_t top[64], left[64], nt, nl, sum = 0;
+            get_top(src, w, pitch, bx, by, N, top, &nt);
+            get_left(src, h, pitch, bx, by, N, left, &nl);
+            for (int i = 0; i < N; ++i) sum += top[i] + left[i];
+            const int64_t dc = floordiv(sum + N, 2 * N);
+            const int64_t tr = top[N - 1], bl = left[N - 1];
+            int64_t edc = 0, epl = 0;
+            for (int i = 0; i < N; ++i)
+                for (int j = 0; j < N; ++j) {
+                    const int64_t o = src[(int64_t)(by + i) * pitch + bx + j];
+                    const int64_t pl = ((N - 1 - j) * left[i] + (j + 1) * tr + (N - 1 - i) * top[j] +
+                                        (i + 1) * bl + N) >> (l2 + 1);
+                    const int64_t rd = (int16_t)(uint16_t)(o - (int16_t)dc);
+                    const int64_t rp = (int16_t)(uint16_t)(o - (int16_t)pl);
+                    edc += rd * rd;
+                    epl += rp * rp;
+                }
+            const int use_dc = edc <= epl;
+            for (int i = 0; i < N; ++i)
+                for (int j = 0; j < N; ++j) {
+                    int64_t p = use_dc ? dc : ((N - 1 - j) * left[i] + (j + 1) * tr + (N - 1 - i) * top[j] +
+                                               (i + 1) * bl + N) >> (l2 + 1);
+                    p = (int16_t)p;                         /* the predictor's int16 store */
+                    recon[(int64_t)(by + i) * pitch + bx + j] = (int16_t)(p < 0 ? 0 : p > 255 ? 255 : p);
+                }
+            stats[0] += 1;
+            stats[1] += use_dc;
+            stats[2] += !use_dc;
+            stats[3] += edc;
+            stats[4] += epl;
+        }
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            const int64_t d = (int64_t)(uint8_t)src[(int64_t)y * pitch + x] -
+                              (int64_t)(uint8_t)recon[(int64_t)y * pitch + x];
+            stats[5] += d * d;
+        }
 }

@@ -47,16 +47,19 @@ def lib():
             "oh_quantize": [P, i64, i32, i64, i32, i32, P],
             "oh_dequantize": [P, i64, i32, P],
             "oh_fwd8x8_quant_plane": [P, P, i32, i32, i32, i32, i32],
+            "oh_fwd8x8_quant_plane_mt": [P, P, i32, i32, i32, i32, i32, i32],
             "oh_intra_rdo_plane": [P, i32, i32, i32, i32, P, P, P, P],
             "oh_tu_pipeline_plane": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P],
             "oh_tu_split": [C.c_uint32, i32, i32, i32, i32],
             "oh_tc32_plane": [P, i32, i32, i32, i32, P, P],
+            "oh_encode_intra_plane": [P, i32, i32, i32, i32, P, P],
         }
         for name, args in sig.items():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = None if name in ("oh_residual", "oh_reconstruct", "oh_clip", "oh_fwd8x8_quant_plane",
-                                         "oh_intra_rdo_plane", "oh_tu_pipeline_plane", "oh_tc32_plane") else C.c_int
+                                         "oh_intra_rdo_plane", "oh_tu_pipeline_plane", "oh_tc32_plane",
+                                         "oh_encode_intra_plane") else C.c_int
         _lib = L
     return _lib
 
@@ -175,6 +178,14 @@ def fwd8x8_quant_plane(res, qp=32, is_intra=True):
     return out
 
 
+def fwd8x8_quant_plane_mt(res, qp=32, is_intra=True, nthreads=1):
+    res = np.ascontiguousarray(res, np.int16)
+    h, w = res.shape
+    out = np.zeros_like(res)
+    _check(lib().oh_fwd8x8_quant_plane_mt(_p(res), _p(out), w, h, w, int(qp), int(is_intra), int(nthreads)))
+    return out
+
+
 def intra_rdo_plane(src, qp=32):
     src = np.ascontiguousarray(src, np.int16)
     h, w = src.shape
@@ -208,3 +219,24 @@ def tc32_plane(src, qp=32):
     rec = np.zeros(src.shape, np.int16)
     lib().oh_tc32_plane(_p(src), w, h, w, int(qp), _p(lvl), _p(rec))
     return lvl, rec
+
+
+def encode_intra_plane(src, block_size):
+    """One plane of encode_frame_intra; returns (recon int16, stats int64[6])."""
+    src = np.ascontiguousarray(src).astype(np.int16)
+    h, w = src.shape
+    rec = np.zeros(src.shape, np.int16)
+    st = np.zeros(6, np.int64)
+    lib().oh_encode_intra_plane(_p(src), w, h, w, int(block_size), _p(rec), _p(st))
+    return rec, st
+
+
+def encode_frame_intra(y, u, v, block_size):
+    """encode_frame_intra (__main__.py:142-189): chroma block = max(4, bs // 2)."""
+    out, tot = [], np.zeros(6, np.int64)
+    for k, p in enumerate((y, u, v)):
+        bs = block_size if k == 0 else max(4, block_size // 2)
+        r, st = encode_intra_plane(p, bs)
+        out.append(r)
+        tot += st
+    return out, tot

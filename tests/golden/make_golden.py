@@ -381,6 +381,58 @@ def gen_metrics(M):
     return out
 
 
+def gen_encode(ref_path):
+    """The reference's frame-level intra driver (__main__.py:142-189,
+    encode_frame_intra: DC vs planar per block, open loop, recon = clip(best
+    pred), partial blocks left 0) and the demo's totals (__main__.py:55-139,
+    parsed from its printed report).  Own rng (other fixtures unchanged)."""
+    import contextlib
+    import io
+    import re
+    from nano_hevc import __main__ as R   # the reference's driver module
+    from nano_hevc.frame import Frame, Plane
+    assert os.path.abspath(R.__file__).startswith(os.path.abspath(ref_path)), R.__file__
+    rng = np.random.default_rng(777)
+    out = {}
+    cases = []
+    # (a) random 8-bit YUV420p bytes with ragged dims (partial blocks at 16/32)
+    w, h = 72, 40
+    raw = rng.integers(0, 256, size=w * h * 3 // 2).astype(np.uint8).tobytes()
+    out["e_a_yuv"] = np.frombuffer(raw, np.uint8).copy()
+    for bs in (4, 8, 16, 32):
+        cases.append(("a", bs, Frame.from_yuv420p(raw, h, w)))
+    # (b) the reference's demo frame (int16 planes)
+    fb = R.create_test_frame(48, 80)
+    out["e_b_y"], out["e_b_u"], out["e_b_v"] = fb.y.data, fb.u.data, fb.v.data
+    for bs in (4, 8, 16):
+        cases.append(("b", bs, fb))
+    # (c) full-range int16 planes (residual_block's int16 wrap)
+    fc = Frame(Plane(rng.integers(-32768, 32768, size=(32, 48)).astype(np.int16)),
+               Plane(rng.integers(-32768, 32768, size=(16, 24)).astype(np.int16)),
+               Plane(rng.integers(-32768, 32768, size=(16, 24)).astype(np.int16)))
+    out["e_c_y"], out["e_c_u"], out["e_c_v"] = fc.y.data, fc.u.data, fc.v.data
+    cases.append(("c", 8, fc))
+    for tag, bs, fr in cases:
+        recon, stats = R.encode_frame_intra(fr, bs)
+        k = f"e_{tag}_bs{bs}"
+        out[k + "_ry"], out[k + "_ru"], out[k + "_rv"] = recon.y.data, recon.u.data, recon.v.data
+        out[k + "_stats"] = np.array([stats["blocks"], stats["dc"], stats["planar"]], np.int64)
+        out[k + "_psnr_y"] = np.float64(R.psnr(fr.y.data.astype(np.uint8), recon.y.data.astype(np.uint8)))
+    # demo_predictions report (luma only): wins and total energies, PSNR text
+    for (dh, dw, bs) in ((64, 64, 8), (48, 80, 4), (72, 40, 16)):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            R.demo_predictions(dh, dw, bs)
+        txt = buf.getvalue()
+        out[f"d_{dh}x{dw}_bs{bs}_y"] = R.create_test_frame(dh, dw).y.data
+        num = lambda pat: int(re.search(pat, txt).group(1).replace(",", ""))
+        out[f"d_{dh}x{dw}_bs{bs}"] = np.array([
+            num(r"Total blocks:\s+(\d+)"), num(r"DC wins:\s+(\d+)"), num(r"Planar wins:\s+(\d+)"),
+            num(r"DC total residual energy:\s+([\d,]+)"), num(r"Planar total residual energy:\s+([\d,]+)")], np.int64)
+        out[f"d_{dh}x{dw}_bs{bs}_psnr_text"] = np.array(re.search(r"PSNR \(best mode\): (\S+) dB", txt).group(1))
+    return out
+
+
 def plane_hash_1080p(T, Q):
     rng = np.random.default_rng(20260)
     plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
@@ -402,6 +454,7 @@ def main():
         "planes.npz": gen_planes(I, T, Q, rng),
         "metrics.npz": gen_metrics(M),
         "cfg5.npz": gen_cfg5(I, T, Q, M),
+        "encode.npz": gen_encode(ref),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

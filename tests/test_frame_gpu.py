@@ -1,0 +1,129 @@
+"""GPU parity for the frame-level rows:
+
+* encode_frame_intra (__main__.py:142-189) through nh_encode_intra_planes
+  against the reference's recorded outputs (tests/golden/encode.npz: recon
+  planes, stats, Y-PSNR, the demo's printed totals) and the CPU restatement
+  (oracle/) on multi-frame streams;
+* the YUV420p byte <-> int16 casts (frame.py astype) against numpy.
+Bit-exact everywhere (integer work; PSNR compared as float64 equality)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402  (checker only)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    from nano_hevc import _lib
+    assert _lib.device_count() > 0 and torch.cuda.is_available(), "the gpu tests need an MI355X"
+    return torch
+
+
+def _frame_case(g, tag):
+    from nano_hevc.frame import Frame, Plane
+    if tag == "a":   # uint8 planes, as Frame.from_yuv420p builds them
+        return Frame.from_yuv420p(g["e_a_yuv"].tobytes(), 40, 72)
+    return Frame(Plane(g[f"e_{tag}_y"]), Plane(g[f"e_{tag}_u"]), Plane(g[f"e_{tag}_v"]))
+
+
+@pytest.mark.parametrize("tag,bs", [("a", 4), ("a", 8), ("a", 16), ("a", 32), ("b", 4), ("b", 8), ("b", 16),
+                                    ("c", 8)])
+def test_encode_frame_intra_golden(torch_dev, golden, tag, bs):
+    from nano_hevc.encoder import encode_frame_intra
+    from nano_hevc.metrics import psnr
+    g = golden("encode.npz")
+    fr = _frame_case(g, tag)
+    recon, stats = encode_frame_intra(fr, bs)
+    k = f"e_{tag}_bs{bs}"
+    for pl, s in ((recon.y, "_ry"), (recon.u, "_ru"), (recon.v, "_rv")):
+        assert pl.data.dtype == np.int16
+        assert np.array_equal(pl.data, g[k + s]), (k, s)
+    assert [stats["blocks"], stats["dc"], stats["planar"]] == list(g[k + "_stats"])
+    assert psnr(fr.y.data.astype(np.uint8), recon.y.data.astype(np.uint8)) == g[k + "_psnr_y"]
+
+
+@pytest.mark.parametrize("key", ["d_64x64_bs8", "d_48x80_bs4", "d_72x40_bs16"])
+def test_demo_totals_golden(torch_dev, golden, key):
+    from nano_hevc.encoder import create_test_frame, prediction_stats
+    g = golden("encode.npz")
+    h, w = (int(v) for v in key.split("_")[1].split("x"))
+    bs = int(key.split("bs")[1])
+    fr = create_test_frame(h, w)
+    assert np.array_equal(fr.y.data, g[key + "_y"])
+    st = prediction_stats(fr.y, bs)
+    assert [st["blocks"], st["dc_wins"], st["planar_wins"], st["dc_energy"], st["planar_energy"]] == list(g[key])
+    assert f"{st['psnr']:.2f}" == str(g[key + "_psnr_text"])
+
+
+def _synth_stream(torch, nf, w, h, seed, kind):
+    rng = np.random.default_rng(seed)
+    fe = w * h + 2 * (w // 2) * (h // 2)
+    if kind == "noise":
+        return rng.integers(0, 256, size=nf * fe).astype(np.uint8)
+    out = []
+    for f in range(nf):   # gradient + noise "natural" content per plane
+        for (pw, ph) in ((w, h), (w // 2, h // 2), (w // 2, h // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            out.append(np.clip(60 + (3 * xx + 2 * yy + 17 * f) % 150 + rng.integers(-9, 10, (ph, pw)), 0, 255)
+                       .astype(np.uint8).reshape(-1))
+    return np.concatenate(out)
+
+
+@pytest.mark.parametrize("w,h,bs,kind,src_i16", [(352, 288, 8, "natural", False), (200, 136, 16, "noise", False),
+                                                  (104, 72, 32, "natural", True), (96, 40, 4, "noise", True),
+                                                  (128, 128, 64, "natural", False)])
+def test_encode_stream_vs_oracle(torch_dev, w, h, bs, kind, src_i16):
+    from nano_hevc import gpu
+    torch = torch_dev
+    nf = 3
+    host = _synth_stream(torch, nf, w, h, 11 + bs, kind)
+    dev = torch.from_numpy(host).cuda()
+    if src_i16:
+        dev = gpu.widen_u8(dev)
+    rec = torch.full((dev.numel(),), -7, dtype=torch.int16, device="cuda")
+    rec8 = torch.zeros((dev.numel(),), dtype=torch.uint8, device="cuda")
+    st = gpu.encode_intra_yuv420(dev, w, h, bs, recon=rec, recon_u8=rec8).cpu().numpy()
+    rec_h, rec8_h = rec.cpu().numpy(), rec8.cpu().numpy()
+    fe = gpu.yuv420_frame_elems(w, h)
+    cw, ch = w // 2, h // 2
+    for f in range(nf):
+        fr = host[f * fe:(f + 1) * fe]
+        parts = [(0, h, w, bs), (w * h, ch, cw, gpu.chroma_block_size(bs)),
+                 (w * h + cw * ch, ch, cw, gpu.chroma_block_size(bs))]
+        for k, (o, ph, pw, pbs) in enumerate(parts):
+            r, s = O.encode_intra_plane(fr[o:o + ph * pw].reshape(ph, pw), pbs)
+            assert np.array_equal(rec_h[f * fe + o:f * fe + o + ph * pw].reshape(ph, pw), r), (f, k)
+            assert np.array_equal(rec8_h[f * fe + o:f * fe + o + ph * pw], r.reshape(-1).astype(np.uint8))
+            assert np.array_equal(st[f, k], s), (f, k, st[f, k], s)
+
+
+def test_encode_4k_stream_stats_vs_oracle(torch_dev):
+    """Full-size (4K YUV420) stream: every plane's stats word equals the oracle's."""
+    from nano_hevc import gpu
+    torch = torch_dev
+    w, h, nf = 3840, 2160, 2
+    host = _synth_stream(torch, nf, w, h, 5, "natural")
+    st = gpu.encode_intra_yuv420(torch.from_numpy(host).cuda(), w, h, 8).cpu().numpy()
+    fe = gpu.yuv420_frame_elems(w, h)
+    for f in range(nf):
+        fr = host[f * fe:(f + 1) * fe]
+        _, s = O.encode_intra_plane(fr[:w * h].reshape(h, w), 8)
+        assert np.array_equal(st[f, 0], s)
+
+
+@pytest.mark.parametrize("n,off", [(0, 0), (1, 0), (15, 0), (16, 0), (4097, 0), (3 * 1920 * 1080 // 2, 0),
+                                   (1000, 3), (777, 1)])
+def test_widen_narrow_vs_numpy(torch_dev, n, off):
+    from nano_hevc import gpu
+    torch = torch_dev
+    rng = np.random.default_rng(n + off)
+    b = rng.integers(0, 256, size=n + off).astype(np.uint8)
+    src = torch.from_numpy(b).cuda()[off:]          # misaligned views take the scalar path
+    w = gpu.widen_u8(src.contiguous() if off == 0 else src)
+    assert np.array_equal(w.cpu().numpy(), b[off:].astype(np.int16))
+    v = rng.integers(-32768, 32768, size=n + off).astype(np.int16)
+    t = torch.from_numpy(v).cuda()[off:]
+    assert np.array_equal(gpu.narrow_u8(t).cpu().numpy(), v[off:].astype(np.uint8))

@@ -194,3 +194,40 @@ def test_cfg5_plane(golden):
     for qp in (22, 37):
         l, r = O.tc32_plane(g["p5_src"], qp)
         assert np.array_equal(l, g[f"p5_lvl_qp{qp}"]) and np.array_equal(r, g[f"p5_rec_qp{qp}"]), qp
+
+
+@pytest.mark.parametrize("threads", [2, 3, 8, 64])
+def test_oracle_threaded_plane_equals_single(threads):
+    """The all-cores CPU baseline (bench.py cpu_baseline) computes what the
+    single-thread restatement does, ragged plane sizes included."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(99)
+    for h, w in ((72, 104), (37, 50), (8, 8), (7, 64)):
+        r = rng.integers(-32768, 32768, (h, w)).astype(np.int16)
+        assert np.array_equal(O.fwd8x8_quant_plane_mt(r, 27, False, threads), O.fwd8x8_quant_plane(r, 27, False))
+
+
+def test_oracle_encode_frame_intra_golden(golden):
+    """oh_encode_intra_plane against the reference's encode_frame_intra outputs
+    (recon planes, stats, Y-PSNR) and the demo's printed totals."""
+    g = golden("encode.npz")
+    raw = g["e_a_yuv"]
+    w, h = 72, 40
+    ys, cs = w * h, (w // 2) * (h // 2)
+    frames = {"a": (raw[:ys].reshape(h, w), raw[ys:ys + cs].reshape(h // 2, w // 2), raw[ys + cs:].reshape(h // 2, w // 2))}
+    for t in "bc":
+        frames[t] = (g[f"e_{t}_y"], g[f"e_{t}_u"], g[f"e_{t}_v"])
+    for tag, bss in (("a", (4, 8, 16, 32)), ("b", (4, 8, 16)), ("c", (8,))):
+        y, u, v = frames[tag]
+        for bs in bss:
+            k = f"e_{tag}_bs{bs}"
+            (ry, ru, rv), st = O.encode_frame_intra(y, u, v, bs)
+            for a, s in ((ry, "_ry"), (ru, "_ru"), (rv, "_rv")):
+                assert np.array_equal(a, g[k + s]), (k, s)
+            assert list(st[:3]) == list(g[k + "_stats"])
+            _, sy = O.encode_intra_plane(y, bs)
+            assert 10 * np.log10(255 ** 2 / (np.float64(sy[5]) / np.float64(y.size))) == g[k + "_psnr_y"]
+    for key in ("d_64x64_bs8", "d_48x80_bs4", "d_72x40_bs16"):
+        _, st = O.encode_intra_plane(g[key + "_y"], int(key.split("bs")[1]))
+        assert list(st[:5]) == list(g[key])
+        assert f"{10 * np.log10(255 ** 2 / (np.float64(st[5]) / g[key + '_y'].size)):.2f}" == str(g[key + "_psnr_text"])

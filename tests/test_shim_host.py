@@ -71,3 +71,25 @@ def test_frame_containers_roundtrip():
     pool.release(i)
     with pytest.raises(ValueError):
         pool.release(i)
+
+
+def test_create_test_frame_matches_reference(golden):
+    """encoder.create_test_frame (host data generation) == the reference's demo frame."""
+    from nano_hevc.encoder import create_test_frame
+    g = golden("encode.npz")
+    fb = create_test_frame(48, 80)
+    for p, k in ((fb.y, "e_b_y"), (fb.u, "e_b_u"), (fb.v, "e_b_v")):
+        assert p.data.dtype == np.int16 and np.array_equal(p.data, g[k])
+    for key in ("d_64x64_bs8", "d_48x80_bs4", "d_72x40_bs16"):
+        h, w = (int(v) for v in key.split("_")[1].split("x"))
+        assert np.array_equal(create_test_frame(h, w).y.data, g[key + "_y"])
+
+
+def test_encoder_fails_loudly_without_device():
+    """No CPU fallback for the frame driver either."""
+    import torch
+    from nano_hevc.encoder import create_test_frame, encode_frame_intra
+    if torch.cuda.is_available():
+        pytest.skip("a device is present")
+    with pytest.raises(Exception):
+        encode_frame_intra(create_test_frame(16, 16), 8)

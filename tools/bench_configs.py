@@ -6,6 +6,10 @@
   cfg5  8K YUV420, every 32x32 block through the chain: butterfly vs int8-MFMA,
         plus the frame's Y-PSNR (metrics.psnr semantics) for both variants and,
         with --check, the oracle's PSNR on the same frame.
+  enc   encode_frame_intra (__main__.py:142-189, DC vs planar per block, 8x8 luma /
+        4x4 chroma) over a stream of 4K YUV420p byte frames -> int16 recon + stats;
+        HBM roofline at 3 B/sample (1 B source read + 2 B recon write).
+  io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
 
 Synthetic 8-bit content (gradient + seeded noise) resident in HBM; HIP events
 on the launch stream; one JSON line per config.
@@ -64,12 +68,13 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
-    ap.add_argument("--configs", default="3,4,5")
+    ap.add_argument("--configs", default="3,4,5,enc,io")
+    ap.add_argument("--enc-frames", type=int, default=64)
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     _lib.load()
     torch.cuda.set_device(0)
-    cfgs = {int(c) for c in args.configs.split(",")}
+    cfgs = {int(c) if c.isdigit() else c for c in args.configs.split(",")}
 
     if 3 in cfgs:
         W, H = 1920, 1080
@@ -140,6 +145,51 @@ def main():
             line["psnr_y_oracle"] = float(10 * np.log10(255 ** 2 / mse))
             line["psnr_matches_oracle"] = line["psnr_y_oracle"] == res["mfma_i8"]["psnr_y"]
         print(json.dumps(line), flush=True)
+
+    if "enc" in cfgs or "io" in cfgs:
+        W, H = 3840, 2160
+        nf = args.enc_frames
+        fe = gpu.yuv420_frame_elems(W, H)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(17)
+        planes = []
+        for pw, ph, sd in ((W, H, 1), (W // 2, H // 2, 2), (W // 2, H // 2, 3)):
+            planes.append(synth_plane(ph, pw, sd).to(torch.uint8).reshape(-1))
+        frame = torch.cat(planes)
+        stream_u8 = frame.repeat(nf)
+        samples = stream_u8.numel()
+        if "enc" in cfgs:
+            rec = torch.empty(samples, dtype=torch.int16, device="cuda")
+            stats = torch.zeros((2 * nf + nf, gpu.ENC_STATS), dtype=torch.int64, device="cuda")
+            sets = gpu.yuv420_plane_sets(nf, W, H)
+
+            def run_enc():
+                gpu.encode_intra_planes(stream_u8, sets, [8, 4], recon=rec, stats=stats)
+            ms = timed(run_enc, args.reps)
+            stats.zero_()
+            st = gpu.encode_intra_yuv420(stream_u8[:fe], W, H, 8).cpu().numpy()
+            mse = np.float64(st[0, 0, 5]) / np.float64(W * H)
+            gbs = samples * 3 / ms / 1e6
+            print(json.dumps({"config": "enc: encode_frame_intra (DC vs planar, 8x8 luma / 4x4 chroma) over a 4K "
+                                        "YUV420p uint8 stream -> int16 recon + per-plane stats",
+                              "frames": nf, "ms_per_launch": ms, "frames_per_s": nf / ms * 1e3,
+                              "blocks_per_s": int(st[0, :, 0].sum()) * nf / ms * 1e3,
+                              "roofline": {"bound": "hbm", "bytes_per_sample": 3, "achieved_GBps": gbs,
+                                           "peak_GBps": 8000.0, "frac": gbs / 8000.0},
+                              "frame0": {"blocks": int(st[0, :, 0].sum()), "dc": int(st[0, :, 1].sum()),
+                                         "planar": int(st[0, :, 2].sum()),
+                                         "psnr_y": float(10 * np.log10(255 ** 2 / mse))}}), flush=True)
+        if "io" in cfgs:
+            wide = torch.empty(samples, dtype=torch.int16, device="cuda")
+            back = torch.empty(samples, dtype=torch.uint8, device="cuda")
+            ms_w = timed(lambda: gpu.widen_u8(stream_u8, out=wide), args.reps)
+            ms_n = timed(lambda: gpu.narrow_u8(wide, out=back), args.reps)
+            ok = bool(torch.equal(back, stream_u8))
+            print(json.dumps({"config": "io: YUV420p bytes <-> int16 planes (frame.py astype casts), 4K stream",
+                              "frames": nf, "widen_ms": ms_w, "narrow_ms": ms_n,
+                              "widen_GBps": samples * 3 / ms_w / 1e6, "narrow_GBps": samples * 3 / ms_n / 1e6,
+                              "frac_widen": samples * 3 / ms_w / 1e6 / 8000.0,
+                              "frac_narrow": samples * 3 / ms_n / 1e6 / 8000.0, "round_trip_exact": ok}), flush=True)
 
 
 if __name__ == "__main__":
