@@ -373,22 +373,251 @@ __global__ void __launch_bounds__(256) k_encode_small(EncArgs a) {
     }
 }
 
-// Blocks per lane for N = 4 / 8 (loads in flight vs registers).  Tuning knob
-// for measurement: NH_ENC_UNROLL="u4,u8" (each 1, 2 or 4), read once.
-static void small_unroll(int& u4, int& u8) {
-    static int c4 = 0, c8 = 0;
-    if (!c4) {
-        int a = 4, b = 2;
-        if (const char* e = getenv("NH_ENC_UNROLL")) sscanf(e, "%d,%d", &a, &b);
-        c4 = (a == 1 || a == 2 || a == 4) ? a : 4;
-        c8 = (b == 1 || b == 2 || b == 4) ? b : 2;
+// 8-bit sources (YUV420p bytes -- the reference CLI's input), N in {4, 8}:
+// the same lane-per-block walk in packed 16-bit arithmetic.  Samples are
+// unpacked two per dword (v_perm); planar numerators
+//   ((N-1-x)L + (x+1)tr + N + (y+1)bl) + (N-1-y)T[x]  <= 2N*255 + N < 2^16
+// come from two v_pk_mad_u16 (exact mod 2^16, hence exact) and a packed
+// shift; residual energies accumulate with v_dot2_i32_i16.  A weighted
+// average of 8-bit neighbours lies in [0, 255], so clip_to_pixel_range is the
+// identity and the int16 recon pairs are stored as computed.
+typedef unsigned short v2us __attribute__((ext_vector_type(2)));
+typedef short v2s __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2us as_us(unsigned v) { return __builtin_bit_cast(v2us, v); }
+__device__ __forceinline__ v2s as_s(v2us v) { return __builtin_bit_cast(v2s, v); }
+__device__ __forceinline__ unsigned as_u(v2us v) { return __builtin_bit_cast(unsigned, v); }
+__device__ __forceinline__ v2us pair_u8(unsigned w, int k) {   // bytes 2k, 2k+1 of w, zero-extended
+    return as_us(__builtin_amdgcn_perm(0u, w, k ? 0x0c030c02u : 0x0c010c00u));
+}
+
+template <int N>
+struct BlkU8 {   // one block's raw rows (4 samples per dword) and top row
+    unsigned o[N][N / 4], top[N / 4];
+    int x0, y0;
+    bool act, full;
+};
+
+template <int N>
+__device__ __forceinline__ void load_blk_u8(const EncArgs& a, const uint8_t* src, uint32_t b, BlkU8<N>& k) {
+    constexpr int W = N / 4;
+    k.act = b < a.nblk;
+    const uint32_t by = k.act ? fdiv(b, a.nbx) : 0, bx = k.act ? b - by * a.nbx.d : 0;
+    k.x0 = bx * N;
+    k.y0 = by * N;
+    k.full = k.act && k.x0 + N <= a.w && k.y0 + N <= a.h;
+    const uint8_t* blk = src + (int64_t)k.y0 * a.pitch + k.x0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        if constexpr (W == 1) {
+            k.o[i][0] = k.full ? *(const unsigned*)(blk + (int64_t)i * a.pitch) : 0u;
+        } else {
+            const v2u r = k.full ? *(const v2u*)(blk + (int64_t)i * a.pitch) : v2u{0u, 0u};
+            k.o[i][0] = r[0];
+            k.o[i][1] = r[1];
+        }
     }
-    u4 = c4;
-    u8 = c8;
+    if constexpr (W == 1) {
+        k.top[0] = k.full && k.y0 > 0 ? *(const unsigned*)(blk - a.pitch) : 0x80808080u;
+    } else {
+        const v2u r = k.full && k.y0 > 0 ? *(const v2u*)(blk - a.pitch) : v2u{0x80808080u, 0x80808080u};
+        k.top[0] = r[0];
+        k.top[1] = r[1];
+    }
+}
+
+struct EncStats {
+    int64_t blocks = 0, dc = 0, edc = 0, epl = 0, sse = 0;
+};
+
+// Decide one block per lane and store its recon row by row.  Every lane of the
+// wave must call this (the left column comes from the previous lane).
+template <int N>
+__device__ __forceinline__ void decide_blk_u8(const EncArgs& a, const uint8_t* src, int64_t off, int lane,
+                                              const BlkU8<N>& k, EncStats& st) {
+    constexpr int L2 = N == 4 ? 2 : 3, W = N / 4;
+    int left[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) left[i] = (int)(__shfl_up(k.o[i][W - 1], 1, 64) >> 24);
+    if (k.x0 == 0) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) left[i] = 128;
+    } else if (lane == 0 && k.full) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) left[i] = src[(int64_t)(k.y0 + i) * a.pitch + k.x0 - 1];
+    }
+    unsigned tsum = 0;
+#pragma unroll
+    for (int q = 0; q < W; ++q) tsum = __builtin_amdgcn_udot4(k.top[q], 0x01010101u, tsum, false);
+    int lsum = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) lsum += left[i];
+    const unsigned dc = (tsum + lsum + N) >> (L2 + 1);
+    const unsigned tr = k.top[W - 1] >> 24, bl = left[N - 1];
+    const v2us dc2 = {(unsigned short)dc, (unsigned short)dc};
+    v2us T2[N / 2], X2[N / 2];
+#pragma unroll
+    for (int q = 0; q < N / 2; ++q) {
+        T2[q] = pair_u8(k.top[q >> 1], q & 1);
+        X2[q] = v2us{(unsigned short)(2 * q), (unsigned short)(2 * q + 1)};
+    }
+    // row y: num(x) = [(N-1)L + tr + N + (y+1)bl] + x(tr - L) + (N-1-y) T[x]
+    auto planar_row = [&](int y, int q) -> v2us {
+        const unsigned short cy = (unsigned short)((N - 1) * left[y] + tr + N + (y + 1) * bl);
+        const unsigned short dy = (unsigned short)(tr - left[y]);
+        const unsigned short sy = (unsigned short)(N - 1 - y);
+        const v2us c2 = {cy, cy}, d2 = {dy, dy}, s2 = {sy, sy};
+        return (T2[q] * s2 + (X2[q] * d2 + c2)) >> (unsigned short)(L2 + 1);
+    };
+    int edc = 0, epl = 0;
+#pragma unroll
+    for (int y = 0; y < N; ++y)
+#pragma unroll
+        for (int q = 0; q < N / 2; ++q) {
+            const v2us o2 = pair_u8(k.o[y][q >> 1], q & 1);
+            const v2s rd = as_s(o2 - dc2), rp = as_s(o2 - planar_row(y, q));
+            edc = __builtin_amdgcn_sdot2(rd, rd, edc, false);
+            epl = __builtin_amdgcn_sdot2(rp, rp, epl, false);
+        }
+    if (k.full) {
+        const bool use_dc = edc <= epl;
+        int sse = 0;
+#pragma unroll
+        for (int y = 0; y < N; ++y) {
+            unsigned rv[N / 2];
+#pragma unroll
+            for (int q = 0; q < N / 2; ++q) {
+                const v2us v = use_dc ? dc2 : planar_row(y, q);
+                const v2s d = as_s(pair_u8(k.o[y][q >> 1], q & 1) - v);
+                sse = __builtin_amdgcn_sdot2(d, d, sse, false);
+                rv[q] = as_u(v);
+            }
+            const int64_t i = off + (int64_t)(k.y0 + y) * a.pitch + k.x0;
+            if (a.rec) {
+                if constexpr (N == 4) __builtin_nontemporal_store(v2u{rv[0], rv[1]}, (v2u*)(a.rec + i));
+                else __builtin_nontemporal_store(v4u{rv[0], rv[1], rv[2], rv[3]}, (v4u*)(a.rec + i));
+            }
+            if (a.rec8) {
+                if constexpr (N == 4) *(unsigned*)(a.rec8 + i) = __builtin_amdgcn_perm(rv[1], rv[0], 0x06040200u);
+                else *(v2u*)(a.rec8 + i) = v2u{__builtin_amdgcn_perm(rv[1], rv[0], 0x06040200u),
+                                               __builtin_amdgcn_perm(rv[3], rv[2], 0x06040200u)};
+            }
+        }
+        st.sse += sse;
+        st.blocks += 1;
+        st.dc += use_dc;
+        st.edc += edc;
+        st.epl += epl;
+    } else if (k.act) {   // samples outside full blocks: recon stays 0
+        for (int y = k.y0; y < k.y0 + N && y < a.h; ++y)
+            for (int x = k.x0; x < k.x0 + N && x < a.w; ++x) {
+                const int64_t i = (int64_t)y * a.pitch + x;
+                if (a.rec) a.rec[off + i] = 0;
+                if (a.rec8) a.rec8[off + i] = 0;
+                const int d = src[i];
+                st.sse += d * d;
+            }
+    }
+}
+
+__device__ __forceinline__ void flush_enc_stats(const EncArgs& a, int p, EncStats st) {
+    __shared__ int64_t part[4][5];
+    const int lane = threadIdx.x & 63;
+    int64_t v[5] = {st.blocks, st.dc, st.edc, st.epl, st.sse};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        for (int m = 32; m > 0; m >>= 1) v[k] += __shfl_xor(v[k], m, 64);
+        if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t[5];
+        for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+        int64_t* s = a.stats + (int64_t)p * NH_ENC_STATS;
+        const int64_t add[NH_ENC_STATS] = {t[0], t[1], t[0] - t[1], t[2], t[3], t[4]};
+        for (int k = 0; k < NH_ENC_STATS; ++k)
+            if (add[k]) atomicAdd((unsigned long long*)(s + k), (unsigned long long)add[k]);
+    }
+}
+
+// U blocks per lane per pass, loads first; PIPE: the next pass's blocks are
+// loaded before this pass's blocks are decided (the grid is capped so that a
+// workgroup makes several passes).
+template <int N, int U, bool PIPE>
+__global__ void __launch_bounds__(256) k_encode_u8(EncArgs a) {
+    const int p = blockIdx.y;
+    const int g = p / a.ppg, c = p - g * a.ppg;
+    const int64_t off = a.base + (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
+    const uint8_t* src = static_cast<const uint8_t*>(a.src) + off;
+    const int lane = threadIdx.x & 63;
+    const uint32_t stride = gridDim.x * 256u * U;
+    EncStats st;
+    uint32_t b0 = blockIdx.x * 256u * U;
+    BlkU8<N> cur[U];
+    if (PIPE && b0 < a.nblk) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_blk_u8<N>(a, src, b0 + u * 256u + threadIdx.x, cur[u]);
+    }
+    for (; b0 < a.nblk; b0 += stride) {
+        BlkU8<N> nxt[U];
+        if constexpr (PIPE) {
+            if (b0 + stride < a.nblk) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) load_blk_u8<N>(a, src, b0 + stride + u * 256u + threadIdx.x, nxt[u]);
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) load_blk_u8<N>(a, src, b0 + u * 256u + threadIdx.x, cur[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) decide_blk_u8<N>(a, src, off, lane, cur[u], st);
+        if constexpr (PIPE) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+    }
+    flush_enc_stats(a, p, st);
+}
+
+// Launch shape of the N = 4 / 8 kernels: blocks per lane per pass (u4, u8),
+// prefetching form (pipe) and its total workgroup cap.  Tuning knob for
+// measurement: NH_ENC_TUNE="u4,u8,pipe,cap", read once.
+struct EncTune {
+    int u4 = 1, u8 = 1, pipe = 1, cap = 4096;   // measured best (profiles/r01/frame)
+};
+static const EncTune& enc_tune() {
+    static EncTune t;
+    static bool init = false;
+    if (!init) {
+        init = true;
+        if (const char* e = getenv("NH_ENC_TUNE")) {
+            EncTune r;
+            if (sscanf(e, "%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap) >= 2 &&
+                (r.u4 == 1 || r.u4 == 2 || r.u4 == 4) && (r.u8 == 1 || r.u8 == 2 || r.u8 == 4) && r.cap > 0)
+                t = r;
+        }
+    }
+    return t;
+}
+static void small_unroll(int& u4, int& u8) {
+    u4 = enc_tune().u4;
+    u8 = enc_tune().u8;
 }
 
 template <class T, int N, bool AL>
 static void launch_small(int u, const EncArgs& a, dim3 grid, hipStream_t s) {
+    if constexpr (std::is_same<T, uint8_t>::value && AL) {   // packed 16-bit path
+        if (enc_tune().pipe) {
+            if (u == 1) k_encode_u8<N, 1, true><<<grid, 256, 0, s>>>(a);
+            else if (u == 2) k_encode_u8<N, 2, true><<<grid, 256, 0, s>>>(a);
+            else k_encode_u8<N, 4, true><<<grid, 256, 0, s>>>(a);
+        } else {
+            if (u == 1) k_encode_u8<N, 1, false><<<grid, 256, 0, s>>>(a);
+            else if (u == 2) k_encode_u8<N, 2, false><<<grid, 256, 0, s>>>(a);
+            else k_encode_u8<N, 4, false><<<grid, 256, 0, s>>>(a);
+        }
+        return;
+    }
     if (u == 1) k_encode_small<T, N, 1, AL><<<grid, 256, 0, s>>>(a);
     else if (u == 2) k_encode_small<T, N, 2, AL><<<grid, 256, 0, s>>>(a);
     else k_encode_small<T, N, 4, AL><<<grid, 256, 0, s>>>(a);
@@ -493,7 +722,10 @@ int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set*
         small_unroll(u4, u8);
         const int64_t per_wg = n == 4 ? 256 * u4 : n == 8 ? 256 * u8 : 256 / n;   // blocks per workgroup pass
         const int64_t wgs = (nblk + per_wg - 1) / per_wg;
-        const dim3 grid((unsigned)std::min<int64_t>(wgs, 512), (unsigned)planes);
+        int64_t cap = 512;   // <= 512 workgroups (atomics) per plane
+        if (src_is_u8 && al && (n == 4 || n == 8) && enc_tune().pipe)
+            cap = std::max<int64_t>(1, std::min<int64_t>(512, enc_tune().cap / planes));
+        const dim3 grid((unsigned)std::min<int64_t>(wgs, cap), (unsigned)planes);
         const int rc = src_is_u8 ? launch_encode<uint8_t>(n, al, a, grid, s) : launch_encode<int16_t>(n, al, a, grid, s);
         if (rc) return rc;
         NH_HIP(hipGetLastError());
