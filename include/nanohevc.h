@@ -123,6 +123,15 @@ int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_
  * compute). */
 int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                    int nsets, int qp, int is_intra, int variant, void* stream);
+/* The hot path plus the level-side helpers of quant.py:153-178 fused as an
+ * epilogue: per full 8x8 block, d_nnz[i] =
+ * count_nonzero(levels) (0..64; is_all_zero == (d_nnz[i] == 0)) and d_bits[i] =
+ * int(estimate_bits(levels)) (float64 sum in numpy's order, truncated).  Blocks
+ * are numbered set by set in the launch's order (plane, block row, block
+ * column).  Either output may be NULL; d_lvl as nh_fwd8x8_quant_planes.  The
+ * first call with d_bits on a device fills a static 210 KB term table. */
+int nh_fwd8x8_quant_planes_ex(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,
+                              int qp, int is_intra, uint8_t* d_nnz, int32_t* d_bits, void* stream);
 /* Measurement helper (not a product path): copies d_in to d_out over the same
  * blocks with the hot kernel's exact access pattern -- the achievable-bandwidth
  * ceiling for that pattern.  policy: as the variant's cache policy (0..3). */

@@ -20,6 +20,7 @@
 //   * workgroups never straddle two plane sets, so the set lookup is scalar.
 // Roofline: 128 B in + 128 B out per block (HBM-bound; ~1.2k VALU ops/block).
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 
@@ -31,6 +32,7 @@ struct SetDev {
     uint32_t nblocks;
     uint32_t wg_start;  // first workgroup of this set
     FastDiv bpp, bpr, ppg;
+    uint32_t blk0;      // index of this set's first block in the launch (epilogue outputs)
 };
 
 struct Fused8Args {
@@ -72,8 +74,13 @@ __device__ __forceinline__ void load_block(const int16_t* src, int32_t pitch, v4
 }
 
 // One 8x8 block: raw int16 rows -> int16 level rows (the whole fused computation).
+// row_fn(i, L) sees each row's 8 levels as they are produced (epilogues).
+struct NoRowFn {
+    __device__ __forceinline__ void operator()(int, const int32_t (&)[8]) const {}
+};
+template <class RowFn = NoRowFn>
 __device__ __forceinline__ void dct8_quant_block(const v4i (&raw)[8], v4i (&outv)[8], const QuantS& q,
-                                                 uint32_t h_v, uint32_t hneg_v) {
+                                                 uint32_t h_v, uint32_t hneg_v, RowFn&& row_fn = RowFn()) {
     uint32_t X[8][8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -102,6 +109,7 @@ __device__ __forceinline__ void dct8_quant_block(const v4i (&raw)[8], v4i (&outv
         int32_t L[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) L[j] = quant_s((int32_t)y[j] >> 8, q, h_v, hneg_v);
+        row_fn(i, L);
         int w[4];
 #pragma unroll
         for (int m = 0; m < 4; ++m) w[m] = (int)__builtin_amdgcn_perm((uint32_t)L[2 * m + 1], (uint32_t)L[2 * m], 0x05040100u);
@@ -137,6 +145,93 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     dct8_quant_block(raw, outv, a.q, h_v, hneg_v);
 #pragma unroll
     for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
+}
+
+// ---------------------------------------------------------------------------
+// Level-side epilogue (quant.py:153-178): per block
+//   nnz  = count_nonzero(levels)            (uint8; is_all_zero == !nnz)
+//   bits = int(estimate_bits(levels))       (int32)
+// estimate_bits = np.sum(log2(|l|+1) + (|l|>0)*2) in float64: the 64 terms of
+// an 8x8 block are summed in numpy's pairwise order for n = 64 (8 running
+// accumulators over the flattened block, then ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))).
+// Terms come from a table built on the device with the same log2 expression
+// as nh_estimate_bits (|level| <= 26214 for N = 8).
+// ---------------------------------------------------------------------------
+constexpr int kEbTab = 26215;
+__device__ double g_eb_tab[kEbTab];
+
+__global__ void k_init_eb_tab() {
+    const int a = blockIdx.x * 256 + threadIdx.x;
+    if (a < kEbTab) g_eb_tab[a] = a ? log2((double)(a + 1)) + 2.0 : 0.0;
+}
+
+struct EpiArgs {
+    uint8_t* nnz;
+    int32_t* bits;
+};
+
+constexpr int kEbLds = 1024;   // terms for |level| < 1024 staged in LDS (8 KB per workgroup)
+
+template <int POLICY, bool BITS, int WAVES>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant_epi(Fused8Args a, EpiArgs e) {
+    __shared__ double tab[BITS ? kEbLds : 1];
+    if constexpr (BITS) {
+#pragma unroll
+        for (int k = 0; k < kEbLds / 256; ++k) tab[k * 256 + threadIdx.x] = g_eb_tab[k * 256 + threadIdx.x];
+        __syncthreads();
+    }
+    SetDev S;
+    select_set(a, S);
+    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
+    asm volatile("" : "+v"(h_v), "+v"(hneg_v));
+    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    if (b >= S.nblocks) return;
+    const int64_t off = block_offset(S, b);
+    v4i raw[8], outv[8];
+    load_block<POLICY>(a.in + off, S.pitch, raw);
+    dct8_quant_block(raw, outv, a.q, h_v, hneg_v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
+    int nz = 0;
+    bool big = false;
+    double r[8];
+    // row by row (r[c] = numpy's running sum c over the flattened block); the
+    // fast path reads only the LDS table, blocks with a |level| >= kEbLds
+    // (rare: low QP) are summed again from the full table below
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int w[4] = {outv[i].x, outv[i].y, outv[i].z, outv[i].w};
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int l = (int16_t)(c & 1 ? (w[c >> 1] >> 16) : (w[c >> 1] & 0xffff));
+            const int av = l < 0 ? -l : l;
+            nz += av != 0;
+            if constexpr (BITS) {
+                big |= av >= kEbLds;
+                const double t = tab[av < kEbLds ? av : 0];   // tab[0] == 0
+                r[c] = i ? r[c] + t : t;
+            }
+        }
+        if constexpr (BITS) __builtin_amdgcn_sched_barrier(0);   // <= 8 term loads in flight
+    }
+    if constexpr (BITS) {
+        if (big) {
+#pragma unroll 1
+            for (int i = 0; i < 8; ++i) {
+                const int w[4] = {outv[i].x, outv[i].y, outv[i].z, outv[i].w};
+#pragma unroll
+                for (int c = 0; c < 8; ++c) {
+                    const int l = (int16_t)(c & 1 ? (w[c >> 1] >> 16) : (w[c >> 1] & 0xffff));
+                    const double t = g_eb_tab[l < 0 ? -l : l];
+                    r[c] = i ? r[c] + t : t;
+                }
+            }
+        }
+    }
+    const uint32_t gb = S.blk0 + b;
+    if (e.nnz) e.nnz[gb] = (uint8_t)nz;
+    if constexpr (BITS)
+        e.bits[gb] = (int32_t)(((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])));
 }
 
 // Persistent, software-pipelined form: a fixed grid of workgroups walks the
@@ -243,7 +338,7 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
     qp0.off = is_intra ? (1u << shift) / 3 : (1u << shift) / 6;
     qp0.shift = shift;
     a.q = make_quants(qp0);
-    uint64_t wg = 0;
+    uint64_t wg = 0, blk = 0;
     for (int k = 0; k < nsets; ++k) {
         const nh_plane_set& p = sets[k];
         if (p.width < 0 || p.height < 0 || p.pitch < p.width || p.planes_per_group < 1 || p.num_groups < 0 ||
@@ -265,10 +360,12 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
         d.bpp = make_fastdiv(bpp ? (uint32_t)bpp : 1);
         d.bpr = make_fastdiv(bpr ? (uint32_t)bpr : 1);
         d.ppg = make_fastdiv((uint32_t)p.planes_per_group);
+        d.blk0 = (uint32_t)blk;
+        blk += nb;
         wg += (nb + 255) / 256;
     }
     for (int k = nsets; k < NH_MAX_PLANE_SETS; ++k) a.set[k].wg_start = 0xffffffffu;
-    if (wg >= (1ull << 31)) return NH_EARG;
+    if (wg >= (1ull << 31) || blk >= (1ull << 32)) return NH_EARG;
     total_wg = (uint32_t)wg;
     return NH_OK;
 }
@@ -357,6 +454,36 @@ extern "C" int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t
         case 2: k_probe_linear<2><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
         default: k_probe_linear<3><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
     }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int nh_fwd8x8_quant_planes_ex(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,
+                                         int qp, int is_intra, uint8_t* d_nnz, int32_t* d_bits, void* stream) {
+    Fused8Args a;
+    uint32_t wg = 0;
+    int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+    if (rc) return rc;
+    if (!wg) return NH_OK;
+    hipStream_t s = as_stream(stream);
+    if (d_bits) {   // the term table, once per device (stream-ordered before first use)
+        static std::mutex mu;
+        static bool ready[64] = {};
+        int dev = 0;
+        NH_HIP(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(mu);
+        if (dev < 0 || dev >= 64) return NH_EARG;
+        if (!ready[dev]) {
+            k_init_eb_tab<<<(kEbTab + 255) / 256, 256, 0, s>>>();
+            NH_HIP(hipGetLastError());
+            NH_HIP(hipStreamSynchronize(s));
+            ready[dev] = true;
+        }
+    }
+    EpiArgs e{d_nnz, d_bits};
+    // occupancy targets: the largest without spills (bits: 104 VGPRs, nnz only: 75)
+    if (d_bits) k_fwd8x8_quant_epi<1, true, 4><<<wg, 256, 0, s>>>(a, e);
+    else k_fwd8x8_quant_epi<1, false, 5><<<wg, 256, 0, s>>>(a, e);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

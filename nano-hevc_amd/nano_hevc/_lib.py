@@ -54,6 +54,7 @@ SIGNATURES = {
     "nh_sse_i16": ([P, P, I64, P, VP], I32),
     "nh_fwd8x8_quant_planes": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, VP], I32),
     "nh_fwd8x8_quant_planes_variant": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, I32, VP], I32),
+    "nh_fwd8x8_quant_planes_ex": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, P, P, VP], I32),
     "nh_probe_copy8x8_planes": ([P, P, C.POINTER(PlaneSet), I32, I32, VP], I32),
     "nh_probe_copy_linear": ([P, P, I64, I32, I32, VP], I32),
     "nh_fwd_transform_batch": ([P, P, I64, I32, I32, VP], I32),

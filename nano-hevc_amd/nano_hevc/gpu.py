@@ -70,6 +70,18 @@ def blocks_in(sets: Sequence[PlaneSet]) -> int:
 DEFAULT_VARIANT = 5   # nontemporal loads+stores, >= 5 waves/SIMD (see nh_fused8x8.hip)
 
 
+def sets_fit(sets: Sequence[PlaneSet], numel: int, what: str):
+    """Host-side bounds check before a launch: every plane of every set must lie
+    inside a buffer of ``numel`` elements (a kernel never sees the size)."""
+    for s in sets:
+        if s.num_groups <= 0 or s.width <= 0 or s.height <= 0:
+            continue
+        last = s.base + (s.num_groups - 1) * s.group_stride + (s.planes_per_group - 1) * s.plane_stride + \
+            (s.height - 1) * s.pitch + s.width
+        if s.base < 0 or s.plane_stride < 0 or s.group_stride < 0 or last > numel:
+            raise ValueError(f"{what}: a plane set reaches outside the buffer ({last} > {numel} elements)")
+
+
 def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = True, out=None,
                  variant: int = DEFAULT_VARIANT, stream=None):
     """Forward 8x8 DCT (transform.py:154-196) + quantize_block (quant.py:126-137) on
@@ -80,11 +92,35 @@ def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = T
     if out is None:
         out = torch.zeros_like(res)
     _need(out, torch.int16, "fwd8x8_quant(out)")
+    sets_fit(sets, min(res.numel(), out.numel()), "fwd8x8_quant")
     arr = (PlaneSet * len(sets))(*sets)
     check(_lib.load().nh_fwd8x8_quant_planes_variant(res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp),
                                                      int(bool(is_intra)), int(variant), C.c_void_p(_stream(stream))),
           "fwd8x8_quant")
     return out
+
+
+def fwd8x8_quant_ex(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = True, out=None,
+                    nnz: bool = True, bits: bool = True, stream=None):
+    """fwd8x8_quant plus the level-side helpers of quant.py:153-178 per block,
+    fused.  Returns (levels, nnz, bits): nnz = count_nonzero
+    (uint8; is_all_zero == nnz == 0) and bits = int(estimate_bits) (int32) of
+    every full 8x8 block, numbered set by set in the launch's order; either may
+    be skipped (None)."""
+    torch = _torch()
+    _need(res, torch.int16, "fwd8x8_quant_ex(res)")
+    if out is None:
+        out = torch.zeros_like(res)
+    _need(out, torch.int16, "fwd8x8_quant_ex(out)")
+    sets_fit(sets, min(res.numel(), out.numel()), "fwd8x8_quant_ex")
+    nb = blocks_in(sets)
+    t_nnz = torch.empty(nb, dtype=torch.uint8, device=res.device) if nnz else None
+    t_bits = torch.empty(nb, dtype=torch.int32, device=res.device) if bits else None
+    arr = (PlaneSet * len(sets))(*sets)
+    check(_lib.load().nh_fwd8x8_quant_planes_ex(
+        res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp), int(bool(is_intra)),
+        t_nnz.data_ptr() if nnz else None, t_bits.data_ptr() if bits else None, C.c_void_p(_stream(stream))))
+    return out, t_nnz, t_bits
 
 
 def fwd8x8_quant_plane(res2d, qp: int = 32, is_intra: bool = True, out=None, stream=None):
@@ -251,11 +287,7 @@ def encode_intra_planes(src, sets: Sequence[PlaneSet], block_sizes: Sequence[int
     if len(block_sizes) != len(sets):
         raise ValueError("encode_intra_planes: one block size per plane set")
     nplanes = sum(s.planes_per_group * s.num_groups for s in sets)
-    for s in sets:
-        last = s.base + (s.num_groups - 1) * s.group_stride + (s.planes_per_group - 1) * s.plane_stride + \
-            (s.height - 1) * s.pitch + s.width
-        if s.num_groups and s.width and s.height and last > src.numel():
-            raise ValueError("encode_intra_planes: a plane set reaches past the end of src")
+    sets_fit(sets, src.numel(), "encode_intra_planes")
     if stats is None:
         stats = torch.zeros((nplanes, ENC_STATS), dtype=torch.int64, device=src.device)
     _need(stats, torch.int64, "encode_intra_planes(stats)")

@@ -11,6 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 from oracle import oracle as O  # noqa: E402  (checker only)
+from natural import natural_residual  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
@@ -252,6 +253,32 @@ def test_fused8x8_4k_yuv420_stream_vs_oracle(nh, torch_dev):
             assert np.array_equal(out[o:o + p.size].reshape(p.shape), O.fwd8x8_quant_plane(p, 32)), (f, c)
 
 
+def test_fused8x8_natural_residual_stream_vs_oracle(nh, torch_dev):
+    """D-1 (b): "natural" residuals (gradient + noise frames minus the open-loop
+    DC prediction) of a 4K YUV420 stream, every block against the oracle, at
+    QP 22 and 32 (intra) and QP 37 (inter)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H = 2, 3840, 2160
+    rng = np.random.default_rng(2024)
+    planes = []
+    for f in range(F):
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            src = np.clip(40 + (3 * xx + 2 * yy + 13 * f) % 170 + (xx // 97) * 5 + rng.integers(-12, 13, (ph, pw)),
+                          0, 255)
+            planes.append(natural_residual(src))
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sets = gpu.yuv420_plane_sets(F, W, H)
+    for qp, intra in ((22, True), (32, True), (37, False)):
+        out = gpu.fwd8x8_quant(d, sets, qp, intra).cpu().numpy()
+        o = 0
+        for p in planes:
+            assert np.array_equal(out[o:o + p.size].reshape(p.shape), O.fwd8x8_quant_plane(p, qp, intra)), (qp, o)
+            o += p.size
+
+
 # ------------------------------------------------------------------ config 3 / config 4 drivers
 
 def test_intra_rdo_golden(nh, torch_dev, golden):
@@ -455,3 +482,59 @@ def test_tu_pipeline_int16_extremes(nh, torch_dev):
         l, r, t = gpu.tu_pipeline_plane(torch.from_numpy(src).cuda(), ctb, int(not luma), 5, 3, luma)
         el, er, et = O.tu_pipeline_plane(src, ctb, int(not luma), 5, 3, luma)
         assert np.array_equal(l.cpu().numpy(), el) and np.array_equal(r.cpu().numpy(), er)
+
+
+# ------------------------------------------------------------------ f-4: fused level-side epilogue
+
+def _ref_level_helpers(lv, sets):
+    """count_nonzero / estimate_bits (quant.py:153-173) of every full 8x8 block,
+    in the launch's block order, with the reference's own numpy formula."""
+    nnz, bits = [], []
+    for s in sets:
+        for g in range(s.num_groups):
+            for c in range(s.planes_per_group):
+                o = s.base + g * s.group_stride + c * s.plane_stride
+                p = lv[o:o + s.height * s.pitch].reshape(s.height, s.pitch)[:s.height // 8 * 8, :s.width // 8 * 8]
+                blk = p.reshape(s.height // 8, 8, s.width // 8, 8).transpose(0, 2, 1, 3).reshape(-1, 64)
+                a = np.abs(blk.astype(np.int32))
+                nnz.append(np.count_nonzero(blk, axis=1))
+                bits.append(np.sum(np.log2(a + 1) + (a > 0) * 2, axis=1).astype(np.int64))   # int() of a float >= 0
+    return np.concatenate(nnz), np.concatenate(bits)
+
+
+@pytest.mark.parametrize("qp,intra,kind", [(32, True, "noise"), (4, True, "noise"), (22, False, "natural"),
+                                           (0, True, "int16")])
+def test_fused8x8_epilogue_vs_reference_helpers(nh, torch_dev, qp, intra, kind):
+    torch = torch_dev
+    from nano_hevc import gpu, quant
+    F, W, H = 2, 352, 288
+    fe = gpu.yuv420_frame_elems(W, H)
+    rng = np.random.default_rng(qp + 7)
+    if kind == "int16":
+        buf = rng.integers(-32768, 32768, size=F * fe).astype(np.int16)
+    elif kind == "noise":
+        buf = rng.integers(-255, 256, size=F * fe).astype(np.int16)
+    else:
+        planes = []
+        for f in range(F):
+            for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+                yy, xx = np.mgrid[0:ph, 0:pw]
+                planes.append(natural_residual(np.clip(60 + (2 * xx + yy + f) % 150 + rng.integers(-9, 10, (ph, pw)),
+                                                       0, 255)).reshape(-1))
+        buf = np.concatenate(planes)
+    d = torch.from_numpy(buf).cuda()
+    sets = gpu.yuv420_plane_sets(F, W, H)
+    lv, nnz, bits = gpu.fwd8x8_quant_ex(d, sets, qp, intra)
+    lv = lv.cpu().numpy()
+    assert np.array_equal(lv, gpu.fwd8x8_quant(d, sets, qp, intra).cpu().numpy())
+    enz, ebits = _ref_level_helpers(lv, sets)
+    assert np.array_equal(nnz.cpu().numpy(), enz)
+    assert np.array_equal(bits.cpu().numpy(), ebits)
+    # spot-check the vectorised expectation against the drop-in per-block helpers
+    blk = lv[:8 * W].reshape(8, W)[:, :64].reshape(8, 8, 8).transpose(1, 0, 2)
+    for k in range(8):
+        b32 = blk[k].astype(np.int32)
+        assert quant.count_nonzero(b32) == enz[k] and quant.estimate_bits(b32) == ebits[k]
+    # optional outputs
+    _, n2, b2 = gpu.fwd8x8_quant_ex(d, sets, qp, intra, bits=False)
+    assert b2 is None and torch.equal(n2, nnz)

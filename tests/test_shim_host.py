@@ -93,3 +93,17 @@ def test_encoder_fails_loudly_without_device():
         pytest.skip("a device is present")
     with pytest.raises(Exception):
         encode_frame_intra(create_test_frame(16, 16), 8)
+
+
+def test_natural_residual_helper_matches_reference_dc():
+    """CPU check of tests/natural.py (used by the D-1 (b) GPU parity test)
+    against intra_dc_predict's rule (intra.py:46-62) on a few blocks."""
+    from natural import natural_residual
+    rng = np.random.default_rng(3)
+    src = rng.integers(0, 256, (24, 32)).astype(np.int64)
+    res = natural_residual(src)
+    for by, bx in ((0, 0), (0, 8), (8, 0), (16, 24)):
+        top = np.full(8, 128) if by == 0 else src[by - 1, bx:bx + 8]
+        left = np.full(8, 128) if bx == 0 else src[by:by + 8, bx - 1]
+        dc = (int(top.sum()) + int(left.sum()) + 8) // 16
+        assert np.array_equal(res[by:by + 8, bx:bx + 8], (src[by:by + 8, bx:bx + 8] - dc).astype(np.int16))

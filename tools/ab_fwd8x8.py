@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="1,5,9,13")
+    ap.add_argument("--epilogue", action="store_true", help="also time the fused level-side epilogue (ex, exnnz)")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     L = _lib.load()
@@ -55,11 +56,19 @@ def main():
         elif name.startswith("probe"):
             _lib.check(L.nh_probe_copy8x8_planes(res.data_ptr(), o.data_ptr(), arr, len(sets), int(name[5:]),
                                                  C.c_void_p(st.cuda_stream)))
+        elif name == "ex":        # + fused count_nonzero / estimate_bits epilogue (261 B/block)
+            _lib.check(L.nh_fwd8x8_quant_planes_ex(res.data_ptr(), o.data_ptr(), arr, len(sets), 32, 1,
+                                                   ex_nnz.data_ptr(), ex_bits.data_ptr(), C.c_void_p(st.cuda_stream)))
+        elif name == "exnnz":     # + count_nonzero only (257 B/block)
+            _lib.check(L.nh_fwd8x8_quant_planes_ex(res.data_ptr(), o.data_ptr(), arr, len(sets), 32, 1,
+                                                   ex_nnz.data_ptr(), None, C.c_void_p(st.cuda_stream)))
         else:
             gpu.fwd8x8_quant(res, sets, 32, True, out=o, variant=int(name[1:]), stream=st)
 
     names = (["torch_copy"] + [f"probe{p}" for p in range(4)] + [f"linear{p}g{g}" for p in (0, 1) for g in (0, 4096)]
-             + [f"v{v}" for v in variants])
+             + [f"v{v}" for v in variants] + (["ex", "exnnz"] if args.epilogue else []))
+    ex_nnz = torch.empty(nblk, dtype=torch.uint8, device="cuda")
+    ex_bits = torch.empty(nblk, dtype=torch.int32, device="cuda")
     for n in names:
         outs[n] = torch.zeros_like(res)
     times = {n: [] for n in names}
@@ -81,7 +90,7 @@ def main():
     for n in names:
         med, mn = statistics.median(times[n]), min(times[n])
         e = {"ms_median": med, "ms_min": mn, "GBps_median": bytes_per / med / 1e6, "GBps_best": bytes_per / mn / 1e6}
-        if n.startswith("v") and ref is not None:
+        if (n.startswith("v") or n.startswith("ex")) and ref is not None:
             e["equal_v0"] = bool(torch.equal(outs[n], ref))
         rep["results"][n] = e
     print(json.dumps(rep, indent=1))
