@@ -186,6 +186,25 @@ int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t
  * (int32 D) with the lane maps the config-5 MFMA kernel assumes. */
 int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream);
 
+/* Config 3, CLOSED loop: the same
+ * 35-mode chain per full 8x8 block, blocks in raster order, neighbours from
+ * the reconstruction built so far (BlockView rules on a zero-initialised
+ * recon plane; left reference = the N reconstructed samples, extended by the
+ * reference's replicate-last rule).  Scheduled as a wavefront: one wave per
+ * block row, rows claimed in order by ticket, each waiting on the row above.
+ * Planes of every set are independent.  d_modes: (h/8)*(w/8) per plane,
+ * planes numbered set by set (g * planes_per_group + c); d_lvl (int32) and
+ * d_recon (int16) use the source layout (recon outside full blocks = 0);
+ * d_sse: one int64 per plane, ACCUMULATED.  d_work: caller-owned device
+ * memory of nh_intra_rdo_closed_workspace_bytes() bytes (zeroed by the call).
+ * A wavefront wait that cannot complete sets the status word instead of
+ * hanging: read it with nh_intra_rdo_closed_status (0 = ok). */
+int64_t nh_intra_rdo_closed_workspace_bytes(const nh_plane_set* sets, int nsets);
+int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp,
+                               uint8_t* d_modes, int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse,
+                               void* d_work, void* stream);
+int nh_intra_rdo_closed_status(const void* d_work, int* status, void* stream);
+
 /* ---- Frame I/O and the frame-level intra driver ----
  * Frame.from_yuv420p / Plane.from_buffer + .astype(np.int16) (frame.py:44-54,
  * :87-110) and Frame.to_yuv420p / PackedFrame.to_yuv420p's .astype(np.uint8)

@@ -36,6 +36,115 @@ struct RdoSlotLds {
 
 __device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
 
+// One lane's mode of the cfg-3 chain on an 8x8 block whose samples and
+// neighbours are in L: prediction (planar / DC / angular, intra.py:46-207) ->
+// residual -> fwd DCT -> quant -> dequant -> inv DCT -> recon -> clip -> SSE.
+// Returns the SSE; P receives the clipped recon, Lv the levels.  ref: this
+// lane's 26-entry angular reference scratch (LDS).
+__device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, int16_t* ref,
+                                                         const QuantParams& qp, int dq_scale, int dq_per,
+                                                         int32_t (&P)[64], int32_t (&Lv)[64]) {
+    if (mode == 0) {            // planar, intra.py:81-113, tr=top[-1], bl=left[-1] (__main__.py:168-169)
+        const int32_t tr = L.topN[7], bl = L.leftN[7];
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int x = 0; x < 8; ++x)
+                P[y * 8 + x] = ((7 - x) * L.leftN[y] + (x + 1) * tr + (7 - y) * L.topN[x] + (y + 1) * bl + 8) >> 4;
+    } else if (mode == 1) {     // DC, intra.py:46-62
+        int32_t s = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s += L.topN[k] + L.leftN[k];
+        const int32_t dc = (s + 8) >> 4;   // floor division by 16
+#pragma unroll
+        for (int k = 0; k < 64; ++k) P[k] = dc;
+    } else {                    // angular, intra.py:116-207
+        const int angle = intra_angle(mode - 2);
+        const bool vert = mode >= 18;
+        const int16_t* pri = vert ? L.topA : L.leftA;
+        const int16_t* sec = vert ? L.leftA : L.topA;
+        const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
+        // _build_ref_array (intra.py:159-188): ref[8+i], i in [-8, 16]
+        for (int i = 0; i < 26; ++i) ref[i] = 0;
+        ref[8] = pri[0];
+        for (int i = 1; i <= 16; ++i) ref[8 + i] = pri[i < np ? i : np - 1];
+        if (angle < 0) {
+            const int inv = inv_angle(angle), next = (8 * angle) >> 5;
+            for (int i = -1; i > next - 1; --i) {
+                int proj = ((i + 1) * inv + 128) >> 8;
+                if (proj < ns) ref[8 + i] = sec[proj];
+            }
+        }
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+#pragma unroll
+            for (int x = 0; x < 8; ++x) {
+                const int base = vert ? x : y, scan = vert ? y : x;
+                const int proj = (scan + 1) * angle;
+                const int idx = 8 + base + 1 + (proj >> 5);
+                const int f = proj & 31;
+                const int32_t a = ref[idx];
+                int32_t v;
+                if (f == 0) v = a;
+                else {
+                    const int32_t b = ref[idx + 1];
+                    v = wrap16((32 - f) * a + f * b + 16) >> 5;   // int16 arithmetic (D8)
+                }
+                P[y * 8 + x] = v;
+            }
+    }
+    uint32_t X[8][8];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) X[k / 8][k % 8] = (uint32_t)(int32_t)wrap16((int32_t)L.orig[k] - P[k]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {           // pass 1: columns
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = X[k][j];
+        fwd_dct<8, Mul24>(x, y, 128u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)y[i] >> 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {           // pass 2: rows, then quant / dequant
+        uint32_t y[8];
+        fwd_dct<8, Mul24>(X[i], y, 128u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int32_t c = (int32_t)y[j] >> 8;
+            const int32_t l = quant_i32(c, qp);
+            Lv[i * 8 + j] = l;
+            X[i][j] = (uint32_t)dequant_i32(l, dq_scale, dq_per);
+        }
+    }
+    // inverse pass 1: columns (transform.py:221-227)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        uint32_t yv[8], x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) yv[k] = X[k][j];
+        inv_dct<8, Mul24>(yv, x, 128u);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)x[i] >> 8);
+    }
+    unsigned long long sse = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {           // inverse pass 2: rows, recon, SSE
+        uint32_t x[8];
+        inv_dct<8, Mul24>(X[i], x, 128u);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int32_t rr = wrap16((int32_t)x[j] >> 8);               // rres.astype(int16)
+            int32_t rc = wrap16(P[i * 8 + j] + rr);                       // reconstruct_block (int16 wrap)
+            rc = rc < 0 ? 0 : (rc > 255 ? 255 : rc);                      // clip_to_pixel_range(., 8)
+            P[i * 8 + j] = rc;
+            const int32_t d = wrap16((int32_t)L.orig[i * 8 + j] - rc);   // residual_block(orig, recon)
+            sse += (unsigned long long)(d * d);
+        }
+    }
+    return sse;
+}
+
 __global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
                                                     int32_t* lvl, int16_t* recon, unsigned long long* sse_out) {
@@ -91,114 +200,12 @@ __global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ 
     const bool active = lane_on && S[lane_on ? slot : 0].valid;
     RdoSlotLds& L = S[lane_on ? slot : 0];
 
-    // ---- prediction (int32 registers holding int16 values) ----
+    // ---- the mode's chain ----
     int32_t P[64];
-    if (active) {
-        if (mode == 0) {            // planar, intra.py:81-113, tr=top[-1], bl=left[-1] (__main__.py:168-169)
-            const int32_t tr = L.topN[7], bl = L.leftN[7];
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-#pragma unroll
-                for (int x = 0; x < 8; ++x)
-                    P[y * 8 + x] = ((7 - x) * L.leftN[y] + (x + 1) * tr + (7 - y) * L.topN[x] + (y + 1) * bl + 8) >> 4;
-        } else if (mode == 1) {     // DC, intra.py:46-62
-            int32_t s = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s += L.topN[k] + L.leftN[k];
-            const int32_t dc = (s + 8) >> 4;   // floor division by 16
-#pragma unroll
-            for (int k = 0; k < 64; ++k) P[k] = dc;
-        } else {                    // angular, intra.py:116-207
-            const int angle = intra_angle(mode - 2);
-            const bool vert = mode >= 18;
-            const int16_t* pri = vert ? L.topA : L.leftA;
-            const int16_t* sec = vert ? L.leftA : L.topA;
-            const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
-            int16_t* ref = refs[t];
-            // _build_ref_array (intra.py:159-188): ref[8+i], i in [-8, 16]
-            for (int i = 0; i < 26; ++i) ref[i] = 0;
-            ref[8] = pri[0];
-            for (int i = 1; i <= 16; ++i) ref[8 + i] = pri[i < np ? i : np - 1];
-            if (angle < 0) {
-                const int inv = inv_angle(angle), next = (8 * angle) >> 5;
-                for (int i = -1; i > next - 1; --i) {
-                    int proj = ((i + 1) * inv + 128) >> 8;
-                    if (proj < ns) ref[8 + i] = sec[proj];
-                }
-            }
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-#pragma unroll
-                for (int x = 0; x < 8; ++x) {
-                    const int base = vert ? x : y, scan = vert ? y : x;
-                    const int proj = (scan + 1) * angle;
-                    const int idx = 8 + base + 1 + (proj >> 5);
-                    const int f = proj & 31;
-                    const int32_t a = ref[idx];
-                    int32_t v;
-                    if (f == 0) v = a;
-                    else {
-                        const int32_t b = ref[idx + 1];
-                        v = wrap16((32 - f) * a + f * b + 16) >> 5;   // int16 arithmetic (D8)
-                    }
-                    P[y * 8 + x] = v;
-                }
-        }
-    }
-
-    // ---- residual -> fwd DCT -> quant -> dequant -> inv DCT -> recon -> SSE ----
     unsigned long long key = ULLONG_MAX;
-    uint32_t X[8][8];
     int32_t Lv[64];
     if (active) {
-#pragma unroll
-        for (int k = 0; k < 64; ++k) X[k / 8][k % 8] = (uint32_t)(int32_t)wrap16((int32_t)L.orig[k] - P[k]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {           // pass 1: columns
-            uint32_t x[8], y[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) x[k] = X[k][j];
-            fwd_dct<8, Mul24>(x, y, 128u);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)y[i] >> 8);
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {           // pass 2: rows, then quant / dequant
-            uint32_t y[8];
-            fwd_dct<8, Mul24>(X[i], y, 128u);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int32_t c = (int32_t)y[j] >> 8;
-                const int32_t l = quant_i32(c, qp);
-                Lv[i * 8 + j] = l;
-                X[i][j] = (uint32_t)dequant_i32(l, dq_scale, dq_per);
-            }
-        }
-        // inverse pass 1: columns (transform.py:221-227)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            uint32_t yv[8], x[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) yv[k] = X[k][j];
-            inv_dct<8, Mul24>(yv, x, 128u);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)x[i] >> 8);
-        }
-        unsigned long long sse = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {           // inverse pass 2: rows, recon, SSE
-            uint32_t x[8];
-            inv_dct<8, Mul24>(X[i], x, 128u);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int32_t rr = wrap16((int32_t)x[j] >> 8);               // rres.astype(int16)
-                int32_t rc = wrap16(P[i * 8 + j] + rr);                       // reconstruct_block (int16 wrap)
-                rc = rc < 0 ? 0 : (rc > 255 ? 255 : rc);                      // clip_to_pixel_range(., 8)
-                P[i * 8 + j] = rc;
-                const int32_t d = wrap16((int32_t)L.orig[i * 8 + j] - rc);   // residual_block(orig, recon)
-                sse += (unsigned long long)(d * d);
-            }
-        }
+        const unsigned long long sse = rdo8_chain(L, mode, refs[t], qp, dq_scale, dq_per, P, Lv);
         key = (sse << 6) | (unsigned long long)mode;
         atomicMin(&L.best, key);
     }
@@ -215,6 +222,180 @@ __global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ 
 #pragma unroll
             for (int j = 0; j < 8; ++j) { lrow[j] = Lv[i * 8 + j]; rrow[j] = (int16_t)P[i * 8 + j]; }
         }
+    }
+}
+
+// ===========================================================================
+// Config 3, closed loop: blocks in raster order, neighbours
+// from the reconstruction.  Wavefront schedule: one wave per block row; rows
+// are claimed by an atomic ticket (plane-major, top to bottom), so a wave only
+// ever waits for a row claimed earlier by a running wave (forward progress).
+// Before block bx of row r the wave waits until row r-1 has finished blocks
+// 0..bx+1 (the top and top-right references).
+// Cross-wave data: the only samples another row reads are block bottom rows,
+// kept in a per-plane line buffer (workspace) that is written and read with
+// system-scope relaxed atomics (write-through stores / coherent loads, no L2
+// writeback or invalidate -- the per-XCD L2s are not coherent, and agent-scope
+// release/acquire would flush/invalidate the whole L2 every block).  The
+// progress counter is stored after s_waitcnt vmcnt(0) has retired the line
+// stores.  One line per plane suffices: row r+1 overwrites row r's entries
+// line[x0..x0+7] (block bx) only once row r has finished block bx+1, and row
+// r's later reads (block bx+2 on) start at x0+15; the top-left sample is
+// carried from the previous block's top read because the row has already
+// overwritten that entry itself.  A wait longer than kSpinLimit polls sets a status
+// error and the launch drains instead of hanging.
+// ===========================================================================
+struct ClosedSet {
+    int64_t base, plane_stride, group_stride;
+    int32_t w, h, pitch, ppg;
+    int32_t bw, bh, row0, plane0;   // first global row / plane of this set
+    int64_t mode0;                  // first mode-map entry of this set
+    int64_t line0;                  // first line-buffer word of this set
+    int32_t lw;                     // line-buffer words per plane
+};
+struct ClosedArgs {
+    const int16_t* src;
+    int32_t* lvl;
+    int16_t* rec;
+    uint8_t* modes;
+    int64_t* sse;                   // per plane (accumulated)
+    int32_t* work;                  // [0] ticket, [1] status, [2 + row] blocks done, then line buffers
+    ClosedSet set[NH_MAX_PLANE_SETS];
+    int32_t nsets, total_rows;
+    int64_t lines0;                 // word offset of the line buffers in work
+    int64_t lines_total;            // line-buffer words
+    QuantParams qp;
+    int32_t dq_scale, dq_per;
+};
+constexpr int kSpinLimit = 1 << 20;   // ~1 s of polling; a legitimate wait is a few block steps
+
+__device__ __forceinline__ int ld_sys(const int32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(int32_t* p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
+    __shared__ RdoSlotLds L;
+    __shared__ int16_t refs[64][26];
+    __shared__ int16_t leftcol[8];
+    __shared__ int32_t topw[9];
+    __shared__ int row_s, stall_s;
+    const int lane = threadIdx.x;
+    for (;;) {
+        if (lane == 0) {
+            row_s = atomicAdd(&a.work[0], 1);
+            stall_s = 0;
+        }
+        __syncthreads();
+        const int row = row_s;
+        if (row >= a.total_rows) break;
+        int si = 0;
+        for (int k = 1; k < a.nsets; ++k)
+            if (row >= a.set[k].row0) si = k;
+        const ClosedSet& S = a.set[si];
+        const int local = row - S.row0, pl = local / S.bh, by = local - pl * S.bh;
+        const int g = pl / S.ppg, c = pl - g * S.ppg;
+        const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
+        const int16_t* src = a.src + off;
+        int16_t* rec = a.rec + off;
+        int32_t* lvl = a.lvl + off;
+        int32_t* line = a.work + a.lines0 + S.line0 + (int64_t)pl * S.lw;   // int16 pairs
+        const int y0 = by * 8;
+        int16_t tl_next = 128;   // recon(y0-1, x0-1) for the next block
+        for (int bx = 0; bx < S.bw; ++bx) {
+            const int x0 = bx * 8;
+            if (by > 0 && lane == 0) {   // wait for the top / top-right references
+                const int need = bx + 2 < S.bw ? bx + 2 : S.bw;
+                int spins = 0;
+                while (ld_sys(&a.work[2 + row - 1]) < need) {
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                    // give up on our own limit, or as soon as any wave has given up
+                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
+                        atomicMax(&a.work[1], 1);
+                        stall_s = 1;
+                        break;
+                    }
+                }
+            }
+            __syncthreads();
+            if (stall_s) break;
+            // top row x0-1 .. x0+15 of the row above: 9 line words from word x0/2 - 1
+            if (by > 0 && lane < 9) topw[lane] = (x0 == 0 && lane == 0) ? 0 : ld_sys(line + x0 / 2 - 1 + lane);
+            __syncthreads();
+            // block samples and neighbours (block.py:38-55 on the reconstruction)
+            {
+                const int k = lane;
+                L.orig[k] = src[(int64_t)(y0 + k / 8) * S.pitch + x0 + (k % 8)];
+                if (k < 16) {
+                    int16_t v = 128;
+                    if (y0 > 0 && x0 + k < S.w) {
+                        const int xi = k + 1;   // sample x0 + k = halfword 2 + k of topw
+                        v = (int16_t)(topw[(xi + 1) >> 1] >> (((xi + 1) & 1) * 16));
+                    }
+                    L.topA[1 + k] = v;
+                    if (k < 8) L.topN[k] = v;
+                } else if (k < 24) {
+                    const int kk = k - 16;
+                    const int16_t v = x0 == 0 ? (int16_t)128 : leftcol[kk];
+                    L.leftA[1 + kk] = v;
+                    L.leftN[kk] = v;
+                } else if (k == 24) {
+                    const int16_t tl = (y0 == 0 || x0 == 0) ? (int16_t)128 : tl_next;
+                    L.topA[0] = tl;
+                    L.leftA[0] = tl;
+                    L.ntA = 1 + (y0 == 0 ? 16 : min(16, S.w - x0));
+                    L.nlA = 1 + 8;   // get_left_neighbors(N): the reconstructed samples only
+                }
+            }
+            __syncthreads();
+            tl_next = L.topA[8];   // recon(y0-1, x0+7): the next block's top-left
+            int32_t P[64], Lv[64];
+            unsigned long long key = ULLONG_MAX;
+            if (lane < kModes) key = (rdo8_chain(L, lane, refs[lane], a.qp, a.dq_scale, a.dq_per, P, Lv) << 6) | lane;
+            unsigned long long best = key;
+            for (int m = 32; m > 0; m >>= 1) {
+                const unsigned long long o = __shfl_xor(best, m, 64);
+                best = o < best ? o : best;
+            }
+            if (key == best) {   // the winning mode (lowest SSE, lowest mode on ties)
+                a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)lane;
+                atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], best >> 6);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        lvl[(int64_t)(y0 + i) * S.pitch + x0 + j] = Lv[i * 8 + j];
+                        rec[(int64_t)(y0 + i) * S.pitch + x0 + j] = (int16_t)P[i * 8 + j];
+                    }
+                    leftcol[i] = (int16_t)P[i * 8 + 7];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)   // this block's bottom row -> line (coherent stores)
+                    st_sys(line + x0 / 2 + q, (int)(((uint32_t)(uint16_t)P[56 + 2 * q + 1] << 16) |
+                                                    (uint32_t)(uint16_t)P[56 + 2 * q]));
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line stores retired
+                st_sys(&a.work[2 + row], bx + 1);
+            }
+            __syncthreads();
+        }
+        __syncthreads();
+        if (stall_s) break;   // the whole launch is failing: leave (status word set)
+    }
+}
+
+// Samples outside full 8x8 blocks read as 0 (Frame.zeros) by the closed loop.
+__global__ void k_zero_partial(int16_t* rec, ClosedSet S, int nplanes) {
+    const int p = blockIdx.y;
+    if (p >= nplanes) return;
+    const int g = p / S.ppg, c = p - g * S.ppg;
+    int16_t* r = rec + S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
+    const int fw = S.bw * 8, fh = S.bh * 8;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < (int64_t)S.w * S.h; i += (int64_t)gridDim.x * 256) {
+        const int y = (int)(i / S.w), x = (int)(i - (int64_t)y * S.w);
+        if (x >= fw || y >= fh) r[(int64_t)y * S.pitch + x] = 0;
     }
 }
 
@@ -470,5 +651,99 @@ extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitc
     NH_TU(32, false);
 #undef NH_TU
     NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+static int closed_layout(const nh_plane_set* sets, int nsets, ClosedArgs& a, int64_t& modes_total) {
+    if (!sets || nsets < 1 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
+    int64_t rows = 0, planes = 0, modes = 0, lines = 0;
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& p = sets[k];
+        if (p.width < 8 || p.height < 0 || p.pitch < p.width || p.planes_per_group < 1 || p.num_groups < 0 ||
+            p.width > 65535 || p.height > 65535)
+            return NH_EARG;
+        ClosedSet& S = a.set[k];
+        S.base = p.base;
+        S.plane_stride = p.plane_stride;
+        S.group_stride = p.group_stride;
+        S.w = p.width;
+        S.h = p.height;
+        S.pitch = p.pitch;
+        S.ppg = p.planes_per_group;
+        S.bw = p.width / 8;
+        S.bh = p.height / 8;
+        S.row0 = (int32_t)rows;
+        S.plane0 = (int32_t)planes;
+        S.mode0 = modes;
+        S.lw = (p.width + 1) / 2 + 16;   // int16 pairs + slack for the top-right read past the edge
+        S.line0 = lines;
+        const int64_t np = (int64_t)p.planes_per_group * p.num_groups;
+        rows += np * S.bh;
+        planes += np;
+        modes += np * S.bw * S.bh;
+        lines += np * S.lw;
+        if (rows >= (1ll << 30)) return NH_EARG;
+    }
+    a.nsets = nsets;
+    a.total_rows = (int32_t)rows;
+    a.lines0 = 2 + rows;
+    a.lines_total = lines;
+    modes_total = modes;
+    return NH_OK;
+}
+
+extern "C" int64_t nh_intra_rdo_closed_workspace_bytes(const nh_plane_set* sets, int nsets) {
+    ClosedArgs a;
+    int64_t m = 0;
+    if (closed_layout(sets, nsets, a, m)) return -1;
+    return 4ll * (a.lines0 + a.lines_total);
+}
+
+extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp,
+                                          uint8_t* d_modes, int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse,
+                                          void* d_work, void* stream) {
+    if (!d_src || !d_modes || !d_lvl || !d_recon || !d_sse || !d_work) {
+        set_error("nh_intra_rdo_planes_closed: null argument");
+        return NH_EARG;
+    }
+    ClosedArgs a;
+    int64_t modes_total = 0;
+    if (closed_layout(sets, nsets, a, modes_total)) {
+        set_error("nh_intra_rdo_planes_closed: bad plane sets (width >= 8, pitch >= width)");
+        return NH_EARG;
+    }
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    a.src = d_src;
+    a.lvl = d_lvl;
+    a.rec = d_recon;
+    a.modes = d_modes;
+    a.sse = d_sse;
+    a.work = (int32_t*)d_work;
+    a.qp = qparams(qp, 3, true);
+    a.dq_scale = dequant_scale(rem);
+    a.dq_per = per;
+    hipStream_t s = as_stream(stream);
+    NH_HIP(hipMemsetAsync(d_work, 0, 4ull * (a.lines0 + a.lines_total), s));
+    for (int k = 0; k < nsets; ++k) {
+        const int np = sets[k].planes_per_group * sets[k].num_groups;
+        if (np > 0 && np <= 65535) k_zero_partial<<<dim3(64, np), 256, 0, s>>>(d_recon, a.set[k], np);
+        else if (np > 65535) return NH_EARG;
+    }
+    if (a.total_rows > 0) {
+        // persistent waves: enough to cover every row, capped at what can be resident (2 waves/SIMD)
+        const int waves = a.total_rows < 2048 ? a.total_rows : 2048;
+        k_intra_rdo8_closed<<<waves, 64, 0, s>>>(a);
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int nh_intra_rdo_closed_status(const void* d_work, int* status, void* stream) {
+    if (!d_work || !status) return NH_EARG;
+    int32_t v = 0;
+    NH_HIP(hipMemcpyAsync(&v, (const int32_t*)d_work + 1, 4, hipMemcpyDeviceToHost, as_stream(stream)));
+    NH_HIP(hipStreamSynchronize(as_stream(stream)));
+    *status = v;
     return NH_OK;
 }

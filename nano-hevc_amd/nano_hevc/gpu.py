@@ -191,6 +191,42 @@ def intra_rdo_plane(src, qp: int = 32, pitch: int | None = None, stream=None):
     return modes, lvl, rec, sse
 
 
+def intra_rdo_closed(src, sets: Sequence[PlaneSet], qp: int = 32, lvl=None, rec=None, stream=None):
+    """Config 3 in CLOSED loop over every plane of ``sets``:
+    raster block order, neighbours from the reconstruction, wavefront schedule
+    on the device.  Returns (modes uint8 [sum of per-plane (h/8)*(w/8)],
+    lvl int32, recon int16 (source layout), sse int64 per plane)."""
+    torch = _torch()
+    _need(src, torch.int16, "intra_rdo_closed(src)")
+    sets_fit(sets, src.numel(), "intra_rdo_closed")
+    L = _lib.load()
+    arr = (PlaneSet * len(sets))(*sets)
+    wb = int(L.nh_intra_rdo_closed_workspace_bytes(arr, len(sets)))
+    if wb < 0:
+        raise ValueError("intra_rdo_closed: bad plane sets")
+    nmodes = sum((s.width // 8) * (s.height // 8) * s.planes_per_group * s.num_groups for s in sets)
+    nplanes = sum(s.planes_per_group * s.num_groups for s in sets)
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int32, device=src.device)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    _need(lvl, torch.int32, "intra_rdo_closed(lvl)")
+    _need(rec, torch.int16, "intra_rdo_closed(rec)")
+    if lvl.numel() < src.numel() or rec.numel() < src.numel():
+        raise ValueError("intra_rdo_closed: lvl / rec smaller than src")
+    modes = torch.zeros(max(1, nmodes), dtype=torch.uint8, device=src.device)
+    sse = torch.zeros(max(1, nplanes), dtype=torch.int64, device=src.device)
+    work = torch.empty((wb + 3) // 4, dtype=torch.int32, device=src.device)
+    st = C.c_void_p(_stream(stream))
+    check(L.nh_intra_rdo_planes_closed(src.data_ptr(), arr, len(sets), int(qp), modes.data_ptr(), lvl.data_ptr(),
+                                       rec.data_ptr(), sse.data_ptr(), work.data_ptr(), st))
+    status = C.c_int(0)
+    check(L.nh_intra_rdo_closed_status(work.data_ptr(), C.byref(status), st))
+    if status.value:
+        raise RuntimeError("intra_rdo_closed: the wavefront stalled (device status word set)")
+    return modes[:nmodes], lvl, rec, sse[:nplanes]
+
+
 def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
                       row0: int = 0, row1: int = 1 << 30, lvl=None, rec=None, tu=None, work=None, stream=None):
     """Config 4 on one int16 plane (H, W), CTU rows [row0, row1).

@@ -393,9 +393,14 @@ static int64_t tu_chain(const int16_t* orig, const int16_t* pred, int N, int use
     return sse;
 }
 
-/* cfg 3: 35-mode open-loop RDO per full 8x8 block. */
-void oh_intra_rdo_plane(const int16_t* src, int w, int h, int pitch, int qp,
-                        uint8_t* modes, int32_t* lvl, int16_t* recon, int64_t* sse_total) {
+/* cfg 3: 35-mode RDO per full 8x8 block.  Open loop: the
+ * neighbours come from the source plane (D12).  Closed loop:
+ * blocks in raster order, neighbours from the reconstruction built so far
+ * (zero-initialised like Frame.zeros, frame.py:81-88) with the BlockView rules
+ * (block.py:38-55), the left reference limited to the N reconstructed samples
+ * (get_left_neighbors(N)); intra.py's short-reference rule (D6) extends it. */
+static void intra_rdo_plane(const int16_t* src, int w, int h, int pitch, int qp, int closed,
+                            uint8_t* modes, int32_t* lvl, int16_t* recon, int64_t* sse_total) {
     const int N = 8;
     int16_t orig[64], pred[64], best_rec[64];
     int32_t best_lvl[64], l[64];
@@ -404,16 +409,20 @@ void oh_intra_rdo_plane(const int16_t* src, int w, int h, int pitch, int qp,
     int64_t nt, nl, nt2, nl2;
     int64_t total = 0;
     int bw = w / 8;
+    const int16_t* nb = closed ? recon : src;   /* the plane neighbours are read from */
+    if (closed)
+        for (int y = 0; y < h; ++y)
+            for (int x = 0; x < w; ++x) recon[(int64_t)y * pitch + x] = 0;
     for (int by = 0; by + N <= h; by += N)
         for (int bx = 0; bx + N <= w; bx += N) {
             for (int i = 0; i < N; ++i)
                 for (int j = 0; j < N; ++j) orig[i * N + j] = src[(int64_t)(by + i) * pitch + bx + j];
-            get_top(src, w, pitch, bx, by, N, topN, &nt);
-            get_left(src, h, pitch, bx, by, N, leftN, &nl);
-            int64_t tl = (by == 0 || bx == 0) ? 128 : src[(int64_t)(by - 1) * pitch + bx - 1];
+            get_top(nb, w, pitch, bx, by, N, topN, &nt);
+            get_left(nb, h, pitch, bx, by, N, leftN, &nl);
+            int64_t tl = (by == 0 || bx == 0) ? 128 : nb[(int64_t)(by - 1) * pitch + bx - 1];
             top2[0] = tl; left2[0] = tl;
-            get_top(src, w, pitch, bx, by, 2 * N, top2 + 1, &nt2);
-            get_left(src, h, pitch, bx, by, 2 * N, left2 + 1, &nl2);
+            get_top(nb, w, pitch, bx, by, 2 * N, top2 + 1, &nt2);
+            get_left(nb, h, pitch, bx, by, closed ? N : 2 * N, left2 + 1, &nl2);
             int64_t best = -1; int bm = 0;
             for (int m = 0; m < 35; ++m) {
                 if (m == 0) oh_intra_planar(topN, nt, leftN, nl, topN[nt - 1], leftN[nl - 1], N, 3, pred);
@@ -439,6 +448,16 @@ void oh_intra_rdo_plane(const int16_t* src, int w, int h, int pitch, int qp,
                 }
         }
     if (sse_total) *sse_total = total;
+}
+
+void oh_intra_rdo_plane(const int16_t* src, int w, int h, int pitch, int qp,
+                        uint8_t* modes, int32_t* lvl, int16_t* recon, int64_t* sse_total) {
+    intra_rdo_plane(src, w, h, pitch, qp, 0, modes, lvl, recon, sse_total);
+}
+
+void oh_intra_rdo_plane_closed(const int16_t* src, int w, int h, int pitch, int qp,
+                               uint8_t* modes, int32_t* lvl, int16_t* recon, int64_t* sse_total) {
+    intra_rdo_plane(src, w, h, pitch, qp, 1, modes, lvl, recon, sse_total);
 }
 
 /* cfg 4 TU split decision: a seeded integer hash. */

@@ -49,6 +49,7 @@ def lib():
             "oh_fwd8x8_quant_plane": [P, P, i32, i32, i32, i32, i32],
             "oh_fwd8x8_quant_plane_mt": [P, P, i32, i32, i32, i32, i32, i32],
             "oh_intra_rdo_plane": [P, i32, i32, i32, i32, P, P, P, P],
+            "oh_intra_rdo_plane_closed": [P, i32, i32, i32, i32, P, P, P, P],
             "oh_tu_pipeline_plane": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P],
             "oh_tu_split": [C.c_uint32, i32, i32, i32, i32],
             "oh_tc32_plane": [P, i32, i32, i32, i32, P, P],
@@ -58,7 +59,7 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = None if name in ("oh_residual", "oh_reconstruct", "oh_clip", "oh_fwd8x8_quant_plane",
-                                         "oh_intra_rdo_plane", "oh_tu_pipeline_plane", "oh_tc32_plane",
+                                         "oh_intra_rdo_plane", "oh_intra_rdo_plane_closed", "oh_tu_pipeline_plane", "oh_tc32_plane",
                                          "oh_encode_intra_plane") else C.c_int
         _lib = L
     return _lib
@@ -186,14 +187,15 @@ def fwd8x8_quant_plane_mt(res, qp=32, is_intra=True, nthreads=1):
     return out
 
 
-def intra_rdo_plane(src, qp=32):
+def intra_rdo_plane(src, qp=32, closed=False):
     src = np.ascontiguousarray(src, np.int16)
     h, w = src.shape
     modes = np.zeros((h // 8, w // 8), np.uint8)
     lvl = np.zeros(src.shape, np.int32)
     rec = np.zeros(src.shape, np.int16)
     sse = np.zeros(1, np.int64)
-    lib().oh_intra_rdo_plane(_p(src), w, h, w, int(qp), _p(modes), _p(lvl), _p(rec), _p(sse))
+    fn = lib().oh_intra_rdo_plane_closed if closed else lib().oh_intra_rdo_plane
+    fn(_p(src), w, h, w, int(qp), _p(modes), _p(lvl), _p(rec), _p(sse))
     return modes, lvl, rec, int(sse[0])
 
 

@@ -433,6 +433,55 @@ def gen_encode(ref_path):
     return out
 
 
+def gen_closed(I, T, Q):
+    """Closed-loop config 3, composed from the reference's own
+    pieces: raster block order, neighbours fetched with BlockView
+    (block.py:38-55) from the reconstruction Plane built so far
+    (Plane.zeros, frame.py:41-43), left reference = get_left_neighbors(N)
+    (the reconstructed samples only), top = get_top_neighbors(2N).  Own rng."""
+    from nano_hevc.block import BlockView
+    from nano_hevc.frame import Plane
+    rng = np.random.default_rng(9090)
+    out = {}
+    yy, xx = np.mgrid[0:48, 0:72]
+    cases = {"c3a": (np.clip(70 + 2 * xx + yy + rng.integers(-15, 16, size=xx.shape), 0, 255).astype(np.int16), 32),
+             "c3b": (rng.integers(0, 256, size=(29, 37)).astype(np.int16), 22),       # partial blocks
+             "c3c": (np.clip(128 + ((xx // 8 + yy // 8) % 2) * 90 - 45 + rng.integers(-3, 4, size=xx.shape),
+                             0, 255).astype(np.int16), 37)}
+    n = 8
+    for key, (src, qp) in cases.items():
+        h, w = src.shape
+        recon = Plane.zeros(h, w, np.int16)
+        modes = np.zeros((h // n, w // n), np.uint8)
+        lvl = np.zeros(src.shape, np.int32)
+        total = 0
+        for by in range(0, h - n + 1, n):
+            for bx in range(0, w - n + 1, n):
+                blk = BlockView(recon, bx, by, n)
+                orig = src[by:by + n, bx:bx + n]
+                top, left, tl = blk.get_top_neighbors(), blk.get_left_neighbors(), blk.get_top_left_neighbor()
+                topa = np.concatenate([[tl], blk.get_top_neighbors(2 * n)]).astype(np.int16)
+                lefta = np.concatenate([[tl], blk.get_left_neighbors(n)]).astype(np.int16)
+                best = None
+                for m in range(35):
+                    if m == 0:
+                        pred = I.intra_planar_predict(top, left, int(top[-1]), int(left[-1]), n)
+                    elif m == 1:
+                        pred = I.intra_dc_predict(top, left, n)
+                    else:
+                        pred = I.intra_angular_predict(topa, lefta, tl, m, n)
+                    l, r, sse = _chain(I, T, Q, orig, pred, qp, False)
+                    if best is None or sse < best[0]:
+                        best = (sse, m, l, r)
+                total += best[0]
+                modes[by // n, bx // n] = best[1]
+                lvl[by:by + n, bx:bx + n] = best[2]
+                blk.write_pixels(best[3])
+        out.update({f"{key}_src": src, f"{key}_qp": np.int64(qp), f"{key}_modes": modes, f"{key}_lvl": lvl,
+                    f"{key}_rec": recon.data, f"{key}_sse": np.int64(total)})
+    return out
+
+
 def plane_hash_1080p(T, Q):
     rng = np.random.default_rng(20260)
     plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
@@ -455,6 +504,7 @@ def main():
         "metrics.npz": gen_metrics(M),
         "cfg5.npz": gen_cfg5(I, T, Q, M),
         "encode.npz": gen_encode(ref),
+        "closed.npz": gen_closed(I, T, Q),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

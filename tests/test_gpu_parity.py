@@ -538,3 +538,79 @@ def test_fused8x8_epilogue_vs_reference_helpers(nh, torch_dev, qp, intra, kind):
     # optional outputs
     _, n2, b2 = gpu.fwd8x8_quant_ex(d, sets, qp, intra, bits=False)
     assert b2 is None and torch.equal(n2, nnz)
+
+
+# ------------------------------------------------------------------ f-1: closed-loop config 3 (wavefront)
+
+@pytest.mark.parametrize("key", ["c3a", "c3b", "c3c"])
+def test_intra_rdo_closed_golden(nh, torch_dev, golden, key):
+    """Closed loop vs planes composed from the reference's own BlockView /
+    Plane / predictor / transform / quant functions (make_golden.gen_closed)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    g = golden("closed.npz")
+    src = g[key + "_src"]
+    h, w = src.shape
+    d = torch.from_numpy(src.reshape(-1).copy()).cuda()
+    modes, lvl, rec, sse = gpu.intra_rdo_closed(d, [gpu.plane_set(0, w, h, w)], int(g[key + "_qp"]))
+    assert np.array_equal(modes.cpu().numpy().reshape(h // 8, w // 8), g[key + "_modes"])
+    assert np.array_equal(lvl.cpu().numpy().reshape(h, w), g[key + "_lvl"])
+    assert np.array_equal(rec.cpu().numpy().reshape(h, w), g[key + "_rec"])
+    assert int(sse.cpu()[0]) == int(g[key + "_sse"])
+
+
+@pytest.mark.parametrize("F,W,H,qp", [(4, 352, 288, 32), (2, 200, 104, 22)])
+def test_intra_rdo_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp):
+    """Many planes at once (concurrent wavefronts, rows of different planes
+    interleaved by the ticket order): every plane equals the sequential oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(F * 1000 + qp)
+    planes = []
+    for f in range(F):
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            planes.append(np.clip(50 + (2 * xx + 3 * yy + 11 * f) % 160 + rng.integers(-10, 11, (ph, pw)), 0, 255)
+                          .astype(np.int16))
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sets = gpu.yuv420_plane_sets(F, W, H)
+    modes, lvl, rec, sse = gpu.intra_rdo_closed(d, sets, qp)
+    modes, lvl, rec, sse = modes.cpu().numpy(), lvl.cpu().numpy(), rec.cpu().numpy(), sse.cpu().numpy()
+    # plane order of the outputs: all Y planes (set 0), then U, V of each frame (set 1)
+    order = [3 * f for f in range(F)] + [3 * f + c for f in range(F) for c in (1, 2)]
+    offs = np.cumsum([0] + [p.size for p in planes])
+    m0 = 0
+    for k, pi in enumerate(order):
+        p = planes[pi]
+        ph, pw = p.shape
+        em, el, er, es = O.intra_rdo_plane(p, qp, closed=True)
+        n = (ph // 8) * (pw // 8)
+        assert np.array_equal(modes[m0:m0 + n].reshape(ph // 8, pw // 8), em), (k, pi)
+        m0 += n
+        o = offs[pi]
+        assert np.array_equal(lvl[o:o + p.size].reshape(p.shape), el), (k, pi)
+        assert np.array_equal(rec[o:o + p.size].reshape(p.shape), er), (k, pi)
+        assert int(sse[k]) == es
+    # the closed loop is a different encoder than the open loop
+    _, _, ro, _ = O.intra_rdo_plane(planes[0], qp)
+    assert not np.array_equal(ro, rec[:planes[0].size].reshape(planes[0].shape))
+
+
+def test_intra_rdo_closed_ragged_and_int16(nh, torch_dev):
+    """Partial blocks (recon 0 there, and read as 0 by the top-right references)
+    and full-range int16 sources."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(55)
+    for src, qp in ((rng.integers(0, 256, (45, 67)).astype(np.int16), 27),
+                    (rng.integers(-32768, 32768, (24, 40)).astype(np.int16), 12)):
+        h, w = src.shape
+        d = torch.from_numpy(src.reshape(-1).copy()).cuda()
+        rec_in = torch.full((h * w,), 777, dtype=torch.int16, device="cuda")
+        modes, lvl, rec, sse = gpu.intra_rdo_closed(d, [gpu.plane_set(0, w, h, w)], qp, rec=rec_in)
+        em, el, er, es = O.intra_rdo_plane(src, qp, closed=True)
+        assert np.array_equal(modes.cpu().numpy().reshape(h // 8, w // 8), em)
+        assert np.array_equal(rec.cpu().numpy().reshape(h, w), er)
+        assert np.array_equal(lvl.cpu().numpy().reshape(h, w)[:h // 8 * 8, :w // 8 * 8], el[:h // 8 * 8, :w // 8 * 8])
+        assert int(sse.cpu()[0]) == es

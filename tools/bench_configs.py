@@ -10,6 +10,9 @@
         4x4 chroma) over a stream of 4K YUV420p byte frames -> int16 recon + stats;
         HBM roofline at 3 B/sample (1 B source read + 2 B recon write).
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
+  closed  config 3 in CLOSED loop (neighbours from the reconstruction, wavefront
+        schedule) over a batch of 1080p YUV420 frames; with --check, frame 0's
+        luma against the oracle.
 
 Synthetic 8-bit content (gradient + seeded noise) resident in HBM; HIP events
 on the launch stream; one JSON line per config.
@@ -70,6 +73,7 @@ def main():
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
     ap.add_argument("--configs", default="3,4,5,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
+    ap.add_argument("--closed-frames", type=int, default=8)
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     _lib.load()
@@ -190,6 +194,35 @@ def main():
                               "widen_GBps": samples * 3 / ms_w / 1e6, "narrow_GBps": samples * 3 / ms_n / 1e6,
                               "frac_widen": samples * 3 / ms_w / 1e6 / 8000.0,
                               "frac_narrow": samples * 3 / ms_n / 1e6 / 8000.0, "round_trip_exact": ok}), flush=True)
+
+    if "closed" in cfgs:
+        W, H = 1920, 1080
+        nf = args.closed_frames
+        planes = []
+        for f in range(nf):
+            planes += [synth_plane(H, W, 11 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 12 + 3 * f).reshape(-1),
+                       synth_plane(H // 2, W // 2, 13 + 3 * f).reshape(-1)]
+        stream = torch.cat(planes)
+        sets = gpu.yuv420_plane_sets(nf, W, H)
+        lvl = torch.zeros(stream.shape, dtype=torch.int32, device="cuda")
+        rec = torch.zeros(stream.shape, dtype=torch.int16, device="cuda")
+        ms = timed(lambda: gpu.intra_rdo_closed(stream, sets, args.qp, lvl=lvl, rec=rec), max(2, args.reps // 3))
+        modes, _, rec, sse = gpu.intra_rdo_closed(stream, sets, args.qp, lvl=lvl, rec=rec)
+        nblk = modes.numel()
+        line = {"config": "cfg3 closed loop: 35-mode RDO per 8x8, neighbours from the reconstruction, "
+                          "row wavefront on the device, 1080p YUV420 frames",
+                "frames": nf, "ms_per_launch": ms, "ms_per_frame": ms / nf, "frames_per_s": nf / ms * 1e3,
+                "blocks_per_s": nblk / ms * 1e3, "sse_y_frame0": int(sse[0].item()),
+                "note": "one wave per block row; a frame's latency is ~(W/8 + 2*H/8) block steps"}
+        if args.check:
+            from oracle import oracle as O   # checker only
+            y = stream[:W * H].view(H, W).cpu().numpy()
+            t0 = time.perf_counter()
+            em, _, er, es = O.intra_rdo_plane(y, args.qp, closed=True)
+            line["oracle_seconds_luma"] = time.perf_counter() - t0
+            line["luma0_matches_oracle"] = bool(np.array_equal(rec[:W * H].view(H, W).cpu().numpy(), er)
+                                                and int(sse[0].item()) == es)
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
