@@ -134,7 +134,9 @@ int nh_fwd8x8_quant_planes_ex(const int16_t* d_res, int16_t* d_lvl, const nh_pla
                               int qp, int is_intra, uint8_t* d_nnz, int32_t* d_bits, void* stream);
 /* Measurement helper (not a product path): copies d_in to d_out over the same
  * blocks with the hot kernel's exact access pattern -- the achievable-bandwidth
- * ceiling for that pattern.  policy: as the variant's cache policy (0..3). */
+ * ceiling for that pattern.  policy: as the variant's cache policy (0..3),
+ * + 4 * shape for 2-blocks-per-thread pattern probes (1 horizontal pair, 2
+ * lane-interleaved pair, 3 vertical pair; policies 0/1 only). */
 int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, const nh_plane_set* sets, int nsets,
                             int policy, void* stream);
 /* Measurement helper: plain linear 16-B-per-lane streaming copy of nelems
@@ -175,6 +177,14 @@ int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb,
                          uint32_t seed, int qp, int is_luma, int row0, int row1,
                          int32_t* d_lvl, int16_t* d_recon, uint8_t* d_tu, void* d_work,
                          void* stream);
+/* The same over every plane of one plane set in one launch per TU size (a
+ * stream of frames): plane p = g * planes_per_group + c has plane id
+ * plane_id + c (e.g. the U+V set of yuv420 frames: plane_id 1 -> U 1, V 2),
+ * d_lvl / d_recon use the source layout, d_tu holds (h/4)*(w/4) entries per
+ * plane in plane order. */
+int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
+                          uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
+                          int16_t* d_recon, uint8_t* d_tu, void* stream);
 
 /* Config 5: every full 32x32 block of an int16 source plane through the
  * config-4 chain at N=32.  variant 0 = butterfly

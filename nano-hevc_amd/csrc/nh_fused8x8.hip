@@ -234,6 +234,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         e.bits[gb] = (int32_t)(((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])));
 }
 
+// Vertical-pair form: one thread = blocks b and b + blocks_per_row (block rows
+// 2r and 2r+1 of the set's linear row numbering; a pair may straddle two
+// planes, block_offset handles that).  16 row loads in flight per lane; the
+// pattern probe of this shape streams ~4 % faster than the one-block form
+// (profiles/r01/ab_shapes.json).
+template <int POLICY, int WAVES>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant_v2(Fused8Args a) {
+    SetDev S;
+    select_set(a, S);
+    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
+    asm volatile("" : "+v"(h_v), "+v"(hneg_v));
+    const uint32_t t = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    const uint32_t r = fdiv(t, S.bpr), c = t - r * S.bpr.d;
+    const uint32_t b0 = 2 * r * S.bpr.d + c, b1 = b0 + S.bpr.d;
+    if (b0 >= S.nblocks) return;
+    const bool two = b1 < S.nblocks;
+    const int64_t o0 = block_offset(S, b0), o1 = two ? block_offset(S, b1) : o0;
+    v4i raw0[8], raw1[8], outv[8];
+    load_block<POLICY>(a.in + o0, S.pitch, raw0);
+    if (two) load_block<POLICY>(a.in + o1, S.pitch, raw1);
+    dct8_quant_block(raw0, outv, a.q, h_v, hneg_v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o0 + (int64_t)i * S.pitch, outv[i]);
+    if (two) {
+        dct8_quant_block(raw1, outv, a.q, h_v, hneg_v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o1 + (int64_t)i * S.pitch, outv[i]);
+    }
+}
+
 // Persistent, software-pipelined form: a fixed grid of workgroups walks the
 // 256-block tiles with stride gridDim.x; each thread prefetches its block of
 // the NEXT tile (8 x 16 B) before computing the current one, so every wave
@@ -309,6 +339,31 @@ __global__ void __launch_bounds__(256) k_probe_copy8x8(Fused8Args a) {
     for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, raw[i]);
 }
 
+// Shape probes (same copy, 2 blocks per thread): SHAPE 1 = the horizontally
+// adjacent pair (b, b+1: 32 B per row per lane), 2 = lane-interleaved pair
+// (b, b+64 within a wave's 128 blocks: two contiguous 1 KiB runs per row),
+// 3 = vertical pair (b, b + blocks_per_row: 16 rows).  Blocks are taken in
+// pairs of the set's block walk; the launch has twice the workgroups needed.
+template <int POLICY, int SHAPE>
+__global__ void __launch_bounds__(256) k_probe_copy8x8_pair(Fused8Args a) {
+    SetDev S;
+    select_set(a, S);
+    const uint32_t t = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    uint32_t b0, b1;
+    if (SHAPE == 1) { b0 = 2 * t; b1 = b0 + 1; }
+    else if (SHAPE == 2) { b0 = (t / 64) * 128 + (t % 64); b1 = b0 + 64; }
+    else { const uint32_t r = t / S.bpr.d, c = t - r * S.bpr.d; b0 = 2 * r * S.bpr.d + c; b1 = b0 + S.bpr.d; }
+    if (b1 >= S.nblocks) return;   // (probe: a ragged tail is skipped)
+    const int64_t o0 = block_offset(S, b0), o1 = block_offset(S, b1);
+    v4i r0[8], r1[8];
+    load_block<POLICY>(a.in + o0, S.pitch, r0);
+    load_block<POLICY>(a.in + o1, S.pitch, r1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o0 + (int64_t)i * S.pitch, r0[i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o1 + (int64_t)i * S.pitch, r1[i]);
+}
+
 // Memory-only probe: plain linear streaming copy of n 16-B chunks (grid-stride),
 // the HBM ceiling this device reaches with the simplest possible pattern.
 template <int POLICY>
@@ -319,8 +374,10 @@ __global__ void __launch_bounds__(256) k_probe_linear(const int16_t* __restrict_
         st16<POLICY>(out + i * 8, ld16<POLICY>(in + i * 8));
 }
 
+// pairs: 1 = one thread per vertical block pair (rows 2r, 2r+1 of the set's
+// linear block-row numbering): per set ceil(rows/2) * blocks_per_row threads.
 static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
-                      int is_intra, Fused8Args& a, uint32_t& total_wg) {
+                      int is_intra, Fused8Args& a, uint32_t& total_wg, int pairs = 0) {
     if (!d_res || !d_lvl || !sets || nsets < 1 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
     if (((uintptr_t)d_res & 15) || ((uintptr_t)d_lvl & 15)) {
         set_error("fwd8x8: buffers must be 16-byte aligned");
@@ -362,7 +419,8 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
         d.ppg = make_fastdiv((uint32_t)p.planes_per_group);
         d.blk0 = (uint32_t)blk;
         blk += nb;
-        wg += (nb + 255) / 256;
+        const uint64_t nthr = pairs ? (rows * planes + 1) / 2 * bpr : nb;
+        wg += (nthr + 255) / 256;
     }
     for (int k = nsets; k < NH_MAX_PLANE_SETS; ++k) a.set[k].wg_start = 0xffffffffu;
     if (wg >= (1ull << 31) || blk >= (1ull << 32)) return NH_EARG;
@@ -380,14 +438,27 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
                                               int nsets, int qp, int is_intra, int variant, void* stream) {
     // variant = cache policy (0..3, see ld16/st16) + 4 * occupancy class (0 compiler, 1 >= 5 waves/SIMD)
     //           + 8 * persistent software-pipelined form (grid = min(tiles, 256 CUs x 8))
-    const int policy = variant & 3, occ = (variant >> 2) & 1, pipe = variant >> 3;
-    if (variant < 0 || pipe > 1) return NH_EARG;
+    //           + 16 * vertical block pair per thread (with occ: >= 4 waves/SIMD)
+    const int policy = variant & 3, occ = (variant >> 2) & 1, pipe = (variant >> 3) & 1, pair = (variant >> 4) & 1;
+    if (variant < 0 || variant > 31 || (pipe && pair)) return NH_EARG;
     Fused8Args a;
     uint32_t wg = 0;
-    int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+    int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg, pair);
     if (rc) return rc;
     if (!wg) return NH_OK;
     hipStream_t s = as_stream(stream);
+    if (pair) {
+#define NH_V(P) do { if (occ) k_fwd8x8_quant_v2<P, 4><<<wg, 256, 0, s>>>(a); else k_fwd8x8_quant_v2<P, 1><<<wg, 256, 0, s>>>(a); } while (0)
+        switch (policy) {
+            case 0: NH_V(0); break;
+            case 1: NH_V(1); break;
+            case 2: NH_V(2); break;
+            default: NH_V(3); break;
+        }
+#undef NH_V
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
     if (pipe) {
         const uint32_t g = wg < 2048u ? wg : 2048u;
 #define NH_P(P) do { if (occ) k_fwd8x8_quant_pipe<P, 4><<<g, 256, 0, s>>>(a, wg); else k_fwd8x8_quant_pipe<P, 1><<<g, 256, 0, s>>>(a, wg); } while (0)
@@ -423,13 +494,25 @@ extern "C" int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, cons
 
 extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, const nh_plane_set* sets, int nsets,
                                        int policy, void* stream) {
-    if (policy < 0 || policy > 3) return NH_EARG;
+    // policy = cache policy (0..3) + 4 * shape (0 = the kernel's pattern, 1..3 = pair probes)
+    const int shape = policy >> 2;
+    policy &= 3;
+    if (shape < 0 || shape > 3) return NH_EARG;
     Fused8Args a;
     uint32_t wg = 0;
     int rc = build_args(d_in, d_out, sets, nsets, 32, 1, a, wg);
     if (rc) return rc;
     if (!wg) return NH_OK;
     hipStream_t s = as_stream(stream);
+    if (shape) {
+#define NH_PP(P) do { if (shape == 1) k_probe_copy8x8_pair<P, 1><<<wg, 256, 0, s>>>(a); \
+                      else if (shape == 2) k_probe_copy8x8_pair<P, 2><<<wg, 256, 0, s>>>(a); \
+                      else k_probe_copy8x8_pair<P, 3><<<wg, 256, 0, s>>>(a); } while (0)
+        if (policy == 1) NH_PP(1); else NH_PP(0);
+#undef NH_PP
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
     switch (policy) {
         case 0: k_probe_copy8x8<0><<<wg, 256, 0, s>>>(a); break;
         case 1: k_probe_copy8x8<1><<<wg, 256, 0, s>>>(a); break;

@@ -9,8 +9,10 @@
 // planes generated from the reference functions pin them.
 #include <hip/hip_runtime.h>
 #include <climits>
+#include <cstdlib>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
+#include "nh_tree.hpp"
 
 namespace nh {
 
@@ -409,66 +411,85 @@ __global__ void k_zero_partial(int16_t* rec, ClosedSet S, int nplanes) {
 //                  full residual -> transform -> quant -> dequant -> inverse ->
 //                  recon chain with exact int32/int64 arithmetic.
 // ===========================================================================
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x;
-}
-__device__ __forceinline__ bool tu_split(uint32_t seed, int plane_id, int x, int y, int size) {
-    uint32_t k = mix32(seed ^ (0x9E3779B9U * (uint32_t)(plane_id + 1)));
-    k = mix32(k ^ (uint32_t)x);
-    k = mix32(k ^ ((uint32_t)y * 0x85ebca6bU));
-    k = mix32(k ^ (uint32_t)size);
-    return (k & 3u) < 2u;
-}
-
-// Leaf of the seeded quadtree containing sample (ux, uy):
-// descend from the CTB root, at most 3 hash evaluations.  Returns its size.
-__device__ __forceinline__ int tu_leaf(int w, int h, int ctb, int plane_id, uint32_t seed, int ux, int uy) {
-    int s = ctb, x = (ux / ctb) * ctb, y = (uy / ctb) * ctb;
-    while (s > 4 && ((x + s > w) || (y + s > h) || tu_split(seed, plane_id, x, y, s))) {
-        s >>= 1;
-        x += (ux >= x + s) ? s : 0;
-        y += (uy >= y + s) ? s : 0;
-    }
-    return s;
-}
-
 // MODE kAll (config 5): TU idx is the idx-th full NxN block of the plane in
 // raster order (grid_bw blocks per row, grid_n blocks), no TU map.
-// MODE kTree (config 4): idx walks the N-aligned positions of CTU rows
-// [row0, row1); a position is a TU iff its quadtree leaf is exactly NxN
-// (tu_leaf) -- no lists, no atomics, deterministic; the TU writes its map.
+// MODE kTree (config 4): the workgroup's candidates are N-aligned positions of
+// CTU rows [row0, row1); a position is a TU iff its quadtree leaf is exactly
+// NxN (tu_leaf) -- no global lists or atomics, deterministic; the TU writes
+// its map.
 // Multiplies are 24-bit (v_mad_i32_i24): exact for the whole chain because the
 // residual is int16 (forward operands < 2^21), dequantized coefficients are
 // ~|c|*2^20/2^(17+log2N) < 2^19, and inverse pass-2 operands are a >> S of an
 // int32 sum bounded by 2^27 -> < 2^21.
-enum { kAll = 0, kTree = 1 };
-struct TreeArgs {
-    int ctb, plane_id, y_base;   // y_base: first sample row of the band
-    uint32_t seed;
-};
+// Candidates per workgroup: kTree walks every N-aligned position but only
+// ~1/2 (N = 32) to ~1/6 (N = 4, 8) of them are TUs of that size, so a
+// workgroup tests R * G positions, compacts the TUs into an LDS list (wave
+// ballots, no global atomics) and runs the chain over the list in rounds of G.
+
+template <int N, int MODE>
+constexpr int tu_cands_per_wg() { return (256 / N) * (MODE == 1 ? (N == 32 ? 2 : 4) : 1); }
 
 template <int N, bool DST, int MODE>
 __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, int32_t* lvl,
                                                     int16_t* recon, uint8_t* tu_log2, int grid_bw, int grid_n,
                                                     TreeArgs ta) {
-    constexpr int G = 256 / N;            // TUs per workgroup
+    constexpr int G = 256 / N;            // TUs per round
     constexpr int P = N + 1;              // padded LDS row
     constexpr int S = Log2<N>::v + 5;
+    constexpr int K = tu_cands_per_wg<N, MODE>();
+    {   // this workgroup's plane of the batch
+        const int pz = blockIdx.y, gz = pz / ta.ppg, cz = pz - gz * ta.ppg;
+        const int64_t poff = (int64_t)gz * ta.group_stride + (int64_t)cz * ta.plane_stride;
+        src += poff;
+        lvl += poff;
+        recon += poff;
+        if (tu_log2) tu_log2 += (int64_t)pz * ta.tu_plane;
+        ta.plane_id += cz;
+    }
     __shared__ int32_t tile[G][N][P];
     __shared__ int16_t orig[G][N][N];
     __shared__ int16_t topv[G][N], leftv[G][N];
     __shared__ long long e_dc[G][N], e_pl[G][N];
+    __shared__ uint32_t list[MODE == kTree ? K : 1];
+    __shared__ int wave_cnt[4], list_n;
     const int g = threadIdx.x / N, t = threadIdx.x % N;
-    const uint32_t idx = blockIdx.x * G + g;
-    bool active = idx < (uint32_t)grid_n;
+    int ntu;
+    if constexpr (MODE == kTree) {
+        // phase 1: which candidate positions are TUs of size N (tu_leaf), compacted
+        const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+        if (threadIdx.x == 0) list_n = 0;
+        __syncthreads();
+        for (int k0 = 0; k0 < K; k0 += 256) {
+            const int k = k0 + threadIdx.x;
+            const uint32_t c = blockIdx.x * (uint32_t)K + k;
+            bool f = false;
+            if (k < K && c < (uint32_t)grid_n) {
+                const int cx = (c % grid_bw) * N, cy = (c / grid_bw) * N + ta.y_base;
+                f = (cx + N <= w) && (cy + N <= h) && tu_leaf(w, h, ta.ctb, ta.plane_id, ta.seed, cx, cy) == N;
+            }
+            const uint64_t m = __ballot(f);
+            if (lane == 0) wave_cnt[wv] = __popcll(m);
+            __syncthreads();
+            int base = list_n;
+            for (int q = 0; q < wv; ++q) base += wave_cnt[q];
+            if (f) list[base + __popcll(m & ((1ull << lane) - 1))] = c;
+            __syncthreads();
+            if (threadIdx.x == 0) list_n += wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+            __syncthreads();
+        }
+        ntu = list_n;
+    } else {
+        ntu = grid_n - (int)(blockIdx.x * G);
+        ntu = ntu < G ? ntu : G;
+    }
+    for (int r0 = 0; r0 < ntu; r0 += G) {   // rounds of G TUs (uniform over the workgroup)
+    bool active = r0 + g < ntu;
     int x0 = 0, y0 = 0;
     if (active) {
+        const uint32_t idx = MODE == kTree ? list[r0 + g] : blockIdx.x * G + g;
         x0 = (idx % grid_bw) * N;
         y0 = (idx / grid_bw) * N + (MODE == kTree ? ta.y_base : 0);
-        if constexpr (MODE == kTree)
-            active = (x0 + N <= w) && (y0 + N <= h) && tu_leaf(w, h, ta.ctb, ta.plane_id, ta.seed, x0, y0) == N;
     }
     if (active) {
         // neighbours (block.py:38-50): count N, 128 outside the plane (full TUs: no truncation)
@@ -567,6 +588,8 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
             for (int j = 0; j < N / 4; ++j) tu_log2[(int64_t)(y0 / 4 + t) * w4 + x0 / 4 + j] = (uint8_t)Log2<N>::v;
         }
     }
+    __syncthreads();   // the next round reuses the LDS tiles
+    }
 }
 
 static void qp_split(int qp, int* per, int* rem) {
@@ -621,13 +644,23 @@ extern "C" int64_t nh_tu_workspace_bytes(int w, int h, int ctb) {
     return 0;   // no scratch: TUs are found by per-size grid walks (k_tu_process kTree)
 }
 
-extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb, int plane_id,
-                                    uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
-                                    int16_t* d_recon, uint8_t* d_tu, void* d_work, void* stream) {
-    (void)d_work;
-    if (!d_src || !d_lvl || !d_recon || !d_tu || pitch < w || w <= 0 || h <= 0) return NH_EARG;
+namespace nh {
+// nh_tc32.hip: config 4's 32x32 TUs on the int8 matrix cores
+int tc32_mfma_tree(const int16_t* src, int w, int h, int pitch, const QuantParams& qp, int dq_scale, int dq_per,
+                   int32_t* lvl, int16_t* rec, uint8_t* tu, int bw, int n, const TreeArgs& ta, unsigned planes,
+                   hipStream_t s);
+}  // namespace nh
+
+extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
+                                     uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
+                                     int16_t* d_recon, uint8_t* d_tu, void* stream) {
+    if (!d_src || !set || !d_lvl || !d_recon || !d_tu) return NH_EARG;
+    const int w = set->width, h = set->height, pitch = set->pitch;
+    const int64_t planes = (int64_t)set->planes_per_group * set->num_groups;
+    if (pitch < w || w <= 0 || h <= 0 || set->planes_per_group < 1 || planes < 0 || planes > 65535) return NH_EARG;
     if (ctb != 4 && ctb != 8 && ctb != 16 && ctb != 32) return NH_EVALUE;
     if ((w & 3) || (h & 3) || w > 65535 || h > 65535) return NH_EARG;
+    if (!planes) return NH_OK;
     hipStream_t s = as_stream(stream);
     const int rows = (h + ctb - 1) / ctb;
     if (row0 < 0) row0 = 0;
@@ -638,20 +671,55 @@ extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitc
     const int dqs = dequant_scale(rem);
     const int yb = row0 * ctb, ye = row1 * ctb < h ? row1 * ctb : h;
     TreeArgs ta{ctb, plane_id, yb, seed};
+    ta.ppg = set->planes_per_group;
+    ta.group_stride = set->group_stride;
+    ta.plane_stride = set->plane_stride;
+    ta.tu_plane = (int64_t)(h / 4) * (w / 4);
+    const int16_t* src = d_src + set->base;
+    int32_t* lvl = d_lvl + set->base;
+    int16_t* rec = d_recon + set->base;
 #define NH_TU(NN, DST)                                                                                       \
     do {                                                                                                     \
         const int bw = w / NN, bh = (ye - yb + NN - 1) / NN, n = bw * bh;                                   \
         if (NN <= ctb && n > 0)                                                                              \
-            k_tu_process<NN, DST, kTree><<<(n + 256 / NN - 1) / (256 / NN), 256, 0, s>>>(                    \
-                d_src, w, h, pitch, qparams(qp, Log2<NN>::v, true), dqs, per, d_lvl, d_recon, d_tu, bw, n, ta); \
+            k_tu_process<NN, DST, kTree><<<dim3((n + tu_cands_per_wg<NN, kTree>() - 1) / tu_cands_per_wg<NN, kTree>(), \
+                                                (unsigned)planes), 256, 0, s>>>(                                 \
+                src, w, h, pitch, qparams(qp, Log2<NN>::v, true), dqs, per, lvl, rec, d_tu, bw, n, ta);          \
     } while (0)
     if (is_luma) NH_TU(4, true); else NH_TU(4, false);
     NH_TU(8, false);
     NH_TU(16, false);
-    NH_TU(32, false);
+    // 32x32 TUs: int8 MFMA (the config-5 A/B winner) where the layout allows its
+    // 16-B row accesses; NH_TU32_BUTTERFLY=1 forces the butterfly (A/B only)
+    static int tu32_bf = -1;
+    if (tu32_bf < 0) {
+        const char* e = getenv("NH_TU32_BUTTERFLY");
+        tu32_bf = e && atoi(e) == 1;
+    }
+    const bool mfma_ok = !tu32_bf && !(pitch & 7) && !((ta.group_stride | ta.plane_stride) & 7) &&
+                         !(((uintptr_t)src | (uintptr_t)lvl | (uintptr_t)rec) & 15);
+    if (ctb == 32 && mfma_ok) {
+        const int bw = w / 32, bh = (ye - yb + 31) / 32, n = bw * bh;
+        if (n > 0) {
+            const int rc = tc32_mfma_tree(src, w, h, pitch, qparams(qp, 5, true), dqs, per, lvl, rec, d_tu, bw, n, ta,
+                                          (unsigned)planes, s);
+            if (rc) return rc;
+        }
+    } else {
+        NH_TU(32, false);
+    }
 #undef NH_TU
     NH_HIP(hipGetLastError());
     return NH_OK;
+}
+
+extern "C" int nh_tu_pipeline_plane(const int16_t* d_src, int w, int h, int pitch, int ctb, int plane_id,
+                                    uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
+                                    int16_t* d_recon, uint8_t* d_tu, void* d_work, void* stream) {
+    (void)d_work;
+    nh_plane_set one{0, 0, 0, w, h, pitch, 1, 1, 0};
+    return nh_tu_pipeline_planes(d_src, &one, ctb, plane_id, seed, qp, is_luma, row0, row1, d_lvl, d_recon, d_tu,
+                                 stream);
 }
 
 static int closed_layout(const nh_plane_set* sets, int nsets, ClosedArgs& a, int64_t& modes_total) {

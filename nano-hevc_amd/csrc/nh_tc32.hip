@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
+#include "nh_tree.hpp"
 
 namespace nh {
 
@@ -125,16 +126,35 @@ __device__ __forceinline__ int32_t wrap16i(int32_t v) { return (int16_t)(uint16_
 
 constexpr int kOP = 40;  // LDS row pitch (elements) of the per-wave tiles: 16-B aligned rows
 
+// TREE (config 4's 32x32 TUs): block b walks the 32-aligned positions of the
+// band (rows from ta.y_base) of plane blockIdx.y of the batch, and a wave only
+// proceeds where the seeded quadtree's leaf is exactly 32x32 (tu_leaf); it
+// then also writes its 8x8 entries of the TU map.  Same per-TU chain as
+// k_tu_process<32>.
+template <bool TREE>
 __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                    int nbx, int nblk, QuantParams qp, int dq_scale, int dq_per,
-                                                   int32_t* lvl, int16_t* recon) {
+                                                   int32_t* lvl, int16_t* recon, TreeArgs ta, uint8_t* tu_log2) {
     __shared__ int16_t s_orig[4][32][kOP];
     __shared__ int32_t s_dq[4][32][kOP];
     __shared__ int16_t s_top[4][32], s_left[4][32];
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
     const int b = blockIdx.x * 4 + wv;
     if (b >= nblk) return;                       // whole wave exits together
-    const int x0 = (b % nbx) * 32, y0 = (b / nbx) * 32;
+    if constexpr (TREE) {   // this workgroup's plane of the batch
+        const int pz = blockIdx.y, gz = pz / ta.ppg, cz = pz - gz * ta.ppg;
+        const int64_t poff = (int64_t)gz * ta.group_stride + (int64_t)cz * ta.plane_stride;
+        src += poff;
+        lvl += poff;
+        recon += poff;
+        tu_log2 += (int64_t)pz * ta.tu_plane;
+        ta.plane_id += cz;
+    }
+    const int x0 = (b % nbx) * 32, y0 = (b / nbx) * 32 + (TREE ? ta.y_base : 0);
+    if constexpr (TREE) {
+        if (x0 + 32 > w || y0 + 32 > h || tu_leaf(w, h, ta.ctb, ta.plane_id, ta.seed, x0, y0) != 32) return;
+        tu_log2[(int64_t)(y0 / 4 + (l >> 3)) * (w / 4) + x0 / 4 + (l & 7)] = 5;
+    }
 
     // ---- load the block (2 x 16 B per lane) and its neighbours (block.py:38-50) ----
     {
@@ -290,11 +310,28 @@ extern "C" int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int 
     p.shift = 14 + per + 5;
     p.mf = quant_scale(rem);
     p.off = (uint32_t)((1ull << p.shift) / 3);
-    k_tc32_mfma<<<(nblk + 3) / 4, 256, 0, s>>>(d_src, w, h, pitch, nbx, nblk, p, dequant_scale(rem), per, d_lvl,
-                                               d_recon);
+    k_tc32_mfma<false><<<(nblk + 3) / 4, 256, 0, s>>>(d_src, w, h, pitch, nbx, nblk, p, dequant_scale(rem), per,
+                                                      d_lvl, d_recon, TreeArgs{}, nullptr);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
+
+namespace nh {
+// Config 4's 32x32 TUs on the int8 matrix cores (called by nh_tu_pipeline_planes).
+int tc32_mfma_tree(const int16_t* src, int w, int h, int pitch, const QuantParams& qp, int dq_scale, int dq_per,
+                   int32_t* lvl, int16_t* rec, uint8_t* tu, int bw, int n, const TreeArgs& ta, unsigned planes,
+                   hipStream_t s) {
+    if ((pitch & 7) || (((uintptr_t)src | (uintptr_t)lvl | (uintptr_t)rec) & 15) ||
+        ((ta.group_stride | ta.plane_stride) & 7))
+        return NH_EARG;   // the MFMA kernel's vector row accesses need 16-B aligned rows
+    int rc = ensure_basis(s);
+    if (rc) return rc;
+    k_tc32_mfma<true><<<dim3((n + 3) / 4, planes), 256, 0, s>>>(src, w, h, pitch, bw, n, qp, dq_scale, dq_per, lvl, rec,
+                                                                ta, tu);
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+}  // namespace nh
 
 extern "C" int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream) {
     if (!d_a || !d_b || !d_d) return NH_EARG;

@@ -249,6 +249,32 @@ def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_
     return lvl, rec, tu
 
 
+def tu_pipeline_planes(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
+                       row0: int = 0, row1: int = 1 << 30, lvl=None, rec=None, tu=None, stream=None):
+    """Config 4 over every plane of one plane set in one launch per TU size
+    (plane p = g*ppg + c gets plane id plane_id + c).  Returns (lvl int32,
+    recon int16 -- source layout --, tu uint8 (planes, h/4, w/4))."""
+    torch = _torch()
+    _need(src, torch.int16, "tu_pipeline_planes(src)")
+    sets_fit([pset], src.numel(), "tu_pipeline_planes")
+    planes = pset.planes_per_group * pset.num_groups
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int32, device=src.device)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    if tu is None:
+        tu = torch.zeros((planes, pset.height // 4, pset.width // 4), dtype=torch.uint8, device=src.device)
+    _need(lvl, torch.int32, "tu_pipeline_planes(lvl)")
+    _need(rec, torch.int16, "tu_pipeline_planes(rec)")
+    _need(tu, torch.uint8, "tu_pipeline_planes(tu)")
+    if lvl.numel() < src.numel() or rec.numel() < src.numel() or tu.numel() < planes * (pset.height // 4) * (pset.width // 4):
+        raise ValueError("tu_pipeline_planes: output too small")
+    check(_lib.load().nh_tu_pipeline_planes(src.data_ptr(), C.byref(pset), int(ctb), int(plane_id), int(seed) & 0xffffffff,
+                                            int(qp), int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)),
+                                            lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(), C.c_void_p(_stream(stream))))
+    return lvl, rec, tu
+
+
 def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=None):
     """Config 5 on one int16 plane (H, W), W % 8 == 0: every full
     32x32 block through the chain.  variant 0 = butterfly, 1 = int8 MFMA.

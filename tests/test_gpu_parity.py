@@ -328,7 +328,8 @@ def test_tu_pipeline_golden(nh, torch_dev, golden):
     assert np.array_equal(l.cpu().numpy(), g["p4u_lvl"]) and np.array_equal(r.cpu().numpy(), g["p4u_rec"])
 
 
-@pytest.mark.parametrize("h,w,ctb,luma,seed", [(136, 200, 32, True, 7), (68, 100, 16, False, 7), (64, 64, 32, True, 99)])
+@pytest.mark.parametrize("h,w,ctb,luma,seed", [(136, 200, 32, True, 7), (68, 100, 16, False, 7), (64, 64, 32, True, 99),
+                                                 (132, 196, 32, True, 5)])   # pitch % 8 != 0: butterfly 32x32
 def test_tu_pipeline_vs_oracle_and_bands(nh, torch_dev, h, w, ctb, luma, seed):
     """Whole plane, then the same plane as CTU-row bands (the multi-GPU shard
     unit): bands must tile the plane and agree with the oracle."""
@@ -614,3 +615,58 @@ def test_intra_rdo_closed_ragged_and_int16(nh, torch_dev):
         assert np.array_equal(rec.cpu().numpy().reshape(h, w), er)
         assert np.array_equal(lvl.cpu().numpy().reshape(h, w)[:h // 8 * 8, :w // 8 * 8], el[:h // 8 * 8, :w // 8 * 8])
         assert int(sse.cpu()[0]) == es
+
+
+@pytest.mark.parametrize("variant", [17, 21, 9, 13])
+def test_fused8x8_launch_variants_equal(nh, torch_dev, variant):
+    """Every A/B launch form (pipelined 9/13, vertical block pair 17/21) gives
+    the default kernel's levels: a 4K YUV420 stream (135 chroma block rows: pairs
+    straddle planes) and ragged planes with an odd number of block rows."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(variant)
+    F, W, H = 3, 3840, 2160
+    fe = gpu.yuv420_frame_elems(W, H)
+    buf = torch.from_numpy(rng.integers(-32768, 32768, size=F * fe).astype(np.int16)).cuda()
+    sets = gpu.yuv420_plane_sets(F, W, H)
+    ref = gpu.fwd8x8_quant(buf, sets, 27, True)
+    assert torch.equal(gpu.fwd8x8_quant(buf, sets, 27, True, variant=variant), ref)
+    plane = rng.integers(-255, 256, size=(3 * 40 * 56,)).astype(np.int16)   # 3 planes of 40x56: 5 block rows each
+    d = torch.from_numpy(plane).cuda()
+    s1 = [gpu.plane_set(0, 56, 40, 56, 1, 3, 0, 40 * 56)]
+    out = gpu.fwd8x8_quant(d, s1, 32, False, variant=variant).cpu().numpy()
+    for k in range(3):
+        p = plane[k * 2240:(k + 1) * 2240].reshape(40, 56)
+        assert np.array_equal(out[k * 2240:(k + 1) * 2240].reshape(40, 56), O.fwd8x8_quant_plane(p, 32, False))
+
+
+@pytest.mark.parametrize("W,H,rows", [(640, 360, (0, 1 << 30)), (200, 120, (1, 3))])
+def test_tu_pipeline_planes_batched_vs_oracle(nh, torch_dev, W, H, rows):
+    """Config 4 over a whole YUV420 stream in one launch per TU size and plane
+    set (luma set: ctb 32, plane id 0; U+V set: ctb 16, ids 1/2): every plane
+    equals the per-plane oracle (also on a CTU-row band)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F = 3
+    rng = np.random.default_rng(W + F)
+    planes = []
+    for f in range(F):
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            planes.append(np.clip(70 + (xx + 2 * yy + 9 * f) % 140 + rng.integers(-20, 21, (ph, pw)), 0, 255).astype(np.int16))
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(F, W, H)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy = gpu.tu_pipeline_planes(d, sy, 32, 0, 4242, 30, True, *rows, lvl=lvl, rec=rec)
+    _, _, tuc = gpu.tu_pipeline_planes(d, suv, 16, 1, 4242, 30, False, *rows, lvl=lvl, rec=rec)
+    lvl, rec, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    offs = np.cumsum([0] + [p.size for p in planes])
+    for k, p in enumerate(planes):
+        f, c = divmod(k, 3)
+        el, er, et = O.tu_pipeline_plane(p, 32 if c == 0 else 16, c, 4242, 30, c == 0, *rows)
+        o = offs[k]
+        assert np.array_equal(lvl[o:o + p.size].reshape(p.shape), el), (f, c)
+        assert np.array_equal(rec[o:o + p.size].reshape(p.shape), er), (f, c)
+        assert np.array_equal(tuy[f] if c == 0 else tuc[2 * f + c - 1], et), (f, c)

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="1,5,9,13")
     ap.add_argument("--epilogue", action="store_true", help="also time the fused level-side epilogue (ex, exnnz)")
+    ap.add_argument("--shapes", action="store_true", help="also time the 2-blocks-per-thread pattern probes")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     L = _lib.load()
@@ -56,6 +57,10 @@ def main():
         elif name.startswith("probe"):
             _lib.check(L.nh_probe_copy8x8_planes(res.data_ptr(), o.data_ptr(), arr, len(sets), int(name[5:]),
                                                  C.c_void_p(st.cuda_stream)))
+        elif name.startswith("shape"):     # shapeS_P: pair probe S with cache policy P
+            sh, pol = name[5:].split("_")
+            _lib.check(L.nh_probe_copy8x8_planes(res.data_ptr(), o.data_ptr(), arr, len(sets), int(pol) + 4 * int(sh),
+                                                 C.c_void_p(st.cuda_stream)))
         elif name == "ex":        # + fused count_nonzero / estimate_bits epilogue (261 B/block)
             _lib.check(L.nh_fwd8x8_quant_planes_ex(res.data_ptr(), o.data_ptr(), arr, len(sets), 32, 1,
                                                    ex_nnz.data_ptr(), ex_bits.data_ptr(), C.c_void_p(st.cuda_stream)))
@@ -66,7 +71,8 @@ def main():
             gpu.fwd8x8_quant(res, sets, 32, True, out=o, variant=int(name[1:]), stream=st)
 
     names = (["torch_copy"] + [f"probe{p}" for p in range(4)] + [f"linear{p}g{g}" for p in (0, 1) for g in (0, 4096)]
-             + [f"v{v}" for v in variants] + (["ex", "exnnz"] if args.epilogue else []))
+             + [f"v{v}" for v in variants] + (["ex", "exnnz"] if args.epilogue else [])
+             + ([f"shape{sh}_{p}" for sh in (1, 2, 3) for p in (0, 1)] if args.shapes else []))
     ex_nnz = torch.empty(nblk, dtype=torch.uint8, device="cuda")
     ex_bits = torch.empty(nblk, dtype=torch.int32, device="cuda")
     for n in names:

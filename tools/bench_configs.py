@@ -9,6 +9,7 @@
   enc   encode_frame_intra (__main__.py:142-189, DC vs planar per block, 8x8 luma /
         4x4 chroma) over a stream of 4K YUV420p byte frames -> int16 recon + stats;
         HBM roofline at 3 B/sample (1 B source read + 2 B recon write).
+  4b    config 4 batched: 16 4K YUV420 frames in one launch per TU size and plane set.
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
   closed  config 3 in CLOSED loop (neighbours from the reconstruction, wavefront
         schedule) over a batch of 1080p YUV420 frames; with --check, frame 0's
@@ -71,7 +72,7 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
-    ap.add_argument("--configs", default="3,4,5,enc,io")
+    ap.add_argument("--configs", default="3,4,4b,5,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
     ap.add_argument("--closed-frames", type=int, default=8)
     args = ap.parse_args()
@@ -115,6 +116,30 @@ def main():
         print(json.dumps({"config": "cfg4 4K YUV420 mixed 4/8/16/32 TUs per CTU (DC/planar + full chain)",
                           "ms_per_frame": ms, "frames_per_s": 1e3 / ms, "samples_per_s": samples / ms * 1e3,
                           "samples_by_tu_size": hist, "psnr_y": psnr_dev(planes[0][0], bufs[0][1])}), flush=True)
+
+    if "4b" in cfgs:   # config 4 batched: the whole stream in 2 plane sets x 4 TU sizes = 8 launches
+        W, H, nf = 3840, 2160, 16
+        planes = []
+        for f in range(nf):
+            planes += [synth_plane(H, W, 40 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 41 + 3 * f).reshape(-1),
+                       synth_plane(H // 2, W // 2, 42 + 3 * f).reshape(-1)]
+        stream = torch.cat(planes)
+        sy, suv = gpu.yuv420_plane_sets(nf, W, H)
+        lv = torch.zeros(stream.shape, dtype=torch.int32, device="cuda")
+        rc = torch.zeros(stream.shape, dtype=torch.int16, device="cuda")
+        tuy = torch.zeros((nf, H // 4, W // 4), dtype=torch.uint8, device="cuda")
+        tuc = torch.zeros((2 * nf, H // 8, W // 8), dtype=torch.uint8, device="cuda")
+
+        def run4b():
+            gpu.tu_pipeline_planes(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy)
+            gpu.tu_pipeline_planes(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc)
+        ms = timed(run4b, args.reps)
+        samples = stream.numel()
+        print(json.dumps({"config": "cfg4 batched: 16 x 4K YUV420 frames, mixed 4/8/16/32 TUs per CTU, 8 launches",
+                          "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "frames_per_s": nf / ms * 1e3,
+                          "samples_per_s": samples / ms * 1e3,
+                          "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
+                          "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}), flush=True)
 
     if 5 in cfgs:
         W, H = 7680, 4320
