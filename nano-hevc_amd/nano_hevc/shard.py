@@ -157,3 +157,70 @@ def gather_to_root(local, layouts_total_elems: List[int], dist, group=None):
         return [b.view(torch.uint8)[:m * es].view(local.dtype) for b, m in zip(bufs, layouts_total_elems)]
     dist.gather(send, dst=0, group=group)
     return None
+
+
+# ---------------------------------------------------------------------------
+# Config 4 (mixed TUs): CTU-row bands of full frames.  The
+# TU chain reads the source row above its band (block.py:38-50), so every rank
+# holds the whole input stream and computes only its bands (rotation as
+# above); reconstructed bands are packed, gathered to rank 0 and unpacked.
+# ---------------------------------------------------------------------------
+
+def cfg4_plan(rank: int, world: int, frames: int) -> List[Tuple[int, int, int]]:
+    """(band, first frame, count) per band this rank processes: the frames
+    f = first, first + world, ... (band_of(rank, f, world) == band)."""
+    plan = []
+    for b in range(world):
+        f0 = (b - rank) % world
+        cnt = len(range(f0, frames, world))
+        if cnt:
+            plan.append((b, f0, cnt))
+    return plan
+
+
+def _band_views(stream, f: int, y0: int, y1: int, width: int, height: int):
+    """Flat slices [Y rows y0..y1, U rows y0/2..y1/2, V rows ...] of frame f."""
+    cw, ch = width // 2, height // 2
+    fe = width * height + 2 * cw * ch
+    base = f * fe
+    c0, c1 = y0 // 2, y1 // 2
+    u = base + width * height
+    v = u + cw * ch
+    return [stream[base + width * y0:base + width * y1], stream[u + cw * c0:u + cw * c1],
+            stream[v + cw * c0:v + cw * c1]]
+
+
+def cfg4_pack(stream, rank: int, world: int, frames: int, width: int, height: int):
+    """This rank's reconstructed bands of a full-frame stream, packed band-major
+    (frames in plan order, Y then U then V rows of each) into one flat tensor."""
+    import torch
+    bands = ctu_bands(height, world)
+    parts = []
+    for b, f0, cnt in cfg4_plan(rank, world, frames):
+        y0, y1 = bands[b]
+        for f in range(f0, frames, world):
+            parts += _band_views(stream, f, y0, y1, width, height)
+    return torch.cat(parts) if parts else stream[:0].clone()
+
+
+def cfg4_unpack(packed, rank: int, world: int, frames: int, width: int, height: int, stream):
+    """Inverse of cfg4_pack: write rank ``rank``'s bands into the full stream."""
+    bands = ctu_bands(height, world)
+    o = 0
+    for b, f0, cnt in cfg4_plan(rank, world, frames):
+        y0, y1 = bands[b]
+        for f in range(f0, frames, world):
+            for view in _band_views(stream, f, y0, y1, width, height):
+                view.copy_(packed[o:o + view.numel()])
+                o += view.numel()
+    return o
+
+
+def cfg4_packed_elems(rank: int, world: int, frames: int, width: int, height: int) -> int:
+    bands = ctu_bands(height, world)
+    cw = width // 2
+    n = 0
+    for b, f0, cnt in cfg4_plan(rank, world, frames):
+        y0, y1 = bands[b]
+        n += cnt * (width * (y1 - y0) + 2 * cw * (y1 // 2 - y0 // 2))
+    return n

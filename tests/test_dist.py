@@ -119,3 +119,77 @@ def test_gloo_world2_band_shard_and_gather():
         p.join(120)
         assert p.exitcode == 0
     assert q.get() is True
+
+
+# ---------------------------------------------------------------- config 4: bands of full frames
+
+def _cfg4_worker(rank, world, port, w, h, n, q):
+    """Each rank holds the full stream, computes only its CTU-row bands (the
+    oracle stands in for the device kernel: same row0/row1 contract as
+    nh_tu_pipeline_planes), packs them, gathers to rank 0; rank 0 unpacks and
+    must get exactly the unsharded reconstruction."""
+    from oracle import oracle as O
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    frames = _frames(n, w, h, 11)
+    cw, ch = w // 2, h // 2
+    stream = np.concatenate(frames)
+    rec = np.zeros_like(stream)
+    bands = shard.ctu_bands(h, world)
+
+    def planes_of(f):
+        base = f * (w * h + 2 * cw * ch)
+        return [(base, h, w, 32, 0), (base + w * h, ch, cw, 16, 1), (base + w * h + cw * ch, ch, cw, 16, 2)]
+
+    for b, f0, cnt in shard.cfg4_plan(rank, world, n):
+        y0, y1 = bands[b]
+        r0, r1 = y0 // 32, (y1 + 31) // 32
+        for f in range(f0, n, world):
+            for off, ph, pw, ctb, pid in planes_of(f):
+                _, r, _ = O.tu_pipeline_plane(stream[off:off + ph * pw].reshape(ph, pw), ctb, pid, 77, 30, pid == 0, r0, r1)
+                rows = slice(y0, y1) if pid == 0 else slice(y0 // 2, y1 // 2)
+                rec[off:off + ph * pw].reshape(ph, pw)[rows] = r[rows]
+    packed = shard.cfg4_pack(torch.from_numpy(rec), rank, world, n, w, h)
+    assert packed.numel() == shard.cfg4_packed_elems(rank, world, n, w, h)
+    sizes = [shard.cfg4_packed_elems(r, world, n, w, h) for r in range(world)]
+    got = shard.gather_to_root(packed, sizes, dist)
+    if rank == 0:
+        full = torch.zeros(stream.size, dtype=torch.int16)
+        for r in range(world):
+            assert shard.cfg4_unpack(got[r], r, world, n, w, h, full) == sizes[r]
+        exp = np.zeros_like(stream)
+        for f in range(n):
+            for off, ph, pw, ctb, pid in planes_of(f):
+                _, r, _ = O.tu_pipeline_plane(stream[off:off + ph * pw].reshape(ph, pw), ctb, pid, 77, 30, pid == 0)
+                exp[off:off + ph * pw] = r.ravel()
+        q.put(bool(np.array_equal(full.numpy(), exp)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 4), (3, 5)])
+def test_gloo_cfg4_band_shard_pack_gather(world, n):
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    w, h = 96, 112        # 4 luma CTU rows (3.5 -> partial), ragged chroma
+    procs = [ctx.Process(target=_cfg4_worker, args=(r, world, port, w, h, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    assert q.get() is True
+
+
+def test_cfg4_plan_covers_every_band_once():
+    for world in range(1, 9):
+        for n in (1, world, 3 * world + 1):
+            seen = {}
+            for r in range(world):
+                for b, f0, cnt in shard.cfg4_plan(r, world, n):
+                    for f in range(f0, n, world):
+                        assert (f, b) not in seen
+                        seen[(f, b)] = r
+                        assert shard.band_of(r, f, world) == b
+            assert len(seen) == n * world
