@@ -617,9 +617,10 @@ def test_intra_rdo_closed_ragged_and_int16(nh, torch_dev):
         assert int(sse.cpu()[0]) == es
 
 
-@pytest.mark.parametrize("variant", [17, 21, 9, 13])
+@pytest.mark.parametrize("variant", [17, 21, 9, 13, 33, 97, 32, 35, 129, 128])
 def test_fused8x8_launch_variants_equal(nh, torch_dev, variant):
-    """Every A/B launch form (pipelined 9/13, vertical block pair 17/21) gives
+    """Every A/B launch form (pipelined 9/13, vertical block pair 17/21, stripe
+    form by LDS-DMA 33/32/35, register-staged 97, persistent double-buffered 129/128) gives
     the default kernel's levels: a 4K YUV420 stream (135 chroma block rows: pairs
     straddle planes) and ragged planes with an odd number of block rows."""
     torch = torch_dev
@@ -670,3 +671,13 @@ def test_tu_pipeline_planes_batched_vs_oracle(nh, torch_dev, W, H, rows):
         assert np.array_equal(lvl[o:o + p.size].reshape(p.shape), el), (f, c)
         assert np.array_equal(rec[o:o + p.size].reshape(p.shape), er), (f, c)
         assert np.array_equal(tuy[f] if c == 0 else tuc[2 * f + c - 1], et), (f, c)
+
+
+def test_fused8x8_stripe_form_needs_contiguous_rows(nh, torch_dev):
+    """The stripe form (variant 33) walks a tile as one contiguous range: a plane
+    whose pitch is not 8 * (width // 8) is refused, never silently mis-read."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    d = torch.zeros(64 * 72, dtype=torch.int16, device="cuda")
+    with pytest.raises(ValueError, match="stripe form"):
+        gpu.fwd8x8_quant(d, [gpu.plane_set(0, 60, 64, 72)], 32, True, variant=33)

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--variants", default="1,5,9,13")
     ap.add_argument("--epilogue", action="store_true", help="also time the fused level-side epilogue (ex, exnnz)")
     ap.add_argument("--shapes", action="store_true", help="also time the 2-blocks-per-thread pattern probes")
+    ap.add_argument("--stripe", action="store_true", help="also time the stripe-form copy probes (LDS-DMA / register staging)")
+    ap.add_argument("--rowwave", action="store_true", help="also time the row-per-wave and M-chunks-per-thread linear probes")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     L = _lib.load()
@@ -72,7 +74,9 @@ def main():
 
     names = (["torch_copy"] + [f"probe{p}" for p in range(4)] + [f"linear{p}g{g}" for p in (0, 1) for g in (0, 4096)]
              + [f"v{v}" for v in variants] + (["ex", "exnnz"] if args.epilogue else [])
-             + ([f"shape{sh}_{p}" for sh in (1, 2, 3) for p in (0, 1)] if args.shapes else []))
+             + ([f"shape{sh}_{p}" for sh in (1, 2, 3) for p in (0, 1)] if args.shapes else [])
+             + ([f"shape{sh}_{p}" for sh in (4, 5) for p in (0, 1)] if args.stripe else [])
+             + ([f"shape{sh}_1" for sh in (6, 7)] + [f"linear{1 + 4 * lm}g0" for lm in (1, 2, 3)] if args.rowwave else []))
     ex_nnz = torch.empty(nblk, dtype=torch.uint8, device="cuda")
     ex_bits = torch.empty(nblk, dtype=torch.int32, device="cuda")
     for n in names:
