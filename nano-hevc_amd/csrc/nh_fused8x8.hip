@@ -647,6 +647,28 @@ __global__ void __launch_bounds__(64 * R) k_probe_rowwave(Fused8Args a) {
     for (int i = 0; i < RPW; ++i) st16<POLICY>(a.out + off + (int64_t)(w * RPW + i) * S.pitch, v[i]);
 }
 
+// Row-per-wave probe through LDS with the two workgroup barriers a row-per-lane
+// kernel needs (rows in, exchange, levels out): wave w loads row w of 64 blocks,
+// ds_write, barrier, every lane reads another lane's chunk back (the transpose
+// traffic), barrier, wave w stores row w.
+template <int POLICY>
+__global__ void __launch_bounds__(512) k_probe_rowwave_lds(Fused8Args a) {
+    __shared__ v4i t0[512];
+    SetDev S;
+    select_set(a, S);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t b = (blockIdx.x - S.wg_start) * 64u + lane;
+    const bool ok = b < S.nblocks;
+    const int64_t off = ok ? block_offset(S, b) + (int64_t)w * S.pitch : 0;
+    if (ok) t0[threadIdx.x] = ld16<POLICY>(a.in + off);
+    __syncthreads();
+    v4i v = t0[(threadIdx.x * 8 + (threadIdx.x >> 6)) & 511];   // a transposed read
+    __syncthreads();
+    t0[(threadIdx.x * 8 + (threadIdx.x >> 6)) & 511] = v;
+    __syncthreads();
+    if (ok) st16<POLICY>(a.out + off, t0[threadIdx.x]);
+}
+
 // pairs: 1 = one thread per vertical block pair (rows 2r, 2r+1 of the set's
 // linear block-row numbering): per set ceil(rows/2) * blocks_per_row threads.
 static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
@@ -907,7 +929,7 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
     policy &= 3;
     if (shape == 4 || shape == 5)
         return run_stripe(d_in, d_out, sets, nsets, 32, 1, policy, shape == 5, true, as_stream(stream));
-    if (shape == 6 || shape == 7) {   // row-per-wave probes: 8 waves x 1 row, 4 waves x 2 rows per 64 blocks
+    if (shape >= 6 && shape <= 8) {   // row-per-wave probes: 8 waves x 1 row, 4 waves x 2 rows per 64 blocks, 8 x 1 via LDS
         Fused8Args a;
         uint32_t wg = 0;
         int rc = build_args(d_in, d_out, sets, nsets, 32, 1, a, wg);
@@ -919,7 +941,8 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
         }
         if (!wg64) return NH_OK;
         hipStream_t s = as_stream(stream);
-#define NH_RW(P) do { if (shape == 6) k_probe_rowwave<P, 8><<<(unsigned)wg64, 512, 0, s>>>(a); \
+#define NH_RW(P) do { if (shape == 8) k_probe_rowwave_lds<P><<<(unsigned)wg64, 512, 0, s>>>(a); \
+                      else if (shape == 6) k_probe_rowwave<P, 8><<<(unsigned)wg64, 512, 0, s>>>(a); \
                       else k_probe_rowwave<P, 4><<<(unsigned)wg64, 256, 0, s>>>(a); } while (0)
         if (policy == 1) NH_RW(1); else NH_RW(0);
 #undef NH_RW

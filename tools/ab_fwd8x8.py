@@ -76,7 +76,7 @@ def main():
              + [f"v{v}" for v in variants] + (["ex", "exnnz"] if args.epilogue else [])
              + ([f"shape{sh}_{p}" for sh in (1, 2, 3) for p in (0, 1)] if args.shapes else [])
              + ([f"shape{sh}_{p}" for sh in (4, 5) for p in (0, 1)] if args.stripe else [])
-             + ([f"shape{sh}_1" for sh in (6, 7)] + [f"linear{1 + 4 * lm}g0" for lm in (1, 2, 3)] if args.rowwave else []))
+             + ([f"shape{sh}_1" for sh in (6, 7, 8)] + [f"linear{1 + 4 * lm}g0" for lm in (1, 2, 3)] if args.rowwave else []))
     ex_nnz = torch.empty(nblk, dtype=torch.uint8, device="cuda")
     ex_bits = torch.empty(nblk, dtype=torch.int32, device="cuda")
     for n in names:

@@ -6,7 +6,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r01n}
+TAG=${TAG:-r01o}
 echo "== pytest variants" && \
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "variants or stripe or fused8x8" > gpurun_out/pytest_var_${TAG}.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_var_${TAG}.log; [ $rc -eq 0 ] && \
 echo "== A/B" && \
