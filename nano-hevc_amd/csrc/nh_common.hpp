@@ -200,7 +200,7 @@ struct QuantS {
     uint32_t hneg;   // 2^(shift-1) - 1 - h
     int32_t sh;      // shift - 1
 };
-static inline QuantS make_quants(const QuantParams& q) {
+__host__ __device__ inline QuantS make_quants(const QuantParams& q) {
     QuantS r;
     r.mh = (int32_t)(q.mf / 2);
     r.h = q.off >> 1;

@@ -33,71 +33,210 @@ struct RdoSlotLds {
     int16_t topN[8], leftN[8];
     int32_t ntA, nlA;              // lengths of topA / leftA (9..17)
     int32_t valid;
+    int32_t wide;                  // some orig sample outside [0, 255] (SSE needs 64-bit terms)
     unsigned long long best;
+    uint32_t planar[64];           // mode 0 prediction (intra.py:81-113) as (p, 0) pairs, row-major
+    uint32_t dcv[8];               // mode 1 prediction (intra.py:46-62) as (dc, 0) pairs
 };
+constexpr int kRefStride = 27;
+__device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }     // per-lane angular pair array: 25 pairs, odd stride (LDS banks)
 
-__device__ __forceinline__ int16_t wrap16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
+// The per-block part of the prediction, once per block (not per mode lane):
+// planar (tr = top[-1], bl = left[-1], __main__.py:168-169) and DC; also flags
+// samples outside 8 bits.  k = 0..63 sample index of this thread.
+__device__ __forceinline__ void rdo8_block_prep(RdoSlotLds& B, int k) {
+    const int y = k >> 3, x = k & 7;
+    const int32_t tr = B.topN[7], bl = B.leftN[7];
+    const int32_t p = ((7 - x) * B.leftN[y] + (x + 1) * tr + (7 - y) * B.topN[x] + (y + 1) * bl + 8) >> 4;
+    B.planar[k] = (uint32_t)p & 0xffffu;
+    const int32_t o = B.orig[k];
+    if (o < 0 || o > 255) atomicOr(&B.wide, 1);
+    if (k < 8) {
+        int32_t sum = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sum += B.topN[i] + B.leftN[i];
+        B.dcv[k] = (uint32_t)((sum + 8) >> 4) & 0xffffu;   // floor division by 16 (D7)
+    }
+}
+
+// Quantizer / dequantizer of the chain with uniform parameters.  Exact for any
+// int16 plane: the residual is int16, so |coeff| <= 2^17 (quant_s's range) and
+// |level| <= 26214; dequant = (l * dqs + dqr) >> dqsh with dqs = scale << max(0,
+// per-4) <= 1152, i.e. quant.py:112-123 without its int64 (|l * dqs| < 2^25).
+struct RdoQ {
+    QuantS qs;
+    uint32_t h_v, hneg_v, dqr_v;   // VGPR operands
+    int32_t dqs, dqsh;
+};
+__device__ __forceinline__ RdoQ make_rdoq(const QuantParams& qp, int dq_scale, int dq_per) {
+    RdoQ r;
+    r.qs = make_quants(qp);
+    r.h_v = r.qs.h;
+    r.hneg_v = r.qs.hneg;
+    r.dqs = dq_per < 4 ? dq_scale : dq_scale << (dq_per - 4);
+    r.dqr_v = dq_per < 4 ? 1u << (3 - dq_per) : 0u;
+    r.dqsh = dq_per < 4 ? 4 - dq_per : 0;
+    asm volatile("" : "+v"(r.h_v), "+v"(r.hneg_v), "+v"(r.dqr_v));
+    return r;
+}
+__device__ __forceinline__ int32_t dequant_s(int32_t l, const RdoQ& q) {
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3\n\t"
+        "v_ashrrev_i32_e32 %0, %4, %0"
+        : "=&v"(r) : "v"(l), "s"(q.dqs), "v"(q.dqr_v), "s"(q.dqsh));
+    return r;
+}
+
+typedef short v2s __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ v2s as_v2s(uint32_t u) { return __builtin_bit_cast(v2s, u); }
+__device__ __forceinline__ uint32_t as_u32(v2s v) { return __builtin_bit_cast(uint32_t, v); }
+// v_dot2_i32_i16 (VOP3P, +16): the builtin selects the accumulating dot2c form,
+// which needs an extra move and hazard nops per sample
+__device__ __forceinline__ int dot2_16(uint32_t a, uint32_t w) {
+    int r;
+    asm("v_dot2_i32_i16 %0, %1, %2, 16" : "=v"(r) : "v"(a), "v"(w));
+    return r;
+}
+__device__ __forceinline__ uint32_t dot2_acc(uint32_t a, uint32_t acc) {   // acc + a.x^2 + a.y^2 (int16 lanes)
+    uint32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %1, %2" : "=v"(r) : "v"(a), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ uint32_t pack16(int32_t lo, int32_t hi) {
+    return __builtin_amdgcn_perm((uint32_t)hi, (uint32_t)lo, 0x05040100u);
+}
+
+// INTRA_PRED_ANGLE[mode - 2] (intra.py:24-30) and INV_ANGLE (intra.py:32-34)
+// for a per-lane mode without a memory table (a constexpr array indexed by a
+// lane value compiles to a global load): the 9 magnitudes {0,2,5,9,13,17,21,26,32}
+// packed 6 bits each, indexed by the distance to mode 10 / 26.
+__device__ __forceinline__ int intra_angle_alu(int mode) {
+    constexpr uint64_t kMag = 0ull | (2ull << 6) | (5ull << 12) | (9ull << 18) | (13ull << 24) | (17ull << 30) |
+                              (21ull << 36) | (26ull << 42) | (32ull << 48);
+    const int d = mode < 18 ? 10 - mode : mode - 26;   // > 0: positive angle
+    const int k = d < 0 ? -d : d;
+    const int m = (int)((kMag >> (6 * k)) & 63);
+    return d < 0 ? -m : m;
+}
+__device__ __forceinline__ int inv_angle_alu(int angle) {   // angle < 0: -round(8192 / |angle|)
+    constexpr uint64_t kLo = 4096ull | (1638ull << 13) | (910ull << 26) | (630ull << 39);
+    constexpr uint64_t kHi = 482ull | (390ull << 13) | (315ull << 26) | (256ull << 39);
+    const int a = -angle;   // 2, 5, 9, 13, 17, 21, 26, 32
+    const int k = a == 2 ? 0 : a == 5 ? 1 : a == 9 ? 2 : a == 13 ? 3 : a == 17 ? 4 : a == 21 ? 5 : a == 26 ? 6 : 7;
+    const uint64_t t = k < 4 ? kLo : kHi;
+    return -(int)((t >> (13 * (k & 3))) & 8191);
+}
+
+// Inverse pass 2 (rows) + rres.astype(int16) + reconstruct_block (int16 wrap) +
+// clip_to_pixel_range(., 8) + residual_energy(residual_block(orig, recon)).
+// WIDE = false: every orig sample is 8-bit, so |d| <= 255 and the 64 squares
+// sum in 32 bits with v_dot2; otherwise 64-bit terms.
+template <bool WIDE>
+__device__ __forceinline__ unsigned long long rdo8_recon_sse(uint32_t (&X)[8][8], const uint32_t* opk,
+                                                             uint32_t (&Rpk)[32]) {
+    const v2s zero = {0, 0}, maxv = {255, 255};
+    unsigned long long sse = 0;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        uint32_t x[8];
+        inv_dct<8, Mul24>(X[i], x, 128u);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const v2s rr = as_v2s(pack16((int32_t)x[2 * m] >> 8, (int32_t)x[2 * m + 1] >> 8));
+            v2s rc = as_v2s(Rpk[i * 4 + m]) + rr;
+            rc = __builtin_elementwise_min(__builtin_elementwise_max(rc, zero), maxv);
+            Rpk[i * 4 + m] = as_u32(rc);
+            const v2s d = as_v2s(opk[i * 4 + m]) - rc;
+            if constexpr (!WIDE) {
+                acc = dot2_acc(as_u32(d), acc);
+            } else {
+                const int32_t d0 = d.x, d1 = d.y;
+                sse += (unsigned long long)((uint32_t)(d0 * d0) + (uint32_t)(d1 * d1));
+            }
+        }
+    }
+    return WIDE ? sse : (unsigned long long)acc;
+}
 
 // One lane's mode of the cfg-3 chain on an 8x8 block whose samples and
 // neighbours are in L: prediction (planar / DC / angular, intra.py:46-207) ->
 // residual -> fwd DCT -> quant -> dequant -> inv DCT -> recon -> clip -> SSE.
-// Returns the SSE; P receives the clipped recon, Lv the levels.  ref: this
-// lane's 26-entry angular reference scratch (LDS).
-__device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, int16_t* ref,
-                                                         const QuantParams& qp, int dq_scale, int dq_per,
-                                                         int32_t (&P)[64], int32_t (&Lv)[64]) {
-    if (mode == 0) {            // planar, intra.py:81-113, tr=top[-1], bl=left[-1] (__main__.py:168-169)
-        const int32_t tr = L.topN[7], bl = L.leftN[7];
-#pragma unroll
-        for (int y = 0; y < 8; ++y)
-#pragma unroll
-            for (int x = 0; x < 8; ++x)
-                P[y * 8 + x] = ((7 - x) * L.leftN[y] + (x + 1) * tr + (7 - y) * L.topN[x] + (y + 1) * bl + 8) >> 4;
-    } else if (mode == 1) {     // DC, intra.py:46-62
-        int32_t s = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += L.topN[k] + L.leftN[k];
-        const int32_t dc = (s + 8) >> 4;   // floor division by 16
-#pragma unroll
-        for (int k = 0; k < 64; ++k) P[k] = dc;
-    } else {                    // angular, intra.py:116-207
-        const int angle = intra_angle(mode - 2);
-        const bool vert = mode >= 18;
+// Returns the SSE; Rpk receives the clipped recon, Lpk the levels (int16 pairs,
+// row-major; |level| <= 26214).  refp: this lane's angular pair scratch (LDS).
+//
+// Prediction is one code path for all 35 modes: Q[s][b] (scan s, base b) =
+// ((32-f_s) * r[i] + f_s * r[i+1] + 16) >> 5 in int16 arithmetic (D8), i =
+// 9 + b + (proj_s >> 5), read as one (r[i], r[i+1]) pair and one v_dot2; for
+// f_s == 0 the same dot with weights (32, 0) and a 27-bit extract gives r[i]
+// unwrapped (intra.py:204-206).  Planar and DC lanes read their block's
+// precomputed prediction through the same path (f = 0).  P = Q for vertical
+// modes and planar/DC, P = Q^T for horizontal modes (intra.py:153-156).
+__device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, uint32_t* refp,
+                                                         const RdoQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
+    const uint32_t* rowp[8];
+    uint32_t wf[8], wd[8];
+    bool vert = true;
+    if (mode >= 2) {            // _build_ref_array (intra.py:159-188) as pairs
+        const int angle = intra_angle_alu(mode);
+        vert = mode >= 18;
         const int16_t* pri = vert ? L.topA : L.leftA;
         const int16_t* sec = vert ? L.leftA : L.topA;
         const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
-        // _build_ref_array (intra.py:159-188): ref[8+i], i in [-8, 16]
-        for (int i = 0; i < 26; ++i) ref[i] = 0;
-        ref[8] = pri[0];
-        for (int i = 1; i <= 16; ++i) ref[8 + i] = pri[i < np ? i : np - 1];
+        int32_t r[25];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = 0;
+        r[8] = pri[0];
+#pragma unroll
+        for (int i = 1; i <= 16; ++i) r[8 + i] = pri[i < np ? i : np - 1];
         if (angle < 0) {
-            const int inv = inv_angle(angle), next = (8 * angle) >> 5;
-            for (int i = -1; i > next - 1; --i) {
-                int proj = ((i + 1) * inv + 128) >> 8;
-                if (proj < ns) ref[8 + i] = sec[proj];
+            const int inv = inv_angle_alu(angle), next = (8 * angle) >> 5;
+#pragma unroll
+            for (int i = -1; i >= -8; --i) {
+                const int proj = ((i + 1) * inv + 128) >> 8;
+                if (i >= next && proj < ns) r[8 + i] = sec[proj];
             }
         }
 #pragma unroll
-        for (int y = 0; y < 8; ++y)
+        for (int i = 0; i < 24; ++i) refp[i] = pack16(r[i], r[i + 1]);
+        refp[24] = (uint32_t)r[24] & 0xffffu;
 #pragma unroll
-            for (int x = 0; x < 8; ++x) {
-                const int base = vert ? x : y, scan = vert ? y : x;
-                const int proj = (scan + 1) * angle;
-                const int idx = 8 + base + 1 + (proj >> 5);
-                const int f = proj & 31;
-                const int32_t a = ref[idx];
-                int32_t v;
-                if (f == 0) v = a;
-                else {
-                    const int32_t b = ref[idx + 1];
-                    v = wrap16((32 - f) * a + f * b + 16) >> 5;   // int16 arithmetic (D8)
-                }
-                P[y * 8 + x] = v;
-            }
+        for (int s = 0; s < 8; ++s) {
+            const int proj = (s + 1) * angle, f = proj & 31;
+            rowp[s] = refp + 9 + (proj >> 5);
+            wf[s] = (uint32_t)(32 - f) | ((uint32_t)f << 16);
+            wd[s] = f ? 11u : 27u;
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            rowp[s] = mode == 0 ? L.planar + 8 * s : L.dcv;
+            wf[s] = 32u;
+            wd[s] = 27u;
+        }
     }
-    uint32_t X[8][8];
+    int32_t Q[8][8];
 #pragma unroll
-    for (int k = 0; k < 64; ++k) X[k / 8][k % 8] = (uint32_t)(int32_t)wrap16((int32_t)L.orig[k] - P[k]);
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const int t = dot2_16(rowp[s][b], wf[s]);
+            Q[s][b] = __builtin_amdgcn_sbfe(t, 5u, wd[s]);
+        }
+    uint32_t X[8][8];
+    const uint32_t* opk = (const uint32_t*)L.orig;
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t pv = pack16(Q[y][2 * m], Q[y][2 * m + 1]);
+            const uint32_t ph = pack16(Q[2 * m][y], Q[2 * m + 1][y]);
+            const uint32_t pp = vert ? pv : ph;
+            Rpk[y * 4 + m] = pp;                                   // prediction, until the recon replaces it
+            const uint32_t d = as_u32(as_v2s(opk[y * 4 + m]) - as_v2s(pp));   // residual_block: int16 wrap
+            X[y][2 * m] = (uint32_t)(int32_t)(int16_t)(d & 0xffffu);
+            X[y][2 * m + 1] = (uint32_t)((int32_t)d >> 16);
+        }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {           // pass 1: columns
         uint32_t x[8], y[8];
@@ -111,13 +250,14 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
     for (int i = 0; i < 8; ++i) {           // pass 2: rows, then quant / dequant
         uint32_t y[8];
         fwd_dct<8, Mul24>(X[i], y, 128u);
+        int32_t l[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int32_t c = (int32_t)y[j] >> 8;
-            const int32_t l = quant_i32(c, qp);
-            Lv[i * 8 + j] = l;
-            X[i][j] = (uint32_t)dequant_i32(l, dq_scale, dq_per);
+            l[j] = quant_s((int32_t)y[j] >> 8, q.qs, q.h_v, q.hneg_v);
+            X[i][j] = (uint32_t)dequant_s(l[j], q);
         }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) Lpk[i * 4 + m] = pack16(l[2 * m], l[2 * m + 1]);
     }
     // inverse pass 1: columns (transform.py:221-227)
 #pragma unroll
@@ -129,29 +269,16 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
 #pragma unroll
         for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)x[i] >> 8);
     }
-    unsigned long long sse = 0;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {           // inverse pass 2: rows, recon, SSE
-        uint32_t x[8];
-        inv_dct<8, Mul24>(X[i], x, 128u);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int32_t rr = wrap16((int32_t)x[j] >> 8);               // rres.astype(int16)
-            int32_t rc = wrap16(P[i * 8 + j] + rr);                       // reconstruct_block (int16 wrap)
-            rc = rc < 0 ? 0 : (rc > 255 ? 255 : rc);                      // clip_to_pixel_range(., 8)
-            P[i * 8 + j] = rc;
-            const int32_t d = wrap16((int32_t)L.orig[i * 8 + j] - rc);   // residual_block(orig, recon)
-            sse += (unsigned long long)(d * d);
-        }
-    }
-    return sse;
+    // inverse pass 2: rows, recon, SSE (two copies: 8-bit blocks sum d^2 in 32 bits)
+    return L.wide ? rdo8_recon_sse<true>(X, opk, Rpk) : rdo8_recon_sse<false>(X, opk, Rpk);
 }
 
-__global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
+template <int WAVES>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
                                                     int32_t* lvl, int16_t* recon, unsigned long long* sse_out) {
     __shared__ RdoSlotLds S[kRdoSlots];
-    __shared__ int16_t refs[kRdoSlots * kModes][26];
+    __shared__ uint32_t refs[kRdoSlots * kModes][kRefStride];
     const int bw = w / 8, bh = h / 8;
     const int nblk = bw * bh;
     const int t = threadIdx.x;
@@ -159,55 +286,77 @@ __global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ 
     const bool lane_on = slot < kRdoSlots;
 
     // ---- cooperative load of the 7 blocks' samples and neighbours ----
-    for (int e = t; e < kRdoSlots * 64; e += 256) {
-        int sl = e / 64, k = e % 64;
-        int b = blockIdx.x * kRdoSlots + sl;
-        if (b < nblk) {
-            int by = b / bw, bx = b - by * bw;
-            S[sl].orig[k] = src[(int64_t)(by * 8 + k / 8) * pitch + bx * 8 + (k % 8)];
-        }
+    // Every global load is issued before the first LDS write, so the workgroup
+    // waits for one memory latency, not one per loop trip.
+    const int b0 = blockIdx.x * kRdoSlots;
+    int16_t vo0 = 0, vo1 = 0, vn = 128, vtl = 128;
+    auto orig_at = [&](int e) -> const int16_t* {
+        const int b = b0 + e / 64, k = e % 64;
+        const int by = b / bw, bx = b - by * bw;
+        return src + (int64_t)(by * 8 + k / 8) * pitch + bx * 8 + (k % 8);
+    };
+    const bool o0 = b0 + t / 64 < nblk;                          // e = t (t < 256 <= 448)
+    const bool o1 = t + 256 < kRdoSlots * 64 && b0 + (t + 256) / 64 < nblk;
+    if (o0) vo0 = *orig_at(t);
+    if (o1) vo1 = *orig_at(t + 256);
+    const int nsl = t / 32, nk = t % 32;                         // neighbour sample (t < 224)
+    const bool nv = t < kRdoSlots * 32 && b0 + nsl < nblk;
+    int nby = 0, nbx = 0;
+    if (nv) {
+        const int b = b0 + nsl;
+        nby = b / bw;
+        nbx = b - nby * bw;
+        const int x = nbx * 8, y = nby * 8;
+        // top row samples x..x+15 (block.py:38-43) / left column y..y+15 (block.py:45-50)
+        const bool top = nk < 16;
+        const int kk = nk - 16;
+        const bool in = top ? (y > 0 && x + nk < w) : (x > 0 && y + kk < h);
+        const int ry = top ? y - 1 : y + kk, rx = top ? x + nk : x - 1;
+        if (in) vn = src[(int64_t)ry * pitch + rx];
     }
-    for (int e = t; e < kRdoSlots * 32; e += 256) {
-        int sl = e / 32, k = e % 32;
-        int b = blockIdx.x * kRdoSlots + sl;
-        if (b >= nblk) continue;
-        int by = b / bw, bx = b - by * bw, x = bx * 8, y = by * 8;
-        if (k < 16) {   // top row samples x..x+15 (block.py:38-43)
-            int16_t v = 128;
-            if (y > 0 && x + k < w) v = src[(int64_t)(y - 1) * pitch + x + k];
-            S[sl].topA[1 + k] = v;
-            if (k < 8) S[sl].topN[k] = v;
-        } else {        // left column samples y..y+15 (block.py:45-50)
-            int kk = k - 16;
-            int16_t v = 128;
-            if (x > 0 && y + kk < h) v = src[(int64_t)(y + kk) * pitch + x - 1];
-            S[sl].leftA[1 + kk] = v;
-            if (kk < 8) S[sl].leftN[kk] = v;
+    const bool tv = t < kRdoSlots && b0 + t < nblk;
+    int tby = 0, tbx = 0;
+    if (tv) {
+        tby = (b0 + t) / bw;
+        tbx = b0 + t - tby * bw;
+        if (tby > 0 && tbx > 0) vtl = src[(int64_t)(tby * 8 - 1) * pitch + tbx * 8 - 1];
+    }
+    if (o0) S[t / 64].orig[t % 64] = vo0;
+    if (o1) S[(t + 256) / 64].orig[(t + 256) % 64] = vo1;
+    if (nv) {
+        if (nk < 16) {
+            S[nsl].topA[1 + nk] = vn;
+            if (nk < 8) S[nsl].topN[nk] = vn;
+        } else {
+            S[nsl].leftA[1 + nk - 16] = vn;
+            if (nk < 24) S[nsl].leftN[nk - 16] = vn;
         }
     }
     if (t < kRdoSlots) {
-        int b = blockIdx.x * kRdoSlots + t;
-        S[t].valid = b < nblk;
-        if (b < nblk) {
-            int by = b / bw, bx = b - by * bw, x = bx * 8, y = by * 8;
-            int16_t tl = (y == 0 || x == 0) ? (int16_t)128 : src[(int64_t)(y - 1) * pitch + x - 1];
-            S[t].topA[0] = tl;
-            S[t].leftA[0] = tl;
+        S[t].valid = tv;
+        if (tv) {
+            const int x = tbx * 8, y = tby * 8;
+            S[t].topA[0] = vtl;
+            S[t].leftA[0] = vtl;
             S[t].ntA = 1 + (y == 0 ? 16 : min(16, w - x));
             S[t].nlA = 1 + (x == 0 ? 16 : min(16, h - y));
         }
         S[t].best = ULLONG_MAX;
+        S[t].wide = 0;
     }
+    __syncthreads();
+    for (int e = t; e < kRdoSlots * 64; e += 256)
+        if (S[e / 64].valid) rdo8_block_prep(S[e / 64], e % 64);
     __syncthreads();
     const bool active = lane_on && S[lane_on ? slot : 0].valid;
     RdoSlotLds& L = S[lane_on ? slot : 0];
+    const RdoQ rq = make_rdoq(qp, dq_scale, dq_per);
 
     // ---- the mode's chain ----
-    int32_t P[64];
+    uint32_t P[32], Lv[32];
     unsigned long long key = ULLONG_MAX;
-    int32_t Lv[64];
     if (active) {
-        const unsigned long long sse = rdo8_chain(L, mode, refs[t], qp, dq_scale, dq_per, P, Lv);
+        const unsigned long long sse = rdo8_chain(L, mode, refs[t], rq, P, Lv);
         key = (sse << 6) | (unsigned long long)mode;
         atomicMin(&L.best, key);
     }
@@ -222,7 +371,10 @@ __global__ void __launch_bounds__(256) k_intra_rdo8(const int16_t* __restrict__ 
             int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
             int16_t* rrow = recon + (int64_t)(by * 8 + i) * pitch + bx * 8;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { lrow[j] = Lv[i * 8 + j]; rrow[j] = (int16_t)P[i * 8 + j]; }
+            for (int j = 0; j < 8; ++j) {
+                lrow[j] = (int32_t)(int16_t)(Lv[i * 4 + j / 2] >> (16 * (j & 1)));
+                rrow[j] = (int16_t)(P[i * 4 + j / 2] >> (16 * (j & 1)));
+            }
         }
     }
 }
@@ -280,11 +432,12 @@ __device__ __forceinline__ void st_sys(int32_t* p, int v) {
 
 __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
     __shared__ RdoSlotLds L;
-    __shared__ int16_t refs[64][26];
+    __shared__ uint32_t refs[64][kRefStride];
     __shared__ int16_t leftcol[8];
     __shared__ int32_t topw[9];
     __shared__ int row_s, stall_s;
     const int lane = threadIdx.x;
+    const RdoQ rq = make_rdoq(a.qp, a.dq_scale, a.dq_per);
     for (;;) {
         if (lane == 0) {
             row_s = atomicAdd(&a.work[0], 1);
@@ -350,13 +503,16 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
                     L.leftA[0] = tl;
                     L.ntA = 1 + (y0 == 0 ? 16 : min(16, S.w - x0));
                     L.nlA = 1 + 8;   // get_left_neighbors(N): the reconstructed samples only
+                    L.wide = 0;
                 }
             }
             __syncthreads();
+            rdo8_block_prep(L, lane);
+            __syncthreads();
             tl_next = L.topA[8];   // recon(y0-1, x0+7): the next block's top-left
-            int32_t P[64], Lv[64];
+            uint32_t P[32], Lv[32];
             unsigned long long key = ULLONG_MAX;
-            if (lane < kModes) key = (rdo8_chain(L, lane, refs[lane], a.qp, a.dq_scale, a.dq_per, P, Lv) << 6) | lane;
+            if (lane < kModes) key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
             unsigned long long best = key;
             for (int m = 32; m > 0; m >>= 1) {
                 const unsigned long long o = __shfl_xor(best, m, 64);
@@ -369,15 +525,14 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
                 for (int i = 0; i < 8; ++i) {
 #pragma unroll
                     for (int j = 0; j < 8; ++j) {
-                        lvl[(int64_t)(y0 + i) * S.pitch + x0 + j] = Lv[i * 8 + j];
-                        rec[(int64_t)(y0 + i) * S.pitch + x0 + j] = (int16_t)P[i * 8 + j];
+                        lvl[(int64_t)(y0 + i) * S.pitch + x0 + j] = (int32_t)(int16_t)(Lv[i * 4 + j / 2] >> (16 * (j & 1)));
+                        rec[(int64_t)(y0 + i) * S.pitch + x0 + j] = (int16_t)(P[i * 4 + j / 2] >> (16 * (j & 1)));
                     }
-                    leftcol[i] = (int16_t)P[i * 8 + 7];
+                    leftcol[i] = (int16_t)(P[i * 4 + 3] >> 16);
                 }
 #pragma unroll
                 for (int q = 0; q < 4; ++q)   // this block's bottom row -> line (coherent stores)
-                    st_sys(line + x0 / 2 + q, (int)(((uint32_t)(uint16_t)P[56 + 2 * q + 1] << 16) |
-                                                    (uint32_t)(uint16_t)P[56 + 2 * q]));
+                    st_sys(line + x0 / 2 + q, (int)P[28 + q]);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line stores retired
                 st_sys(&a.work[2 + row], bx + 1);
             }
@@ -633,7 +788,13 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
     int per, rem;
     qp_split(qp, &per, &rem);
     const unsigned grid = (unsigned)((nblk + kRdoSlots - 1) / kRdoSlots);
-    k_intra_rdo8<<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
+    // NH_RDO_WAVES=3: register allocation for 3 waves/SIMD (spills) -- A/B knob
+    static const int waves = [] { const char* e = getenv("NH_RDO_WAVES"); return e ? atoi(e) : 0; }();
+    if (waves == 3)
+        k_intra_rdo8<3><<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
+                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse);
+    else
+        k_intra_rdo8<1><<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
                                                       d_modes, d_lvl, d_recon, (unsigned long long*)d_sse);
     NH_HIP(hipGetLastError());
     return NH_OK;
