@@ -131,13 +131,13 @@ __device__ __forceinline__ int select_set(const Fused8Args& a, SetDev& S) {
 
 // One thread = one block.  POLICY: cache policy (ld16/st16); WAVES: minimum
 // waves per SIMD requested from the register allocator (1 = compiler choice).
-template <int POLICY, int WAVES>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant(Fused8Args a) {
+template <int POLICY, int WAVES, int TPB = 256>
+__global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant(Fused8Args a) {
     SetDev S;
     select_set(a, S);
     uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
     asm volatile("" : "+v"(h_v), "+v"(hneg_v));  // pin the two offsets in VGPRs
-    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    const uint32_t b = (blockIdx.x - S.wg_start) * (uint32_t)TPB + threadIdx.x;
     if (b >= S.nblocks) return;
     const int64_t off = block_offset(S, b);
     v4i raw[8], outv[8];
@@ -672,7 +672,7 @@ __global__ void __launch_bounds__(512) k_probe_rowwave_lds(Fused8Args a) {
 // pairs: 1 = one thread per vertical block pair (rows 2r, 2r+1 of the set's
 // linear block-row numbering): per set ceil(rows/2) * blocks_per_row threads.
 static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
-                      int is_intra, Fused8Args& a, uint32_t& total_wg, int pairs = 0) {
+                      int is_intra, Fused8Args& a, uint32_t& total_wg, int pairs = 0, int tpb = 256) {
     if (!d_res || !d_lvl || !sets || nsets < 1 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
     if (((uintptr_t)d_res & 15) || ((uintptr_t)d_lvl & 15)) {
         set_error("fwd8x8: buffers must be 16-byte aligned");
@@ -715,7 +715,7 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
         d.blk0 = (uint32_t)blk;
         blk += nb;
         const uint64_t nthr = pairs ? (rows * planes + 1) / 2 * bpr : nb;
-        wg += (nthr + 255) / 256;
+        wg += (nthr + tpb - 1) / tpb;
     }
     for (int k = nsets; k < NH_MAX_PLANE_SETS; ++k) a.set[k].wg_start = 0xffffffffu;
     if (wg >= (1ull << 31) || blk >= (1ull << 32)) return NH_EARG;
@@ -863,8 +863,27 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           + 8 * persistent software-pipelined form (grid = min(tiles, 256 CUs x 8))
     //           + 16 * vertical block pair per thread (with occ: >= 4 waves/SIMD)
     //           + 32 * stripe form (linear HBM walk through LDS; +64: register staging instead of LDS-DMA)
-    const int policy = variant & 3, occ = (variant >> 2) & 1, pipe = (variant >> 3) & 1, pair = (variant >> 4) & 1;
     //           + 128 * persistent double-buffered stripe form (LDS-DMA of the next tile under this one)
+    //           + 256 * k: the plain form with 512 (k=1), 1024 (k=2) or 128 (k=3) threads per workgroup
+    if (variant >= 256) {
+        const int k = variant >> 8, pol = variant & 3, oc = (variant >> 2) & 1;
+        if (k > 3 || (variant & 248)) return NH_EARG;
+        const int tpb = k == 1 ? 512 : k == 2 ? 1024 : 128;
+        Fused8Args a;
+        uint32_t wg = 0;
+        int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg, 0, tpb);
+        if (rc) return rc;
+        if (!wg) return NH_OK;
+        hipStream_t s = as_stream(stream);
+#define NH_T(P, T) do { if (oc) k_fwd8x8_quant<P, 5, T><<<wg, T, 0, s>>>(a); else k_fwd8x8_quant<P, 1, T><<<wg, T, 0, s>>>(a); } while (0)
+#define NH_TT(P) do { if (tpb == 512) NH_T(P, 512); else if (tpb == 1024) NH_T(P, 1024); else NH_T(P, 128); } while (0)
+        if (pol == 1) NH_TT(1); else NH_TT(0);
+#undef NH_TT
+#undef NH_T
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
+    const int policy = variant & 3, occ = (variant >> 2) & 1, pipe = (variant >> 3) & 1, pair = (variant >> 4) & 1;
     if (variant >= 128 && variant < 132)
         return run_stripe_pipe(d_res, d_lvl, sets, nsets, qp, is_intra, policy, as_stream(stream));
     if (variant >= 32 && variant < 128 && !(variant & 28))
