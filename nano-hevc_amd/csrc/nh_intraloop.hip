@@ -276,19 +276,26 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
 template <int WAVES>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
-                                                    int32_t* lvl, int16_t* recon, unsigned long long* sse_out) {
+                                                    int32_t* lvl, int16_t* recon, unsigned long long* sse_out,
+                                                    uint32_t ngroups) {
     __shared__ RdoSlotLds S[kRdoSlots];
     __shared__ uint32_t refs[kRdoSlots * kModes][kRefStride];
+    __shared__ unsigned long long sse_part[4];
     const int bw = w / 8, bh = h / 8;
     const int nblk = bw * bh;
     const int t = threadIdx.x;
     const int slot = t / kModes, mode = t - slot * kModes;
     const bool lane_on = slot < kRdoSlots;
+    // Persistent: a workgroup walks groups of 7 blocks with stride gridDim.x and
+    // adds its SSE to *sse_out ONCE (one 64-bit word takes ~90 atomic adds/us:
+    // an atomic per block serialised the whole launch).
+    unsigned long long my_sse = 0;
+    for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
 
     // ---- cooperative load of the 7 blocks' samples and neighbours ----
     // Every global load is issued before the first LDS write, so the workgroup
     // waits for one memory latency, not one per loop trip.
-    const int b0 = blockIdx.x * kRdoSlots;
+    const int b0 = (int)grp * kRdoSlots;
     int16_t vo0 = 0, vo1 = 0, vn = 128, vtl = 128;
     auto orig_at = [&](int e) -> const int16_t* {
         const int b = b0 + e / 64, k = e % 64;
@@ -362,10 +369,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     }
     __syncthreads();
     if (active && key == L.best) {
-        const int b = blockIdx.x * kRdoSlots + slot;
+        const int b = b0 + slot;
         const int by = b / bw, bx = b - by * bw;
         modes[b] = (uint8_t)mode;
-        if (sse_out) atomicAdd(sse_out, key >> 6);
+        my_sse += key >> 6;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
@@ -376,6 +383,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
                 rrow[j] = (int16_t)(P[i * 4 + j / 2] >> (16 * (j & 1)));
             }
         }
+    }
+    __syncthreads();   // S / refs are refilled by the next group
+    }
+    if (sse_out) {
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) my_sse += __shfl_xor(my_sse, m, 64);
+        if ((t & 63) == 0) sse_part[t >> 6] = my_sse;
+        __syncthreads();
+        if (t == 0) atomicAdd(sse_out, sse_part[0] + sse_part[1] + sse_part[2] + sse_part[3]);
     }
 }
 
@@ -459,6 +475,7 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
         int32_t* line = a.work + a.lines0 + S.line0 + (int64_t)pl * S.lw;   // int16 pairs
         const int y0 = by * 8;
         int16_t tl_next = 128;   // recon(y0-1, x0-1) for the next block
+        unsigned long long row_sse = 0;   // added to the plane's word once per row, not per block
         for (int bx = 0; bx < S.bw; ++bx) {
             const int x0 = bx * 8;
             if (by > 0 && lane == 0) {   // wait for the top / top-right references
@@ -520,7 +537,7 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
             }
             if (key == best) {   // the winning mode (lowest SSE, lowest mode on ties)
                 a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)lane;
-                atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], best >> 6);
+                row_sse += best >> 6;
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -538,6 +555,9 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
             }
             __syncthreads();
         }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) row_sse += __shfl_xor(row_sse, m, 64);
+        if (lane == 0 && row_sse) atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], row_sse);
         __syncthreads();
         if (stall_s) break;   // the whole launch is failing: leave (status word set)
     }
@@ -787,15 +807,24 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
     if (!nblk) return NH_OK;
     int per, rem;
     qp_split(qp, &per, &rem);
-    const unsigned grid = (unsigned)((nblk + kRdoSlots - 1) / kRdoSlots);
-    // NH_RDO_WAVES=3: register allocation for 3 waves/SIMD (spills) -- A/B knob
+    const uint32_t ngroups = (uint32_t)((nblk + kRdoSlots - 1) / kRdoSlots);
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 256;
+        return n;
+    }();
+    // as many workgroups as fit (2 per CU at 2 waves/SIMD, 3 at 3), every workgroup the same number of groups +-1
     static const int waves = [] { const char* e = getenv("NH_RDO_WAVES"); return e ? atoi(e) : 0; }();
+    const uint32_t cap = (uint32_t)cus * (waves == 3 ? 3 : 2), iters = (ngroups + cap - 1) / cap;
+    const unsigned grid = (ngroups + iters - 1) / iters;
+    // NH_RDO_WAVES=3: register allocation for 3 waves/SIMD (spills) -- A/B knob
     if (waves == 3)
         k_intra_rdo8<3><<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
-                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse);
+                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse, ngroups);
     else
         k_intra_rdo8<1><<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
-                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse);
+                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse, ngroups);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
