@@ -262,4 +262,34 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
     return (t + n) >> f.l;
 }
 
+// Quantizer / dequantizer of the intra chains (configs 3-5) with uniform
+// parameters, in 32 bits.  Exact whenever the residual is int16: the
+// coefficients of every transform (DST4, DCT4..32) are then |c| <= 2^17
+// (quant_s's range), |level| <= 52428 (N = 4, QP 0) fits the 24-bit multiply,
+// and dequant = (l * dqs + dqr) >> dqsh with dqs = scale << max(0, per-4) is
+// quant.py:112-123 without its int64: |l * dqs| < 2^22 at every QP and size.
+struct ChainQ {
+    QuantS qs;
+    uint32_t h_v, hneg_v, dqr_v;   // VGPR operands
+    int32_t dqs, dqsh;
+};
+__device__ __forceinline__ ChainQ make_chainq(const QuantParams& qp, int dq_scale, int dq_per) {
+    ChainQ r;
+    r.qs = make_quants(qp);
+    r.h_v = r.qs.h;
+    r.hneg_v = r.qs.hneg;
+    r.dqs = dq_per < 4 ? dq_scale : dq_scale << (dq_per - 4);
+    r.dqr_v = dq_per < 4 ? 1u << (3 - dq_per) : 0u;
+    r.dqsh = dq_per < 4 ? 4 - dq_per : 0;
+    asm volatile("" : "+v"(r.h_v), "+v"(r.hneg_v), "+v"(r.dqr_v));
+    return r;
+}
+__device__ __forceinline__ int32_t dequant_s(int32_t l, const ChainQ& q) {
+    int32_t r;
+    asm("v_mad_i32_i24 %0, %1, %2, %3\n\t"
+        "v_ashrrev_i32_e32 %0, %4, %0"
+        : "=&v"(r) : "v"(l), "s"(q.dqs), "v"(q.dqr_v), "s"(q.dqsh));
+    return r;
+}
+
 }  // namespace nh

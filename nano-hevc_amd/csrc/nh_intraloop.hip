@@ -59,34 +59,6 @@ __device__ __forceinline__ void rdo8_block_prep(RdoSlotLds& B, int k) {
     }
 }
 
-// Quantizer / dequantizer of the chain with uniform parameters.  Exact for any
-// int16 plane: the residual is int16, so |coeff| <= 2^17 (quant_s's range) and
-// |level| <= 26214; dequant = (l * dqs + dqr) >> dqsh with dqs = scale << max(0,
-// per-4) <= 1152, i.e. quant.py:112-123 without its int64 (|l * dqs| < 2^25).
-struct RdoQ {
-    QuantS qs;
-    uint32_t h_v, hneg_v, dqr_v;   // VGPR operands
-    int32_t dqs, dqsh;
-};
-__device__ __forceinline__ RdoQ make_rdoq(const QuantParams& qp, int dq_scale, int dq_per) {
-    RdoQ r;
-    r.qs = make_quants(qp);
-    r.h_v = r.qs.h;
-    r.hneg_v = r.qs.hneg;
-    r.dqs = dq_per < 4 ? dq_scale : dq_scale << (dq_per - 4);
-    r.dqr_v = dq_per < 4 ? 1u << (3 - dq_per) : 0u;
-    r.dqsh = dq_per < 4 ? 4 - dq_per : 0;
-    asm volatile("" : "+v"(r.h_v), "+v"(r.hneg_v), "+v"(r.dqr_v));
-    return r;
-}
-__device__ __forceinline__ int32_t dequant_s(int32_t l, const RdoQ& q) {
-    int32_t r;
-    asm("v_mad_i32_i24 %0, %1, %2, %3\n\t"
-        "v_ashrrev_i32_e32 %0, %4, %0"
-        : "=&v"(r) : "v"(l), "s"(q.dqs), "v"(q.dqr_v), "s"(q.dqsh));
-    return r;
-}
-
 typedef short v2s __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2s as_v2s(uint32_t u) { return __builtin_bit_cast(v2s, u); }
 __device__ __forceinline__ uint32_t as_u32(v2s v) { return __builtin_bit_cast(uint32_t, v); }
@@ -173,7 +145,7 @@ __device__ __forceinline__ unsigned long long rdo8_recon_sse(uint32_t (&X)[8][8]
 // precomputed prediction through the same path (f = 0).  P = Q for vertical
 // modes and planar/DC, P = Q^T for horizontal modes (intra.py:153-156).
 __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, uint32_t* refp,
-                                                         const RdoQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
+                                                         const ChainQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
     const uint32_t* rowp[8];
     uint32_t wf[8], wd[8];
     bool vert = true;
@@ -273,24 +245,25 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
     return L.wide ? rdo8_recon_sse<true>(X, opk, Rpk) : rdo8_recon_sse<false>(X, opk, Rpk);
 }
 
-template <int WAVES>
+template <int WAVES, bool ONESHOT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
                                                     int32_t* lvl, int16_t* recon, unsigned long long* sse_out,
                                                     uint32_t ngroups) {
     __shared__ RdoSlotLds S[kRdoSlots];
     __shared__ uint32_t refs[kRdoSlots * kModes][kRefStride];
-    __shared__ unsigned long long sse_part[4];
+    __shared__ unsigned long long wg_sse;
     const int bw = w / 8, bh = h / 8;
     const int nblk = bw * bh;
     const int t = threadIdx.x;
     const int slot = t / kModes, mode = t - slot * kModes;
     const bool lane_on = slot < kRdoSlots;
-    // Persistent: a workgroup walks groups of 7 blocks with stride gridDim.x and
-    // adds its SSE to *sse_out ONCE (one 64-bit word takes ~90 atomic adds/us:
-    // an atomic per block serialised the whole launch).
-    unsigned long long my_sse = 0;
-    for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    // A workgroup adds its SSE to *sse_out ONCE (one 64-bit word takes ~90
+    // atomic adds/us: an atomic per block serialised the whole launch).
+    // ONESHOT: one group of 7 blocks per workgroup; else persistent, groups
+    // walked with stride gridDim.x.
+    if (t == 0) wg_sse = 0;   // (first read after the barriers below)
+    auto body = [&](const uint32_t grp) __attribute__((always_inline)) {
 
     // ---- cooperative load of the 7 blocks' samples and neighbours ----
     // Every global load is issued before the first LDS write, so the workgroup
@@ -357,7 +330,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     __syncthreads();
     const bool active = lane_on && S[lane_on ? slot : 0].valid;
     RdoSlotLds& L = S[lane_on ? slot : 0];
-    const RdoQ rq = make_rdoq(qp, dq_scale, dq_per);
+    const ChainQ rq = make_chainq(qp, dq_scale, dq_per);
 
     // ---- the mode's chain ----
     uint32_t P[32], Lv[32];
@@ -372,7 +345,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         const int b = b0 + slot;
         const int by = b / bw, bx = b - by * bw;
         modes[b] = (uint8_t)mode;
-        my_sse += key >> 6;
+        atomicAdd(&wg_sse, key >> 6);   // LDS: no register lives across the loop
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
@@ -385,14 +358,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         }
     }
     __syncthreads();   // S / refs are refilled by the next group
+    };
+    if constexpr (ONESHOT) {
+        body(blockIdx.x);
+    } else {
+        for (uint32_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) body(grp);
     }
-    if (sse_out) {
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) my_sse += __shfl_xor(my_sse, m, 64);
-        if ((t & 63) == 0) sse_part[t >> 6] = my_sse;
-        __syncthreads();
-        if (t == 0) atomicAdd(sse_out, sse_part[0] + sse_part[1] + sse_part[2] + sse_part[3]);
-    }
+    if (sse_out && t == 0) atomicAdd(sse_out, wg_sse);   // after the last barrier
 }
 
 // ===========================================================================
@@ -453,7 +425,7 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
     __shared__ int32_t topw[9];
     __shared__ int row_s, stall_s;
     const int lane = threadIdx.x;
-    const RdoQ rq = make_rdoq(a.qp, a.dq_scale, a.dq_per);
+    const ChainQ rq = make_chainq(a.qp, a.dq_scale, a.dq_per);
     for (;;) {
         if (lane == 0) {
             row_s = atomicAdd(&a.work[0], 1);
@@ -629,6 +601,7 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     __shared__ uint32_t list[MODE == kTree ? K : 1];
     __shared__ int wave_cnt[4], list_n;
     const int g = threadIdx.x / N, t = threadIdx.x % N;
+    const ChainQ cq = make_chainq(qp, dq_scale, dq_per);
     int ntu;
     if constexpr (MODE == kTree) {
         // phase 1: which candidate positions are TUs of size N (tu_leaf), compacted
@@ -723,9 +696,9 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
         int32_t* lrow = lvl + (int64_t)(y0 + t) * pitch + x0;
 #pragma unroll
         for (int j = 0; j < N; ++j) {
-            const int32_t l = quant_i32(rshift_round<S>(r[j]), qp);
+            const int32_t l = quant_s(rshift_round<S>(r[j]), cq.qs, cq.h_v, cq.hneg_v);
             lrow[j] = l;
-            v[j] = (uint32_t)dequant_i32(l, dq_scale, dq_per);
+            v[j] = (uint32_t)dequant_s(l, cq);
         }
     }
     __syncthreads();
@@ -814,17 +787,27 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
             n = 256;
         return n;
     }();
-    // as many workgroups as fit (2 per CU at 2 waves/SIMD, 3 at 3), every workgroup the same number of groups +-1
-    static const int waves = [] { const char* e = getenv("NH_RDO_WAVES"); return e ? atoi(e) : 0; }();
-    const uint32_t cap = (uint32_t)cus * (waves == 3 ? 3 : 2), iters = (ngroups + cap - 1) / cap;
-    const unsigned grid = (ngroups + iters - 1) / iters;
-    // NH_RDO_WAVES=3: register allocation for 3 waves/SIMD (spills) -- A/B knob
-    if (waves == 3)
-        k_intra_rdo8<3><<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
-                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse, ngroups);
-    else
-        k_intra_rdo8<1><<<grid, 256, 0, as_stream(stream)>>>(d_src, w, h, pitch, qparams(qp, 3, true), dequant_scale(rem), per,
-                                                      d_modes, d_lvl, d_recon, (unsigned long long*)d_sse, ngroups);
+    // Launch form (A/B knob NH_RDO_FORM, read once): 0 = one group per
+    // workgroup (default), 1 = persistent at the compiler's register
+    // allocation, 2 = persistent forced to 2 waves/SIMD.
+    static const int form = [] { const char* e = getenv("NH_RDO_FORM"); return e ? atoi(e) : 0; }();
+    const hipStream_t s = as_stream(stream);
+    const QuantParams q = qparams(qp, 3, true);
+    unsigned long long* sse = (unsigned long long*)d_sse;
+    if (form == 0) {
+        k_intra_rdo8<1, true><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
+                                                     d_recon, sse, ngroups);
+    } else {
+        // as many workgroups as fit, every workgroup the same number of groups +-1
+        const uint32_t cap = (uint32_t)cus * (form == 2 ? 2 : 1), iters = (ngroups + cap - 1) / cap;
+        const unsigned grid = (ngroups + iters - 1) / iters;
+        if (form == 2)
+            k_intra_rdo8<2, false><<<grid, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
+                                                       d_recon, sse, ngroups);
+        else
+            k_intra_rdo8<1, false><<<grid, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
+                                                       d_recon, sse, ngroups);
+    }
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
     const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
     const int b = blockIdx.x * 4 + wv;
     if (b >= nblk) return;                       // whole wave exits together
+    const ChainQ cq = make_chainq(qp, dq_scale, dq_per);   // 32-bit quant/dequant (int16 residual)
     if constexpr (TREE) {   // this workgroup's plane of the batch
         const int pz = blockIdx.y, gz = pz / ta.ppg, cz = pz - gz * ta.ppg;
         const int64_t poff = (int64_t)gz * ta.group_stride + (int64_t)cz * ta.plane_stride;
@@ -220,8 +221,8 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int g = 4 * q + e;
-            L4[e] = quant_i32(rshift_round<10>((uint32_t)acc[g]), qp);
-            s_dq[wv][r][crow(g, hh)] = dequant_i32(L4[e], dq_scale, dq_per);
+            L4[e] = quant_s(rshift_round<10>((uint32_t)acc[g]), cq.qs, cq.h_v, cq.hneg_v);
+            s_dq[wv][r][crow(g, hh)] = dequant_s(L4[e], cq);
         }
         *(v4i_t*)(lrow + 8 * q + 4 * hh) = v4i_t{L4[0], L4[1], L4[2], L4[3]};
     }
