@@ -450,6 +450,8 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
         unsigned long long row_sse = 0;   // added to the plane's word once per row, not per block
         for (int bx = 0; bx < S.bw; ++bx) {
             const int x0 = bx * 8;
+            // this block's source sample: independent of the wait, issued before it
+            const int16_t ov = src[(int64_t)(y0 + lane / 8) * S.pitch + x0 + (lane % 8)];
             if (by > 0 && lane == 0) {   // wait for the top / top-right references
                 const int need = bx + 2 < S.bw ? bx + 2 : S.bw;
                 int spins = 0;
@@ -472,7 +474,7 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
             // block samples and neighbours (block.py:38-55 on the reconstruction)
             {
                 const int k = lane;
-                L.orig[k] = src[(int64_t)(y0 + k / 8) * S.pitch + x0 + (k % 8)];
+                L.orig[k] = ov;
                 if (k < 16) {
                     int16_t v = 128;
                     if (y0 > 0 && x0 + k < S.w) {
@@ -640,11 +642,18 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
         y0 = (idx / grid_bw) * N + (MODE == kTree ? ta.y_base : 0);
     }
     if (active) {
-        // neighbours (block.py:38-50): count N, 128 outside the plane (full TUs: no truncation)
-        topv[g][t] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + t];
-        leftv[g][t] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + t) * pitch + x0 - 1];
+        // neighbours (block.py:38-50): count N, 128 outside the plane (full TUs: no truncation).
+        // All N + 2 loads are issued before the first LDS write (one memory
+        // latency per round, not one per sample).
+        int16_t ov[N];
 #pragma unroll
-        for (int i = 0; i < N; ++i) orig[g][i][t] = src[(int64_t)(y0 + i) * pitch + x0 + t];
+        for (int i = 0; i < N; ++i) ov[i] = src[(int64_t)(y0 + i) * pitch + x0 + t];
+        const int16_t tv = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + t];
+        const int16_t lv = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + t) * pitch + x0 - 1];
+        topv[g][t] = tv;
+        leftv[g][t] = lv;
+#pragma unroll
+        for (int i = 0; i < N; ++i) orig[g][i][t] = ov[i];
     }
     __syncthreads();
     // DC (intra.py:46-62) and planar (intra.py:81-113) for column t
