@@ -604,6 +604,8 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
     __shared__ int wave_cnt[4], list_n;
     const int g = threadIdx.x / N, t = threadIdx.x % N;
     const ChainQ cq = make_chainq(qp, dq_scale, dq_per);
+    // recon rows as vectors when every row start is 16-B aligned (x0 is a multiple of N)
+    const bool rec_vec = ((uintptr_t)recon & 15) == 0 && (pitch & 7) == 0;
     int ntu;
     if constexpr (MODE == kTree) {
         // phase 1: which candidate positions are TUs of size N (tu_leaf), compacted
@@ -734,11 +736,24 @@ __global__ void __launch_bounds__(256) k_tu_process(const int16_t* __restrict__ 
         for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[g][t][k];
         inv1d<N, DST, Mul24>(v, r);
         int16_t* rrow = recon + (int64_t)(y0 + t) * pitch + x0;
+        uint32_t rcp[N / 2];
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const int32_t rr = wrap16(rshift_round<S>(r[j]));
-            int32_t rc = wrap16(pred_at(t, j) + rr);
-            rrow[j] = (int16_t)(rc < 0 ? 0 : (rc > 255 ? 255 : rc));
+        for (int j = 0; j < N; j += 2) {
+            int32_t rc2[2];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int32_t rr = wrap16(rshift_round<S>(r[j + q]));
+                const int32_t rc = wrap16(pred_at(t, j + q) + rr);
+                rc2[q] = rc < 0 ? 0 : (rc > 255 ? 255 : rc);
+            }
+            rcp[j / 2] = (uint32_t)rc2[0] | ((uint32_t)rc2[1] << 16);
+        }
+        if (rec_vec) {   // one row = N int16: 8..64 B vector stores
+            constexpr int A = 2 * N < 16 ? 2 * N : 16;
+            __builtin_memcpy(__builtin_assume_aligned(rrow, A), rcp, 2 * N);
+        } else {
+#pragma unroll
+            for (int j = 0; j < N; ++j) rrow[j] = (int16_t)(rcp[j / 2] >> (16 * (j & 1)));
         }
         if (MODE == kTree && t < N / 4) {
             const int w4 = w / 4;
