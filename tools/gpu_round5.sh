@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r01k}
+TAG=${TAG:-r01ae}
 echo "== smoke" && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1; rc=$?; tail -2 gpurun_out/smoke_${TAG}.log; [ $rc -eq 0 ] && \
 echo "== pytest -m gpu" && \
