@@ -418,7 +418,8 @@ __device__ __forceinline__ void st_sys(int32_t* p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
+template <int WAVES>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8_closed(ClosedArgs a) {
     __shared__ RdoSlotLds L;
     __shared__ uint32_t refs[64][kRefStride];
     __shared__ int16_t leftcol[8];
@@ -510,6 +511,14 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
                 best = o < best ? o : best;
             }
             if (key == best) {   // the winning mode (lowest SSE, lowest mode on ties)
+                // publish first (the next row waits on it): the bottom row -> line
+                // (coherent stores), retire them, then the progress counter; the
+                // block's outputs go out after, off the wavefront's critical path
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    st_sys(line + x0 / 2 + q, (int)P[28 + q]);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line stores retired
+                st_sys(&a.work[2 + row], bx + 1);
                 a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)lane;
                 row_sse += best >> 6;
 #pragma unroll
@@ -521,11 +530,6 @@ __global__ void __launch_bounds__(64) k_intra_rdo8_closed(ClosedArgs a) {
                     }
                     leftcol[i] = (int16_t)(P[i * 4 + 3] >> 16);
                 }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)   // this block's bottom row -> line (coherent stores)
-                    st_sys(line + x0 / 2 + q, (int)P[28 + q]);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line stores retired
-                st_sys(&a.work[2 + row], bx + 1);
             }
             __syncthreads();
         }
@@ -998,7 +1002,11 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
     if (a.total_rows > 0) {
         // persistent waves: enough to cover every row, capped at what can be resident (2 waves/SIMD)
         const int waves = a.total_rows < 2048 ? a.total_rows : 2048;
-        k_intra_rdo8_closed<<<waves, 64, 0, s>>>(a);
+        {   // NH_CLOSED_WAVES=2: register allocation for 2 waves/SIMD (spills) -- A/B knob
+            static const int cw = [] { const char* e = getenv("NH_CLOSED_WAVES"); return e ? atoi(e) : 1; }();
+            if (cw == 2) k_intra_rdo8_closed<2><<<waves, 64, 0, s>>>(a);
+            else k_intra_rdo8_closed<1><<<waves, 64, 0, s>>>(a);
+        }
     }
     NH_HIP(hipGetLastError());
     return NH_OK;
