@@ -210,14 +210,17 @@ def _chain(I, T, Q, orig, pred, qp, use_dst):
     return lvl, rec, sse
 
 
-def ref_plane_cfg3(I, T, Q, src, qp):
+def ref_plane_cfg3(I, T, Q, src, qp, rows=None):
+    """rows = (first, last) block rows to compute (open loop: rows are
+    independent); outside them the outputs stay 0."""
     h, w = src.shape
     n = 8
     modes = np.zeros((h // n, w // n), np.uint8)
     lvl = np.zeros(src.shape, np.int32)
     rec = np.zeros(src.shape, np.int16)
     total = 0
-    for by in range(0, h - n + 1, n):
+    r0, r1 = rows if rows else (0, h // n)
+    for by in range(r0 * n, min(h - n + 1, r1 * n), n):
         for bx in range(0, w - n + 1, n):
             orig = src[by:by + n, bx:bx + n]
             top, left, tl = _neighbors(src, bx, by, n)
@@ -258,7 +261,8 @@ def tu_split(seed, plane_id, x, y, size):
     return (k & 3) < 2
 
 
-def ref_plane_cfg4(I, T, Q, src, ctb, plane_id, seed, qp, is_luma):
+def ref_plane_cfg4(I, T, Q, src, ctb, plane_id, seed, qp, is_luma, ctu_rows=None):
+    """ctu_rows = (first, last) CTU rows to compute (open loop: independent)."""
     h, w = src.shape
     lvl = np.zeros(src.shape, np.int32)
     rec = np.zeros(src.shape, np.int16)
@@ -290,7 +294,8 @@ def ref_plane_cfg4(I, T, Q, src, ctb, plane_id, seed, qp, is_luma):
         if not over:
             one(x, y, s)
 
-    for cy in range((h + ctb - 1) // ctb):
+    c0, c1 = ctu_rows if ctu_rows else (0, (h + ctb - 1) // ctb)
+    for cy in range(c0, c1):
         for cx in range((w + ctb - 1) // ctb):
             tree(cx * ctb, cy * ctb, ctb)
     return lvl, rec, tul

@@ -1,0 +1,109 @@
+"""Reference parity at BASELINE.json's full sizes: the GPU outputs hash to the
+REFERENCE's own outputs on the same seeded frames.
+
+tests/golden/fullsize.json holds sha256 hashes of what the reference's
+functions, composed as DESIGN.md §3.3-3.5 / §3.7 define the drivers, produce
+on the frames of tests/golden/fullsize_inputs.py (generated in the build
+container by tests/golden/make_fullsize.py; the reference never travels here):
+config 3 on a 1080p YUV420 frame in open and closed loop, config 4 on a 4K
+YUV420 frame, config 5 on an 8K luma plane (int8-MFMA and butterfly kernels).
+"""
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import fullsize_inputs as FI  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+FIX = os.path.join(HERE, "golden", "fullsize.json")
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module")
+def ref():
+    with open(FIX) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "the gpu tests need an MI355X"
+    torch.cuda.set_device(0)
+    return torch
+
+
+def test_cfg3_1080p_open_loop_equals_reference(ref, torch_dev):
+    torch = torch_dev
+    from nano_hevc import gpu
+    for k, src in enumerate(FI.cfg3_frame()):
+        m, l, r, s = gpu.intra_rdo_plane(torch.from_numpy(src).cuda(), FI.CFG3_QP)
+        e = ref[f"cfg3_p{k}"]
+        assert sha(m.cpu().numpy()) == e["modes"], k
+        assert sha(l.cpu().numpy()) == e["lvl"], k
+        assert sha(r.cpu().numpy()) == e["rec"], k
+        assert int(s.item()) == e["sse"], k
+
+
+def test_cfg3_1080p_closed_loop_equals_reference(ref, torch_dev):
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = FI.cfg3_frame()
+    h, w = planes[0].shape
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    modes, lvl, rec, sse = gpu.intra_rdo_closed(torch.from_numpy(buf).cuda(), gpu.yuv420_plane_sets(1, w, h),
+                                                FI.CLOSED_QP)
+    modes, lvl, rec, sse = modes.cpu().numpy(), lvl.cpu().numpy(), rec.cpu().numpy(), sse.cpu().numpy()
+    off = moff = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        nb = (ph // 8) * (pw // 8)
+        e = ref[f"closed_p{k}"]
+        assert sha(modes[moff:moff + nb].reshape(ph // 8, pw // 8)) == e["modes"], k
+        assert sha(lvl[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], k
+        assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
+        assert int(sse[k]) == e["sse"], k
+        off += ph * pw
+        moff += nb
+
+
+def test_cfg4_4k_equals_reference(ref, torch_dev):
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = FI.cfg4_frame()
+    h, w = planes[0].shape
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(1, w, h)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy = gpu.tu_pipeline_planes(d, sy, 32, 0, FI.CFG4_SEED, FI.CFG4_QP, True, lvl=lvl, rec=rec)
+    _, _, tuc = gpu.tu_pipeline_planes(d, suv, 16, 1, FI.CFG4_SEED, FI.CFG4_QP, False, lvl=lvl, rec=rec)
+    lvl, rec, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    off = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        e = ref[f"cfg4_p{k}"]
+        assert sha(lvl[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], k
+        assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
+        assert sha(tuy[0] if k == 0 else tuc[k - 1]) == e["tu"], k
+        off += ph * pw
+
+
+@pytest.mark.parametrize("variant", [1, 0])   # int8 MFMA, butterfly
+def test_cfg5_8k_luma_equals_reference(ref, torch_dev, variant):
+    torch = torch_dev
+    from nano_hevc import gpu
+    src = FI.cfg5_plane()
+    l, r = gpu.tc32_plane(torch.from_numpy(src).cuda(), FI.CFG5_QP, variant)
+    assert sha(l.cpu().numpy()) == ref["cfg5_y"]["lvl"]
+    assert sha(r.cpu().numpy()) == ref["cfg5_y"]["rec"]

@@ -231,3 +231,28 @@ def test_oracle_encode_frame_intra_golden(golden):
         _, st = O.encode_intra_plane(g[key + "_y"], int(key.split("bs")[1]))
         assert list(st[:5]) == list(g[key])
         assert f"{10 * np.log10(255 ** 2 / (np.float64(st[5]) / g[key + '_y'].size)):.2f}" == str(g[key + "_psnr_text"])
+
+
+def test_oracle_at_full_size_equals_reference():
+    """The CPU restatement at BASELINE sizes (1080p open + closed loop, 4K mixed
+    TUs, 8K 32x32) hashes to the reference's outputs (tests/golden/fullsize.json,
+    tests/golden/make_fullsize.py).  ~25 s."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    import fullsize_inputs as FI
+
+    def sha(a):
+        return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+    with open(os.path.join(GOLDEN, "fullsize.json")) as f:
+        ref = json.load(f)
+    for k, src in enumerate(FI.cfg3_frame()):
+        m, l, r, s = O.intra_rdo_plane(src, FI.CFG3_QP)
+        assert (sha(m), sha(l), sha(r), s) == tuple(ref[f"cfg3_p{k}"][x] for x in ("modes", "lvl", "rec", "sse")), k
+        m, l, r, s = O.intra_rdo_plane(src, FI.CLOSED_QP, closed=True)
+        assert (sha(m), sha(l), sha(r), s) == tuple(ref[f"closed_p{k}"][x] for x in ("modes", "lvl", "rec", "sse")), k
+    for k, src in enumerate(FI.cfg4_frame()):
+        l, r, t = O.tu_pipeline_plane(src, 32 if k == 0 else 16, k, FI.CFG4_SEED, FI.CFG4_QP, k == 0)
+        assert (sha(l), sha(r), sha(t)) == tuple(ref[f"cfg4_p{k}"][x] for x in ("lvl", "rec", "tu")), k
+    l, r = O.tc32_plane(FI.cfg5_plane(), FI.CFG5_QP)
+    assert (sha(l), sha(r)) == (ref["cfg5_y"]["lvl"], ref["cfg5_y"]["rec"])
