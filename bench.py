@@ -123,7 +123,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--frames", type=int, default=128, help="4K YUV420 frames per GPU per step")
     ap.add_argument("--qp", type=int, default=32)
-    ap.add_argument("--variant", type=int, default=5, help="launch variant (nanohevc.h); 5 = default")
+    ap.add_argument("--variant", type=int, default=4341, help="launch variant (nanohevc.h); 4341 = default")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget, split between the 1-thread and all-threads legs")
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: steps of the gather-inclusive phase")
     ap.add_argument("--no-cpu-baseline", action="store_true")

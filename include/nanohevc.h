@@ -120,7 +120,10 @@ int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_
  * 2 nontemporal loads, 3 nontemporal stores) + 4 * occupancy class
  * (0 compiler choice, 1 >= 5 waves/SIMD; 4 for the pipelined form) + 8 *
  * persistent software-pipelined form (next tile's loads under this tile's
- * compute). */
+ * compute); + 16 vertical block pair; 32..131 stripe forms; 256*k workgroup
+ * sizes; 2048+p store policies; 4096 + 16*c + 5: variant 5 with XCD-aware
+ * workgroup order, 2^c workgroups per XCD run (c = 15: 1/8 of the grid per
+ * XCD -- the default launch, 4341).  Full list in nh_fused8x8.hip. */
 int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                    int nsets, int qp, int is_intra, int variant, void* stream);
 /* The hot path plus the level-side helpers of quant.py:153-178 fused as an

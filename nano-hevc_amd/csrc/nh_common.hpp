@@ -262,6 +262,20 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
     return (t + n) >> f.l;
 }
 
+// ---------------------------------------------------------------------------
+// XCD-aware workgroup order for one-shot streaming grids.  The dispatcher deals
+// workgroup i to XCD i % 8; renumbering so that XCD x runs the x-th eighth of
+// the logical workgroups gives each XCD one contiguous address stream (instead
+// of all 8 XCDs interleaving over one window) -- +5..10 % on the 8x8 DCT+quant
+// stream.  A bijection on [0, nwg): ids past the last whole
+// group of 8 keep their number.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t xcd_eighths(uint32_t bid, uint32_t nwg) {
+    const uint32_t q = nwg >> 3;
+    if (bid >= q * 8u) return bid;
+    return (bid & 7u) * q + (bid >> 3);
+}
+
 // Quantizer / dequantizer of the intra chains (configs 3-5) with uniform
 // parameters, in 32 bits.  Exact whenever the residual is int16: the
 // coefficients of every transform (DST4, DCT4..32) are then |c| <= 2^17

@@ -26,8 +26,8 @@ typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 // 8 samples per thread: an 8-B load and ONE 16-B store, so every store
 // instruction of a wave covers 1 KB contiguously.
 __global__ void __launch_bounds__(256) k_widen(const uint8_t* __restrict__ in, int16_t* __restrict__ out,
-                                               int64_t nchunks, int64_t n) {
-    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+                                               int64_t nchunks, int64_t n, int xcd) {
+    const int64_t i = (xcd ? xcd_eighths(blockIdx.x, gridDim.x) : blockIdx.x) * 256ll + threadIdx.x;
     if (i < nchunks) {
         const v2u b = __builtin_nontemporal_load((const v2u*)in + i);
         v4u o;   // 8 bytes -> 8 int16, zero-extended (uint8 values are non-negative)
@@ -44,8 +44,8 @@ __global__ void __launch_bounds__(256) k_widen(const uint8_t* __restrict__ in, i
 
 // 8 samples per thread: ONE 16-B load and an 8-B store.
 __global__ void __launch_bounds__(256) k_narrow(const int16_t* __restrict__ in, uint8_t* __restrict__ out,
-                                                int64_t nchunks, int64_t n) {
-    const int64_t i = blockIdx.x * 256ll + threadIdx.x;
+                                                int64_t nchunks, int64_t n, int xcd) {
+    const int64_t i = (xcd ? xcd_eighths(blockIdx.x, gridDim.x) : blockIdx.x) * 256ll + threadIdx.x;
     if (i < nchunks) {
         const v4u a = __builtin_nontemporal_load((const v4u*)in + i);
         v2u o;   // low byte of each int16 (numpy's wrapping astype(np.uint8))
@@ -84,6 +84,7 @@ struct EncArgs {
     int32_t w, h, pitch, ppg;
     FastDiv nbx;             // blocks per row (partial included)
     uint32_t nblk;
+    uint32_t xcd;            // k_encode_u8: XCD-aware workgroup order (NH_ENC_TUNE 5th field, A/B)
 };
 
 template <int N, class V>
@@ -545,14 +546,22 @@ __device__ __forceinline__ void flush_enc_stats(const EncArgs& a, int p, EncStat
 // workgroup makes several passes).
 template <int N, int U, bool PIPE>
 __global__ void __launch_bounds__(256) k_encode_u8(EncArgs a) {
-    const int p = blockIdx.y;
+    // XCD-aware order over the (slot, plane) grid: XCD x runs the x-th eighth
+    // of the planes' workgroup slots (xcd_eighths), else the hardware order
+    uint32_t wx = blockIdx.x, wy = blockIdx.y;
+    if (a.xcd) {
+        const uint32_t l = xcd_eighths(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+        wy = l / gridDim.x;
+        wx = l - wy * gridDim.x;
+    }
+    const int p = wy;
     const int g = p / a.ppg, c = p - g * a.ppg;
     const int64_t off = a.base + (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
     const uint8_t* src = static_cast<const uint8_t*>(a.src) + off;
     const int lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * 256u * U;
     EncStats st;
-    uint32_t b0 = blockIdx.x * 256u * U;
+    uint32_t b0 = wx * 256u * U;
     BlkU8<N> cur[U];
     if (PIPE && b0 < a.nblk) {
 #pragma unroll
@@ -581,9 +590,10 @@ __global__ void __launch_bounds__(256) k_encode_u8(EncArgs a) {
 
 // Launch shape of the N = 4 / 8 kernels: blocks per lane per pass (u4, u8),
 // prefetching form (pipe) and its total workgroup cap.  Tuning knob for
-// measurement: NH_ENC_TUNE="u4,u8,pipe,cap", read once.
+// measurement: NH_ENC_TUNE="u4,u8,pipe,cap[,xcd]", read once.
 struct EncTune {
     int u4 = 1, u8 = 1, pipe = 1, cap = 4096;   // measured best (profiles/r01/frame)
+    int xcd = 0;   // XCD-aware workgroup order: 0.480 vs 0.487 ms per 64 4K frames without it (profiles/r01/xcd)
 };
 static const EncTune& enc_tune() {
     static EncTune t;
@@ -592,7 +602,7 @@ static const EncTune& enc_tune() {
         init = true;
         if (const char* e = getenv("NH_ENC_TUNE")) {
             EncTune r;
-            if (sscanf(e, "%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap) >= 2 &&
+            if (sscanf(e, "%d,%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap, &r.xcd) >= 2 &&
                 (r.u4 == 1 || r.u4 == 2 || r.u4 == 4) && (r.u8 == 1 || r.u8 == 2 || r.u8 == 4) && r.cap > 0)
                 t = r;
         }
@@ -654,7 +664,7 @@ int nh_widen_u8_i16(const uint8_t* d_in, int16_t* d_out, int64_t n, void* stream
     const hipStream_t s = as_stream(stream);
     if (((uintptr_t)d_in & 7) == 0 && ((uintptr_t)d_out & 15) == 0) {
         const int64_t chunks = n / 8, threads = chunks + (n - chunks * 8);
-        k_widen<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n);
+        k_widen<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n, xcd_order());
     } else {
         k_widen_scalar<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(d_in, d_out, n);
     }
@@ -668,7 +678,7 @@ int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* strea
     const hipStream_t s = as_stream(stream);
     if (((uintptr_t)d_in & 15) == 0 && ((uintptr_t)d_out & 7) == 0) {
         const int64_t chunks = n / 8, threads = chunks + (n - chunks * 8);
-        k_narrow<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n);
+        k_narrow<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n, xcd_order());
     } else {
         k_narrow_scalar<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(d_in, d_out, n);
     }
@@ -714,6 +724,7 @@ int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set*
         }
         a.nbx = make_fastdiv((uint32_t)nbx);
         a.nblk = (uint32_t)nblk;
+        a.xcd = enc_tune().xcd;
         // vector row access when every row start is 16-element aligned
         const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
         const bool al = al16(d_src) && (!d_recon || al16(d_recon)) && (!d_recon_u8 || al16(d_recon_u8)) &&

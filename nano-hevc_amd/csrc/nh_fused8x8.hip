@@ -41,20 +41,25 @@ struct Fused8Args {
     SetDev set[NH_MAX_PLANE_SETS];
     int32_t nsets;
     QuantS q;
+    uint32_t xcd_chunk;   // k_fwd8x8_quant<..., XCD=true> (the default launch): workgroups per XCD run
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 
 // Cache policy of the streaming accesses: 0 default, 1 nontemporal loads and
-// stores, 2 nontemporal loads only, 3 nontemporal stores only.
+// stores, 2 nontemporal loads only, 3 nontemporal stores only; A/B only:
+// 4 nontemporal loads + write-through `sc0 sc1` stores (the line leaves L2),
+// 5 nontemporal loads + `sc1` stores.
 template <int POLICY>
 __device__ __forceinline__ v4i ld16(const int16_t* p) {
-    if constexpr (POLICY == 1 || POLICY == 2) return __builtin_nontemporal_load((const v4i*)p);
+    if constexpr (POLICY == 1 || POLICY == 2 || POLICY >= 4) return __builtin_nontemporal_load((const v4i*)p);
     else return *(const v4i*)p;
 }
 template <int POLICY>
 __device__ __forceinline__ void st16(int16_t* p, v4i v) {
     if constexpr (POLICY == 1 || POLICY == 3) __builtin_nontemporal_store(v, (v4i*)p);
+    else if constexpr (POLICY == 4) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POLICY == 5) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
     else *(v4i*)p = v;
 }
 
@@ -117,27 +122,40 @@ __device__ __forceinline__ void dct8_quant_block(const v4i (&raw)[8], v4i (&outv
     }
 }
 
-__device__ __forceinline__ int select_set(const Fused8Args& a, SetDev& S) {
+__device__ __forceinline__ int select_set(const Fused8Args& a, SetDev& S, uint32_t wid) {
     int s = 0;
 #pragma unroll
     for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
-        if (k < a.nsets && blockIdx.x >= a.set[k].wg_start) s = k;
+        if (k < a.nsets && wid >= a.set[k].wg_start) s = k;
     S = a.set[0];
 #pragma unroll
     for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
         if (s == k) S = a.set[k];
     return s;
 }
+__device__ __forceinline__ int select_set(const Fused8Args& a, SetDev& S) { return select_set(a, S, blockIdx.x); }
+
+// XCD-aware workgroup order: with chunk C the 8C consecutive hardware ids of a
+// super-group are renumbered so that XCD x gets C consecutive logical
+// workgroups; C = nwg / 8 is xcd_eighths (nh_common.hpp).  The last partial
+// super-group keeps the identity order, so the map is a bijection.
+__device__ __forceinline__ uint32_t xcd_logical_wg(uint32_t bid, uint32_t chunk) {
+    const uint32_t span = 8u * chunk, sup = bid / span;
+    if ((sup + 1) * span > gridDim.x) return bid;
+    const uint32_t w = bid - sup * span;
+    return sup * span + (w & 7u) * chunk + (w >> 3);
+}
 
 // One thread = one block.  POLICY: cache policy (ld16/st16); WAVES: minimum
 // waves per SIMD requested from the register allocator (1 = compiler choice).
-template <int POLICY, int WAVES, int TPB = 256>
+template <int POLICY, int WAVES, int TPB = 256, bool XCD = false>
 __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant(Fused8Args a) {
+    const uint32_t wid = XCD ? xcd_logical_wg(blockIdx.x, a.xcd_chunk) : blockIdx.x;
     SetDev S;
-    select_set(a, S);
+    select_set(a, S, wid);
     uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
     asm volatile("" : "+v"(h_v), "+v"(hneg_v));  // pin the two offsets in VGPRs
-    const uint32_t b = (blockIdx.x - S.wg_start) * (uint32_t)TPB + threadIdx.x;
+    const uint32_t b = (wid - S.wg_start) * (uint32_t)TPB + threadIdx.x;
     if (b >= S.nblocks) return;
     const int64_t off = block_offset(S, b);
     v4i raw[8], outv[8];
@@ -180,11 +198,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         for (int k = 0; k < kEbLds / 256; ++k) tab[k * 256 + threadIdx.x] = g_eb_tab[k * 256 + threadIdx.x];
         __syncthreads();
     }
+    const uint32_t wid = xcd_eighths(blockIdx.x, gridDim.x);   // XCD-aware order, as the default launch
     SetDev S;
-    select_set(a, S);
+    select_set(a, S, wid);
     uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
     asm volatile("" : "+v"(h_v), "+v"(hneg_v));
-    const uint32_t b = (blockIdx.x - S.wg_start) * 256u + threadIdx.x;
+    const uint32_t b = (wid - S.wg_start) * 256u + threadIdx.x;
     if (b >= S.nblocks) return;
     const int64_t off = block_offset(S, b);
     v4i raw[8], outv[8];
@@ -605,9 +624,10 @@ __global__ void __launch_bounds__(256) k_probe_copy8x8_pair(Fused8Args a) {
 // the HBM ceiling this device reaches with the simplest possible pattern.
 template <int POLICY>
 __global__ void __launch_bounds__(256) k_probe_linear(const int16_t* __restrict__ in, int16_t* __restrict__ out,
-                                                     int64_t nchunks) {
+                                                     int64_t nchunks, int xcd) {
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nchunks; i += stride)
+    const uint32_t wid = xcd ? xcd_eighths(blockIdx.x, gridDim.x) : blockIdx.x;
+    for (int64_t i = (int64_t)wid * 256 + threadIdx.x; i < nchunks; i += stride)
         st16<POLICY>(out + i * 8, ld16<POLICY>(in + i * 8));
 }
 
@@ -855,7 +875,7 @@ static int run_stripe(const int16_t* d_in, int16_t* d_out, const nh_plane_set* s
 
 using namespace nh;
 
-static constexpr int kDefaultVariant = 5;
+static constexpr int kDefaultVariant = 4096 + 16 * 15 + 5;   // 4341
 
 extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets,
                                               int nsets, int qp, int is_intra, int variant, void* stream) {
@@ -865,6 +885,33 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           + 32 * stripe form (linear HBM walk through LDS; +64: register staging instead of LDS-DMA)
     //           + 128 * persistent double-buffered stripe form (LDS-DMA of the next tile under this one)
     //           + 256 * k: the plain form with 512 (k=1), 1024 (k=2) or 128 (k=3) threads per workgroup
+    //           2048 + p: the plain form (>= 5 waves/SIMD) with store policy p = 4 / 5 (see st16)
+    //           4096 + 16 * c + 5: the default form with XCD-aware workgroup order, chunk 2^c (c = 15: 1/8 of the grid)
+    if (variant >= 4096 && variant < 4096 + 16 * 16) {
+        const int c = (variant - 4096) >> 4;
+        if ((variant & 15) != 5) return NH_EARG;
+        Fused8Args a;
+        uint32_t wg = 0;
+        int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+        if (rc) return rc;
+        if (!wg) return NH_OK;
+        a.xcd_chunk = c == 15 ? (wg / 8 ? wg / 8 : 1) : (1u << c);
+        k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, as_stream(stream)>>>(a);
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
+    if (variant == 2052 || variant == 2053) {
+        Fused8Args a;
+        uint32_t wg = 0;
+        int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+        if (rc) return rc;
+        if (!wg) return NH_OK;
+        hipStream_t s = as_stream(stream);
+        if (variant == 2052) k_fwd8x8_quant<4, 5><<<wg, 256, 0, s>>>(a);
+        else k_fwd8x8_quant<5, 5><<<wg, 256, 0, s>>>(a);
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
     if (variant >= 256) {
         const int k = variant >> 8, pol = variant & 3, oc = (variant >> 2) & 1;
         if (k > 3 || (variant & 248)) return NH_EARG;
@@ -934,9 +981,11 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
 
 extern "C" int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,
                                       int qp, int is_intra, void* stream) {
-    // default launch = variant 5: nontemporal loads+stores (streamed once, keep
-    // them out of L2/MALL) and >= 5 waves/SIMD (74 VGPRs -> 6 waves); fastest
-    // in the interleaved A/B (profiles/r01/ab_variants.json).
+    // default launch = variant 4341: variant 5 (nontemporal loads+stores --
+    // streamed once, kept out of L2/MALL -- and >= 5 waves/SIMD: 74 VGPRs -> 6
+    // waves) with the XCD-aware workgroup order (XCD x streams the x-th
+    // eighth of the launch): +5..10 % over variant 5 in the interleaved A/B
+    // (profiles/r01/ab_xcd_*.json).
     return nh_fwd8x8_quant_planes_variant(d_res, d_lvl, sets, nsets, qp, is_intra, kDefaultVariant, stream);
 }
 
@@ -997,7 +1046,10 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
 extern "C" int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t nelems, int policy, int grid,
                                     void* stream) {
     // policy = cache policy (0..3) + 4 * log2(M): M > 1 = k_probe_linear_m (grid ignored)
-    const int lm = policy >> 2;
+    //          + 16: XCD-aware workgroup order (xcd_eighths; M = 1 only)
+    const int xcd = (policy >> 4) & 1;
+    const int lm = (policy >> 2) & 3;
+    if (policy >> 5 || (xcd && lm)) return NH_EARG;
     policy &= 3;
     if (!d_in || !d_out || nelems < 0 || (nelems & 7) || lm < 0 || lm > 3) return NH_EARG;
     hipStream_t s = as_stream(stream);
@@ -1018,10 +1070,10 @@ extern "C" int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t
     if (g > (1 << 30)) g = 1 << 30;
     if (!chunks) return NH_OK;
     switch (policy) {
-        case 0: k_probe_linear<0><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
-        case 1: k_probe_linear<1><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
-        case 2: k_probe_linear<2><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
-        default: k_probe_linear<3><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks); break;
+        case 0: k_probe_linear<0><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+        case 1: k_probe_linear<1><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+        case 2: k_probe_linear<2><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+        default: k_probe_linear<3><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
     }
     NH_HIP(hipGetLastError());
     return NH_OK;

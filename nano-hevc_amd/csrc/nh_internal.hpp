@@ -3,6 +3,7 @@
 // per-block entry points, and argument checks.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <mutex>
 #include <string>
 #include "../../include/nanohevc.h"
@@ -39,6 +40,16 @@ int staging_reserve(Staging& s, size_t bytes);
 int staging_upload(Staging& s, size_t off, const void* src, size_t bytes);
 int staging_download(Staging& s, void* dst, size_t off, size_t bytes);
 int staging_finish(Staging& s, int* status_out);  // sync + fetch kernel status word
+
+// XCD-aware workgroup order of the streaming frame kernels (xcd_eighths,
+// nh_common.hpp): on unless NH_XCD_ORDER=0 (A/B knob), read once.
+inline bool xcd_order() {
+    static const bool on = [] {
+        const char* e = getenv("NH_XCD_ORDER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }

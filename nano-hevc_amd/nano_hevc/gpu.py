@@ -67,7 +67,7 @@ def blocks_in(sets: Sequence[PlaneSet]) -> int:
     return sum((s.width // 8) * (s.height // 8) * s.planes_per_group * s.num_groups for s in sets)
 
 
-DEFAULT_VARIANT = 5   # nontemporal loads+stores, >= 5 waves/SIMD (see nh_fused8x8.hip)
+DEFAULT_VARIANT = 4341   # nontemporal loads+stores, >= 5 waves/SIMD, XCD-aware order (see nh_fused8x8.hip)
 
 
 def sets_fit(sets: Sequence[PlaneSet], numel: int, what: str):

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--shapes", action="store_true", help="also time the 2-blocks-per-thread pattern probes")
     ap.add_argument("--stripe", action="store_true", help="also time the stripe-form copy probes (LDS-DMA / register staging)")
     ap.add_argument("--rowwave", action="store_true", help="also time the row-per-wave and M-chunks-per-thread linear probes")
+    ap.add_argument("--xcd", action="store_true", help="also time the linear copy with the XCD-aware workgroup order")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     L = _lib.load()
@@ -76,7 +77,8 @@ def main():
              + [f"v{v}" for v in variants] + (["ex", "exnnz"] if args.epilogue else [])
              + ([f"shape{sh}_{p}" for sh in (1, 2, 3) for p in (0, 1)] if args.shapes else [])
              + ([f"shape{sh}_{p}" for sh in (4, 5) for p in (0, 1)] if args.stripe else [])
-             + ([f"shape{sh}_1" for sh in (6, 7, 8)] + [f"linear{1 + 4 * lm}g0" for lm in (1, 2, 3)] if args.rowwave else []))
+             + ([f"shape{sh}_1" for sh in (6, 7, 8)] + [f"linear{1 + 4 * lm}g0" for lm in (1, 2, 3)] if args.rowwave else [])
+             + (["linear16g0", "linear17g0"] if args.xcd else []))
     ex_nnz = torch.empty(nblk, dtype=torch.uint8, device="cuda")
     ex_bits = torch.empty(nblk, dtype=torch.int32, device="cuda")
     for n in names:

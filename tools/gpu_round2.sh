@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r01c}
 echo "== pytest -m gpu" && \
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_${TAG}.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu_${TAG}.log; [ $rc -eq 0 ] && \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_gpu_${TAG}.log; [ $rc -eq 0 ] && \
 echo "== bench" && \
 timeout -k 10 300 python bench.py --steps 30 --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err && cat gpurun_out/bench_${TAG}.json && \
 echo "== 2-rank rehearsal (gloo, shared GPU)" && \

@@ -6,11 +6,11 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r01u}
+TAG=${TAG:-r01ah}
 echo "== pytest variants" && \
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "variants or stripe or fused8x8" > gpurun_out/pytest_var_${TAG}.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_var_${TAG}.log; [ $rc -eq 0 ] && \
 echo "== A/B" && \
-timeout -k 10 400 python tools/ab_fwd8x8.py --variants 0,5,261,517,773,1 --rounds 10 > gpurun_out/ab_stripe_${TAG}.json 2> gpurun_out/ab_stripe_${TAG}.err && python -c "
+timeout -k 10 400 python tools/ab_fwd8x8.py --variants 0,5,1,2052,2053 --rounds 10 > gpurun_out/ab_stripe_${TAG}.json 2> gpurun_out/ab_stripe_${TAG}.err && python -c "
 import json; d=json.load(open('gpurun_out/ab_stripe_${TAG}.json'))
 for k,v in d['results'].items(): print(k, round(v['GBps_median']), round(v['GBps_best']), v.get('equal_v0',''))" && \
 echo "== done"
