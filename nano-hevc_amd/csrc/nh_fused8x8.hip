@@ -886,17 +886,24 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           + 128 * persistent double-buffered stripe form (LDS-DMA of the next tile under this one)
     //           + 256 * k: the plain form with 512 (k=1), 1024 (k=2) or 128 (k=3) threads per workgroup
     //           2048 + p: the plain form (>= 5 waves/SIMD) with store policy p = 4 / 5 (see st16)
-    //           4096 + 16 * c + 5: the default form with XCD-aware workgroup order, chunk 2^c (c = 15: 1/8 of the grid)
+    //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p) with XCD-aware workgroup
+    //           order, chunk 2^c workgroups (c = 15: 1/8 of the grid); 4341 = policy 1, eighths: the default
     if (variant >= 4096 && variant < 4096 + 16 * 16) {
-        const int c = (variant - 4096) >> 4;
-        if ((variant & 15) != 5) return NH_EARG;
+        const int c = (variant - 4096) >> 4, pol = variant & 3;
+        if ((variant & 12) != 4) return NH_EARG;
         Fused8Args a;
         uint32_t wg = 0;
         int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
         if (rc) return rc;
         if (!wg) return NH_OK;
         a.xcd_chunk = c == 15 ? (wg / 8 ? wg / 8 : 1) : (1u << c);
-        k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, as_stream(stream)>>>(a);
+        hipStream_t s = as_stream(stream);
+        switch (pol) {
+            case 0: k_fwd8x8_quant<0, 5, 256, true><<<wg, 256, 0, s>>>(a); break;
+            case 1: k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, s>>>(a); break;
+            case 2: k_fwd8x8_quant<2, 5, 256, true><<<wg, 256, 0, s>>>(a); break;
+            default: k_fwd8x8_quant<3, 5, 256, true><<<wg, 256, 0, s>>>(a); break;
+        }
         NH_HIP(hipGetLastError());
         return NH_OK;
     }
