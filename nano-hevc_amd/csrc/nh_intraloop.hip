@@ -547,6 +547,144 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     }
 }
 
+// Tagged-line form (default): the line buffer holds 64-bit words
+// (tag << 32 | int16 pair), written with one single-copy-atomic coherent store
+// per word, tag = producing block row + 1.  A row polls the 8 words of the top
+// and top-right blocks directly until their tags name the row above, so the
+// wait and the reference read are ONE coherent round trip per block (the
+// progress-counter form needs two: poll the counter, then read the line), and
+// no vmcnt(0) orders a progress store behind the line stores.  WAR safety is
+// the progress form's argument (row r+1 overwrites block bx's words only after
+// reading them for blocks bx-1 and bx; the top-left sample is carried).  Words
+// past the last full block are never written: they read as 0 without a wait.
+// The winner hands its recon / levels to the wave through LDS and the 64
+// lanes store one sample each (2 store instructions instead of 128
+// single-lane ones on the row's critical path).
+template <int WAVES>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8_closed_tag(ClosedArgs a) {
+    __shared__ RdoSlotLds L;
+    __shared__ uint32_t refs[64][kRefStride];
+    __shared__ uint32_t outP[32], outL[32];   // the winner's recon / level pairs, row-major
+    __shared__ int32_t topw[9];
+    __shared__ int row_s, stall_s, win_s;
+    const int lane = threadIdx.x;
+    const ChainQ rq = make_chainq(a.qp, a.dq_scale, a.dq_per);
+    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
+    for (;;) {
+        if (lane == 0) {
+            row_s = atomicAdd(&a.work[0], 1);
+            stall_s = 0;
+        }
+        __syncthreads();
+        const int row = row_s;
+        if (row >= a.total_rows) break;
+        int si = 0;
+        for (int k = 1; k < a.nsets; ++k)
+            if (row >= a.set[k].row0) si = k;
+        const ClosedSet& S = a.set[si];
+        const int local = row - S.row0, pl = local / S.bh, by = local - pl * S.bh;
+        const int g = pl / S.ppg, c = pl - g * S.ppg;
+        const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
+        const int16_t* src = a.src + off;
+        int16_t* rec = a.rec + off;
+        int32_t* lvl = a.lvl + off;
+        uint64_t* line = lines + S.line0 + (int64_t)pl * S.lw;
+        const int y0 = by * 8, full_words = S.bw * 4;
+        int16_t tl_next = 128;
+        unsigned long long row_sse = 0;
+        for (int bx = 0; bx < S.bw; ++bx) {
+            const int x0 = bx * 8;
+            const int16_t ov = src[(int64_t)(y0 + lane / 8) * S.pitch + x0 + (lane % 8)];
+            if (by > 0) {
+                // lanes 0..7: words x0/2 .. x0/2+7 (samples x0 .. x0+15) of the row above
+                const int wi = x0 / 2 + lane;
+                const bool need = lane < 8 && wi < full_words;
+                uint32_t val = 0;
+                int spins = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (need) {
+                        const uint64_t v = ld_sys64(line + wi);
+                        ok = (int)(v >> 32) == by;
+                        val = (uint32_t)v;
+                    }
+                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;   // every needed word is there
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
+                        if (lane == 0) atomicMax(&a.work[1], 1);
+                        stall_s = 1;
+                        break;
+                    }
+                }
+                if (lane < 8) topw[1 + lane] = (int32_t)val;
+            }
+            __syncthreads();
+            if (stall_s) break;
+            {
+                const int k = lane;
+                L.orig[k] = ov;
+                if (k < 16) {
+                    int16_t v = 128;
+                    if (y0 > 0 && x0 + k < S.w) v = (int16_t)(topw[1 + (k >> 1)] >> ((k & 1) * 16));
+                    L.topA[1 + k] = v;
+                    if (k < 8) L.topN[k] = v;
+                } else if (k < 24) {
+                    const int kk = k - 16;
+                    const int16_t v = x0 == 0 ? (int16_t)128 : (int16_t)(outP[kk * 4 + 3] >> 16);
+                    L.leftA[1 + kk] = v;
+                    L.leftN[kk] = v;
+                } else if (k == 24) {
+                    const int16_t tl = (y0 == 0 || x0 == 0) ? (int16_t)128 : tl_next;
+                    L.topA[0] = tl;
+                    L.leftA[0] = tl;
+                    L.ntA = 1 + (y0 == 0 ? 16 : min(16, S.w - x0));
+                    L.nlA = 1 + 8;
+                    L.wide = 0;
+                }
+            }
+            __syncthreads();
+            rdo8_block_prep(L, lane);
+            __syncthreads();
+            tl_next = L.topA[8];
+            uint32_t P[32], Lv[32];
+            unsigned long long key = ULLONG_MAX;
+            if (lane < kModes) key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
+            unsigned long long best = key;
+            for (int m = 32; m > 0; m >>= 1) {
+                const unsigned long long o = __shfl_xor(best, m, 64);
+                best = o < best ? o : best;
+            }
+            if (key == best) {
+                // publish the bottom row first (the next row polls these words)
+                const uint64_t tag = (uint64_t)(uint32_t)(by + 1) << 32;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) st_sys64(line + x0 / 2 + q, tag | P[28 + q]);
+#pragma unroll
+                for (int q = 0; q < 32; ++q) {
+                    outP[q] = P[q];
+                    outL[q] = Lv[q];
+                }
+                win_s = lane;
+                row_sse += best >> 6;
+            }
+            __syncthreads();
+            {   // every lane stores one sample of the winner's block
+                const int i = lane >> 3, j = lane & 7;
+                const int64_t e = (int64_t)(y0 + i) * S.pitch + x0 + j;
+                rec[e] = (int16_t)(outP[i * 4 + j / 2] >> (16 * (j & 1)));
+                lvl[e] = (int32_t)(int16_t)(outL[i * 4 + j / 2] >> (16 * (j & 1)));
+                if (lane == 0) a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)win_s;
+            }
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) row_sse += __shfl_xor(row_sse, m, 64);
+        if (lane == 0 && row_sse) atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], row_sse);
+        __syncthreads();
+        if (stall_s) break;
+    }
+}
+
 // Samples outside full 8x8 blocks read as 0 (Frame.zeros) by the closed loop.
 __global__ void k_zero_partial(int16_t* rec, ClosedSet S, int nplanes) {
     const int p = blockIdx.y;
@@ -961,7 +1099,7 @@ static int closed_layout(const nh_plane_set* sets, int nsets, ClosedArgs& a, int
     }
     a.nsets = nsets;
     a.total_rows = (int32_t)rows;
-    a.lines0 = 2 + rows;
+    a.lines0 = (2 + rows + 1) & ~1ll;   // 8-B aligned: the tagged form's 64-bit line words
     a.lines_total = lines;
     modes_total = modes;
     return NH_OK;
@@ -971,7 +1109,7 @@ extern "C" int64_t nh_intra_rdo_closed_workspace_bytes(const nh_plane_set* sets,
     ClosedArgs a;
     int64_t m = 0;
     if (closed_layout(sets, nsets, a, m)) return -1;
-    return 4ll * (a.lines0 + a.lines_total);
+    return 4ll * a.lines0 + 8ll * a.lines_total;   // 64-bit line words (the int32 form uses half)
 }
 
 extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp,
@@ -999,7 +1137,11 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
     a.dq_scale = dequant_scale(rem);
     a.dq_per = per;
     hipStream_t s = as_stream(stream);
-    NH_HIP(hipMemsetAsync(d_work, 0, 4ull * (a.lines0 + a.lines_total), s));
+    if ((uintptr_t)d_work & 7) {
+        set_error("nh_intra_rdo_planes_closed: workspace must be 8-byte aligned");
+        return NH_EARG;
+    }
+    NH_HIP(hipMemsetAsync(d_work, 0, 4ull * a.lines0 + 8ull * a.lines_total, s));
     for (int k = 0; k < nsets; ++k) {
         const int np = sets[k].planes_per_group * sets[k].num_groups;
         if (np > 0 && np <= 65535) k_zero_partial<<<dim3(64, np), 256, 0, s>>>(d_recon, a.set[k], np);
@@ -1008,10 +1150,17 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
     if (a.total_rows > 0) {
         // persistent waves: enough to cover every row, capped at what can be resident (2 waves/SIMD)
         const int waves = a.total_rows < 2048 ? a.total_rows : 2048;
-        {   // NH_CLOSED_WAVES=2: register allocation for 2 waves/SIMD (spills) -- A/B knob
+        {   // A/B knobs: NH_CLOSED_WAVES=2 register allocation for 2 waves/SIMD (spills);
+            // NH_CLOSED_FORM=0 the progress-counter form (default 1: tagged line words)
             static const int cw = [] { const char* e = getenv("NH_CLOSED_WAVES"); return e ? atoi(e) : 1; }();
-            if (cw == 2) k_intra_rdo8_closed<2><<<waves, 64, 0, s>>>(a);
-            else k_intra_rdo8_closed<1><<<waves, 64, 0, s>>>(a);
+            static const int cf = [] { const char* e = getenv("NH_CLOSED_FORM"); return e ? atoi(e) : 1; }();
+            if (cf == 0) {
+                if (cw == 2) k_intra_rdo8_closed<2><<<waves, 64, 0, s>>>(a);
+                else k_intra_rdo8_closed<1><<<waves, 64, 0, s>>>(a);
+            } else {
+                if (cw == 2) k_intra_rdo8_closed_tag<2><<<waves, 64, 0, s>>>(a);
+                else k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
+            }
         }
     }
     NH_HIP(hipGetLastError());
