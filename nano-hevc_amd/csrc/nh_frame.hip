@@ -85,6 +85,7 @@ struct EncArgs {
     FastDiv nbx;             // blocks per row (partial included)
     uint32_t nblk;
     uint32_t xcd;            // k_encode_u8: XCD-aware workgroup order (NH_ENC_TUNE 5th field, A/B)
+    uint32_t nostats;        // A/B probe only (NH_ENC_TUNE 6th field): skip the stats atomics
 };
 
 template <int N, class V>
@@ -206,7 +207,7 @@ __global__ void __launch_bounds__(256) k_encode_dcpl(EncArgs a) {
         if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && !a.nostats) {
         int64_t t[5];
         for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
         int64_t* s = a.stats + (int64_t)p * NH_ENC_STATS;
@@ -364,7 +365,7 @@ __global__ void __launch_bounds__(256) k_encode_small(EncArgs a) {
         if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && !a.nostats) {
         int64_t t[5];
         for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
         int64_t* s = a.stats + (int64_t)p * NH_ENC_STATS;
@@ -531,7 +532,7 @@ __device__ __forceinline__ void flush_enc_stats(const EncArgs& a, int p, EncStat
         if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && !a.nostats) {
         int64_t t[5];
         for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
         int64_t* s = a.stats + (int64_t)p * NH_ENC_STATS;
@@ -593,7 +594,8 @@ __global__ void __launch_bounds__(256) k_encode_u8(EncArgs a) {
 // measurement: NH_ENC_TUNE="u4,u8,pipe,cap[,xcd]", read once.
 struct EncTune {
     int u4 = 1, u8 = 1, pipe = 1, cap = 4096;   // measured best (profiles/r01/frame)
-    int xcd = 0;   // XCD-aware workgroup order: 0.480 vs 0.487 ms per 64 4K frames without it (profiles/r01/xcd)
+    int xcd = 0;       // XCD-aware workgroup order: 0.480 vs 0.487 ms per 64 4K frames without it (profiles/r01/xcd)
+    int nostats = 0;   // A/B probe only: skip the stats atomics (stats are then wrong)
 };
 static const EncTune& enc_tune() {
     static EncTune t;
@@ -602,7 +604,7 @@ static const EncTune& enc_tune() {
         init = true;
         if (const char* e = getenv("NH_ENC_TUNE")) {
             EncTune r;
-            if (sscanf(e, "%d,%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap, &r.xcd) >= 2 &&
+            if (sscanf(e, "%d,%d,%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap, &r.xcd, &r.nostats) >= 2 &&
                 (r.u4 == 1 || r.u4 == 2 || r.u4 == 4) && (r.u8 == 1 || r.u8 == 2 || r.u8 == 4) && r.cap > 0)
                 t = r;
         }
@@ -725,6 +727,7 @@ int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set*
         a.nbx = make_fastdiv((uint32_t)nbx);
         a.nblk = (uint32_t)nblk;
         a.xcd = enc_tune().xcd;
+        a.nostats = enc_tune().nostats;
         // vector row access when every row start is 16-element aligned
         const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
         const bool al = al16(d_src) && (!d_recon || al16(d_recon)) && (!d_recon_u8 || al16(d_recon_u8)) &&
