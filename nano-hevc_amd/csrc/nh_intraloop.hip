@@ -245,6 +245,199 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
     return L.wide ? rdo8_recon_sse<true>(X, opk, Rpk) : rdo8_recon_sse<false>(X, opk, Rpk);
 }
 
+// ---------------------------------------------------------------------------
+// Lane-pair form of the chain (closed loop): one mode on TWO lanes, l and
+// l ^ 32 (half h = l >> 5), so a block step's VALU path is about half as long.
+// A half owns columns 4h..4h+3 for the column passes and rows 4h..4h+3 for the
+// row passes; the transposes between passes are register-pair swaps with the
+// partner lane (v_permlane32_swap, one VALU op per dword).  Same arithmetic,
+// element for element, as rdo8_chain (bit-exact by construction).
+//   column layout: X[u][v] = (row u, column 4h+v), u 0..7, v 0..3
+//   row layout:    X[i][c] = (row 4h+i, column c), X[4+i][c] = (row 4h+i, column 4+c), i, c 0..3
+// pair_swap on (X[i][v], X[4+i][v]) maps one layout to the other (an involution).
+// ---------------------------------------------------------------------------
+// v_permlane32_swap exchanges the upper 32 lanes of its first operand with the
+// lower 32 lanes of its second: lanes 0-31 send r1 and receive the partner's r0
+// into r1, lanes 32-63 send r0 and receive the partner's r1 into r0.
+__device__ __forceinline__ void pair_swap(uint32_t& r0, uint32_t& r1) {
+    const auto t = __builtin_amdgcn_permlane32_swap(r0, r1, false, false);
+    r0 = t[0];
+    r1 = t[1];
+}
+__device__ __forceinline__ void pair_transpose(uint32_t (&X)[8][4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) pair_swap(X[i][v], X[4 + i][v]);
+}
+__device__ __forceinline__ uint32_t pair_other(uint32_t x) {   // the partner lane's x
+    const auto t = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (threadIdx.x & 32) ? t[0] : t[1];
+}
+
+// Recon + clip + SSE of this half's 4 rows (row layout X = inverse pass-1
+// output rows), prediction pairs Pp in row layout (Pp[i][m]: row 4h+i pairs
+// m = 0,1 of columns 0..3; Pp[4+i][m]: pairs of columns 4..7).
+template <bool WIDE>
+__device__ __forceinline__ unsigned long long rdo8_pair_recon_sse(uint32_t (&X)[8][4], uint32_t (&Pp)[8][2],
+                                                                  const uint32_t* opk, int h, uint32_t (&Rpk)[16]) {
+    const v2s zero = {0, 0}, maxv = {255, 255};
+    unsigned long long sse = 0;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        uint32_t row[8], x[8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            row[c] = X[i][c];
+            row[4 + c] = X[4 + i][c];
+        }
+        inv_dct<8, Mul24>(row, x, 128u);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const v2s rr = as_v2s(pack16((int32_t)x[2 * m] >> 8, (int32_t)x[2 * m + 1] >> 8));
+            const uint32_t pp = m < 2 ? Pp[i][m] : Pp[4 + i][m - 2];
+            v2s rc = as_v2s(pp) + rr;
+            rc = __builtin_elementwise_min(__builtin_elementwise_max(rc, zero), maxv);
+            Rpk[i * 4 + m] = as_u32(rc);
+            const v2s d = as_v2s(opk[(4 * h + i) * 4 + m]) - rc;
+            if constexpr (!WIDE) {
+                acc = dot2_acc(as_u32(d), acc);
+            } else {
+                const int32_t d0 = d.x, d1 = d.y;
+                sse += (unsigned long long)((uint32_t)(d0 * d0) + (uint32_t)(d1 * d1));
+            }
+        }
+    }
+    return WIDE ? sse : (unsigned long long)acc;
+}
+
+// Returns this half's SSE (rows 4h..4h+3); Rpk / Lpk receive this half's recon /
+// level rows (row-major int16 pairs, Rpk[i*4+m] = row 4h+i, columns 2m, 2m+1).
+__device__ __forceinline__ unsigned long long rdo8_chain_pair(const RdoSlotLds& L, int mode, int h, uint32_t* refp,
+                                                              const ChainQ& q, uint32_t (&Rpk)[16], uint32_t (&Lpk)[16]) {
+    const uint32_t* rp[8];          // per scan line s: pair-array row, weights, extract width
+    uint32_t wf[8], wd[8];
+    bool vert = true;
+    if (mode >= 2) {            // _build_ref_array (intra.py:159-188) as pairs, as rdo8_chain
+        const int angle = intra_angle_alu(mode);
+        vert = mode >= 18;
+        const int16_t* pri = vert ? L.topA : L.leftA;
+        const int16_t* sec = vert ? L.leftA : L.topA;
+        const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
+        int32_t r[25];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = 0;
+        r[8] = pri[0];
+#pragma unroll
+        for (int i = 1; i <= 16; ++i) r[8 + i] = pri[i < np ? i : np - 1];
+        if (angle < 0) {
+            const int inv = inv_angle_alu(angle), next = (8 * angle) >> 5;
+#pragma unroll
+            for (int i = -1; i >= -8; --i) {
+                const int proj = ((i + 1) * inv + 128) >> 8;
+                if (i >= next && proj < ns) r[8 + i] = sec[proj];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 24; ++i) refp[i] = pack16(r[i], r[i + 1]);
+        refp[24] = (uint32_t)r[24] & 0xffffu;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int proj = (s + 1) * angle, f = proj & 31;
+            rp[s] = refp + 9 + (proj >> 5);
+            wf[s] = (uint32_t)(32 - f) | ((uint32_t)f << 16);
+            wd[s] = f ? 11u : 27u;
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            rp[s] = mode == 0 ? L.planar + 8 * s : L.dcv;
+            wf[s] = 32u;
+            wd[s] = 27u;
+        }
+    }
+    // scan lines 4h..4h+3 (the horizontal modes' columns of P)
+    const uint32_t* rpH[4];
+    uint32_t wfH[4], wdH[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        rpH[v] = h ? rp[4 + v] : rp[v];
+        wfH[v] = h ? wf[4 + v] : wf[v];
+        wdH[v] = h ? wd[4 + v] : wd[v];
+    }
+    // prediction P(u, 4h+v) = Q[u][4h+v] (vertical, planar, DC) or Q[4h+v][u] (horizontal)
+    uint32_t X[8][4];
+    uint32_t Pp[8][2];
+    const uint32_t* opk = (const uint32_t*)L.orig;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        int32_t pv[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint32_t* a = vert ? rp[u] + (4 * h + v) : rpH[v] + u;
+            const uint32_t w = vert ? wf[u] : wfH[v];
+            const uint32_t d = vert ? wd[u] : wdH[v];
+            const int t = dot2_16(*a, w);
+            pv[v] = __builtin_amdgcn_sbfe(t, 5u, d);
+        }
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            const uint32_t pp = pack16(pv[2 * m], pv[2 * m + 1]);
+            Pp[u][m] = pp;
+            const uint32_t dd = as_u32(as_v2s(opk[u * 4 + 2 * h + m]) - as_v2s(pp));   // residual_block: int16 wrap
+            X[u][2 * m] = (uint32_t)(int32_t)(int16_t)(dd & 0xffffu);
+            X[u][2 * m + 1] = (uint32_t)((int32_t)dd >> 16);
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {           // forward pass 1: this half's 4 columns
+        uint32_t x[8], y[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = X[k][v];
+        fwd_dct<8, Mul24>(x, y, 128u);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[k][v] = (uint32_t)((int32_t)y[k] >> 8);
+    }
+    pair_transpose(X);                      // -> rows 4h..4h+3
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {           // forward pass 2 + quant + dequant on this half's rows
+        uint32_t row[8], y[8];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            row[c] = X[i][c];
+            row[4 + c] = X[4 + i][c];
+        }
+        fwd_dct<8, Mul24>(row, y, 128u);
+        int32_t l[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) l[j] = quant_s((int32_t)y[j] >> 8, q.qs, q.h_v, q.hneg_v);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            X[i][c] = (uint32_t)dequant_s(l[c], q);
+            X[4 + i][c] = (uint32_t)dequant_s(l[4 + c], q);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) Lpk[i * 4 + m] = pack16(l[2 * m], l[2 * m + 1]);
+    }
+    pair_transpose(X);                      // -> columns 4h..4h+3
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {           // inverse pass 1 (transform.py:221-227)
+        uint32_t yv[8], x[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) yv[k] = X[k][v];
+        inv_dct<8, Mul24>(yv, x, 128u);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) X[k][v] = (uint32_t)((int32_t)x[k] >> 8);
+    }
+    pair_transpose(X);                      // -> rows
+#pragma unroll
+    for (int i = 0; i < 4; ++i)             // the prediction pairs to the row layout too
+#pragma unroll
+        for (int m = 0; m < 2; ++m) pair_swap(Pp[i][m], Pp[4 + i][m]);
+    return L.wide ? rdo8_pair_recon_sse<true>(X, Pp, opk, h, Rpk) : rdo8_pair_recon_sse<false>(X, Pp, opk, h, Rpk);
+}
+
 template <int WAVES, bool ONESHOT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
@@ -346,6 +539,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         const int by = b / bw, bx = b - by * bw;
         modes[b] = (uint8_t)mode;
         atomicAdd(&wg_sse, key >> 6);   // LDS: no register lives across the loop
+        // (A/B: handing the block to the workgroup through LDS for wave-wide
+        // stores measured 0.225 vs 0.222 ms/frame -- the winners' stores overlap
+        // the other wave's chain here; kept in the closed loop, where they do not)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
@@ -411,6 +607,7 @@ struct ClosedArgs {
     int32_t dq_scale, dq_per;
     int32_t order;                  // tagged form: 0 plane-major tickets, 1 row-major across planes
     int32_t max_bh;                 // largest block-row count of any set
+    int32_t probe;                  // timing probe only (NH_CLOSED_PROBE=1): skip the chain (wrong outputs)
 };
 constexpr int kSpinLimit = 1 << 20;   // ~1 s of polling; a legitimate wait is a few block steps
 
@@ -690,7 +887,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             tl_next = L.topA[8];
             uint32_t P[32], Lv[32];
             unsigned long long key = ULLONG_MAX;
-            if (lane < kModes) key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
+            if (a.probe) {
+#pragma unroll
+                for (int q = 0; q < 32; ++q) P[q] = Lv[q] = (uint32_t)L.orig[q];
+                if (lane < kModes) key = lane;
+            } else if (lane < kModes) {
+                key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
+            }
             unsigned long long best = key;
             for (int m = 32; m > 0; m >>= 1) {
                 const unsigned long long o = __shfl_xor(best, m, 64);
@@ -711,6 +914,145 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             }
             __syncthreads();
             {   // every lane stores one sample of the winner's block
+                const int i = lane >> 3, j = lane & 7;
+                const int64_t e = (int64_t)(y0 + i) * S.pitch + x0 + j;
+                rec[e] = (int16_t)(outP[i * 4 + j / 2] >> (16 * (j & 1)));
+                lvl[e] = (int32_t)(int16_t)(outL[i * 4 + j / 2] >> (16 * (j & 1)));
+                if (lane == 0) a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)win_s;
+            }
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) row_sse += __shfl_xor(row_sse, m, 64);
+        if (lane == 0 && row_sse) atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], row_sse);
+        __syncthreads();
+        if (stall_s) break;
+    }
+}
+
+// Lane-pair form (NH_CLOSED_FORM=2): the tagged-line wavefront of
+// k_intra_rdo8_closed_tag with every mode on a lane pair (rdo8_chain_pair):
+// a workgroup of two waves per block row, modes 0..31 on wave 0 (lanes m and
+// m + 32), modes 32..34 on wave 1; the winner is the minimum over both waves.
+template <int WAVES>
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8_closed_pair(ClosedArgs a) {
+    __shared__ RdoSlotLds L;
+    __shared__ uint32_t refs[128][kRefStride];
+    __shared__ uint32_t outP[32], outL[32];   // the winner's recon / level pairs, row-major
+    __shared__ int32_t topw[9];
+    __shared__ unsigned long long wmin[2];
+    __shared__ int row_s, stall_s, win_s;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int h = lane >> 5, mode = wave * 32 + (lane & 31);
+    const bool on = mode < kModes;
+    const ChainQ rq = make_chainq(a.qp, a.dq_scale, a.dq_per);
+    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
+    for (;;) {
+        if (tid == 0) {
+            row_s = atomicAdd(&a.work[0], 1);
+            stall_s = 0;
+        }
+        __syncthreads();
+        const int row = row_s;
+        if (row >= a.total_rows) break;
+        int si, pl, by;
+        closed_ticket(a, row, si, pl, by);
+        const ClosedSet& S = a.set[si];
+        const int g = pl / S.ppg, c = pl - g * S.ppg;
+        const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
+        const int16_t* src = a.src + off;
+        int16_t* rec = a.rec + off;
+        int32_t* lvl = a.lvl + off;
+        uint64_t* line = lines + S.line0 + (int64_t)pl * S.lw;
+        const int y0 = by * 8, full_words = S.bw * 4;
+        int16_t tl_next = 128;
+        unsigned long long row_sse = 0;
+        for (int bx = 0; bx < S.bw; ++bx) {
+            const int x0 = bx * 8;
+            int16_t ov = 0;
+            if (wave == 0) ov = src[(int64_t)(y0 + lane / 8) * S.pitch + x0 + (lane % 8)];
+            if (by > 0 && wave == 0) {
+                const int wi = x0 / 2 + lane;
+                const bool need = lane < 8 && wi < full_words;
+                uint32_t val = 0;
+                int spins = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (need) {
+                        const uint64_t v = ld_sys64(line + wi);
+                        ok = (int)(v >> 32) == by;
+                        val = (uint32_t)v;
+                    }
+                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
+                        if (lane == 0) atomicMax(&a.work[1], 1);
+                        stall_s = 1;
+                        break;
+                    }
+                }
+                if (lane < 8) topw[1 + lane] = (int32_t)val;
+            }
+            __syncthreads();
+            if (stall_s) break;
+            if (wave == 0) {
+                const int k = lane;
+                L.orig[k] = ov;
+                if (k < 16) {
+                    int16_t v = 128;
+                    if (y0 > 0 && x0 + k < S.w) v = (int16_t)(topw[1 + (k >> 1)] >> ((k & 1) * 16));
+                    L.topA[1 + k] = v;
+                    if (k < 8) L.topN[k] = v;
+                } else if (k < 24) {
+                    const int kk = k - 16;
+                    const int16_t v = x0 == 0 ? (int16_t)128 : (int16_t)(outP[kk * 4 + 3] >> 16);
+                    L.leftA[1 + kk] = v;
+                    L.leftN[kk] = v;
+                } else if (k == 24) {
+                    const int16_t tl = (y0 == 0 || x0 == 0) ? (int16_t)128 : tl_next;
+                    L.topA[0] = tl;
+                    L.leftA[0] = tl;
+                    L.ntA = 1 + (y0 == 0 ? 16 : min(16, S.w - x0));
+                    L.nlA = 1 + 8;
+                    L.wide = 0;
+                }
+            }
+            __syncthreads();
+            if (wave == 0) rdo8_block_prep(L, lane);
+            __syncthreads();
+            tl_next = L.topA[8];
+            uint32_t Rp[16], Lp[16];
+            unsigned long long key = ULLONG_MAX;
+            if (on) {
+                const unsigned long long e = rdo8_chain_pair(L, mode, h, refs[tid], rq, Rp, Lp);
+                const uint32_t lo = pair_other((uint32_t)e), hi = pair_other((uint32_t)(e >> 32));
+                key = ((e + (((unsigned long long)hi << 32) | lo)) << 6) | (unsigned long long)mode;
+            }
+            unsigned long long best = key;
+            for (int m = 32; m > 0; m >>= 1) {
+                const unsigned long long o = __shfl_xor(best, m, 64);
+                best = o < best ? o : best;
+            }
+            if (lane == 0) wmin[wave] = best;
+            __syncthreads();
+            best = wmin[0] < wmin[1] ? wmin[0] : wmin[1];
+            if (key == best) {   // the winning mode's two lanes
+                if (h == 1) {    // publish the bottom row (row 7 = this half's row 3) first
+                    const uint64_t tag = (uint64_t)(uint32_t)(by + 1) << 32;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) st_sys64(line + x0 / 2 + q, tag | Rp[12 + q]);
+                } else {
+                    win_s = mode;
+                    row_sse += best >> 6;
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    outP[h * 16 + q] = Rp[q];
+                    outL[h * 16 + q] = Lp[q];
+                }
+            }
+            __syncthreads();
+            if (wave == 0) {   // wave 0 stores one sample per lane
                 const int i = lane >> 3, j = lane & 7;
                 const int64_t e = (int64_t)(y0 + i) * S.pitch + x0 + j;
                 rec[e] = (int16_t)(outP[i * 4 + j / 2] >> (16 * (j & 1)));
@@ -1200,9 +1542,14 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
             static const int cf = [] { const char* e = getenv("NH_CLOSED_FORM"); return e ? atoi(e) : 1; }();
             static const int co = [] { const char* e = getenv("NH_CLOSED_ORDER"); return e ? atoi(e) : 1; }();
             a.order = co ? 1 : 0;
+            static const int cp = [] { const char* e = getenv("NH_CLOSED_PROBE"); return e ? atoi(e) : 0; }();
+            a.probe = cp;
             if (cf == 0) {
                 if (cw == 2) k_intra_rdo8_closed<2><<<waves, 64, 0, s>>>(a);
                 else k_intra_rdo8_closed<1><<<waves, 64, 0, s>>>(a);
+            } else if (cf == 2) {
+                if (cw == 3) k_intra_rdo8_closed_pair<3><<<waves, 128, 0, s>>>(a);
+                else k_intra_rdo8_closed_pair<2><<<waves, 128, 0, s>>>(a);
             } else {
                 if (cw == 2) k_intra_rdo8_closed_tag<2><<<waves, 64, 0, s>>>(a);
                 else k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
