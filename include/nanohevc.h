@@ -195,6 +195,12 @@ int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* set, int ctb
  * exact int8 part splitting).  Identical outputs.  pitch % 8 == 0. */
 int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl,
                   int16_t* d_recon, int variant, void* stream);
+/* Config 5 over every plane of up to NH_MAX_PLANE_SETS plane sets (a stream of
+ * frames): variant 1 = one int8-MFMA launch per set (blockIdx.y = plane),
+ * variant 0 = the butterfly, one launch per plane (A/B).  Levels / recon use
+ * the source layout.  Same per-plane results as nh_tc32_plane. */
+int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
+                   int16_t* d_recon, int variant, void* stream);
 /* Measurement / validation helper: D = A.B for row-major int8 32x32 A, B
  * (int32 D) with the lane maps the config-5 MFMA kernel assumes. */
 int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream);

@@ -142,14 +142,16 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
     const int b = blockIdx.x * 4 + wv;
     if (b >= nblk) return;                       // whole wave exits together
     const ChainQ cq = make_chainq(qp, dq_scale, dq_per);   // 32-bit quant/dequant (int16 residual)
-    if constexpr (TREE) {   // this workgroup's plane of the batch
+    {   // this workgroup's plane of the batch (blockIdx.y; ta.ppg >= 1)
         const int pz = blockIdx.y, gz = pz / ta.ppg, cz = pz - gz * ta.ppg;
         const int64_t poff = (int64_t)gz * ta.group_stride + (int64_t)cz * ta.plane_stride;
         src += poff;
         lvl += poff;
         recon += poff;
-        tu_log2 += (int64_t)pz * ta.tu_plane;
-        ta.plane_id += cz;
+        if constexpr (TREE) {
+            tu_log2 += (int64_t)pz * ta.tu_plane;
+            ta.plane_id += cz;
+        }
     }
     const int x0 = (b % nbx) * 32, y0 = (b / nbx) * 32 + (TREE ? ta.y_base : 0);
     if constexpr (TREE) {
@@ -314,6 +316,60 @@ extern "C" int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int 
     k_tc32_mfma<false><<<(nblk + 3) / 4, 256, 0, s>>>(d_src, w, h, pitch, nbx, nblk, p, dequant_scale(rem), per,
                                                       d_lvl, d_recon, TreeArgs{}, nullptr);
     NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
+                              int16_t* d_recon, int variant, void* stream) {
+    if (!d_src || !d_lvl || !d_recon || !sets || nsets < 0 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
+    if (((uintptr_t)d_src & 15) || ((uintptr_t)d_lvl & 15) || ((uintptr_t)d_recon & 15)) {
+        set_error("tc32_planes: buffers must be 16-byte aligned");
+        return NH_EARG;
+    }
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& S = sets[k];
+        const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
+        if (S.width < 0 || S.height < 0 || S.pitch < S.width || S.planes_per_group < 1 || S.num_groups < 0 ||
+            planes > 65535 || ((S.base | S.plane_stride | S.group_stride | S.pitch) & 7)) {
+            set_error("tc32_planes: plane set must have pitch >= width, 8-element aligned base/pitch/strides");
+            return NH_EARG;
+        }
+    }
+    if (variant != 0 && variant != 1) return NH_EARG;
+    hipStream_t s = as_stream(stream);
+    int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
+    const int per = q / 6, rem = q % 6;
+    QuantParams p;
+    p.shift = 14 + per + 5;
+    p.mf = quant_scale(rem);
+    p.off = (uint32_t)((1ull << p.shift) / 3);
+    if (variant == 1) {
+        int rc = ensure_basis(s);
+        if (rc) return rc;
+    }
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& S = sets[k];
+        const int planes = S.planes_per_group * S.num_groups;
+        const int nbx = S.width / 32, nblk = nbx * (S.height / 32);
+        if (!nblk || !planes) continue;
+        if (variant == 0) {   // butterfly A/B leg: one launch per plane
+            for (int pz = 0; pz < planes; ++pz) {
+                const int gz = pz / S.planes_per_group, cz = pz - gz * S.planes_per_group;
+                const int64_t off = S.base + (int64_t)gz * S.group_stride + (int64_t)cz * S.plane_stride;
+                int rc = tc32_butterfly(d_src + off, S.width, S.height, S.pitch, qp, d_lvl + off, d_recon + off, s);
+                if (rc) return rc;
+            }
+            continue;
+        }
+        TreeArgs ta{};
+        ta.ppg = S.planes_per_group;
+        ta.group_stride = S.group_stride;
+        ta.plane_stride = S.plane_stride;
+        k_tc32_mfma<false><<<dim3((nblk + 3) / 4, planes), 256, 0, s>>>(
+            d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p, dequant_scale(rem), per, d_lvl + S.base,
+            d_recon + S.base, ta, nullptr);
+        NH_HIP(hipGetLastError());
+    }
     return NH_OK;
 }
 

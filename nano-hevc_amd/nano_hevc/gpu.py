@@ -10,6 +10,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
   tc32_plane          -- config 5: 32x32 chain, butterfly or int8-MFMA variant
+  tc32_planes         -- config 5 over a frame stream (one MFMA launch per plane set)
   widen_u8 / narrow_u8 -- frame I/O casts (YUV420p bytes <-> int16 planes)
   encode_intra_yuv420 -- encode_frame_intra (DC vs planar per block) over a frame stream
 """
@@ -286,6 +287,27 @@ def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=N
     rec = torch.zeros((h, w), dtype=torch.int16, device=src.device) if rec is None else rec
     check(_lib.load().nh_tc32_plane(src.data_ptr(), w, h, w, int(qp), lvl.data_ptr(), rec.data_ptr(), int(variant),
                                     C.c_void_p(_stream(stream))), "tc32_plane")
+    return lvl, rec
+
+
+def tc32_planes(src, sets, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=None):
+    """Config 5 over every plane of ``sets`` (e.g. yuv420_plane_sets of a frame
+    stream): one int8-MFMA launch per plane set (variant 1) or the butterfly
+    per plane (variant 0).  Returns (levels int32, recon int16), source layout."""
+    torch = _torch()
+    _need(src, torch.int16, "tc32_planes(src)")
+    sets_fit(sets, src.numel(), "tc32_planes")
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int32, device=src.device)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    _need(lvl, torch.int32, "tc32_planes(lvl)")
+    _need(rec, torch.int16, "tc32_planes(rec)")
+    if lvl.numel() < src.numel() or rec.numel() < src.numel():
+        raise ValueError("tc32_planes: lvl / rec smaller than src")
+    arr = (PlaneSet * len(sets))(*sets)
+    check(_lib.load().nh_tc32_planes(src.data_ptr(), arr, len(sets), int(qp), lvl.data_ptr(), rec.data_ptr(),
+                                     int(variant), C.c_void_p(_stream(stream))), "tc32_planes")
     return lvl, rec
 
 

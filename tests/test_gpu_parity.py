@@ -473,6 +473,37 @@ def test_tc32_mfma_equals_butterfly_and_oracle(nh, torch_dev, kind):
             assert np.array_equal(r.cpu().numpy(), er), (kind, qp, v)
 
 
+@pytest.mark.parametrize("variant", [1, 0])
+def test_tc32_planes_stream_equals_per_plane_and_oracle(nh, torch_dev, variant):
+    """Config 5 batched over a ragged YUV420 frame stream (one MFMA launch per
+    plane set) == the per-plane entry point == the oracle, every plane."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(55)
+    nf, w, h = 3, 208, 136                         # partial 32x32 blocks in every plane (pitches % 8 == 0)
+    sets = gpu.yuv420_plane_sets(nf, w, h)
+    fe = gpu.yuv420_frame_elems(w, h)
+    buf = rng.integers(0, 256, size=nf * fe).astype(np.int16)
+    buf[fe:2 * fe] = rng.integers(-32768, 32768, size=fe)   # frame 1: int16 extremes (3-part split)
+    d = torch.from_numpy(buf).cuda()
+    lvl = torch.full(d.shape, -7, dtype=torch.int32, device="cuda")   # untouched outside full blocks
+    rec = torch.full(d.shape, -7, dtype=torch.int16, device="cuda")
+    gpu.tc32_planes(d, sets, 30, variant, lvl=lvl, rec=rec)
+    lv, rv = lvl.cpu().numpy(), rec.cpu().numpy()
+    for f in range(nf):
+        off = f * fe
+        for (ph, pw) in ((h, w), (h // 2, w // 2), (h // 2, w // 2)):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er = O.tc32_plane(src, 30)
+            pl, pr = gpu.tc32_plane(torch.from_numpy(src.copy()).cuda(), 30, variant)
+            got_l, got_r = lv[off:off + ph * pw].reshape(ph, pw), rv[off:off + ph * pw].reshape(ph, pw)
+            fh, fw = ph // 32 * 32, pw // 32 * 32
+            assert np.array_equal(got_l[:fh, :fw], el[:fh, :fw]) and np.array_equal(got_r[:fh, :fw], er[:fh, :fw]), (f, ph)
+            assert np.array_equal(got_l[:fh, :fw], pl.cpu().numpy()[:fh, :fw]), (f, ph)
+            assert (got_l[fh:, :] == -7).all() and (got_l[:, fw:] == -7).all(), (f, ph)
+            off += ph * pw
+
+
 def test_tu_pipeline_int16_extremes(nh, torch_dev):
     """Config 4 on arbitrary int16 samples: the 24-bit mad bounds hold at every TU size."""
     torch = torch_dev

@@ -71,6 +71,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
+    ap.add_argument("--cfg5-frames", type=int, default=8, help="frames of the batched cfg5 stream")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
     ap.add_argument("--configs", default="3,4,4b,5,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
@@ -174,6 +175,23 @@ def main():
             line["psnr_y_oracle"] = float(10 * np.log10(255 ** 2 / mse))
             line["psnr_matches_oracle"] = line["psnr_y_oracle"] == res["mfma_i8"]["psnr_y"]
         print(json.dumps(line), flush=True)
+        # the same over a stream of frames: one MFMA launch per plane set (nh_tc32_planes)
+        nf = args.cfg5_frames
+        fe = gpu.yuv420_frame_elems(W, H)
+        stream5 = torch.empty(nf * fe, dtype=torch.int16, device="cuda")
+        for f in range(nf):
+            stream5[f * fe:(f + 1) * fe] = torch.cat([p.flatten() for p in planes])
+        sets5 = gpu.yuv420_plane_sets(nf, W, H)
+        lv5 = torch.zeros_like(stream5, dtype=torch.int32)
+        rc5 = torch.zeros_like(stream5)
+        ms = timed(lambda: gpu.tc32_planes(stream5, sets5, args.qp5, 1, lvl=lv5, rec=rc5), args.reps)
+        same = bool(torch.equal(rc5[:W * H].view(H, W), outs[0][1])) and bool(torch.equal(lv5[:W * H].view(H, W), outs[0][0]))
+        samples = nf * fe
+        print(json.dumps({"config": "cfg5 batched: 8K YUV420 frame stream, one int8-MFMA launch per plane set",
+                          "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
+                          "blocks_per_s": nf * nblk / ms * 1e3, "samples_per_s": samples / ms * 1e3,
+                          "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
+                          "frame0_equals_per_plane": same}), flush=True)
 
     if "enc" in cfgs or "io" in cfgs:
         W, H = 3840, 2160
