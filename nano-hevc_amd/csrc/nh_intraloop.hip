@@ -1437,6 +1437,9 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
         NH_TU(32, false);
     }
 #undef NH_TU
+    // (A/B: forking the four size launches onto side streams with events was
+    // slower -- 0.066 -> 0.068-0.071 ms per frame batched, 0.157 -> 0.275 one
+    // plane at a time: profiles/r01/cfg4/cfg4_streams_*.jsonl)
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
