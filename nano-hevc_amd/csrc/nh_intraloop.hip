@@ -51,6 +51,13 @@ __device__ __forceinline__ void rdo8_block_prep(RdoSlotLds& B, int k) {
     B.planar[k] = (uint32_t)p & 0xffffu;
     const int32_t o = B.orig[k];
     if (o < 0 || o > 255) atomicOr(&B.wide, 1);
+    // neighbours outside 8 bits: the residual may leave [-255, 255], so the
+    // packed 16-bit chain (rdo8_chain_n) is not exact -- wide = 2 selects the
+    // 32-bit chain (its SSE in 32 bits is still exact: orig is 8-bit)
+    if (k < 17) {
+        const int32_t t = B.topA[k], l = B.leftA[k];
+        if ((k < B.ntA && (t < 0 || t > 255)) || (k < B.nlA && (l < 0 || l > 255))) atomicOr(&B.wide, 2);
+    }
     if (k < 8) {
         int32_t sum = 0;
 #pragma unroll
@@ -144,8 +151,8 @@ __device__ __forceinline__ unsigned long long rdo8_recon_sse(uint32_t (&X)[8][8]
 // unwrapped (intra.py:204-206).  Planar and DC lanes read their block's
 // precomputed prediction through the same path (f = 0).  P = Q for vertical
 // modes and planar/DC, P = Q^T for horizontal modes (intra.py:153-156).
-__device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, uint32_t* refp,
-                                                         const ChainQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
+// Prediction of one mode into Rpk (int16 pairs along columns, row-major).
+__device__ __forceinline__ void rdo8_predict(const RdoSlotLds& L, int mode, uint32_t* refp, uint32_t (&Rpk)[32]) {
     const uint32_t* rowp[8];
     uint32_t wf[8], wd[8];
     bool vert = true;
@@ -195,17 +202,30 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
             const int t = dot2_16(rowp[s][b], wf[s]);
             Q[s][b] = __builtin_amdgcn_sbfe(t, 5u, wd[s]);
         }
-    uint32_t X[8][8];
-    const uint32_t* opk = (const uint32_t*)L.orig;
 #pragma unroll
     for (int y = 0; y < 8; ++y)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             const uint32_t pv = pack16(Q[y][2 * m], Q[y][2 * m + 1]);
             const uint32_t ph = pack16(Q[2 * m][y], Q[2 * m + 1][y]);
-            const uint32_t pp = vert ? pv : ph;
-            Rpk[y * 4 + m] = pp;                                   // prediction, until the recon replaces it
-            const uint32_t d = as_u32(as_v2s(opk[y * 4 + m]) - as_v2s(pp));   // residual_block: int16 wrap
+            Rpk[y * 4 + m] = vert ? pv : ph;                       // prediction, until the recon replaces it
+        }
+}
+
+__device__ __forceinline__ unsigned long long rdo8_chain_n(const RdoSlotLds& L, const ChainQ& q, uint32_t (&Rpk)[32],
+                                                           uint32_t (&Lpk)[32]);
+
+__device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, uint32_t* refp,
+                                                         const ChainQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
+    rdo8_predict(L, mode, refp, Rpk);
+    if (!L.wide) return rdo8_chain_n(L, q, Rpk, Lpk);   // 8-bit block and neighbours: packed 16-bit chain
+    uint32_t X[8][8];
+    const uint32_t* opk = (const uint32_t*)L.orig;
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const uint32_t d = as_u32(as_v2s(opk[y * 4 + m]) - as_v2s(Rpk[y * 4 + m]));   // residual_block: int16 wrap
             X[y][2 * m] = (uint32_t)(int32_t)(int16_t)(d & 0xffffu);
             X[y][2 * m + 1] = (uint32_t)((int32_t)d >> 16);
         }
@@ -242,7 +262,183 @@ __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, in
         for (int i = 0; i < 8; ++i) X[i][j] = (uint32_t)((int32_t)x[i] >> 8);
     }
     // inverse pass 2: rows, recon, SSE (two copies: 8-bit blocks sum d^2 in 32 bits)
-    return L.wide ? rdo8_recon_sse<true>(X, opk, Rpk) : rdo8_recon_sse<false>(X, opk, Rpk);
+    return (L.wide & 1) ? rdo8_recon_sse<true>(X, opk, Rpk) : rdo8_recon_sse<false>(X, opk, Rpk);
+}
+
+// ---------------------------------------------------------------------------
+// Packed 16-bit chain for 8-bit blocks (wide == 0: orig and every neighbour in
+// [0, 255], so prediction is in [0, 255] and the residual in [-255, 255]).
+// Two independent 8-point vectors a, b travel as int16 pairs (a_k, b_k): the
+// butterfly's add / sub stages are v_pk_add/sub_u16 on both at once, the
+// multiply stages v_dot2_i32_i16 over (k, k') pairs of one vector (int32
+// accumulate, the rounding constant as the accumulator), and ">> 8 then
+// int16" of two int32 results is one v_perm (bytes 1..2 of each).  Exact:
+// every packed operand is the true value in int16 range -- pass-1 E/O <= 510
+// and EE <= 1,020; pass-1 outputs >> 8 <= 510 (row sums of |DCT8| <= 512);
+// pass-2 EE <= 2,040; coefficients |C| <= 1,020; dequantized
+// values <= 720 at every QP (quant.py's shift includes log2 N, its dequant
+// does not: D3/D4); inverse pass-1 outputs >> 8 <= 1,347 (column sums of
+// |DCT8| = 479), pass-2 >> 8 <= 2,520 -- and the int32 sums are the
+// reference's, which never wrap at these sizes (bounds enumerated over QP
+// 0..51 in DESIGN.md §4.3).
+// The same mod-2^32 results as rdo8_chain's 32-bit path, element for element.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t pk_add16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_add_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_sub_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+// acc + a.lo * w.lo + a.hi * w.hi (signed int16 pairs, int32 accumulate)
+__device__ __forceinline__ int32_t dot2w(uint32_t a, uint32_t w, int32_t acc) {
+    int32_t r;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(w), "v"(acc));
+    return r;
+}
+__device__ __forceinline__ uint32_t lo_pair(uint32_t x, uint32_t y) { return __builtin_amdgcn_perm(y, x, 0x05040100u); }  // (x.lo, y.lo)
+__device__ __forceinline__ uint32_t hi_pair(uint32_t x, uint32_t y) { return __builtin_amdgcn_perm(y, x, 0x07060302u); }  // (x.hi, y.hi)
+__device__ __forceinline__ uint32_t shr8_pair(int32_t x, int32_t y) {                                                   // (x >> 8, y >> 8) as int16
+    return __builtin_amdgcn_perm((uint32_t)y, (uint32_t)x, 0x06050201u);
+}
+constexpr uint32_t wpair(int c0, int c1) { return (uint32_t)(uint16_t)(int16_t)c0 | ((uint32_t)(uint16_t)(int16_t)c1 << 16); }
+
+// forward 8-point DCT of the two vectors in P (pairs (a_k, b_k)): ya / yb = bias + DCT8 . a / b
+__device__ __forceinline__ void fwd8_pk2(const uint32_t (&P)[8], int32_t bias, int32_t (&ya)[8], int32_t (&yb)[8]) {
+    uint32_t E[4], O[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        E[k] = pk_add16(P[k], P[7 - k]);
+        O[k] = pk_sub16(P[k], P[7 - k]);
+    }
+    const uint32_t EE0 = pk_add16(E[0], E[3]), EE1 = pk_add16(E[1], E[2]);
+    const uint32_t EO0 = pk_sub16(E[0], E[3]), EO1 = pk_sub16(E[1], E[2]);
+    const uint32_t ee[2] = {lo_pair(EE0, EE1), hi_pair(EE0, EE1)};
+    const uint32_t eo[2] = {lo_pair(EO0, EO1), hi_pair(EO0, EO1)};
+    const uint32_t o01[2] = {lo_pair(O[0], O[1]), hi_pair(O[0], O[1])};
+    const uint32_t o23[2] = {lo_pair(O[2], O[3]), hi_pair(O[2], O[3])};
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        int32_t* y = v ? yb : ya;
+        y[0] = dot2w(ee[v], wpair(64, 64), bias);
+        y[4] = dot2w(ee[v], wpair(64, -64), bias);
+        y[2] = dot2w(eo[v], wpair(dctc<4>(1, 0), dctc<4>(1, 1)), bias);
+        y[6] = dot2w(eo[v], wpair(dctc<4>(3, 0), dctc<4>(3, 1)), bias);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int r = 2 * m + 1;
+            y[r] = dot2w(o23[v], wpair(dctc<8>(r, 2), dctc<8>(r, 3)),
+                         dot2w(o01[v], wpair(dctc<8>(r, 0), dctc<8>(r, 1)), bias));
+        }
+    }
+}
+
+// inverse 8-point DCT of the two vectors in P: xa / xb = bias + DCT8^T . a / b
+__device__ __forceinline__ void inv8_pk2(const uint32_t (&P)[8], int32_t bias, int32_t (&xa)[8], int32_t (&xb)[8]) {
+    const uint32_t y13[2] = {lo_pair(P[1], P[3]), hi_pair(P[1], P[3])};
+    const uint32_t y57[2] = {lo_pair(P[5], P[7]), hi_pair(P[5], P[7])};
+    const uint32_t y04[2] = {lo_pair(P[0], P[4]), hi_pair(P[0], P[4])};
+    const uint32_t y26[2] = {lo_pair(P[2], P[6]), hi_pair(P[2], P[6])};
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        int32_t* x = v ? xb : xa;
+        int32_t O[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n)
+            O[n] = dot2w(y57[v], wpair(dctc<8>(5, n), dctc<8>(7, n)), dot2w(y13[v], wpair(dctc<8>(1, n), dctc<8>(3, n)), 0));
+        const int32_t EO0 = dot2w(y26[v], wpair(dctc<4>(1, 0), dctc<4>(3, 0)), 0);
+        const int32_t EO1 = dot2w(y26[v], wpair(dctc<4>(1, 1), dctc<4>(3, 1)), 0);
+        const int32_t EE0 = dot2w(y04[v], wpair(64, 64), bias);
+        const int32_t EE1 = dot2w(y04[v], wpair(64, -64), bias);
+        const int32_t E[4] = {EE0 + EO0, EE1 + EO1, EE1 - EO1, EE0 - EO0};
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+            x[n] = E[n] + O[n];
+            x[7 - n] = E[n] - O[n];
+        }
+    }
+}
+
+// The chain after prediction (Rpk = prediction pairs along columns) for a
+// wide == 0 block; same outputs as rdo8_chain's 32-bit path.
+__device__ __forceinline__ unsigned long long rdo8_chain_n(const RdoSlotLds& L, const ChainQ& q, uint32_t (&Rpk)[32],
+                                                           uint32_t (&Lpk)[32]) {
+    const uint32_t* opk = (const uint32_t*)L.orig;
+    uint32_t D[8][4];   // residual, (column 2m, 2m+1) pairs per row: D[row][m]
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) D[y][m] = pk_sub16(opk[y * 4 + m], Rpk[y * 4 + m]);   // residual_block
+    uint32_t T[4][8];   // pass-1 output >> 8, (row 2i, 2i+1) pairs per column: T[i][col]
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {           // forward pass 1: columns 2m, 2m+1 (transform.py:179-185)
+        uint32_t P[8];
+        int32_t ya[8], yb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) P[k] = D[k][m];
+        fwd8_pk2(P, 128, ya, yb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            T[i][2 * m] = shr8_pair(ya[2 * i], ya[2 * i + 1]);
+            T[i][2 * m + 1] = shr8_pair(yb[2 * i], yb[2 * i + 1]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {           // forward pass 2: rows 2i, 2i+1, then quant / dequant
+        int32_t za[8], zb[8];
+        fwd8_pk2(T[i], 128, za, zb);
+        int32_t la[8], lb[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            la[j] = quant_s(za[j] >> 8, q.qs, q.h_v, q.hneg_v);
+            lb[j] = quant_s(zb[j] >> 8, q.qs, q.h_v, q.hneg_v);
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            Lpk[(2 * i) * 4 + m] = pack16(la[2 * m], la[2 * m + 1]);
+            Lpk[(2 * i + 1) * 4 + m] = pack16(lb[2 * m], lb[2 * m + 1]);
+            D[2 * i][m] = pack16(dequant_s(la[2 * m], q), dequant_s(la[2 * m + 1], q));          // (col 2m, 2m+1) pairs
+            D[2 * i + 1][m] = pack16(dequant_s(lb[2 * m], q), dequant_s(lb[2 * m + 1], q));
+        }
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {           // inverse pass 1: columns 2m, 2m+1 (transform.py:221-227)
+        uint32_t P[8];
+        int32_t xa[8], xb[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) P[k] = D[k][m];
+        inv8_pk2(P, 128, xa, xb);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            T[i][2 * m] = shr8_pair(xa[2 * i], xa[2 * i + 1]);
+            T[i][2 * m + 1] = shr8_pair(xb[2 * i], xb[2 * i + 1]);
+        }
+    }
+    const v2s zero = {0, 0}, maxv = {255, 255};
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {           // inverse pass 2: rows 2i, 2i+1 + recon + clip + SSE
+        int32_t ra[8], rb[8];
+        inv8_pk2(T[i], 128, ra, rb);
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+            const int y = 2 * i + half;
+            const int32_t* r = half ? rb : ra;
+#pragma unroll
+            for (int m = 0; m < 4; ++m) {
+                const v2s rr = as_v2s(shr8_pair(r[2 * m], r[2 * m + 1]));   // rres.astype(int16)
+                v2s rc = as_v2s(Rpk[y * 4 + m]) + rr;                        // reconstruct_block (int16)
+                rc = __builtin_elementwise_min(__builtin_elementwise_max(rc, zero), maxv);
+                Rpk[y * 4 + m] = as_u32(rc);
+                const v2s d = as_v2s(opk[y * 4 + m]) - rc;
+                acc = dot2_acc(as_u32(d), acc);
+            }
+        }
+    }
+    return (unsigned long long)acc;
 }
 
 // ---------------------------------------------------------------------------
@@ -435,7 +631,7 @@ __device__ __forceinline__ unsigned long long rdo8_chain_pair(const RdoSlotLds& 
     for (int i = 0; i < 4; ++i)             // the prediction pairs to the row layout too
 #pragma unroll
         for (int m = 0; m < 2; ++m) pair_swap(Pp[i][m], Pp[4 + i][m]);
-    return L.wide ? rdo8_pair_recon_sse<true>(X, Pp, opk, h, Rpk) : rdo8_pair_recon_sse<false>(X, Pp, opk, h, Rpk);
+    return (L.wide & 1) ? rdo8_pair_recon_sse<true>(X, Pp, opk, h, Rpk) : rdo8_pair_recon_sse<false>(X, Pp, opk, h, Rpk);
 }
 
 template <int WAVES, bool ONESHOT>
