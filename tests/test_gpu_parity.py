@@ -295,8 +295,11 @@ def test_intra_rdo_golden(nh, torch_dev, golden):
         assert int(sse.item()) == int(g[f"{k}_sse"]), k
 
 
-@pytest.mark.parametrize("h,w,kind", [(64, 96, "natural"), (48, 40, "noise"), (72, 64, "int16")])
+@pytest.mark.parametrize("h,w,kind", [(64, 96, "natural"), (48, 40, "noise"), (72, 64, "int16"), (56, 72, "mixed")])
 def test_intra_rdo_vs_oracle(nh, torch_dev, h, w, kind):
+    """noise: the packed 16-bit chain at its extremes (residuals +-255); int16:
+    the 32-bit chain; mixed: 8-bit blocks whose left / top neighbours are not
+    8-bit (wide = 2: the 32-bit chain with the 32-bit SSE)."""
     torch = torch_dev
     from nano_hevc import gpu
     rng = np.random.default_rng(h * w)
@@ -305,6 +308,10 @@ def test_intra_rdo_vs_oracle(nh, torch_dev, h, w, kind):
         src = np.clip(40 + 3 * xx - yy + rng.integers(-10, 11, size=xx.shape), 0, 255).astype(np.int16)
     elif kind == "noise":
         src = rng.integers(0, 256, size=(h, w)).astype(np.int16)
+    elif kind == "mixed":
+        src = rng.integers(0, 256, size=(h, w)).astype(np.int16)
+        src[:, 15::16] = rng.integers(256, 400, size=src[:, 15::16].shape)    # a right column every other block
+        src[23::24, :] = rng.integers(-300, 0, size=src[23::24, :].shape)     # a bottom row every third block row
     else:   # arbitrary int16 samples: exercises the int16 wraps of residual/recon (D8-like) and 24-bit bounds
         src = rng.integers(-32768, 32768, size=(h, w)).astype(np.int16)
     for qp in (0, 32, 51):
