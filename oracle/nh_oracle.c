@@ -473,7 +473,9 @@ int oh_tu_split(uint32_t seed, int plane_id, int x, int y, int size) {
     return (k & 3u) < 2u;
 }
 
-static void tu_one(const int16_t* src, int w, int h, int pitch, int x, int y, int N,
+/* nb: the plane the TU's neighbours are read from -- the source (open loop,
+ * D12) or the reconstruction built so far (closed loop). */
+static void tu_one(const int16_t* src, const int16_t* nb, int w, int h, int pitch, int x, int y, int N,
                    int qp, int is_luma, int32_t* lvl, int16_t* recon, uint8_t* tu_log2) {
     int16_t orig[1024], dc[1024], pl[1024], r16[1024];
     int32_t l[1024];
@@ -481,8 +483,8 @@ static void tu_one(const int16_t* src, int w, int h, int pitch, int x, int y, in
     int64_t top[32], left[32], nt, nl;
     for (int i = 0; i < N; ++i)
         for (int j = 0; j < N; ++j) orig[i * N + j] = src[(int64_t)(y + i) * pitch + x + j];
-    get_top(src, w, pitch, x, y, N, top, &nt);
-    get_left(src, h, pitch, x, y, N, left, &nl);
+    get_top(nb, w, pitch, x, y, N, top, &nt);
+    get_left(nb, h, pitch, x, y, N, left, &nl);
     /* __main__.py:165-178: DC vs planar by residual energy, DC wins ties */
     oh_intra_dc(top, nt, left, nl, N, 0, dc);
     oh_intra_planar(top, nt, left, nl, top[nt - 1], left[nl - 1], N, log2i(N), pl);
@@ -504,21 +506,21 @@ static void tu_one(const int16_t* src, int w, int h, int pitch, int x, int y, in
         for (int j = 0; j < N / 4; ++j) tu_log2[(int64_t)(y / 4 + i) * w4 + x / 4 + j] = (uint8_t)lg;
 }
 
-static void tu_tree(const int16_t* src, int w, int h, int pitch, int x, int y, int s,
+static void tu_tree(const int16_t* src, const int16_t* nb, int w, int h, int pitch, int x, int y, int s,
                     int plane_id, uint32_t seed, int qp, int is_luma,
                     int32_t* lvl, int16_t* recon, uint8_t* tu_log2) {
     if (x >= w || y >= h) return;
     int overhang = (x + s > w) || (y + s > h);
     if (s > 4 && (overhang || oh_tu_split(seed, plane_id, x, y, s))) {
-        int hs = s / 2;
-        tu_tree(src, w, h, pitch, x, y, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
-        tu_tree(src, w, h, pitch, x + hs, y, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
-        tu_tree(src, w, h, pitch, x, y + hs, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
-        tu_tree(src, w, h, pitch, x + hs, y + hs, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
+        int hs = s / 2;   /* z-order: top-left, top-right, bottom-left, bottom-right */
+        tu_tree(src, nb, w, h, pitch, x, y, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
+        tu_tree(src, nb, w, h, pitch, x + hs, y, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
+        tu_tree(src, nb, w, h, pitch, x, y + hs, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
+        tu_tree(src, nb, w, h, pitch, x + hs, y + hs, hs, plane_id, seed, qp, is_luma, lvl, recon, tu_log2);
         return;
     }
     if (overhang) return;
-    tu_one(src, w, h, pitch, x, y, s, qp, is_luma, lvl, recon, tu_log2);
+    tu_one(src, nb, w, h, pitch, x, y, s, qp, is_luma, lvl, recon, tu_log2);
 }
 
 void oh_tu_pipeline_plane(const int16_t* src, int w, int h, int pitch, int ctb,
@@ -528,7 +530,21 @@ void oh_tu_pipeline_plane(const int16_t* src, int w, int h, int pitch, int ctb,
     if (row1 > rows) row1 = rows;
     for (int cy = row0; cy < row1; ++cy)
         for (int cx = 0; cx * ctb < w; ++cx)
-            tu_tree(src, w, h, pitch, cx * ctb, cy * ctb, ctb, plane_id, seed, qp, is_luma,
+            tu_tree(src, src, w, h, pitch, cx * ctb, cy * ctb, ctb, plane_id, seed, qp, is_luma,
+                    lvl, recon, tu_log2);
+}
+
+/* cfg 4 in closed loop: CTUs in raster order, TUs in z-order,
+ * neighbours from the reconstruction built so far (zero-initialised,
+ * frame.py:41-43) with the BlockView rules (block.py:38-50). */
+void oh_tu_pipeline_plane_closed(const int16_t* src, int w, int h, int pitch, int ctb,
+                                 int plane_id, uint32_t seed, int qp, int is_luma,
+                                 int32_t* lvl, int16_t* recon, uint8_t* tu_log2) {
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) recon[(int64_t)y * pitch + x] = 0;
+    for (int cy = 0; cy * ctb < h; ++cy)
+        for (int cx = 0; cx * ctb < w; ++cx)
+            tu_tree(src, recon, w, h, pitch, cx * ctb, cy * ctb, ctb, plane_id, seed, qp, is_luma,
                     lvl, recon, tu_log2);
 }
 
@@ -538,7 +554,7 @@ void oh_tc32_plane(const int16_t* src, int w, int h, int pitch, int qp, int32_t*
     int w4 = w / 4;
     uint8_t* tmap = (uint8_t*)calloc((size_t)(h / 4 + 1) * (w4 + 1), 1);
     for (int by = 0; by + 32 <= h; by += 32)
-        for (int bx = 0; bx + 32 <= w; bx += 32) tu_one(src, w, h, pitch, bx, by, 32, qp, 1, lvl, recon, tmap);
+        for (int bx = 0; bx + 32 <= w; bx += 32) tu_one(src, src, w, h, pitch, bx, by, 32, qp, 1, lvl, recon, tmap);
     free(tmap);
 }
 

@@ -51,6 +51,7 @@ def lib():
             "oh_intra_rdo_plane": [P, i32, i32, i32, i32, P, P, P, P],
             "oh_intra_rdo_plane_closed": [P, i32, i32, i32, i32, P, P, P, P],
             "oh_tu_pipeline_plane": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P],
+            "oh_tu_pipeline_plane_closed": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, P, P, P],
             "oh_tu_split": [C.c_uint32, i32, i32, i32, i32],
             "oh_tc32_plane": [P, i32, i32, i32, i32, P, P],
             "oh_encode_intra_plane": [P, i32, i32, i32, i32, P, P],
@@ -59,7 +60,8 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = None if name in ("oh_residual", "oh_reconstruct", "oh_clip", "oh_fwd8x8_quant_plane",
-                                         "oh_intra_rdo_plane", "oh_intra_rdo_plane_closed", "oh_tu_pipeline_plane", "oh_tc32_plane",
+                                         "oh_intra_rdo_plane", "oh_intra_rdo_plane_closed", "oh_tu_pipeline_plane",
+                                         "oh_tu_pipeline_plane_closed", "oh_tc32_plane",
                                          "oh_encode_intra_plane") else C.c_int
         _lib = L
     return _lib
@@ -207,6 +209,18 @@ def tu_pipeline_plane(src, ctb, plane_id, seed, qp, is_luma, row0=0, row1=1 << 3
     tul = np.zeros((h // 4, w // 4), np.uint8)
     lib().oh_tu_pipeline_plane(_p(src), w, h, w, ctb, plane_id, seed, qp, int(is_luma), row0, row1,
                                _p(lvl), _p(rec), _p(tul))
+    return lvl, rec, tul
+
+
+def tu_pipeline_plane_closed(src, ctb, plane_id, seed, qp, is_luma):
+    """Config 4 in closed loop: (lvl int32, recon int16, tu log2 uint8)."""
+    src = np.ascontiguousarray(src, np.int16)
+    h, w = src.shape
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    tul = np.zeros((h // 4, w // 4), np.uint8)
+    lib().oh_tu_pipeline_plane_closed(_p(src), w, h, w, ctb, plane_id, seed, qp, int(is_luma),
+                                      _p(lvl), _p(rec), _p(tul))
     return lvl, rec, tul
 
 

@@ -487,6 +487,73 @@ def gen_closed(I, T, Q):
     return out
 
 
+def ref_plane_cfg4_closed(I, T, Q, src, ctb, plane_id, seed, qp, is_luma):
+    """Closed-loop config 4, composed from the reference's own
+    pieces: CTUs in raster order, TUs in quadtree z-order, every TU's top / left
+    neighbours (N samples each) fetched with BlockView (block.py:38-50) from the
+    reconstruction Plane built so far (Plane.zeros, frame.py:41-43), then the
+    open-loop TU's DC-vs-planar choice and chain, recon written back with
+    BlockView.write_pixels."""
+    from nano_hevc.block import BlockView
+    from nano_hevc.frame import Plane
+    h, w = src.shape
+    recon = Plane.zeros(h, w, np.int16)
+    lvl = np.zeros(src.shape, np.int32)
+    tul = np.zeros((h // 4, w // 4), np.uint8)
+
+    def one(x, y, n):
+        blk = BlockView(recon, x, y, n)
+        orig = src[y:y + n, x:x + n]
+        top, left = blk.get_top_neighbors(), blk.get_left_neighbors()
+        dc = I.intra_dc_predict(top, left, n)
+        pl = I.intra_planar_predict(top, left, int(top[-1]), int(left[-1]), n)
+        edc = int(np.sum(I.residual_block(orig, dc).astype(np.int64) ** 2))
+        epl = int(np.sum(I.residual_block(orig, pl).astype(np.int64) ** 2))
+        pred = dc if edc <= epl else pl
+        l, r, _ = _chain(I, T, Q, orig, pred, qp, bool(is_luma and n == 4))
+        lvl[y:y + n, x:x + n] = l
+        blk.write_pixels(r)
+        tul[y // 4:(y + n) // 4, x // 4:(x + n) // 4] = int(np.log2(n))
+
+    def tree(x, y, s):
+        if x >= w or y >= h:
+            return
+        over = (x + s > w) or (y + s > h)
+        if s > 4 and (over or tu_split(seed, plane_id, x, y, s)):
+            hs = s // 2
+            for dy in (0, hs):
+                for dx in (0, hs):
+                    tree(x + dx, y + dy, hs)
+            return
+        if not over:
+            one(x, y, s)
+
+    for cy in range((h + ctb - 1) // ctb):
+        for cx in range((w + ctb - 1) // ctb):
+            tree(cx * ctb, cy * ctb, ctb)
+    return lvl, recon.data, tul
+
+
+def gen_closed4(I, T, Q):
+    """Closed-loop config 4 planes (own rng): luma (CTB 32) with partial CTUs,
+    chroma (CTB 16), 8-bit noise, a ragged plane (w, h not multiples of 4 x CTB)."""
+    rng = np.random.default_rng(4040)
+    out = {}
+    yy, xx = np.mgrid[0:80, 0:104]
+    cases = {
+        "k4y": (np.clip(100 + xx - yy + rng.integers(-20, 21, size=xx.shape), 0, 255).astype(np.int16), 32, 0, True, 32),
+        "k4u": (rng.integers(90, 170, size=(40, 52)).astype(np.int16), 16, 1, False, 32),
+        "k4n": (rng.integers(0, 256, size=(64, 96)).astype(np.int16), 32, 0, True, 22),
+        "k4r": (np.clip(80 + 2 * xx[:45, :70] + rng.integers(-9, 10, size=(45, 70)), 0, 255).astype(np.int16), 32, 0, True, 37),
+    }
+    for key, (src, ctb, pid, luma, qp) in cases.items():
+        l, r, t = ref_plane_cfg4_closed(I, T, Q, src, ctb, pid, 1234, qp, luma)
+        out.update({f"{key}_src": src, f"{key}_ctb": np.int64(ctb), f"{key}_pid": np.int64(pid),
+                    f"{key}_luma": np.int64(luma), f"{key}_qp": np.int64(qp), f"{key}_lvl": l, f"{key}_rec": r,
+                    f"{key}_tu": t})
+    return out
+
+
 def plane_hash_1080p(T, Q):
     rng = np.random.default_rng(20260)
     plane = rng.integers(-255, 256, size=(1080, 1920)).astype(np.int16)
@@ -495,10 +562,23 @@ def plane_hash_1080p(T, Q):
 
 
 def main():
-    ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
+    pos = [a for i, a in enumerate(sys.argv[1:], 1) if not a.startswith("--") and sys.argv[i - 1] != "--only"]
+    ref = pos[0] if pos else "/root/reference"
     warnings.simplefilter("ignore")
     I, T, Q, M = _import_reference(ref)
     rng = np.random.default_rng(1234)
+    if "--only" in sys.argv:   # regenerate one file (own rng), keep the others and their manifest entries
+        name = sys.argv[sys.argv.index("--only") + 1]
+        gen = {"closed4.npz": lambda: gen_closed4(I, T, Q), "closed.npz": lambda: gen_closed(I, T, Q)}[name]
+        p = os.path.join(HERE, name)
+        np.savez_compressed(p, **gen())
+        mp = os.path.join(HERE, "manifest.json")
+        manifest = json.load(open(mp))
+        manifest["files"][name] = hashlib.sha256(open(p, "rb").read()).hexdigest()
+        with open(mp, "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+        print(name, manifest["files"][name])
+        return
     files = {
         "matrices.npz": gen_matrices(T),
         "transform.npz": gen_transform(T, rng),
@@ -510,6 +590,7 @@ def main():
         "cfg5.npz": gen_cfg5(I, T, Q, M),
         "encode.npz": gen_encode(ref),
         "closed.npz": gen_closed(I, T, Q),
+        "closed4.npz": gen_closed4(I, T, Q),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

@@ -256,3 +256,16 @@ def test_oracle_at_full_size_equals_reference():
         assert (sha(l), sha(r), sha(t)) == tuple(ref[f"cfg4_p{k}"][x] for x in ("lvl", "rec", "tu")), k
     l, r = O.tc32_plane(FI.cfg5_plane(), FI.CFG5_QP)
     assert (sha(l), sha(r)) == (ref["cfg5_y"]["lvl"], ref["cfg5_y"]["rec"])
+
+
+def test_oracle_tu_pipeline_closed_golden(golden):
+    """Closed-loop config 4: the oracle equals planes composed
+    from the reference's own BlockView / Plane / predictors / chain
+    (make_golden.gen_closed4); the open-loop pipeline differs on every case."""
+    g = golden("closed4.npz")
+    for k in ("k4y", "k4u", "k4n", "k4r"):
+        args = (g[k + "_src"], int(g[k + "_ctb"]), int(g[k + "_pid"]), 1234, int(g[k + "_qp"]), bool(g[k + "_luma"]))
+        lvl, rec, tu = O.tu_pipeline_plane_closed(*args)
+        assert np.array_equal(lvl, g[k + "_lvl"]) and np.array_equal(rec, g[k + "_rec"]), k
+        assert np.array_equal(tu, g[k + "_tu"]), k
+        assert not np.array_equal(O.tu_pipeline_plane(*args)[1], rec), k
