@@ -189,6 +189,20 @@ int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* set, int ctb
                           uint32_t seed, int qp, int is_luma, int row0, int row1, int32_t* d_lvl,
                           int16_t* d_recon, uint8_t* d_tu, void* stream);
 
+/* Config 4 in CLOSED loop over every plane of one plane set:
+ * CTUs in raster order, TUs in quadtree z-order, every TU's top / left
+ * neighbours from the reconstruction built so far (BlockView rules on a
+ * zero-initialised recon).  Device wavefront over CTU rows; d_work: device
+ * memory of nh_tu_pipeline_closed_workspace_bytes() bytes, 8-B aligned
+ * (zeroed by the call); a wait that cannot complete sets the status word
+ * (read it with nh_intra_rdo_closed_status).  Width and height multiples of 4;
+ * recon / levels of samples outside every TU are left untouched (callers pass
+ * zeroed outputs, as Frame.zeros). */
+int64_t nh_tu_pipeline_closed_workspace_bytes(const nh_plane_set* set, int ctb);
+int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
+                                 uint32_t seed, int qp, int is_luma, int32_t* d_lvl, int16_t* d_recon,
+                                 uint8_t* d_tu, void* d_work, void* stream);
+
 /* Config 5: every full 32x32 block of an int16 source plane through the
  * config-4 chain at N=32.  variant 0 = butterfly
  * (k_tu_process<32>), 1 = int8 matrix cores (v_mfma_i32_32x32x32_i8 with

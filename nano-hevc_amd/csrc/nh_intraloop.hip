@@ -1507,6 +1507,248 @@ static QuantParams qparams(int qp, int log2n, bool intra) {
 }
 
 
+// ===========================================================================
+// Config 4 in closed loop: CTUs in raster order, TUs in
+// quadtree z-order, each TU's top / left neighbours (N samples, BlockView
+// rules) from the reconstruction built so far.  A TU only reads the row above
+// and the column to its left, so CTU (cx, cy) depends on (cx-1, cy) and
+// (cx, cy-1) only.  One wave per CTU row (tickets row-major across planes, so
+// a wave only waits on a CTU row claimed before it); the CTU being coded lives
+// in LDS with its top row and left column (rc[1 + y][1 + x]), so every
+// neighbour read is an LDS read.  The only cross-wave data is each CTU's
+// bottom row, published as tagged 64-bit line words (tag = CTU row + 1, as the
+// config-3 closed loop) that the next CTU row polls before the CTU.  TUs are
+// found by walking the CTU's 4x4 units in Morton order: a unit is a TU origin
+// iff tu_leaf says its leaf starts there (Morton order of leaf origins is the
+// quadtree's z-order).  A TU runs on lanes 0..N-1 (column t, then row t) with
+// the chain of k_tu_process: same arithmetic, same results.
+// ===========================================================================
+struct Closed4Args {
+    const int16_t* src;
+    int32_t* lvl;
+    int16_t* rec;
+    uint8_t* tu;
+    int32_t* work;          // [0] ticket, [1] status; 64-bit line words from int32 word lines0
+    int64_t lines0;
+    int64_t group_stride, plane_stride, tu_plane;
+    int32_t w, h, pitch, ctb, plane_id, ppg, nplanes, crows, ccols, lw, is_luma;
+    uint32_t seed;
+    QuantParams q[4];       // log2 N = 2..5
+    int32_t dqs, dq_per;
+};
+
+template <int N, bool DST>
+__device__ __forceinline__ void tu_closed_one(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
+                                              uint8_t* tu, int x, int y, int lx, int ly, int16_t (*rc)[33],
+                                              int32_t (*tile)[33], const ChainQ& cq) {
+    constexpr int S = Log2<N>::v + 5;
+    const int t = threadIdx.x;
+    const bool on = t < N;
+    int32_t o[N];
+    int32_t topt = 0, leftt = 0;
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) o[i] = src[(int64_t)(y + i) * a.pitch + x + t];
+        topt = rc[ly][lx + 1 + t];       // sample (y - 1, x + t)
+        leftt = rc[ly + 1 + t][lx];      // sample (y + t, x - 1)
+    }
+    // DC (intra.py:46-62): sums over the wave's first N lanes
+    int32_t sum = topt + leftt;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    const int32_t dc = (sum + N) >> (Log2<N>::v + 1);
+    const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168-169)
+    auto planar = [&](int yy, int xx) -> int32_t {
+        return ((N - 1 - xx) * (int32_t)rc[ly + 1 + yy][lx] + (xx + 1) * tr + (N - 1 - yy) * (int32_t)rc[ly][lx + 1 + xx] +
+                (yy + 1) * bl + N) >> (Log2<N>::v + 1);
+    };
+    long long ed = 0, ep = 0;
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            const int32_t d1 = wrap16(o[i] - dc), d2 = wrap16(o[i] - planar(i, t));
+            ed += (long long)d1 * d1;
+            ep += (long long)d2 * d2;
+        }
+    }
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        ed += __shfl_xor(ed, m, 64);
+        ep += __shfl_xor(ep, m, 64);
+    }
+    const bool use_dc = ed <= ep;                        // __main__.py:173: DC wins ties
+    auto pred_at = [&](int yy, int xx) -> int32_t { return use_dc ? dc : planar(yy, xx); };
+    uint32_t v[N], r[N];
+    if (on) {                                            // forward pass 1: column t
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)wrap16(o[k] - pred_at(k, t));
+        fwd1d<N, DST, Mul24>(v, r);
+#pragma unroll
+        for (int i = 0; i < N; ++i) tile[i][t] = rshift_round<S>(r[i]);
+    }
+    __syncthreads();
+    if (on) {                                            // forward pass 2: row t, quant, dequant
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[t][k];
+        fwd1d<N, DST, Mul24>(v, r);
+        int32_t* lrow = lvl + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int32_t l = quant_s(rshift_round<S>(r[j]), cq.qs, cq.h_v, cq.hneg_v);
+            lrow[j] = l;
+            v[j] = (uint32_t)dequant_s(l, cq);
+        }
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+        for (int j = 0; j < N; ++j) tile[t][j] = (int32_t)v[j];
+    }
+    __syncthreads();
+    if (on) {                                            // inverse pass 1: column t
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[k][t];
+        inv1d<N, DST, Mul24>(v, r);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tile[i][t] = rshift_round<S>(r[i]);
+    }
+    __syncthreads();
+    if (on) {                                            // inverse pass 2: row t, reconstruct, clip
+#pragma unroll
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[t][k];
+        inv1d<N, DST, Mul24>(v, r);
+        int16_t* rrow = rec + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int j = 0; j < N; ++j) {
+            const int32_t rr = wrap16(rshift_round<S>(r[j]));
+            int32_t rcv = wrap16(pred_at(t, j) + rr);
+            rcv = rcv < 0 ? 0 : (rcv > 255 ? 255 : rcv);
+            rrow[j] = (int16_t)rcv;
+            rc[ly + 1 + t][lx + 1 + j] = (int16_t)rcv;   // planar / neighbours read rc before this barrier
+        }
+        if (t < N / 4) {
+            const int w4 = a.w / 4;
+            for (int j = 0; j < N / 4; ++j) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + j] = (uint8_t)Log2<N>::v;
+        }
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(64) k_tu_closed(Closed4Args a) {
+    __shared__ int16_t rc[33][33];
+    __shared__ int32_t tile[32][33];
+    __shared__ int row_s, stall_s;
+    const int lane = threadIdx.x;
+    const int ctb = a.ctb;
+    ChainQ cq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
+    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
+    const int total = a.crows * a.nplanes;
+    for (;;) {
+        if (lane == 0) {
+            row_s = atomicAdd(&a.work[0], 1);
+            stall_s = 0;
+        }
+        __syncthreads();
+        const int tk = row_s;
+        if (tk >= total) break;
+        const int cy = tk / a.nplanes, pl = tk - cy * a.nplanes;   // row-major across planes
+        const int g = pl / a.ppg, c = pl - g * a.ppg;
+        const int64_t off = (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
+        const int16_t* src = a.src + off;
+        int32_t* lvl = a.lvl + off;
+        int16_t* rec = a.rec + off;
+        uint8_t* tu = a.tu + (int64_t)pl * a.tu_plane;
+        uint64_t* line = lines + (int64_t)pl * a.lw;
+        const int pid = a.plane_id + c, y0c = cy * ctb;
+        for (int i = lane; i < 33 * 33; i += 64) (&rc[0][0])[i] = 0;   // recon starts as zeros (Frame.zeros)
+        __syncthreads();
+        for (int i = lane; i < ctb; i += 64) rc[1 + i][0] = 128;        // x == 0: left = 128 (block.py:45-50)
+        for (int cx = 0; cx < a.ccols; ++cx) {
+            const int x0c = cx * ctb;
+            // top row of this CTU: 128 at y == 0, else the CTU above's bottom row (tagged line words)
+            if (cy == 0) {
+                for (int i = lane; i < ctb; i += 64) rc[0][1 + i] = 128;
+            } else {
+                const int nw = (min(ctb, a.w - x0c) + 1) / 2;
+                const bool need = lane < nw;
+                uint32_t val = 0;
+                int spins = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (need) {
+                        const uint64_t v = ld_sys64(line + x0c / 2 + lane);
+                        ok = (int)(v >> 32) == cy;
+                        val = (uint32_t)v;
+                    }
+                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
+                        if (lane == 0) atomicMax(&a.work[1], 1);
+                        stall_s = 1;
+                        break;
+                    }
+                }
+                if (need) {
+                    rc[0][1 + 2 * lane] = (int16_t)(val & 0xffffu);
+                    if (2 * lane + 1 < ctb) rc[0][2 + 2 * lane] = (int16_t)(val >> 16);
+                }
+            }
+            __syncthreads();
+            if (stall_s) break;
+            // the CTU's TUs in z-order (Morton order of its 4x4 units)
+            const int units = (ctb / 4) * (ctb / 4);
+            for (int u = 0; u < units; ++u) {
+                int ux = 0, uy = 0;
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    ux |= ((u >> (2 * b)) & 1) << b;
+                    uy |= ((u >> (2 * b + 1)) & 1) << b;
+                }
+                const int x = x0c + 4 * ux, y = y0c + 4 * uy;
+                if (x >= a.w || y >= a.h) continue;
+                const int n = tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y);
+                if ((x & (n - 1)) || (y & (n - 1)) || x + n > a.w || y + n > a.h) continue;
+                const int lx = x - x0c, ly = y - y0c;
+                if (n == 4) {
+                    if (a.is_luma) tu_closed_one<4, true>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[0]);
+                    else tu_closed_one<4, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[0]);
+                } else if (n == 8) {
+                    tu_closed_one<8, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[1]);
+                } else if (n == 16) {
+                    tu_closed_one<16, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[2]);
+                } else {
+                    tu_closed_one<32, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[3]);
+                }
+            }
+            // publish the bottom row (the next CTU row polls it), then slide: right column -> left column
+            if (cy + 1 < a.crows) {
+                const int nw = (min(ctb, a.w - x0c) + 1) / 2;
+                if (lane < nw) {
+                    const uint32_t lo = (uint16_t)rc[ctb][1 + 2 * lane];
+                    const uint32_t hi = 2 * lane + 1 < ctb ? (uint16_t)rc[ctb][2 + 2 * lane] : 0u;
+                    st_sys64(line + x0c / 2 + lane, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
+                }
+            }
+            __syncthreads();
+            int16_t keep = 0;
+            if (lane < ctb) keep = rc[1 + lane][ctb];
+            __syncthreads();
+            for (int i = lane; i < 33 * 33; i += 64) (&rc[0][0])[i] = 0;
+            __syncthreads();
+            if (lane < ctb) rc[1 + lane][0] = keep;
+            __syncthreads();
+        }
+        __syncthreads();
+        if (stall_s) break;
+    }
+}
+
 int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
                    hipStream_t s) {
     const int bw = w / 32, n = bw * (h / 32);
@@ -1636,6 +1878,74 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
     // (A/B: forking the four size launches onto side streams with events was
     // slower -- 0.066 -> 0.068-0.071 ms per frame batched, 0.157 -> 0.275 one
     // plane at a time: profiles/r01/cfg4/cfg4_streams_*.jsonl)
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+static int closed4_layout(const nh_plane_set* set, int ctb, int64_t& lines0, int64_t& lw, int64_t& nplanes) {
+    if (!set || (ctb != 4 && ctb != 8 && ctb != 16 && ctb != 32)) return NH_EARG;
+    if (set->width < 4 || set->height < 0 || set->pitch < set->width || set->planes_per_group < 1 ||
+        set->num_groups < 0 || set->width > 65535 || set->height > 65535 || (set->width & 3) || (set->height & 3))
+        return NH_EARG;
+    nplanes = (int64_t)set->planes_per_group * set->num_groups;
+    if (nplanes > 65535) return NH_EARG;
+    lines0 = 2;   // ticket, status; then 64-bit words (8-B aligned)
+    lw = (set->width + 1) / 2;
+    return NH_OK;
+}
+
+extern "C" int64_t nh_tu_pipeline_closed_workspace_bytes(const nh_plane_set* set, int ctb) {
+    int64_t lines0, lw, np;
+    if (closed4_layout(set, ctb, lines0, lw, np)) return -1;
+    return 4 * lines0 + 8 * lw * np;
+}
+
+extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
+                                            uint32_t seed, int qp, int is_luma, int32_t* d_lvl, int16_t* d_recon,
+                                            uint8_t* d_tu, void* d_work, void* stream) {
+    if (!d_src || !d_lvl || !d_recon || !d_tu || !d_work) return NH_EARG;
+    int64_t lines0, lw, np;
+    if (closed4_layout(set, ctb, lines0, lw, np)) {
+        set_error("nh_tu_pipeline_planes_closed: bad plane set (w, h multiples of 4) or CTB size");
+        return NH_EARG;
+    }
+    if ((uintptr_t)d_work & 7) {
+        set_error("nh_tu_pipeline_planes_closed: workspace must be 8-byte aligned");
+        return NH_EARG;
+    }
+    hipStream_t s = as_stream(stream);
+    NH_HIP(hipMemsetAsync(d_work, 0, 4 * lines0 + 8 * lw * np, s));
+    if (!np || !set->height) return NH_OK;
+    Closed4Args a{};
+    a.src = d_src + set->base;
+    a.lvl = d_lvl + set->base;
+    a.rec = d_recon + set->base;
+    a.tu = d_tu;
+    a.work = (int32_t*)d_work;
+    a.lines0 = lines0;
+    a.group_stride = set->group_stride;
+    a.plane_stride = set->plane_stride;
+    a.tu_plane = (int64_t)(set->height / 4) * (set->width / 4);
+    a.w = set->width;
+    a.h = set->height;
+    a.pitch = set->pitch;
+    a.ctb = ctb;
+    a.plane_id = plane_id;
+    a.ppg = set->planes_per_group;
+    a.nplanes = (int32_t)np;
+    a.crows = (set->height + ctb - 1) / ctb;
+    a.ccols = (set->width + ctb - 1) / ctb;
+    a.lw = (int32_t)lw;
+    a.is_luma = is_luma ? 1 : 0;
+    a.seed = seed;
+    for (int k = 0; k < 4; ++k) a.q[k] = qparams(qp, k + 2, true);
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    a.dqs = dequant_scale(rem);
+    a.dq_per = per;
+    const int64_t rows = (int64_t)a.crows * np;
+    const unsigned waves = (unsigned)(rows < 2048 ? rows : 2048);
+    k_tu_closed<<<waves, 64, 0, s>>>(a);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

@@ -11,6 +11,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
   tc32_plane          -- config 5: 32x32 chain, butterfly or int8-MFMA variant
   tc32_planes         -- config 5 over a frame stream (one MFMA launch per plane set)
+  tu_pipeline_closed  -- config 4 in closed loop (CTU-row wavefront, TUs in z-order)
   widen_u8 / narrow_u8 -- frame I/O casts (YUV420p bytes <-> int16 planes)
   encode_intra_yuv420 -- encode_frame_intra (DC vs planar per block) over a frame stream
 """
@@ -273,6 +274,43 @@ def tu_pipeline_planes(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
     check(_lib.load().nh_tu_pipeline_planes(src.data_ptr(), C.byref(pset), int(ctb), int(plane_id), int(seed) & 0xffffffff,
                                             int(qp), int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)),
                                             lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(), C.c_void_p(_stream(stream))))
+    return lvl, rec, tu
+
+
+def tu_pipeline_closed(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
+                       lvl=None, rec=None, tu=None, stream=None):
+    """Config 4 in CLOSED loop over every plane of one plane
+    set: TUs in z-order with neighbours from the reconstruction, a device
+    wavefront over CTU rows.  Returns (lvl int32, recon int16 -- source
+    layout, zeros outside every TU --, tu uint8 (planes, h/4, w/4))."""
+    torch = _torch()
+    _need(src, torch.int16, "tu_pipeline_closed(src)")
+    sets_fit([pset], src.numel(), "tu_pipeline_closed")
+    planes = pset.planes_per_group * pset.num_groups
+    L = _lib.load()
+    wb = int(L.nh_tu_pipeline_closed_workspace_bytes(C.byref(pset), int(ctb)))
+    if wb < 0:
+        raise ValueError("tu_pipeline_closed: bad plane set (w, h multiples of 4) or CTB size")
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int32, device=src.device)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    if tu is None:
+        tu = torch.zeros((planes, pset.height // 4, pset.width // 4), dtype=torch.uint8, device=src.device)
+    _need(lvl, torch.int32, "tu_pipeline_closed(lvl)")
+    _need(rec, torch.int16, "tu_pipeline_closed(rec)")
+    _need(tu, torch.uint8, "tu_pipeline_closed(tu)")
+    if lvl.numel() < src.numel() or rec.numel() < src.numel() or tu.numel() < planes * (pset.height // 4) * (pset.width // 4):
+        raise ValueError("tu_pipeline_closed: output too small")
+    work = torch.empty((wb + 7) // 8, dtype=torch.int64, device=src.device)
+    st = C.c_void_p(_stream(stream))
+    check(L.nh_tu_pipeline_planes_closed(src.data_ptr(), C.byref(pset), int(ctb), int(plane_id), int(seed) & 0xffffffff,
+                                         int(qp), int(bool(is_luma)), lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(),
+                                         work.data_ptr(), st), "tu_pipeline_closed")
+    status = C.c_int(0)
+    check(L.nh_intra_rdo_closed_status(work.data_ptr(), C.byref(status), st))
+    if status.value:
+        raise RuntimeError("tu_pipeline_closed: the device wavefront stalled (status %d)" % status.value)
     return lvl, rec, tu
 
 

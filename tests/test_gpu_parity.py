@@ -719,3 +719,63 @@ def test_fused8x8_stripe_form_needs_contiguous_rows(nh, torch_dev):
     d = torch.zeros(64 * 72, dtype=torch.int16, device="cuda")
     with pytest.raises(ValueError, match="stripe form"):
         gpu.fwd8x8_quant(d, [gpu.plane_set(0, 60, 64, 72)], 32, True, variant=33)
+
+
+@pytest.mark.parametrize("key", ["k4y", "k4u", "k4n", "k4r"])
+def test_tu_pipeline_closed_golden(nh, torch_dev, golden, key):
+    """Closed-loop config 4 vs planes composed from the reference's own
+    BlockView / Plane / predictors / chain (make_golden.gen_closed4)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    g = golden("closed4.npz")
+    src = g[key + "_src"]
+    h, w = src.shape
+    hh, ww = h // 4 * 4, w // 4 * 4          # the device path takes w, h multiples of 4
+    d = torch.from_numpy(np.ascontiguousarray(src[:hh, :ww]).reshape(-1)).cuda()
+    lvl, rec, tu = gpu.tu_pipeline_closed(d, gpu.plane_set(0, ww, hh, ww), int(g[key + "_ctb"]), int(g[key + "_pid"]),
+                                          1234, int(g[key + "_qp"]), bool(g[key + "_luma"]))
+    lvl, rec = lvl.cpu().numpy().reshape(hh, ww), rec.cpu().numpy().reshape(hh, ww)
+    if (hh, ww) == (h, w):
+        assert np.array_equal(lvl, g[key + "_lvl"]) and np.array_equal(rec, g[key + "_rec"])
+        assert np.array_equal(tu.cpu().numpy()[0], g[key + "_tu"])
+    else:   # ragged plane: the oracle on the multiple-of-4 crop (the fixture pins the oracle itself)
+        el, er, et = O.tu_pipeline_plane_closed(np.ascontiguousarray(src[:hh, :ww]), int(g[key + "_ctb"]),
+                                                int(g[key + "_pid"]), 1234, int(g[key + "_qp"]), bool(g[key + "_luma"]))
+        assert np.array_equal(lvl, el) and np.array_equal(rec, er) and np.array_equal(tu.cpu().numpy()[0], et)
+
+
+@pytest.mark.parametrize("F,W,H,qp", [(3, 104, 72, 32), (2, 136, 104, 12)])
+def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp):
+    """A YUV420 frame stream in two launches (luma CTB 32, chroma CTB 16, plane
+    ids 0 / 1, 2): many CTU wavefronts at once, partial CTUs, 8-bit content and
+    an int16-extreme frame; every plane equals the sequential oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(F * 100 + qp)
+    fe = gpu.yuv420_frame_elems(W, H)
+    buf = np.empty(F * fe, np.int16)
+    off = 0
+    for f in range(F):
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            p = np.clip(60 + (3 * xx + 2 * yy + 7 * f) % 150 + rng.integers(-12, 13, (ph, pw)), 0, 255)
+            if f == 1:
+                p = rng.integers(-32768, 32768, (ph, pw))
+            buf[off:off + ph * pw] = p.reshape(-1)
+            off += ph * pw
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(F, W, H)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, 777, qp, True, lvl=lvl, rec=rec)
+    _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, 777, qp, False, lvl=lvl, rec=rec)
+    lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    off = 0
+    for f in range(F):
+        for k, (pw, ph) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er, et = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, 777, qp, k == 0)
+            assert np.array_equal(lv[off:off + ph * pw].reshape(ph, pw), el), (f, k)
+            assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
+            assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
+            off += ph * pw

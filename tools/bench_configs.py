@@ -11,6 +11,8 @@
         HBM roofline at 3 B/sample (1 B source read + 2 B recon write).
   4b    config 4 batched: 16 4K YUV420 frames in one launch per TU size and plane set.
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
+  closed4 config 4 in CLOSED loop over a 4K YUV420 stream (TUs in z-order, CTU-row
+        wavefront; with --check, frame 0's luma against the oracle).
   closed  config 3 in CLOSED loop (neighbours from the reconstruction, wavefront
         schedule) over a batch of 1080p YUV420 frames; with --check, frame 0's
         luma against the oracle.
@@ -72,6 +74,7 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--cfg5-frames", type=int, default=8, help="frames of the batched cfg5 stream")
+    ap.add_argument("--closed4-frames", type=int, default=16, help="frames of the closed-loop cfg4 stream")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
     ap.add_argument("--configs", default="3,4,4b,5,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
@@ -141,6 +144,34 @@ def main():
                           "samples_per_s": samples / ms * 1e3,
                           "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
                           "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}), flush=True)
+
+    if "closed4" in cfgs:   # config 4 in closed loop: 16 4K YUV420 frames, 2 launches (CTU-row wavefronts)
+        W, H, nf = 3840, 2160, args.closed4_frames
+        planes = []
+        for f in range(nf):
+            planes += [synth_plane(H, W, 40 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 41 + 3 * f).reshape(-1),
+                       synth_plane(H // 2, W // 2, 42 + 3 * f).reshape(-1)]
+        stream = torch.cat(planes)
+        sy, suv = gpu.yuv420_plane_sets(nf, W, H)
+        lv = torch.zeros(stream.shape, dtype=torch.int32, device="cuda")
+        rc = torch.zeros(stream.shape, dtype=torch.int16, device="cuda")
+        tuy = torch.zeros((nf, H // 4, W // 4), dtype=torch.uint8, device="cuda")
+        tuc = torch.zeros((2 * nf, H // 8, W // 8), dtype=torch.uint8, device="cuda")
+
+        def run4c():
+            gpu.tu_pipeline_closed(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy)
+            gpu.tu_pipeline_closed(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc)
+        ms = timed(run4c, max(3, args.reps // 4))
+        line = {"config": "cfg4 closed loop: 4K YUV420 frames, mixed TUs in z-order, neighbours from the reconstruction, "
+                          "CTU-row wavefront on the device", "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
+                "frames_per_s": nf / ms * 1e3, "samples_per_s": stream.numel() / ms * 1e3,
+                "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}
+        if args.check:
+            from oracle import oracle as O   # checker only
+            y = stream[:W * H].view(H, W).cpu().numpy()
+            el, er, _ = O.tu_pipeline_plane_closed(y, 32, 0, 1234, args.qp, True)
+            line["frame0_luma_equals_oracle"] = bool(np.array_equal(er, rc[:W * H].view(H, W).cpu().numpy()))
+        print(json.dumps(line), flush=True)
 
     if 5 in cfgs:
         W, H = 7680, 4320
