@@ -4,6 +4,7 @@ Run in the build container only (imports the reference; the reference never
 travels to the GPU box):
 
     python tests/golden/make_fullsize.py [/root/reference] [--procs 8]
+    python tests/golden/make_fullsize.py --only-closed4     # add config 4 closed loop (3 processes, ~minutes)
 
 Inputs are regenerated from seeds by ``fullsize_inputs`` (numpy only, imported
 by tests/test_fullsize_reference_gpu.py as well), outputs are produced by the
@@ -106,6 +107,12 @@ def _cfg5_band(args):
     return r0, r1, lvl, rec
 
 
+def _cfg4_closed_plane(args):
+    src, ctb, pid, seed, qp, luma = args
+    MG, I, T, Q, _ = _REF
+    return MG.ref_plane_cfg4_closed(I, T, Q, src, ctb, pid, seed, qp, luma)
+
+
 def _bands(nrows, k):
     step = -(-nrows // k)
     return [(a, min(nrows, a + step)) for a in range(0, nrows, step)]
@@ -121,6 +128,20 @@ def main():
     procs = int(sys.argv[sys.argv.index("--procs") + 1]) if "--procs" in sys.argv else 8
     out = {"generator": "tests/golden/make_fullsize.py", "inputs": "tests/golden/fullsize_inputs.py",
            "numpy": np.__version__, "reference": "Luodian/nano-hevc @ /root/reference"}
+    dst = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(HERE, "fullsize.json")
+    if "--only-closed4" in sys.argv:   # add config 4 closed loop to an existing fullsize.json
+        with open(dst) as f:
+            out = json.load(f)
+        t0 = time.time()
+        with mp.get_context("fork").Pool(3, initializer=_init, initargs=(ref,)) as pool:
+            jobs = [(src, 32 if k == 0 else 16, k, FI.CFG4_SEED, FI.CFG4_QP, k == 0)
+                    for k, src in enumerate(FI.cfg4_frame())]
+            for k, (l, r, t) in enumerate(pool.map(_cfg4_closed_plane, jobs)):
+                out[f"closed4_p{k}"] = {"lvl": sha(l), "rec": sha(r), "tu": sha(t)}
+        print("closed4", time.time() - t0, flush=True)
+        with open(dst, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+        return
     with mp.get_context("fork").Pool(procs, initializer=_init, initargs=(ref,)) as pool:
         # config 3, open loop: 1080p YUV420 frame, QP 32
         t0 = time.time()
@@ -171,7 +192,6 @@ def main():
             rec[r0 * 32:r1 * 32] = r[r0 * 32:r1 * 32]
         out["cfg5_y"] = {"lvl": sha(lvl), "rec": sha(rec)}
         print("cfg5", time.time() - t0, flush=True)
-    dst = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(HERE, "fullsize.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1, sort_keys=True)
     print(json.dumps(out, indent=1))
