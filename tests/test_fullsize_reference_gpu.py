@@ -6,7 +6,8 @@ functions, composed as DESIGN.md §3.3-3.5 / §3.7 define the drivers, produce
 on the frames of tests/golden/fullsize_inputs.py (generated in the build
 container by tests/golden/make_fullsize.py; the reference never travels here):
 config 3 on a 1080p YUV420 frame in open and closed loop, config 4 on a 4K
-YUV420 frame, config 5 on an 8K luma plane (int8-MFMA and butterfly kernels).
+YUV420 frame in open and closed loop, config 5 on an 8K luma plane (int8-MFMA
+and butterfly kernels).
 """
 import hashlib
 import json
@@ -107,3 +108,27 @@ def test_cfg5_8k_luma_equals_reference(ref, torch_dev, variant):
     l, r = gpu.tc32_plane(torch.from_numpy(src).cuda(), FI.CFG5_QP, variant)
     assert sha(l.cpu().numpy()) == ref["cfg5_y"]["lvl"]
     assert sha(r.cpu().numpy()) == ref["cfg5_y"]["rec"]
+
+
+def test_cfg4_4k_closed_loop_equals_reference(ref, torch_dev):
+    """Config 4 in closed loop on the 4K YUV420 frame."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = FI.cfg4_frame()
+    h, w = planes[0].shape
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(1, w, h)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, FI.CFG4_SEED, FI.CFG4_QP, True, lvl=lvl, rec=rec)
+    _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, FI.CFG4_SEED, FI.CFG4_QP, False, lvl=lvl, rec=rec)
+    lvl, rec, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    off = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        e = ref[f"closed4_p{k}"]
+        assert sha(lvl[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], k
+        assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
+        assert sha(tuy[0] if k == 0 else tuc[k - 1]) == e["tu"], k
+        off += ph * pw

@@ -235,7 +235,7 @@ def test_oracle_encode_frame_intra_golden(golden):
 
 def test_oracle_at_full_size_equals_reference():
     """The CPU restatement at BASELINE sizes (1080p open + closed loop, 4K mixed
-    TUs, 8K 32x32) hashes to the reference's outputs (tests/golden/fullsize.json,
+    TUs open + closed loop, 8K 32x32) hashes to the reference's outputs (tests/golden/fullsize.json,
     tests/golden/make_fullsize.py).  ~25 s."""
     import sys
     sys.path.insert(0, GOLDEN)
@@ -256,6 +256,9 @@ def test_oracle_at_full_size_equals_reference():
         assert (sha(l), sha(r), sha(t)) == tuple(ref[f"cfg4_p{k}"][x] for x in ("lvl", "rec", "tu")), k
     l, r = O.tc32_plane(FI.cfg5_plane(), FI.CFG5_QP)
     assert (sha(l), sha(r)) == (ref["cfg5_y"]["lvl"], ref["cfg5_y"]["rec"])
+    for k, src in enumerate(FI.cfg4_frame()):   # config 4 in closed loop
+        l, r, t = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, FI.CFG4_SEED, FI.CFG4_QP, k == 0)
+        assert (sha(l), sha(r), sha(t)) == tuple(ref[f"closed4_p{k}"][x] for x in ("lvl", "rec", "tu")), k
 
 
 def test_oracle_tu_pipeline_closed_golden(golden):
