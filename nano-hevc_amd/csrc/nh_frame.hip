@@ -545,8 +545,8 @@ __device__ __forceinline__ void flush_enc_stats(const EncArgs& a, int p, EncStat
 // U blocks per lane per pass, loads first; PIPE: the next pass's blocks are
 // loaded before this pass's blocks are decided (the grid is capped so that a
 // workgroup makes several passes).
-template <int N, int U, bool PIPE>
-__global__ void __launch_bounds__(256) k_encode_u8(EncArgs a) {
+template <int N, int U, bool PIPE, int WAVES = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_encode_u8(EncArgs a) {
     // XCD-aware order over the (slot, plane) grid: XCD x runs the x-th eighth
     // of the planes' workgroup slots (xcd_eighths), else the hardware order
     uint32_t wx = blockIdx.x, wy = blockIdx.y;
@@ -596,6 +596,7 @@ struct EncTune {
     int u4 = 1, u8 = 1, pipe = 1, cap = 4096;   // measured best (profiles/r01/frame)
     int xcd = 0;       // XCD-aware workgroup order: 0.480 vs 0.487 ms per 64 4K frames without it (profiles/r01/xcd)
     int nostats = 0;   // A/B probe only: skip the stats atomics (stats are then wrong)
+    int waves = 0;     // A/B: N = 8 pipelined form with >= 4 waves/SIMD (register cap 128)
 };
 static const EncTune& enc_tune() {
     static EncTune t;
@@ -604,7 +605,7 @@ static const EncTune& enc_tune() {
         init = true;
         if (const char* e = getenv("NH_ENC_TUNE")) {
             EncTune r;
-            if (sscanf(e, "%d,%d,%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap, &r.xcd, &r.nostats) >= 2 &&
+            if (sscanf(e, "%d,%d,%d,%d,%d,%d,%d", &r.u4, &r.u8, &r.pipe, &r.cap, &r.xcd, &r.nostats, &r.waves) >= 2 &&
                 (r.u4 == 1 || r.u4 == 2 || r.u4 == 4) && (r.u8 == 1 || r.u8 == 2 || r.u8 == 4) && r.cap > 0)
                 t = r;
         }
@@ -620,7 +621,8 @@ template <class T, int N, bool AL>
 static void launch_small(int u, const EncArgs& a, dim3 grid, hipStream_t s) {
     if constexpr (std::is_same<T, uint8_t>::value && AL) {   // packed 16-bit path
         if (enc_tune().pipe) {
-            if (u == 1) k_encode_u8<N, 1, true><<<grid, 256, 0, s>>>(a);
+            if (N == 8 && u == 1 && enc_tune().waves == 4) k_encode_u8<N, 1, true, 4><<<grid, 256, 0, s>>>(a);
+            else if (u == 1) k_encode_u8<N, 1, true><<<grid, 256, 0, s>>>(a);
             else if (u == 2) k_encode_u8<N, 2, true><<<grid, 256, 0, s>>>(a);
             else k_encode_u8<N, 4, true><<<grid, 256, 0, s>>>(a);
         } else {
