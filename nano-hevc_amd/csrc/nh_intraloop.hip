@@ -215,10 +215,13 @@ __device__ __forceinline__ void rdo8_predict(const RdoSlotLds& L, int mode, uint
 __device__ __forceinline__ unsigned long long rdo8_chain_n(const RdoSlotLds& L, const ChainQ& q, uint32_t (&Rpk)[32],
                                                            uint32_t (&Lpk)[32]);
 
+// NARROW_ONLY: the caller guarantees wide == 0 (the 32-bit path is not compiled in,
+// which frees ~80 VGPRs: config 3's open loop runs 3 waves/SIMD instead of 2)
+template <bool NARROW_ONLY = false>
 __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, uint32_t* refp,
                                                          const ChainQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
     rdo8_predict(L, mode, refp, Rpk);
-    if (!L.wide) return rdo8_chain_n(L, q, Rpk, Lpk);   // 8-bit block and neighbours: packed 16-bit chain
+    if (NARROW_ONLY || !L.wide) return rdo8_chain_n(L, q, Rpk, Lpk);   // 8-bit block and neighbours: packed 16-bit chain
     uint32_t X[8][8];
     const uint32_t* opk = (const uint32_t*)L.orig;
 #pragma unroll
@@ -634,7 +637,10 @@ __device__ __forceinline__ unsigned long long rdo8_chain_pair(const RdoSlotLds& 
     return (L.wide & 1) ? rdo8_pair_recon_sse<true>(X, Pp, opk, h, Rpk) : rdo8_pair_recon_sse<false>(X, Pp, opk, h, Rpk);
 }
 
-template <int WAVES, bool ONESHOT>
+// CHAIN: 0 = either chain per block; 1 = the packed chain only -- a group with
+// any wide block is marked (modes = 0xFF) and left to the CHAIN 2 launch that
+// follows, which skips every group not so marked (ONESHOT only).
+template <int WAVES, bool ONESHOT, int CHAIN = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
                                                     int32_t* lvl, int16_t* recon, unsigned long long* sse_out,
@@ -652,6 +658,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     // ONESHOT: one group of 7 blocks per workgroup; else persistent, groups
     // walked with stride gridDim.x.
     if (t == 0) wg_sse = 0;   // (first read after the barriers below)
+    if constexpr (CHAIN == 2) {   // fallback launch: only the groups the packed-only launch left
+        if (modes[(int64_t)blockIdx.x * kRdoSlots] != 0xFF) return;
+    }
     auto body = [&](const uint32_t grp) __attribute__((always_inline)) {
 
     // ---- cooperative load of the 7 blocks' samples and neighbours ----
@@ -717,6 +726,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     for (int e = t; e < kRdoSlots * 64; e += 256)
         if (S[e / 64].valid) rdo8_block_prep(S[e / 64], e % 64);
     __syncthreads();
+    if constexpr (CHAIN == 1) {   // a wide block in the group: leave the group to the fallback launch
+        bool any_wide = false;
+#pragma unroll
+        for (int k = 0; k < kRdoSlots; ++k) any_wide |= S[k].valid && S[k].wide;
+        if (any_wide) {
+            if (t < kRdoSlots && S[t].valid) modes[b0 + t] = 0xFF;
+            return;   // uniform over the workgroup; nothing of wg_sse to add
+        }
+    }
     const bool active = lane_on && S[lane_on ? slot : 0].valid;
     RdoSlotLds& L = S[lane_on ? slot : 0];
     const ChainQ rq = make_chainq(qp, dq_scale, dq_per);
@@ -725,7 +743,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     uint32_t P[32], Lv[32];
     unsigned long long key = ULLONG_MAX;
     if (active) {
-        const unsigned long long sse = rdo8_chain(L, mode, refs[t], rq, P, Lv);
+        const unsigned long long sse = rdo8_chain<CHAIN == 1>(L, mode, refs[t], rq, P, Lv);
         key = (sse << 6) | (unsigned long long)mode;
         atomicMin(&L.best, key);
     }
@@ -1781,13 +1799,19 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
         return n;
     }();
     // Launch form (A/B knob NH_RDO_FORM, read once): 0 = one group per
-    // workgroup (default), 1 = persistent at the compiler's register
-    // allocation, 2 = persistent forced to 2 waves/SIMD.
+    // workgroup, packed-chain-only launch + fallback launch (default), 1 =
+    // persistent at the compiler's register allocation, 2 = persistent forced
+    // to 2 waves/SIMD, 3 = one group per workgroup, one launch.
     static const int form = [] { const char* e = getenv("NH_RDO_FORM"); return e ? atoi(e) : 0; }();
     const hipStream_t s = as_stream(stream);
     const QuantParams q = qparams(qp, 3, true);
     unsigned long long* sse = (unsigned long long*)d_sse;
-    if (form == 0) {
+    if (form == 0) {   // the packed-chain-only launch (3 waves/SIMD), then the fallback for groups with wide blocks
+        k_intra_rdo8<1, true, 1><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
+                                                        d_recon, sse, ngroups);
+        k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
+                                                        d_recon, sse, ngroups);
+    } else if (form == 3) {   // A/B: one launch, either chain per block
         k_intra_rdo8<1, true><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
                                                      d_recon, sse, ngroups);
     } else {
