@@ -1555,13 +1555,19 @@ struct Closed4Args {
     int32_t dqs, dq_per;
 };
 
+// cnt TUs of size N at once: lane l codes column / row t = l % N of TU j = l / N
+// (local origin (slx[j], sly[j]) in the CTU); reductions over a TU's N lanes are
+// xor-shuffles inside the aligned N-lane group.  TUs of one batch are
+// independent (none reads another's samples), and the CTU-sized LDS tile holds
+// every TU at its own position.
 template <int N, bool DST>
-__device__ __forceinline__ void tu_closed_one(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
-                                              uint8_t* tu, int x, int y, int lx, int ly, int16_t (*rc)[33],
-                                              int32_t (*tile)[33], const ChainQ& cq) {
+__device__ __forceinline__ void tu_closed_batch(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
+                                                uint8_t* tu, int x0c, int y0c, int cnt, const int* slx, const int* sly,
+                                                int16_t (*rc)[33], int32_t (*tile)[33], const ChainQ& cq) {
     constexpr int S = Log2<N>::v + 5;
-    const int t = threadIdx.x;
-    const bool on = t < N;
+    const int j = threadIdx.x / N, t = threadIdx.x % N;
+    const bool on = j < cnt;
+    const int lx = on ? slx[j] : 0, ly = on ? sly[j] : 0, x = x0c + lx, y = y0c + ly;
     int32_t o[N];
     int32_t topt = 0, leftt = 0;
     if (on) {
@@ -1570,12 +1576,12 @@ __device__ __forceinline__ void tu_closed_one(const Closed4Args& a, const int16_
         topt = rc[ly][lx + 1 + t];       // sample (y - 1, x + t)
         leftt = rc[ly + 1 + t][lx];      // sample (y + t, x - 1)
     }
-    // DC (intra.py:46-62): sums over the wave's first N lanes
+    // DC (intra.py:46-62): sum over the TU's N lanes
     int32_t sum = topt + leftt;
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
     const int32_t dc = (sum + N) >> (Log2<N>::v + 1);
-    const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168-169)
+    const int32_t tr = on ? rc[ly][lx + N] : 0, bl = on ? rc[ly + N][lx] : 0;   // top[-1], left[-1]
     auto planar = [&](int yy, int xx) -> int32_t {
         return ((N - 1 - xx) * (int32_t)rc[ly + 1 + yy][lx] + (xx + 1) * tr + (N - 1 - yy) * (int32_t)rc[ly][lx + 1 + xx] +
                 (yy + 1) * bl + N) >> (Log2<N>::v + 1);
@@ -1590,7 +1596,7 @@ __device__ __forceinline__ void tu_closed_one(const Closed4Args& a, const int16_
         }
     }
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
+    for (int m = 1; m < N; m <<= 1) {
         ed += __shfl_xor(ed, m, 64);
         ep += __shfl_xor(ep, m, 64);
     }
@@ -1602,62 +1608,66 @@ __device__ __forceinline__ void tu_closed_one(const Closed4Args& a, const int16_
         for (int k = 0; k < N; ++k) v[k] = (uint32_t)wrap16(o[k] - pred_at(k, t));
         fwd1d<N, DST, Mul24>(v, r);
 #pragma unroll
-        for (int i = 0; i < N; ++i) tile[i][t] = rshift_round<S>(r[i]);
+        for (int i = 0; i < N; ++i) tile[ly + i][lx + t] = rshift_round<S>(r[i]);
     }
     __syncthreads();
     if (on) {                                            // forward pass 2: row t, quant, dequant
 #pragma unroll
-        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[t][k];
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[ly + t][lx + k];
         fwd1d<N, DST, Mul24>(v, r);
         int32_t* lrow = lvl + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const int32_t l = quant_s(rshift_round<S>(r[j]), cq.qs, cq.h_v, cq.hneg_v);
-            lrow[j] = l;
-            v[j] = (uint32_t)dequant_s(l, cq);
+        for (int jj = 0; jj < N; ++jj) {
+            const int32_t l = quant_s(rshift_round<S>(r[jj]), cq.qs, cq.h_v, cq.hneg_v);
+            lrow[jj] = l;
+            v[jj] = (uint32_t)dequant_s(l, cq);
         }
     }
     __syncthreads();
     if (on) {
 #pragma unroll
-        for (int j = 0; j < N; ++j) tile[t][j] = (int32_t)v[j];
+        for (int jj = 0; jj < N; ++jj) tile[ly + t][lx + jj] = (int32_t)v[jj];
     }
     __syncthreads();
     if (on) {                                            // inverse pass 1: column t
 #pragma unroll
-        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[k][t];
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[ly + k][lx + t];
         inv1d<N, DST, Mul24>(v, r);
     }
     __syncthreads();
     if (on) {
 #pragma unroll
-        for (int i = 0; i < N; ++i) tile[i][t] = rshift_round<S>(r[i]);
+        for (int i = 0; i < N; ++i) tile[ly + i][lx + t] = rshift_round<S>(r[i]);
     }
     __syncthreads();
     if (on) {                                            // inverse pass 2: row t, reconstruct, clip
 #pragma unroll
-        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[t][k];
+        for (int k = 0; k < N; ++k) v[k] = (uint32_t)tile[ly + t][lx + k];
         inv1d<N, DST, Mul24>(v, r);
         int16_t* rrow = rec + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
-        for (int j = 0; j < N; ++j) {
-            const int32_t rr = wrap16(rshift_round<S>(r[j]));
-            int32_t rcv = wrap16(pred_at(t, j) + rr);
-            rcv = rcv < 0 ? 0 : (rcv > 255 ? 255 : rcv);
-            rrow[j] = (int16_t)rcv;
-            rc[ly + 1 + t][lx + 1 + j] = (int16_t)rcv;   // planar / neighbours read rc before this barrier
+        for (int jj = 0; jj < N; ++jj) {
+            const int32_t rr = wrap16(rshift_round<S>(r[jj]));
+            int32_t q = wrap16(pred_at(t, jj) + rr);
+            q = q < 0 ? 0 : (q > 255 ? 255 : q);
+            rrow[jj] = (int16_t)q;
+            // the TU's own samples: no TU of this batch reads them (planar reads the row
+            // above and the column left of each TU, coded in earlier rounds)
+            rc[ly + 1 + t][lx + 1 + jj] = (int16_t)q;
         }
         if (t < N / 4) {
             const int w4 = a.w / 4;
-            for (int j = 0; j < N / 4; ++j) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + j] = (uint8_t)Log2<N>::v;
+            for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)Log2<N>::v;
         }
     }
     __syncthreads();
 }
 
-__global__ void __launch_bounds__(64) k_tu_closed(Closed4Args a) {
+template <int WAVES>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed(Closed4Args a) {
     __shared__ int16_t rc[33][33];
     __shared__ int32_t tile[32][33];
+    __shared__ int owner_of[64], done_of[64], slx[16], sly[16];
     __shared__ int row_s, stall_s;
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
@@ -1719,30 +1729,63 @@ __global__ void __launch_bounds__(64) k_tu_closed(Closed4Args a) {
             }
             __syncthreads();
             if (stall_s) break;
-            // the CTU's TUs in z-order (Morton order of its 4x4 units)
-            const int units = (ctb / 4) * (ctb / 4);
-            for (int u = 0; u < units; ++u) {
-                int ux = 0, uy = 0;
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    ux |= ((u >> (2 * b)) & 1) << b;
-                    uy |= ((u >> (2 * b + 1)) & 1) << b;
+            // the CTU's TUs in dataflow rounds: lane u = 4x4 unit (ux, uy) of the CTU finds its
+            // quadtree leaf (tu_leaf); a TU is ready once the TUs holding the units above and
+            // left of it are done (z-order guarantees they precede it), and every round codes
+            // its ready TUs batched by size -- the same TUs, in an order that respects every
+            // dependency of the sequential z-order walk, so the same results
+            const int U = ctb / 4, UU = U * U;
+            int tn = 0, ox = 0, oy = 0;
+            bool pending = false;
+            if (lane < UU) {
+                const int ux = lane % U, uy = lane / U, x = x0c + 4 * ux, y = y0c + 4 * uy;
+                int own = lane;
+                if (x < a.w && y < a.h) {
+                    const int n = tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y), nu = n / 4;
+                    ox = ux - ux % nu;
+                    oy = uy - uy % nu;
+                    own = oy * U + ox;
+                    pending = ox == ux && oy == uy && x + n <= a.w && y + n <= a.h;
+                    tn = n;
                 }
-                const int x = x0c + 4 * ux, y = y0c + 4 * uy;
-                if (x >= a.w || y >= a.h) continue;
-                const int n = tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y);
-                if ((x & (n - 1)) || (y & (n - 1)) || x + n > a.w || y + n > a.h) continue;
-                const int lx = x - x0c, ly = y - y0c;
-                if (n == 4) {
-                    if (a.is_luma) tu_closed_one<4, true>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[0]);
-                    else tu_closed_one<4, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[0]);
-                } else if (n == 8) {
-                    tu_closed_one<8, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[1]);
-                } else if (n == 16) {
-                    tu_closed_one<16, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[2]);
-                } else {
-                    tu_closed_one<32, false>(a, src, lvl, rec, tu, x, y, lx, ly, rc, tile, cq[3]);
+                owner_of[lane] = own;
+                done_of[lane] = 0;
+            }
+            __syncthreads();
+            for (int round = 0; round < UU && __ballot(pending); ++round) {
+                bool ready = pending;
+                if (pending) {
+                    const int nu = tn / 4;
+                    for (int k = 0; k < nu; ++k) {
+                        if (oy > 0 && !done_of[owner_of[(oy - 1) * U + ox + k]]) ready = false;
+                        if (ox > 0 && !done_of[owner_of[(oy + k) * U + ox - 1]]) ready = false;
+                    }
                 }
+                const uint64_t lt = (1ull << lane) - 1ull;
+#define NH_BATCH(NN, DST, Q)                                                                                 \
+                {                                                                                            \
+                    const uint64_t m = __ballot(ready && tn == NN);                                          \
+                    const int cnt = __popcll(m);                                                             \
+                    if (ready && tn == NN) {                                                                 \
+                        const int k = __popcll(m & lt);                                                      \
+                        slx[k] = ox * 4;                                                                     \
+                        sly[k] = oy * 4;                                                                     \
+                    }                                                                                        \
+                    __syncthreads();                                                                         \
+                    for (int c0 = 0; c0 < cnt; c0 += 64 / NN)                                                \
+                        tu_closed_batch<NN, DST>(a, src, lvl, rec, tu, x0c, y0c, min(cnt - c0, 64 / NN),     \
+                                                 slx + c0, sly + c0, rc, tile, Q);                           \
+                }
+                NH_BATCH(32, false, cq[3]);
+                NH_BATCH(16, false, cq[2]);
+                NH_BATCH(8, false, cq[1]);
+                if (a.is_luma) NH_BATCH(4, true, cq[0]) else NH_BATCH(4, false, cq[0])
+#undef NH_BATCH
+                if (ready) {
+                    done_of[lane] = 1;
+                    pending = false;
+                }
+                __syncthreads();
             }
             // publish the bottom row (the next CTU row polls it), then slide: right column -> left column
             if (cy + 1 < a.crows) {
@@ -1969,7 +2012,10 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     a.dq_per = per;
     const int64_t rows = (int64_t)a.crows * np;
     const unsigned waves = (unsigned)(rows < 2048 ? rows : 2048);
-    k_tu_closed<<<waves, 64, 0, s>>>(a);
+    // A/B knob NH_TU_CLOSED_WAVES: 1 = compiler allocation (218 VGPRs, 2 waves/SIMD), 3 = capped (spills)
+    static const int cw = [] { const char* e = getenv("NH_TU_CLOSED_WAVES"); return e ? atoi(e) : 1; }();
+    if (cw == 3) k_tu_closed<3><<<waves, 64, 0, s>>>(a);
+    else k_tu_closed<1><<<waves, 64, 0, s>>>(a);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
