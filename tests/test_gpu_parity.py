@@ -779,3 +779,19 @@ def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp):
             assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
             assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
             off += ph * pw
+
+
+@pytest.mark.parametrize("ctb", [4, 8, 16])
+def test_tu_pipeline_closed_small_ctb_vs_oracle(nh, torch_dev, ctb):
+    """Closed-loop config 4 with CTBs below 32 (fewer units per CTU, more CTU rows)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(ctb)
+    h, w = 44, 60
+    src = np.clip(90 + rng.integers(-40, 41, (h, w)), 0, 255).astype(np.int16)
+    d = torch.from_numpy(src.reshape(-1).copy()).cuda()
+    lvl, rec, tu = gpu.tu_pipeline_closed(d, gpu.plane_set(0, w, h, w), ctb, 0, 99, 27, True)
+    el, er, et = O.tu_pipeline_plane_closed(src, ctb, 0, 99, 27, True)
+    assert np.array_equal(lvl.cpu().numpy().reshape(h, w), el)
+    assert np.array_equal(rec.cpu().numpy().reshape(h, w), er)
+    assert np.array_equal(tu.cpu().numpy()[0], et)
