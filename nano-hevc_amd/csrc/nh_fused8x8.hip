@@ -375,6 +375,7 @@ struct StripeArgs {
     StripeSetDev set[NH_MAX_PLANE_SETS];
     int32_t nsets;
     QuantS q;
+    int32_t xcd;   // XCD-aware workgroup order (xcd_eighths), A/B
 };
 
 constexpr int kStripeThreads = 512;
@@ -382,16 +383,17 @@ constexpr int kStripeThreads = 512;
 template <int POLICY, int STAGE, bool COPY>
 __global__ void __launch_bounds__(kStripeThreads) k_fwd8x8_quant_stripe(StripeArgs a) {
     extern __shared__ __attribute__((aligned(16))) int16_t tile[];
+    const uint32_t wid = a.xcd ? xcd_eighths(blockIdx.x, gridDim.x) : blockIdx.x;
     int s = 0;
 #pragma unroll
     for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
-        if (k < a.nsets && blockIdx.x >= a.set[k].wg_start) s = k;
+        if (k < a.nsets && wid >= a.set[k].wg_start) s = k;
     StripeSetDev S = a.set[0];
 #pragma unroll
     for (int k = 1; k < NH_MAX_PLANE_SETS; ++k)
         if (s == k) S = a.set[k];
     const uint32_t t = threadIdx.x;
-    const uint32_t wt = blockIdx.x - S.wg_start;
+    const uint32_t wt = wid - S.wg_start;
     const uint32_t p = fdiv(wt, S.tpp), ti = wt - p * S.tpp.d;
     const uint32_t g = fdiv(p, S.ppg), c = p - g * S.ppg.d;
     const uint32_t st0 = ti * S.k;
@@ -854,12 +856,13 @@ static int run_stripe_pipe(const int16_t* d_in, int16_t* d_out, const nh_plane_s
 }
 
 static int run_stripe(const int16_t* d_in, int16_t* d_out, const nh_plane_set* sets, int nsets, int qp, int is_intra,
-                      int policy, bool reg_stage, bool copy, hipStream_t s) {
+                      int policy, bool reg_stage, bool copy, hipStream_t s, bool xcd = false) {
     StripeArgs a;
     uint32_t wg = 0, lds = 0;
     int rc = build_stripe_args(d_in, d_out, sets, nsets, qp, is_intra, reg_stage, a, wg, lds);
     if (rc) return rc;
     if (!wg) return NH_OK;
+    a.xcd = xcd ? 1 : 0;
 #define NH_S(P) (reg_stage ? (copy ? launch_stripe<P, 1, true>(a, wg, lds, s) : launch_stripe<P, 1, false>(a, wg, lds, s)) \
                            : (copy ? launch_stripe<P, 0, true>(a, wg, lds, s) : launch_stripe<P, 0, false>(a, wg, lds, s)))
     switch (policy) {
@@ -886,8 +889,12 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           + 128 * persistent double-buffered stripe form (LDS-DMA of the next tile under this one)
     //           + 256 * k: the plain form with 512 (k=1), 1024 (k=2) or 128 (k=3) threads per workgroup
     //           2048 + p: the plain form (>= 5 waves/SIMD) with store policy p = 4 / 5 (see st16)
+    //           8192 + 32..127: the stripe forms above with the XCD-aware workgroup order (A/B)
     //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p) with XCD-aware workgroup
     //           order, chunk 2^c workgroups (c = 15: 1/8 of the grid); 4341 = policy 1, eighths: the default
+    if (variant >= 8192 + 32 && variant < 8192 + 128 && !((variant - 8192) & 28))   // stripe forms + XCD order (A/B)
+        return run_stripe(d_res, d_lvl, sets, nsets, qp, is_intra, variant & 3, ((variant - 8192) >> 6) & 1, false,
+                          as_stream(stream), true);
     if (variant >= 4096 && variant < 4096 + 16 * 16) {
         const int c = (variant - 4096) >> 4, pol = variant & 3;
         if ((variant & 12) != 4) return NH_EARG;
@@ -1000,10 +1007,11 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
                                        int policy, void* stream) {
     // policy = cache policy (0..3) + 4 * shape (0 = the kernel's pattern, 1..3 = pair probes,
     //          4 = stripe form through LDS by LDS-DMA, 5 = stripe form, register staging)
-    const int shape = policy >> 2;
+    const bool xcd = (policy >> 6) & 1;   // + 64: XCD-aware order (stripe shapes only)
+    const int shape = (policy >> 2) & 15;
     policy &= 3;
     if (shape == 4 || shape == 5)
-        return run_stripe(d_in, d_out, sets, nsets, 32, 1, policy, shape == 5, true, as_stream(stream));
+        return run_stripe(d_in, d_out, sets, nsets, 32, 1, policy, shape == 5, true, as_stream(stream), xcd);
     if (shape >= 6 && shape <= 8) {   // row-per-wave probes: 8 waves x 1 row, 4 waves x 2 rows per 64 blocks, 8 x 1 via LDS
         Fused8Args a;
         uint32_t wg = 0;

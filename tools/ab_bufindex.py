@@ -41,7 +41,26 @@ def main():
         torch.cuda.synchronize()
         return round(nblk * 256 / statistics.median([a.elapsed_time(b) for a, b in evs]) / 1e6)
 
+    import ctypes as C
+    from nano_hevc import _lib
+    L = _lib.load()
+
+    def tcopy(i, o, pol):   # linear streaming copy probe of the same byte count (policy: see nh_probe_copy_linear)
+        args = (bufs[i].data_ptr(), bufs[o].data_ptr(), n // 8 * 8, pol, 0, C.c_void_p(st.cuda_stream))
+        for _ in range(3):
+            _lib.check(L.nh_probe_copy_linear(*args))
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(20)]
+        for a, b in evs:
+            a.record(st)
+            _lib.check(L.nh_probe_copy_linear(*args))
+            b.record(st)
+        torch.cuda.synchronize()
+        return round(nblk * 256 / statistics.median([a.elapsed_time(b) for a, b in evs]) / 1e6)
+
     rep = {"addr_GB": [round((b.data_ptr() - bufs[0].data_ptr()) / 2**30, 2) for b in bufs]}
+    if "--copy" in sys.argv:
+        rep["copy_nt_in0_out_j"] = [tcopy(0, j, 1) for j in range(1, K)]
+        rep["copy_nt_xcd_in0_out_j"] = [tcopy(0, j, 17) for j in range(1, K)]
     for v in vs:
         rep[f"v{v}_in0_out_j"] = [t(0, j, v) for j in range(1, K)]
     if len(vs) == 1:
