@@ -165,6 +165,38 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WAVES)
     for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
 }
 
+// Horizontal-pair form (A/B): one thread = blocks 2p and 2p+1 (left / right
+// neighbours in a block row when blocks per row is even), so a wave covers
+// 2 KiB of each of the 8 rows and a 256-thread workgroup 8 KiB -- about one
+// whole 4K luma stripe row -- with 16 row loads in flight per lane; workgroups
+// in the XCD-aware order.
+template <int POLICY>
+__global__ void __launch_bounds__(256) k_fwd8x8_quant_h2(Fused8Args a) {
+    const uint32_t wid = xcd_eighths(blockIdx.x, gridDim.x);
+    SetDev S;
+    select_set(a, S, wid);
+    uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
+    asm volatile("" : "+v"(h_v), "+v"(hneg_v));
+    const uint32_t b0 = 2u * ((wid - S.wg_start) * 256u + threadIdx.x);
+    if (b0 >= S.nblocks) return;
+    const bool two = b0 + 1 < S.nblocks;
+    const int64_t o0 = block_offset(S, b0), o1 = two ? block_offset(S, b0 + 1) : o0;
+    v4i raw0[8], raw1[8], outv[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        raw0[i] = ld16<POLICY>(a.in + o0 + (int64_t)i * S.pitch);
+        if (two) raw1[i] = ld16<POLICY>(a.in + o1 + (int64_t)i * S.pitch);
+    }
+    dct8_quant_block(raw0, outv, a.q, h_v, hneg_v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o0 + (int64_t)i * S.pitch, outv[i]);
+    if (two) {
+        dct8_quant_block(raw1, outv, a.q, h_v, hneg_v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o1 + (int64_t)i * S.pitch, outv[i]);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Level-side epilogue (quant.py:153-178): per block
 //   nnz  = count_nonzero(levels)            (uint8; is_all_zero == !nnz)
@@ -736,7 +768,7 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
         d.ppg = make_fastdiv((uint32_t)p.planes_per_group);
         d.blk0 = (uint32_t)blk;
         blk += nb;
-        const uint64_t nthr = pairs ? (rows * planes + 1) / 2 * bpr : nb;
+        const uint64_t nthr = pairs == 2 ? (nb + 1) / 2 : pairs ? (rows * planes + 1) / 2 * bpr : nb;
         wg += (nthr + tpb - 1) / tpb;
     }
     for (int k = nsets; k < NH_MAX_PLANE_SETS; ++k) a.set[k].wg_start = 0xffffffffu;
@@ -890,8 +922,25 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           + 256 * k: the plain form with 512 (k=1), 1024 (k=2) or 128 (k=3) threads per workgroup
     //           2048 + p: the plain form (>= 5 waves/SIMD) with store policy p = 4 / 5 (see st16)
     //           8192 + 32..127: the stripe forms above with the XCD-aware workgroup order (A/B)
+    //           16384 + p: horizontal block pair per thread, XCD-aware order, cache policy p (A/B)
     //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p) with XCD-aware workgroup
     //           order, chunk 2^c workgroups (c = 15: 1/8 of the grid); 4341 = policy 1, eighths: the default
+    if (variant >= 16384 && variant < 16388) {   // horizontal-pair form, XCD order, cache policy variant & 3 (A/B)
+        Fused8Args a;
+        uint32_t wg = 0;
+        int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg, 2);
+        if (rc) return rc;
+        if (!wg) return NH_OK;
+        hipStream_t s = as_stream(stream);
+        switch (variant & 3) {
+            case 0: k_fwd8x8_quant_h2<0><<<wg, 256, 0, s>>>(a); break;
+            case 1: k_fwd8x8_quant_h2<1><<<wg, 256, 0, s>>>(a); break;
+            case 2: k_fwd8x8_quant_h2<2><<<wg, 256, 0, s>>>(a); break;
+            default: k_fwd8x8_quant_h2<3><<<wg, 256, 0, s>>>(a); break;
+        }
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
     if (variant >= 8192 + 32 && variant < 8192 + 128 && !((variant - 8192) & 28))   // stripe forms + XCD order (A/B)
         return run_stripe(d_res, d_lvl, sets, nsets, qp, is_intra, variant & 3, ((variant - 8192) >> 6) & 1, false,
                           as_stream(stream), true);
