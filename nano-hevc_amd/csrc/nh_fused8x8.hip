@@ -923,7 +923,8 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           2048 + p: the plain form (>= 5 waves/SIMD) with store policy p = 4 / 5 (see st16)
     //           8192 + 32..127: the stripe forms above with the XCD-aware workgroup order (A/B)
     //           16384 + p: horizontal block pair per thread, XCD-aware order, cache policy p (A/B)
-    //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p) with XCD-aware workgroup
+    //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p; + 8 instead of + 4:
+    //           >= 8 waves/SIMD, p = 1 or 3) with XCD-aware workgroup
     //           order, chunk 2^c workgroups (c = 15: 1/8 of the grid); 4341 = policy 1, eighths: the default
     if (variant >= 16384 && variant < 16388) {   // horizontal-pair form, XCD order, cache policy variant & 3 (A/B)
         Fused8Args a;
@@ -945,8 +946,8 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
         return run_stripe(d_res, d_lvl, sets, nsets, qp, is_intra, variant & 3, ((variant - 8192) >> 6) & 1, false,
                           as_stream(stream), true);
     if (variant >= 4096 && variant < 4096 + 16 * 16) {
-        const int c = (variant - 4096) >> 4, pol = variant & 3;
-        if ((variant & 12) != 4) return NH_EARG;
+        const int c = (variant - 4096) >> 4, pol = variant & 3, occ8 = (variant & 12) == 8;
+        if ((variant & 12) != 4 && !occ8) return NH_EARG;
         Fused8Args a;
         uint32_t wg = 0;
         int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
@@ -954,6 +955,12 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
         if (!wg) return NH_OK;
         a.xcd_chunk = c == 15 ? (wg / 8 ? wg / 8 : 1) : (1u << c);
         hipStream_t s = as_stream(stream);
+        if (occ8) {   // A/B: >= 8 waves/SIMD (64 VGPRs)
+            if (pol == 1) k_fwd8x8_quant<1, 8, 256, true><<<wg, 256, 0, s>>>(a);
+            else k_fwd8x8_quant<3, 8, 256, true><<<wg, 256, 0, s>>>(a);
+            NH_HIP(hipGetLastError());
+            return NH_OK;
+        }
         switch (pol) {
             case 0: k_fwd8x8_quant<0, 5, 256, true><<<wg, 256, 0, s>>>(a); break;
             case 1: k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, s>>>(a); break;
