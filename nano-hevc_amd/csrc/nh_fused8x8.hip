@@ -42,6 +42,7 @@ struct Fused8Args {
     int32_t nsets;
     QuantS q;
     uint32_t xcd_chunk;   // k_fwd8x8_quant<..., XCD=true> (the default launch): workgroups per XCD run
+    uint32_t xcd_rot;     // A/B: XCD x starts its run x * xcd_rot workgroups in (mod the run)
 };
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -145,12 +146,20 @@ __device__ __forceinline__ uint32_t xcd_logical_wg(uint32_t bid, uint32_t chunk)
     const uint32_t w = bid - sup * span;
     return sup * span + (w & 7u) * chunk + (w >> 3);
 }
+__device__ __forceinline__ uint32_t xcd_logical_wg_rot(uint32_t bid, uint32_t chunk, uint32_t rot) {
+    const uint32_t span = 8u * chunk;
+    if (span > gridDim.x || bid >= span) return bid;
+    const uint32_t x = bid & 7u, k = (bid >> 3) + x * rot;
+    return x * chunk + (k >= chunk ? k - chunk : k);   // x * rot < chunk
+}
 
 // One thread = one block.  POLICY: cache policy (ld16/st16); WAVES: minimum
 // waves per SIMD requested from the register allocator (1 = compiler choice).
 template <int POLICY, int WAVES, int TPB = 256, bool XCD = false>
 __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant(Fused8Args a) {
-    const uint32_t wid = XCD ? xcd_logical_wg(blockIdx.x, a.xcd_chunk) : blockIdx.x;
+    const uint32_t wid = !XCD ? blockIdx.x
+                       : a.xcd_rot ? xcd_logical_wg_rot(blockIdx.x, a.xcd_chunk, a.xcd_rot)
+                                   : xcd_logical_wg(blockIdx.x, a.xcd_chunk);
     SetDev S;
     select_set(a, S, wid);
     uint32_t h_v = a.q.h, hneg_v = a.q.hneg;
@@ -926,6 +935,19 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p; + 8 instead of + 4:
     //           >= 8 waves/SIMD, p = 1 or 3) with XCD-aware workgroup
     //           order, chunk 2^c workgroups (c = 15: 1/8 of the grid); 4341 = policy 1, eighths: the default
+    if (variant > 32768 && variant <= 32768 + 8) {   // A/B: eighths with XCD x's run rotated by x * r/8 of a run
+        Fused8Args a;
+        uint32_t wg = 0;
+        int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+        if (rc) return rc;
+        if (!wg) return NH_OK;
+        a.xcd_chunk = wg / 8 ? wg / 8 : 1;
+        a.xcd_rot = (a.xcd_chunk * (uint32_t)(variant - 32768)) / 64u;   // x * rot < chunk for x <= 7
+        if (!a.xcd_rot) a.xcd_rot = 1;
+        k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, as_stream(stream)>>>(a);
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
     if (variant >= 16384 && variant < 16388) {   // horizontal-pair form, XCD order, cache policy variant & 3 (A/B)
         Fused8Args a;
         uint32_t wg = 0;

@@ -655,7 +655,7 @@ def test_intra_rdo_closed_ragged_and_int16(nh, torch_dev):
         assert int(sse.cpu()[0]) == es
 
 
-@pytest.mark.parametrize("variant", [17, 21, 9, 13, 33, 97, 32, 35, 129, 128, 261, 517, 773, 257, 2052, 2053, 4096 + 5, 4096 + 16 * 3 + 5, 4096 + 16 * 15 + 5, 8192 + 33, 8192 + 97, 16384 + 1, 16384, 4096 + 16 * 15 + 9])
+@pytest.mark.parametrize("variant", [17, 21, 9, 13, 33, 97, 32, 35, 129, 128, 261, 517, 773, 257, 2052, 2053, 4096 + 5, 4096 + 16 * 3 + 5, 4096 + 16 * 15 + 5, 8192 + 33, 8192 + 97, 16384 + 1, 16384, 4096 + 16 * 15 + 9, 32768 + 8, 32768 + 1])
 def test_fused8x8_launch_variants_equal(nh, torch_dev, variant):
     """Every A/B launch form (pipelined 9/13, vertical block pair 17/21, stripe
     form by LDS-DMA 33/32/35, register-staged 97, persistent double-buffered 129/128) gives
