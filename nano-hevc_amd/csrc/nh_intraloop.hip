@@ -2011,9 +2011,11 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     a.dqs = dequant_scale(rem);
     a.dq_per = per;
     const int64_t rows = (int64_t)a.crows * np;
-    const unsigned waves = (unsigned)(rows < 2048 ? rows : 2048);
     // A/B knob NH_TU_CLOSED_WAVES: 1 = compiler allocation (218 VGPRs, 2 waves/SIMD), 3 = capped (spills)
     static const int cw = [] { const char* e = getenv("NH_TU_CLOSED_WAVES"); return e ? atoi(e) : 1; }();
+    // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x waves/SIMD)
+    const int64_t cap = cw == 3 ? 3072 : 2048;
+    const unsigned waves = (unsigned)(rows < cap ? rows : cap);
     if (cw == 3) k_tu_closed<3><<<waves, 64, 0, s>>>(a);
     else k_tu_closed<1><<<waves, 64, 0, s>>>(a);
     NH_HIP(hipGetLastError());

@@ -12,6 +12,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   tc32_plane          -- config 5: 32x32 chain, butterfly or int8-MFMA variant
   tc32_planes         -- config 5 over a frame stream (one MFMA launch per plane set)
   tu_pipeline_closed  -- config 4 in closed loop (CTU-row wavefront, TUs in z-order)
+  tu_pipeline_closed_yuv420 -- the same over a YUV420 stream, luma and chroma wavefronts concurrent
   widen_u8 / narrow_u8 -- frame I/O casts (YUV420p bytes <-> int16 planes)
   encode_intra_yuv420 -- encode_frame_intra (DC vs planar per block) over a frame stream
 """
@@ -277,12 +278,10 @@ def tu_pipeline_planes(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
     return lvl, rec, tu
 
 
-def tu_pipeline_closed(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
-                       lvl=None, rec=None, tu=None, stream=None):
-    """Config 4 in CLOSED loop (DESIGN.md §3.8) over every plane of one plane
-    set: TUs in z-order with neighbours from the reconstruction, a device
-    wavefront over CTU rows.  Returns (lvl int32, recon int16 -- source
-    layout, zeros outside every TU --, tu uint8 (planes, h/4, w/4))."""
+def _tu_closed_launch(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int, is_luma: bool,
+                      lvl, rec, tu, st: int):
+    """Stream-ordered launch of the config-4 closed loop over one plane set; returns
+    (lvl, rec, tu, workspace) -- the workspace holds the wavefront status word."""
     torch = _torch()
     _need(src, torch.int16, "tu_pipeline_closed(src)")
     sets_fit([pset], src.numel(), "tu_pipeline_closed")
@@ -303,15 +302,69 @@ def tu_pipeline_closed(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
     if lvl.numel() < src.numel() or rec.numel() < src.numel() or tu.numel() < planes * (pset.height // 4) * (pset.width // 4):
         raise ValueError("tu_pipeline_closed: output too small")
     work = torch.empty((wb + 7) // 8, dtype=torch.int64, device=src.device)
-    st = C.c_void_p(_stream(stream))
     check(L.nh_tu_pipeline_planes_closed(src.data_ptr(), C.byref(pset), int(ctb), int(plane_id), int(seed) & 0xffffffff,
                                          int(qp), int(bool(is_luma)), lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(),
-                                         work.data_ptr(), st), "tu_pipeline_closed")
+                                         work.data_ptr(), C.c_void_p(st)), "tu_pipeline_closed")
+    return lvl, rec, tu, work
+
+
+def _tu_closed_status(work, st: int, what: str):
     status = C.c_int(0)
-    check(L.nh_intra_rdo_closed_status(work.data_ptr(), C.byref(status), st))
+    check(_lib.load().nh_intra_rdo_closed_status(work.data_ptr(), C.byref(status), C.c_void_p(st)))
     if status.value:
-        raise RuntimeError("tu_pipeline_closed: the device wavefront stalled (status %d)" % status.value)
+        raise RuntimeError("%s: the device wavefront stalled (status %d)" % (what, status.value))
+
+
+def tu_pipeline_closed(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
+                       lvl=None, rec=None, tu=None, stream=None):
+    """Config 4 in CLOSED loop (DESIGN.md §3.8) over every plane of one plane
+    set: TUs in z-order with neighbours from the reconstruction, a device
+    wavefront over CTU rows.  Returns (lvl int32, recon int16 -- source
+    layout, zeros outside every TU --, tu uint8 (planes, h/4, w/4))."""
+    st = _stream(stream)
+    lvl, rec, tu, work = _tu_closed_launch(src, pset, ctb, plane_id, seed, qp, is_luma, lvl, rec, tu, st)
+    _tu_closed_status(work, st, "tu_pipeline_closed")
     return lvl, rec, tu
+
+
+_SIDE_STREAMS = {}
+
+
+def tu_pipeline_closed_yuv420(src, luma: PlaneSet, chroma: PlaneSet, seed: int, qp: int = 32,
+                              lvl=None, rec=None, tu_luma=None, tu_chroma=None, stream=None):
+    """Config 4 in closed loop over a YUV420 stream: the luma set (CTB 32,
+    plane id 0) and the chroma set (CTB 16, plane ids 1, 2) -- the two calls
+    of ``tu_pipeline_closed`` -- run as two concurrent device wavefronts, the
+    chroma one on a side stream forked from and joined back into ``stream``.
+    One set's CTU rows alone leave most SIMDs with one latency-bound wave
+    (DESIGN.md §4.4a).  Same results as the two calls in sequence.
+    Returns (lvl, rec, tu_luma, tu_chroma)."""
+    torch = _torch()
+    main = stream if stream is not None else torch.cuda.current_stream()
+    dev = src.device
+    side = _SIDE_STREAMS.get(dev.index)
+    if side is None:
+        side = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int32, device=dev)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=dev)
+    fork = torch.cuda.Event()
+    fork.record(main)
+    side.wait_event(fork)
+    with torch.cuda.stream(side):
+        _, _, tu_chroma, work_c = _tu_closed_launch(src, chroma, 16, 1, seed, qp, False, lvl, rec, tu_chroma,
+                                                    int(side.cuda_stream))
+    _, _, tu_luma, work_y = _tu_closed_launch(src, luma, 32, 0, seed, qp, True, lvl, rec, tu_luma,
+                                              int(main.cuda_stream))
+    join = torch.cuda.Event()
+    join.record(side)
+    main.wait_event(join)
+    for t in (tu_chroma, work_c):
+        t.record_stream(main)
+    _tu_closed_status(work_y, int(main.cuda_stream), "tu_pipeline_closed_yuv420 (luma)")
+    _tu_closed_status(work_c, int(main.cuda_stream), "tu_pipeline_closed_yuv420 (chroma)")
+    return lvl, rec, tu_luma, tu_chroma
 
 
 def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=None):

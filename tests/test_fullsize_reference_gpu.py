@@ -110,8 +110,10 @@ def test_cfg5_8k_luma_equals_reference(ref, torch_dev, variant):
     assert sha(r.cpu().numpy()) == ref["cfg5_y"]["rec"]
 
 
-def test_cfg4_4k_closed_loop_equals_reference(ref, torch_dev):
-    """Config 4 in closed loop on the 4K YUV420 frame."""
+@pytest.mark.parametrize("conc", [False, True])
+def test_cfg4_4k_closed_loop_equals_reference(ref, torch_dev, conc):
+    """Config 4 in closed loop on the 4K YUV420 frame, luma and
+    chroma in sequence or as concurrent wavefronts (tu_pipeline_closed_yuv420)."""
     torch = torch_dev
     from nano_hevc import gpu
     planes = FI.cfg4_frame()
@@ -121,8 +123,11 @@ def test_cfg4_4k_closed_loop_equals_reference(ref, torch_dev):
     sy, suv = gpu.yuv420_plane_sets(1, w, h)
     lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
     rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
-    _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, FI.CFG4_SEED, FI.CFG4_QP, True, lvl=lvl, rec=rec)
-    _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, FI.CFG4_SEED, FI.CFG4_QP, False, lvl=lvl, rec=rec)
+    if conc:
+        _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, FI.CFG4_SEED, FI.CFG4_QP, lvl=lvl, rec=rec)
+    else:
+        _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, FI.CFG4_SEED, FI.CFG4_QP, True, lvl=lvl, rec=rec)
+        _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, FI.CFG4_SEED, FI.CFG4_QP, False, lvl=lvl, rec=rec)
     lvl, rec, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
     off = 0
     for k, p in enumerate(planes):

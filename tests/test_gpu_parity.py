@@ -744,11 +744,14 @@ def test_tu_pipeline_closed_golden(nh, torch_dev, golden, key):
         assert np.array_equal(lvl, el) and np.array_equal(rec, er) and np.array_equal(tu.cpu().numpy()[0], et)
 
 
+@pytest.mark.parametrize("conc", [False, True])
 @pytest.mark.parametrize("F,W,H,qp", [(3, 104, 72, 32), (2, 136, 104, 12)])
-def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp):
+def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
     """A YUV420 frame stream in two launches (luma CTB 32, chroma CTB 16, plane
-    ids 0 / 1, 2): many CTU wavefronts at once, partial CTUs, 8-bit content and
-    an int16-extreme frame; every plane equals the sequential oracle."""
+    ids 0 / 1, 2), in sequence or as concurrent wavefronts on two streams
+    (tu_pipeline_closed_yuv420): many CTU wavefronts at once, partial CTUs,
+    8-bit content and an int16-extreme frame; every plane equals the
+    sequential oracle."""
     torch = torch_dev
     from nano_hevc import gpu
     rng = np.random.default_rng(F * 100 + qp)
@@ -767,8 +770,11 @@ def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp):
     sy, suv = gpu.yuv420_plane_sets(F, W, H)
     lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
     rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
-    _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, 777, qp, True, lvl=lvl, rec=rec)
-    _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, 777, qp, False, lvl=lvl, rec=rec)
+    if conc:
+        _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, 777, qp, lvl=lvl, rec=rec)
+    else:
+        _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, 777, qp, True, lvl=lvl, rec=rec)
+        _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, 777, qp, False, lvl=lvl, rec=rec)
     lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
     off = 0
     for f in range(F):

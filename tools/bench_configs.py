@@ -74,11 +74,12 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--cfg5-frames", type=int, default=8, help="frames of the batched cfg5 stream")
-    ap.add_argument("--closed4-frames", type=int, default=16, help="frames of the closed-loop cfg4 stream")
+    ap.add_argument("--closed4-frames", type=int, default=64, help="frames of the closed-loop cfg4 stream")
+    ap.add_argument("--closed4-seq", action="store_true", help="closed4: luma then chroma (default: concurrent wavefronts)")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
     ap.add_argument("--configs", default="3,4,4b,5,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
-    ap.add_argument("--closed-frames", type=int, default=8)
+    ap.add_argument("--closed-frames", type=int, default=64)
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     _lib.load()
@@ -145,7 +146,7 @@ def main():
                           "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
                           "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}), flush=True)
 
-    if "closed4" in cfgs:   # config 4 in closed loop: 16 4K YUV420 frames, 2 launches (CTU-row wavefronts)
+    if "closed4" in cfgs:   # config 4 in closed loop: 64 4K YUV420 frames, 2 concurrent launches (CTU-row wavefronts)
         W, H, nf = 3840, 2160, args.closed4_frames
         planes = []
         for f in range(nf):
@@ -159,11 +160,15 @@ def main():
         tuc = torch.zeros((2 * nf, H // 8, W // 8), dtype=torch.uint8, device="cuda")
 
         def run4c():
-            gpu.tu_pipeline_closed(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy)
-            gpu.tu_pipeline_closed(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc)
+            if args.closed4_seq:
+                gpu.tu_pipeline_closed(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy)
+                gpu.tu_pipeline_closed(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc)
+            else:   # luma and chroma wavefronts concurrent (two streams)
+                gpu.tu_pipeline_closed_yuv420(stream, sy, suv, 1234, args.qp, lvl=lv, rec=rc, tu_luma=tuy, tu_chroma=tuc)
         ms = timed(run4c, max(3, args.reps // 4))
         line = {"config": "cfg4 closed loop: 4K YUV420 frames, mixed TUs in z-order, neighbours from the reconstruction, "
-                          "CTU-row wavefront on the device", "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
+                          "CTU-row wavefront on the device", "frames": nf,
+                "luma_chroma": "sequential" if args.closed4_seq else "concurrent", "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
                 "frames_per_s": nf / ms * 1e3, "samples_per_s": stream.numel() / ms * 1e3,
                 "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}
         if args.check:
