@@ -600,6 +600,7 @@ struct EncTune {
 };
 static const EncTune& enc_tune() {
     static EncTune t;
+#if NH_AB   // A/B build only: launch shapes from NH_ENC_TUNE (tools/enc_tune_ab.sh)
     static bool init = false;
     if (!init) {
         init = true;
@@ -610,6 +611,7 @@ static const EncTune& enc_tune() {
                 t = r;
         }
     }
+#endif
     return t;
 }
 static void small_unroll(int& u4, int& u8) {

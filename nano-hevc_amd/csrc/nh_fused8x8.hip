@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(WAVES)
     for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + off + (int64_t)i * S.pitch, outv[i]);
 }
 
+#if NH_AB   // A/B launch forms (not in the product library)
 // Horizontal-pair form (A/B): one thread = blocks 2p and 2p+1 (left / right
 // neighbours in a block row when blocks per row is even), so a wave covers
 // 2 KiB of each of the 8 rows and a 256-thread workgroup 8 KiB -- about one
@@ -205,6 +206,8 @@ __global__ void __launch_bounds__(256) k_fwd8x8_quant_h2(Fused8Args a) {
         for (int i = 0; i < 8; ++i) st16<POLICY>(a.out + o1 + (int64_t)i * S.pitch, outv[i]);
     }
 }
+
+#endif  // NH_AB
 
 // ---------------------------------------------------------------------------
 // Level-side epilogue (quant.py:153-178): per block
@@ -294,6 +297,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         e.bits[gb] = (int32_t)(((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7])));
 }
 
+#if NH_AB   // A/B launch forms and memory probes (not in the product library)
 // Vertical-pair form: one thread = blocks b and b + blocks_per_row (block rows
 // 2r and 2r+1 of the set's linear row numbering; a pair may straddle two
 // planes, block_offset handles that).  16 row loads in flight per lane; the
@@ -734,6 +738,8 @@ __global__ void __launch_bounds__(512) k_probe_rowwave_lds(Fused8Args a) {
 
 // pairs: 1 = one thread per vertical block pair (rows 2r, 2r+1 of the set's
 // linear block-row numbering): per set ceil(rows/2) * blocks_per_row threads.
+#endif  // NH_AB
+
 static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets, int qp,
                       int is_intra, Fused8Args& a, uint32_t& total_wg, int pairs = 0, int tpb = 256) {
     if (!d_res || !d_lvl || !sets || nsets < 1 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
@@ -786,6 +792,7 @@ static int build_args(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* 
     return NH_OK;
 }
 
+#if NH_AB   // stripe-form launchers (A/B)
 // Stripe-form launch description (see k_fwd8x8_quant_stripe).  Returns
 // NH_EARG when a set's stripe does not fit the LDS (full blocks per row > 1280).
 constexpr uint32_t kStripeTileBytes = 61440;   // ~60 KiB per workgroup: 2 workgroups per CU
@@ -915,6 +922,8 @@ static int run_stripe(const int16_t* d_in, int16_t* d_out, const nh_plane_set* s
 #undef NH_S
 }
 
+#endif  // NH_AB
+
 }  // namespace nh
 
 using namespace nh;
@@ -935,6 +944,28 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
     //           4096 + 16 * c + 4 + p: the plain form (>= 5 waves/SIMD, cache policy p; + 8 instead of + 4:
     //           >= 8 waves/SIMD, p = 1 or 3) with XCD-aware workgroup
     //           order, chunk 2^c workgroups (c = 15: 1/8 of the grid); 4341 = policy 1, eighths: the default
+    // The product library carries the default (4341) and its plain-order form (5); every other
+    // variant is an A/B form compiled only into libnanohevc_ab.so (make ab).
+    if (variant == kDefaultVariant || variant == 5) {
+        Fused8Args a;
+        uint32_t wg = 0;
+        int rc = build_args(d_res, d_lvl, sets, nsets, qp, is_intra, a, wg);
+        if (rc) return rc;
+        if (!wg) return NH_OK;
+        hipStream_t s = as_stream(stream);
+        if (variant == 5) {
+            k_fwd8x8_quant<1, 5><<<wg, 256, 0, s>>>(a);
+        } else {
+            a.xcd_chunk = wg / 8 ? wg / 8 : 1;
+            k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, s>>>(a);
+        }
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
+#if !NH_AB
+    set_error("fwd8x8: launch variant " + std::to_string(variant) + " is an A/B form (libnanohevc_ab.so, make ab)");
+    return NH_EVALUE;
+#else
     if (variant > 32768 && variant <= 32768 + 8) {   // A/B: eighths with XCD x's run rotated by x * r/8 of a run
         Fused8Args a;
         uint32_t wg = 0;
@@ -1069,6 +1100,7 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
 #undef NH_L
     NH_HIP(hipGetLastError());
     return NH_OK;
+#endif  // NH_AB
 }
 
 extern "C" int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,
@@ -1085,6 +1117,11 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
                                        int policy, void* stream) {
     // policy = cache policy (0..3) + 4 * shape (0 = the kernel's pattern, 1..3 = pair probes,
     //          4 = stripe form through LDS by LDS-DMA, 5 = stripe form, register staging)
+#if !NH_AB
+    (void)d_in; (void)d_out; (void)sets; (void)nsets; (void)policy; (void)stream;
+    set_error("nh_probe_copy8x8_planes: memory probes are in the A/B library only (make ab)");
+    return NH_EVALUE;
+#else
     const bool xcd = (policy >> 6) & 1;   // + 64: XCD-aware order (stripe shapes only)
     const int shape = (policy >> 2) & 15;
     policy &= 3;
@@ -1134,12 +1171,18 @@ extern "C" int nh_probe_copy8x8_planes(const int16_t* d_in, int16_t* d_out, cons
     }
     NH_HIP(hipGetLastError());
     return NH_OK;
+#endif  // NH_AB
 }
 
 extern "C" int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t nelems, int policy, int grid,
                                     void* stream) {
     // policy = cache policy (0..3) + 4 * log2(M): M > 1 = k_probe_linear_m (grid ignored)
     //          + 16: XCD-aware workgroup order (xcd_eighths; M = 1 only)
+#if !NH_AB
+    (void)d_in; (void)d_out; (void)nelems; (void)policy; (void)grid; (void)stream;
+    set_error("nh_probe_copy_linear: memory probes are in the A/B library only (make ab)");
+    return NH_EVALUE;
+#else
     const int xcd = (policy >> 4) & 1;
     const int lm = (policy >> 2) & 3;
     if (policy >> 5 || (xcd && lm)) return NH_EARG;
@@ -1170,6 +1213,7 @@ extern "C" int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t
     }
     NH_HIP(hipGetLastError());
     return NH_OK;
+#endif  // NH_AB
 }
 
 extern "C" int nh_fwd8x8_quant_planes_ex(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,

@@ -41,13 +41,24 @@ int staging_upload(Staging& s, size_t off, const void* src, size_t bytes);
 int staging_download(Staging& s, void* dst, size_t off, size_t bytes);
 int staging_finish(Staging& s, int* status_out);  // sync + fetch kernel status word
 
+// A/B knobs.  The product library (`make`) reads no environment: every knob is
+// its default constant, the losing launch forms are not compiled in, and the
+// knob names do not appear in the binary.  `make ab` builds
+// libnanohevc_ab.so with -DNH_AB=1, where NH_KNOB reads the variable once
+// (tools/ and the A/B parity tests load that library explicitly).
+#ifndef NH_AB
+#define NH_AB 0
+#endif
+#if NH_AB
+#define NH_KNOB(name, dflt) ([] { const char* e_ = getenv(name); return e_ ? atoi(e_) : (dflt); }())
+#else
+#define NH_KNOB(name, dflt) (dflt)
+#endif
+
 // XCD-aware workgroup order of the streaming frame kernels (xcd_eighths,
-// nh_common.hpp): on unless NH_XCD_ORDER=0 (A/B knob), read once.
+// nh_common.hpp): on (A/B build: off with NH_XCD_ORDER=0).
 inline bool xcd_order() {
-    static const bool on = [] {
-        const char* e = getenv("NH_XCD_ORDER");
-        return !(e && e[0] == '0');
-    }();
+    static const bool on = NH_KNOB("NH_XCD_ORDER", 1) != 0;
     return on;
 }
 

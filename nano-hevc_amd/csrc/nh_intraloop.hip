@@ -821,7 +821,7 @@ struct ClosedArgs {
     int32_t dq_scale, dq_per;
     int32_t order;                  // tagged form: 0 plane-major tickets, 1 row-major across planes
     int32_t max_bh;                 // largest block-row count of any set
-    int32_t probe;                  // timing probe only (NH_CLOSED_PROBE=1): skip the chain (wrong outputs)
+    int32_t probe;                  // A/B build only (NH_CLOSED_PROBE=1): skip the chain (wrong outputs); 0 otherwise
 };
 constexpr int kSpinLimit = 1 << 20;   // ~1 s of polling; a legitimate wait is a few block steps
 
@@ -1101,11 +1101,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             tl_next = L.topA[8];
             uint32_t P[32], Lv[32];
             unsigned long long key = ULLONG_MAX;
+#if NH_AB   // timing probe of the A/B build only: skip the chain (wrong outputs)
             if (a.probe) {
 #pragma unroll
                 for (int q = 0; q < 32; ++q) P[q] = Lv[q] = (uint32_t)L.orig[q];
                 if (lane < kModes) key = lane;
-            } else if (lane < kModes) {
+            } else
+#endif
+            if (lane < kModes) {
                 key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
             }
             unsigned long long best = key;
@@ -1835,17 +1838,11 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
     int per, rem;
     qp_split(qp, &per, &rem);
     const uint32_t ngroups = (uint32_t)((nblk + kRdoSlots - 1) / kRdoSlots);
-    static const int cus = [] {
-        int dev = 0, n = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            n = 256;
-        return n;
-    }();
     // Launch form (A/B knob NH_RDO_FORM, read once): 0 = one group per
     // workgroup, packed-chain-only launch + fallback launch (default), 1 =
     // persistent at the compiler's register allocation, 2 = persistent forced
     // to 2 waves/SIMD, 3 = one group per workgroup, one launch.
-    static const int form = [] { const char* e = getenv("NH_RDO_FORM"); return e ? atoi(e) : 0; }();
+    static const int form = NH_KNOB("NH_RDO_FORM", 0);
     const hipStream_t s = as_stream(stream);
     const QuantParams q = qparams(qp, 3, true);
     unsigned long long* sse = (unsigned long long*)d_sse;
@@ -1854,10 +1851,19 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
                                                         d_recon, sse, ngroups);
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
                                                         d_recon, sse, ngroups);
-    } else if (form == 3) {   // A/B: one launch, either chain per block
+    }
+#if NH_AB
+    else if (form == 3) {   // A/B: one launch, either chain per block
         k_intra_rdo8<1, true><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
                                                      d_recon, sse, ngroups);
     } else {
+        static const int cus = [] {
+            int dev = 0, n = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                n = 256;
+            return n;
+        }();
         // as many workgroups as fit, every workgroup the same number of groups +-1
         const uint32_t cap = (uint32_t)cus * (form == 2 ? 2 : 1), iters = (ngroups + cap - 1) / cap;
         const unsigned grid = (ngroups + iters - 1) / iters;
@@ -1868,6 +1874,7 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
             k_intra_rdo8<1, false><<<grid, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
                                                        d_recon, sse, ngroups);
     }
+#endif
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
@@ -1924,11 +1931,7 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
     NH_TU(16, false);
     // 32x32 TUs: int8 MFMA (the config-5 A/B winner) where the layout allows its
     // 16-B row accesses; NH_TU32_BUTTERFLY=1 forces the butterfly (A/B only)
-    static int tu32_bf = -1;
-    if (tu32_bf < 0) {
-        const char* e = getenv("NH_TU32_BUTTERFLY");
-        tu32_bf = e && atoi(e) == 1;
-    }
+    static const bool tu32_bf = NH_KNOB("NH_TU32_BUTTERFLY", 0) == 1;
     const bool mfma_ok = !tu32_bf && !(pitch & 7) && !((ta.group_stride | ta.plane_stride) & 7) &&
                          !(((uintptr_t)src | (uintptr_t)lvl | (uintptr_t)rec) & 15);
     if (ctb == 32 && mfma_ok) {
@@ -2012,12 +2015,15 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     a.dq_per = per;
     const int64_t rows = (int64_t)a.crows * np;
     // A/B knob NH_TU_CLOSED_WAVES: 1 = compiler allocation (218 VGPRs, 2 waves/SIMD), 3 = capped (spills)
-    static const int cw = [] { const char* e = getenv("NH_TU_CLOSED_WAVES"); return e ? atoi(e) : 1; }();
+    static const int cw = NH_KNOB("NH_TU_CLOSED_WAVES", 1);
     // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x waves/SIMD)
     const int64_t cap = cw == 3 ? 3072 : 2048;
     const unsigned waves = (unsigned)(rows < cap ? rows : cap);
+#if NH_AB
     if (cw == 3) k_tu_closed<3><<<waves, 64, 0, s>>>(a);
-    else k_tu_closed<1><<<waves, 64, 0, s>>>(a);
+    else
+#endif
+        k_tu_closed<1><<<waves, 64, 0, s>>>(a);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
@@ -2119,21 +2125,26 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
         const int waves = a.total_rows < 2048 ? a.total_rows : 2048;
         {   // A/B knobs: NH_CLOSED_WAVES=2 register allocation for 2 waves/SIMD (spills);
             // NH_CLOSED_FORM=0 the progress-counter form (default 1: tagged line words)
-            static const int cw = [] { const char* e = getenv("NH_CLOSED_WAVES"); return e ? atoi(e) : 1; }();
-            static const int cf = [] { const char* e = getenv("NH_CLOSED_FORM"); return e ? atoi(e) : 1; }();
-            static const int co = [] { const char* e = getenv("NH_CLOSED_ORDER"); return e ? atoi(e) : 1; }();
+            static const int cw = NH_KNOB("NH_CLOSED_WAVES", 1);
+            static const int cf = NH_KNOB("NH_CLOSED_FORM", 1);
+            static const int co = NH_KNOB("NH_CLOSED_ORDER", 1);
             a.order = co ? 1 : 0;
-            static const int cp = [] { const char* e = getenv("NH_CLOSED_PROBE"); return e ? atoi(e) : 0; }();
-            a.probe = cp;
+            a.probe = NH_KNOB("NH_CLOSED_PROBE", 0);
+#if NH_AB
             if (cf == 0) {
                 if (cw == 2) k_intra_rdo8_closed<2><<<waves, 64, 0, s>>>(a);
                 else k_intra_rdo8_closed<1><<<waves, 64, 0, s>>>(a);
             } else if (cf == 2) {
                 if (cw == 3) k_intra_rdo8_closed_pair<3><<<waves, 128, 0, s>>>(a);
                 else k_intra_rdo8_closed_pair<2><<<waves, 128, 0, s>>>(a);
-            } else {
-                if (cw == 2) k_intra_rdo8_closed_tag<2><<<waves, 64, 0, s>>>(a);
-                else k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
+            } else if (cw == 2) {
+                k_intra_rdo8_closed_tag<2><<<waves, 64, 0, s>>>(a);
+            } else
+#endif
+            {
+                (void)cf;
+                (void)cw;
+                k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
             }
         }
     }

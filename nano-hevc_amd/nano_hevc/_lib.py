@@ -12,6 +12,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnanohevc.so")
+# The A/B build (make ab, -DNH_AB=1): losing launch forms, memory probes and the
+# NH_* environment knobs of tools/.  Never loaded unless asked for explicitly
+# (use_ab(), or a fwd8x8 launch variant that only exists there).
+LIB_AB_PATH = os.path.join(HERE, "libnanohevc_ab.so")
 
 NH_OK, NH_EVALUE, NH_EINDEX, NH_EOVERFLOW, NH_EZERODIV, NH_EARG = 0, -1, -2, -3, -4, -5
 NH_ENODEV, NH_EHIP = -10, -11
@@ -78,15 +82,32 @@ SIGNATURES = {
     "nh_encode_intra_planes": ([P, I32, C.POINTER(PlaneSet), I32, P, P, P, P, VP], I32),
 }
 
-_lib = None
-_load_error = None
+_libs = {}
+_use_ab = False
+
+
+def use_ab(on: bool = True):
+    """Route every later call of this process to the A/B library (tools/ only)."""
+    global _use_ab
+    _use_ab = bool(on)
+
+
+def load_ab():
+    """The A/B library (raises NanoHevcUnavailable if `make ab` was not run)."""
+    return _open(LIB_AB_PATH, "make -C nano-hevc_amd ab")
 
 
 def load():
     """Load libnanohevc.so (raises NanoHevcUnavailable if it was not built)."""
-    global _lib, _load_error
-    if _lib is not None:
-        return _lib
+    if _use_ab:
+        return load_ab()
+    return _open(LIB_PATH, "python -c 'import __graft_entry__ as g; g.build()'")
+
+
+def _open(path, how):
+    L = _libs.get(path)
+    if L is not None:
+        return L
     # One HIP runtime per process: torch wheels bundle their own libamdhip64
     # (SONAME libamdhip64.so.7).  Importing torch first makes that copy the
     # process's runtime, and our DT_NEEDED libamdhip64.so.7 then binds to it
@@ -96,20 +117,18 @@ def load():
         import torch  # noqa: F401
     except Exception:  # pragma: no cover - torch is optional for the C-ABI path
         pass
-    if not os.path.exists(LIB_PATH):
+    if not os.path.exists(path):
         raise NanoHevcUnavailable(
-            f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
-            "(hipcc --offload-arch=gfx950); nano_hevc has no CPU fallback")
+            f"{path} not built: run `{how}` (hipcc --offload-arch=gfx950); nano_hevc has no CPU fallback")
     try:
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
     except OSError as e:  # pragma: no cover
-        _load_error = e
-        raise NanoHevcUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+        raise NanoHevcUnavailable(f"cannot load {path}: {e}") from e
     for name, (args, res) in SIGNATURES.items():
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
-    _lib = L
+    _libs[path] = L
     return L
 
 

@@ -30,10 +30,34 @@ def _torch():
     return torch
 
 
-def _stream(stream=None) -> int:
+def _stream(stream=None, device=None) -> int:
+    """Raw hipStream_t of ``stream``, default: the current stream of ``device``
+    (the tensor's device), not of whichever device happens to be current."""
     torch = _torch()
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    if device is not None and s.device != device:
+        raise ValueError(f"stream on {s.device} but the tensors are on {device}")
     return int(s.cuda_stream)
+
+
+def _plane_intervals(pset: PlaneSet):
+    """[start, end) element range of every plane of a set."""
+    span = (pset.height - 1) * pset.pitch + pset.width if pset.height > 0 and pset.width > 0 else 0
+    for g in range(pset.num_groups):
+        for c in range(pset.planes_per_group):
+            b = pset.base + g * pset.group_stride + c * pset.plane_stride
+            yield b, b + span
+
+
+def sets_disjoint(a: PlaneSet, b: PlaneSet) -> bool:
+    """True when no plane of ``a`` shares an element range with a plane of ``b``."""
+    iv = sorted([(s, e, 0) for s, e in _plane_intervals(a) if e > s] + [(s, e, 1) for s, e in _plane_intervals(b) if e > s])
+    end = {0: -1, 1: -1}
+    for s, e, k in iv:
+        if s < end[1 - k]:
+            return False
+        end[k] = max(end[k], e)
+    return True
 
 
 def _need(t, dtype, what):
@@ -71,6 +95,7 @@ def blocks_in(sets: Sequence[PlaneSet]) -> int:
 
 
 DEFAULT_VARIANT = 4341   # nontemporal loads+stores, >= 5 waves/SIMD, XCD-aware order (see nh_fused8x8.hip)
+PRODUCT_VARIANTS = (DEFAULT_VARIANT, 5)   # 5: the same without the XCD order; the rest are A/B forms (make ab)
 
 
 def sets_fit(sets: Sequence[PlaneSet], numel: int, what: str):
@@ -97,8 +122,9 @@ def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = T
     _need(out, torch.int16, "fwd8x8_quant(out)")
     sets_fit(sets, min(res.numel(), out.numel()), "fwd8x8_quant")
     arr = (PlaneSet * len(sets))(*sets)
-    check(_lib.load().nh_fwd8x8_quant_planes_variant(res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp),
-                                                     int(bool(is_intra)), int(variant), C.c_void_p(_stream(stream))),
+    L = _lib.load() if int(variant) in PRODUCT_VARIANTS else _lib.load_ab()   # the A/B forms live in the A/B build
+    check(L.nh_fwd8x8_quant_planes_variant(res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp),
+                                           int(bool(is_intra)), int(variant), C.c_void_p(_stream(stream, res.device))),
           "fwd8x8_quant")
     return out
 
@@ -122,7 +148,7 @@ def fwd8x8_quant_ex(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool 
     arr = (PlaneSet * len(sets))(*sets)
     check(_lib.load().nh_fwd8x8_quant_planes_ex(
         res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp), int(bool(is_intra)),
-        t_nnz.data_ptr() if nnz else None, t_bits.data_ptr() if bits else None, C.c_void_p(_stream(stream))))
+        t_nnz.data_ptr() if nnz else None, t_bits.data_ptr() if bits else None, C.c_void_p(_stream(stream, res.device))))
     return out, t_nnz, t_bits
 
 
@@ -145,7 +171,7 @@ def fwd_transform_batch(x, use_dst: bool = False, out=None, stream=None):
     b, n = _blocks(x, "fwd_transform_batch")
     out = _torch().empty_like(x) if out is None else out
     check(_lib.load().nh_fwd_transform_batch(x.data_ptr(), out.data_ptr(), b, n, int(bool(use_dst)),
-                                             C.c_void_p(_stream(stream))), "fwd_transform_batch")
+                                             C.c_void_p(_stream(stream, x.device))), "fwd_transform_batch")
     return out
 
 
@@ -154,7 +180,7 @@ def inv_transform_batch(x, use_dst: bool = False, out=None, stream=None):
     b, n = _blocks(x, "inv_transform_batch")
     out = _torch().empty_like(x) if out is None else out
     check(_lib.load().nh_inv_transform_batch(x.data_ptr(), out.data_ptr(), b, n, int(bool(use_dst)),
-                                             C.c_void_p(_stream(stream))), "inv_transform_batch")
+                                             C.c_void_p(_stream(stream, x.device))), "inv_transform_batch")
     return out
 
 
@@ -164,7 +190,7 @@ def quant_batch(c, qp: int, log2size: int, is_intra: bool = True, out=None, stre
     _need(c, torch.int32, "quant_batch")
     out = torch.empty_like(c) if out is None else out
     check(_lib.load().nh_quant_batch(c.data_ptr(), out.data_ptr(), c.numel(), int(qp), int(log2size),
-                                     int(bool(is_intra)), C.c_void_p(_stream(stream))), "quant_batch")
+                                     int(bool(is_intra)), C.c_void_p(_stream(stream, c.device))), "quant_batch")
     return out
 
 
@@ -174,7 +200,7 @@ def dequant_batch(l, qp: int, out=None, stream=None):
     _need(l, torch.int32, "dequant_batch")
     out = torch.empty_like(l) if out is None else out
     check(_lib.load().nh_dequant_batch(l.data_ptr(), out.data_ptr(), l.numel(), int(qp),
-                                       C.c_void_p(_stream(stream))), "dequant_batch")
+                                       C.c_void_p(_stream(stream, l.device))), "dequant_batch")
     return out
 
 
@@ -190,7 +216,7 @@ def intra_rdo_plane(src, qp: int = 32, pitch: int | None = None, stream=None):
     rec = torch.zeros((h, w), dtype=torch.int16, device=dev)
     sse = torch.zeros(1, dtype=torch.int64, device=dev)
     check(_lib.load().nh_intra_rdo_plane(src.data_ptr(), w, h, pitch or w, int(qp), modes.data_ptr(), lvl.data_ptr(),
-                                         rec.data_ptr(), sse.data_ptr(), C.c_void_p(_stream(stream))), "intra_rdo_plane")
+                                         rec.data_ptr(), sse.data_ptr(), C.c_void_p(_stream(stream, src.device))), "intra_rdo_plane")
     return modes, lvl, rec, sse
 
 
@@ -220,7 +246,7 @@ def intra_rdo_closed(src, sets: Sequence[PlaneSet], qp: int = 32, lvl=None, rec=
     modes = torch.zeros(max(1, nmodes), dtype=torch.uint8, device=src.device)
     sse = torch.zeros(max(1, nplanes), dtype=torch.int64, device=src.device)
     work = torch.empty((wb + 3) // 4, dtype=torch.int32, device=src.device)
-    st = C.c_void_p(_stream(stream))
+    st = C.c_void_p(_stream(stream, src.device))
     check(L.nh_intra_rdo_planes_closed(src.data_ptr(), arr, len(sets), int(qp), modes.data_ptr(), lvl.data_ptr(),
                                        rec.data_ptr(), sse.data_ptr(), work.data_ptr(), st))
     status = C.c_int(0)
@@ -248,7 +274,7 @@ def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_
     check(L.nh_tu_pipeline_plane(src.data_ptr(), w, h, w, int(ctb), int(plane_id), int(seed) & 0xFFFFFFFF, int(qp),
                                  int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)), lvl.data_ptr(), rec.data_ptr(),
                                  tu.data_ptr(), work.data_ptr() if work is not None else None,
-                                 C.c_void_p(_stream(stream))), "tu_pipeline_plane")
+                                 C.c_void_p(_stream(stream, src.device))), "tu_pipeline_plane")
     return lvl, rec, tu
 
 
@@ -274,14 +300,21 @@ def tu_pipeline_planes(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
         raise ValueError("tu_pipeline_planes: output too small")
     check(_lib.load().nh_tu_pipeline_planes(src.data_ptr(), C.byref(pset), int(ctb), int(plane_id), int(seed) & 0xffffffff,
                                             int(qp), int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)),
-                                            lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(), C.c_void_p(_stream(stream))))
+                                            lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(), C.c_void_p(_stream(stream, src.device))))
     return lvl, rec, tu
 
 
 def _tu_closed_launch(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int, is_luma: bool,
-                      lvl, rec, tu, st: int):
-    """Stream-ordered launch of the config-4 closed loop over one plane set; returns
-    (lvl, rec, tu, workspace) -- the workspace holds the wavefront status word."""
+                      lvl, rec, tu, strm):
+    """Stream-ordered launch of the config-4 closed loop over one plane set on the
+    torch stream ``strm`` (default outputs are zero-filled on that stream too);
+    returns (lvl, rec, tu, workspace) -- the workspace holds the wavefront status word."""
+    torch = _torch()
+    with torch.cuda.device(src.device), torch.cuda.stream(strm):
+        return _tu_closed_launch_on(src, pset, ctb, plane_id, seed, qp, is_luma, lvl, rec, tu, int(strm.cuda_stream))
+
+
+def _tu_closed_launch_on(src, pset, ctb, plane_id, seed, qp, is_luma, lvl, rec, tu, st: int):
     torch = _torch()
     _need(src, torch.int16, "tu_pipeline_closed(src)")
     sets_fit([pset], src.numel(), "tu_pipeline_closed")
@@ -321,8 +354,10 @@ def tu_pipeline_closed(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
     set: TUs in z-order with neighbours from the reconstruction, a device
     wavefront over CTU rows.  Returns (lvl int32, recon int16 -- source
     layout, zeros outside every TU --, tu uint8 (planes, h/4, w/4))."""
-    st = _stream(stream)
-    lvl, rec, tu, work = _tu_closed_launch(src, pset, ctb, plane_id, seed, qp, is_luma, lvl, rec, tu, st)
+    torch = _torch()
+    strm = stream if stream is not None else torch.cuda.current_stream(src.device)
+    st = _stream(strm, src.device)
+    lvl, rec, tu, work = _tu_closed_launch(src, pset, ctb, plane_id, seed, qp, is_luma, lvl, rec, tu, strm)
     _tu_closed_status(work, st, "tu_pipeline_closed")
     return lvl, rec, tu
 
@@ -340,23 +375,28 @@ def tu_pipeline_closed_yuv420(src, luma: PlaneSet, chroma: PlaneSet, seed: int, 
     (DESIGN.md §4.4a).  Same results as the two calls in sequence.
     Returns (lvl, rec, tu_luma, tu_chroma)."""
     torch = _torch()
-    main = stream if stream is not None else torch.cuda.current_stream()
     dev = src.device
+    main = stream if stream is not None else torch.cuda.current_stream(dev)
+    if main.device != dev:
+        raise ValueError(f"tu_pipeline_closed_yuv420: stream on {main.device} but src on {dev}")
+    if not sets_disjoint(luma, chroma):
+        # the two wavefronts would write shared lvl / rec elements concurrently: code them in sequence
+        lvl, rec, tu_luma = tu_pipeline_closed(src, luma, 32, 0, seed, qp, True, lvl, rec, tu_luma, main)
+        lvl, rec, tu_chroma = tu_pipeline_closed(src, chroma, 16, 1, seed, qp, False, lvl, rec, tu_chroma, main)
+        return lvl, rec, tu_luma, tu_chroma
     side = _SIDE_STREAMS.get(dev.index)
     if side is None:
         side = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
-    if lvl is None:
-        lvl = torch.zeros(src.shape, dtype=torch.int32, device=dev)
-    if rec is None:
-        rec = torch.zeros(src.shape, dtype=torch.int16, device=dev)
+    with torch.cuda.device(dev), torch.cuda.stream(main):   # default outputs zero-filled in order on `main`
+        if lvl is None:
+            lvl = torch.zeros(src.shape, dtype=torch.int32, device=dev)
+        if rec is None:
+            rec = torch.zeros(src.shape, dtype=torch.int16, device=dev)
     fork = torch.cuda.Event()
     fork.record(main)
     side.wait_event(fork)
-    with torch.cuda.stream(side):
-        _, _, tu_chroma, work_c = _tu_closed_launch(src, chroma, 16, 1, seed, qp, False, lvl, rec, tu_chroma,
-                                                    int(side.cuda_stream))
-    _, _, tu_luma, work_y = _tu_closed_launch(src, luma, 32, 0, seed, qp, True, lvl, rec, tu_luma,
-                                              int(main.cuda_stream))
+    _, _, tu_chroma, work_c = _tu_closed_launch(src, chroma, 16, 1, seed, qp, False, lvl, rec, tu_chroma, side)
+    _, _, tu_luma, work_y = _tu_closed_launch(src, luma, 32, 0, seed, qp, True, lvl, rec, tu_luma, main)
     join = torch.cuda.Event()
     join.record(side)
     main.wait_event(join)
@@ -377,7 +417,7 @@ def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=N
     lvl = torch.zeros((h, w), dtype=torch.int32, device=src.device) if lvl is None else lvl
     rec = torch.zeros((h, w), dtype=torch.int16, device=src.device) if rec is None else rec
     check(_lib.load().nh_tc32_plane(src.data_ptr(), w, h, w, int(qp), lvl.data_ptr(), rec.data_ptr(), int(variant),
-                                    C.c_void_p(_stream(stream))), "tc32_plane")
+                                    C.c_void_p(_stream(stream, src.device))), "tc32_plane")
     return lvl, rec
 
 
@@ -398,7 +438,7 @@ def tc32_planes(src, sets, qp: int = 32, variant: int = 1, lvl=None, rec=None, s
         raise ValueError("tc32_planes: lvl / rec smaller than src")
     arr = (PlaneSet * len(sets))(*sets)
     check(_lib.load().nh_tc32_planes(src.data_ptr(), arr, len(sets), int(qp), lvl.data_ptr(), rec.data_ptr(),
-                                     int(variant), C.c_void_p(_stream(stream))), "tc32_planes")
+                                     int(variant), C.c_void_p(_stream(stream, src.device))), "tc32_planes")
     return lvl, rec
 
 
@@ -419,7 +459,7 @@ def widen_u8(src, out=None, stream=None):
     _need(out, torch.int16, "widen_u8(out)")
     if out.numel() != src.numel():
         raise ValueError("widen_u8: size mismatch")
-    check(_lib.load().nh_widen_u8_i16(src.data_ptr(), out.data_ptr(), src.numel(), C.c_void_p(_stream(stream))))
+    check(_lib.load().nh_widen_u8_i16(src.data_ptr(), out.data_ptr(), src.numel(), C.c_void_p(_stream(stream, src.device))))
     return out
 
 
@@ -433,7 +473,7 @@ def narrow_u8(src, out=None, stream=None):
     _need(out, torch.uint8, "narrow_u8(out)")
     if out.numel() != src.numel():
         raise ValueError("narrow_u8: size mismatch")
-    check(_lib.load().nh_narrow_i16_u8(src.data_ptr(), out.data_ptr(), src.numel(), C.c_void_p(_stream(stream))))
+    check(_lib.load().nh_narrow_i16_u8(src.data_ptr(), out.data_ptr(), src.numel(), C.c_void_p(_stream(stream, src.device))))
     return out
 
 
@@ -478,7 +518,7 @@ def encode_intra_planes(src, sets: Sequence[PlaneSet], block_sizes: Sequence[int
     check(_lib.load().nh_encode_intra_planes(
         src.data_ptr(), int(src.dtype == torch.uint8), arr, len(sets), bsz,
         recon.data_ptr() if recon is not None else None, recon_u8.data_ptr() if recon_u8 is not None else None,
-        stats.data_ptr(), C.c_void_p(_stream(stream))))
+        stats.data_ptr(), C.c_void_p(_stream(stream, src.device))))
     return stats
 
 

@@ -68,3 +68,34 @@ def test_oracle_not_imported_by_product():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
                 txt = open(os.path.join(dp, f), errors="replace").read()
                 assert "import oracle" not in txt and "from oracle" not in txt and "nh_oracle" not in txt, f
+
+
+def _undefined_symbols(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1].split("@")[0] for ln in out.splitlines() if ln.strip()}
+
+
+def test_product_library_reads_no_environment():
+    """The shipped library has no A/B knobs: no getenv import and no NH_* knob
+    names (they exist only in the -DNH_AB=1 build, libnanohevc_ab.so)."""
+    from nano_hevc import _lib
+    assert "getenv" not in _undefined_symbols(_lib.LIB_PATH)
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for knob in (b"NH_RDO_FORM", b"NH_TU32_BUTTERFLY", b"NH_TU_CLOSED_WAVES", b"NH_CLOSED_WAVES",
+                 b"NH_CLOSED_FORM", b"NH_CLOSED_ORDER", b"NH_CLOSED_PROBE", b"NH_ENC_TUNE", b"NH_XCD_ORDER"):
+        assert knob not in blob, knob
+    # the losing fwd8x8 launch forms and memory probes are not compiled in either
+    for kern in (b"k_fwd8x8_quant_h2", b"k_fwd8x8_quant_v2", b"k_fwd8x8_quant_stripe", b"k_probe_rowwave",
+                 b"k_intra_rdo8_closed_pair"):
+        assert kern not in blob, kern
+
+
+def test_ab_library_exports_the_same_abi():
+    from nano_hevc import _lib
+    if not os.path.exists(_lib.LIB_AB_PATH):
+        pytest.skip("A/B build absent (make -C nano-hevc_amd ab)")
+    L = _lib.load_ab()
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    assert "getenv" in _undefined_symbols(_lib.LIB_AB_PATH)

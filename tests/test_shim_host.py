@@ -107,3 +107,20 @@ def test_natural_residual_helper_matches_reference_dc():
         left = np.full(8, 128) if bx == 0 else src[by:by + 8, bx - 1]
         dc = (int(top.sum()) + int(left.sum()) + 8) // 16
         assert np.array_equal(res[by:by + 8, bx:bx + 8], (src[by:by + 8, bx:bx + 8] - dc).astype(np.int16))
+
+
+def test_plane_sets_disjoint():
+    """tu_pipeline_closed_yuv420 runs luma and chroma concurrently only when the
+    two sets write disjoint elements (else it codes them in sequence)."""
+    W, H, F = 64, 32, 3
+    y, uv = gpu.yuv420_plane_sets(F, W, H)
+    assert gpu.sets_disjoint(y, uv) and gpu.sets_disjoint(uv, y)
+    assert not gpu.sets_disjoint(y, y)
+    y2, _ = gpu.yuv420_plane_sets(F, W, H, base=W * H - 1)   # overlaps the first frame's Y / U boundary
+    assert not gpu.sets_disjoint(y2, uv)
+    # interleaved rows: pitch 2W, set a on even rows, set b on odd rows -> interval overlap (conservative)
+    a = gpu.plane_set(0, W, 4, 2 * W)
+    b = gpu.plane_set(W, W, 4, 2 * W)
+    assert not gpu.sets_disjoint(a, b)
+    c = gpu.plane_set(8 * W, W, 4, 2 * W)
+    assert gpu.sets_disjoint(a, c)

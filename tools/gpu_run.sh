@@ -1,0 +1,71 @@
+#!/bin/bash
+# The one GPU-session runner (replaces round 1's per-session gpu_roundN.sh).
+#   TAG=r02a tools/gpu_run.sh STEP [STEP ...]
+# Steps (run in the order given, each under its own time limit, stopping at the
+# first failure; outputs under gpurun_out/):
+#   tests      pytest -m gpu over tests/ (one process)
+#   smoke      __graft_entry__.smoke()
+#   bench      bench.py (default line: N=1, cfg 2 hot path, cpu_baseline)
+#   bench4     bench.py --config 4 (CTU-sharded config 4, N=1)
+#   rehearse2  bench.py --gpus 2 on the one GPU (gloo, both ranks on device 0)
+#   prof       rocprofv3 --kernel-trace --stats of bench.py
+#   pmc        the FETCH_SIZE and WRITE_SIZE passes of bench.py (MI355X_MICROARCH.md §HBM)
+#   configs    tools/bench_configs.py (configs 3/4/5 + frame driver)
+#   percall    tools/percall.py (drop-in per-call cost)
+# Extra pytest args: PYTEST_K="-k expr"; bench args: BENCH_ARGS="...".
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r02}
+STEPS=${STEPS:-20}
+FRAMES=${FRAMES:-128}
+PT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
+
+run_step() {
+  case "$1" in
+    tests)
+      echo "== pytest -m gpu"
+      timeout -k 10 900 $PT tests -m gpu $PYTEST_K > gpurun_out/pytest_gpu_${TAG}.log 2>&1; rc=$?
+      tail -5 gpurun_out/pytest_gpu_${TAG}.log; return $rc ;;
+    smoke)
+      echo "== smoke"
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1; rc=$?
+      tail -3 gpurun_out/smoke_${TAG}.log; return $rc ;;
+    bench)
+      echo "== bench"
+      timeout -k 10 300 python bench.py --steps $STEPS --warmup 5 --frames $FRAMES $BENCH_ARGS > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err; rc=$?
+      cat gpurun_out/bench_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/bench_${TAG}.err; return $rc ;;
+    bench4)
+      echo "== bench --config 4"
+      timeout -k 10 300 python bench.py --config 4 --steps 10 --warmup 3 $BENCH_ARGS > gpurun_out/bench4_${TAG}.json 2> gpurun_out/bench4_${TAG}.err; rc=$?
+      cat gpurun_out/bench4_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/bench4_${TAG}.err; return $rc ;;
+    rehearse2)
+      echo "== bench --gpus 2 rehearsal (gloo, one device)"
+      NH_DIST_BACKEND=gloo NH_FORCE_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --frames 32 $BENCH_ARGS > gpurun_out/rehearse2_${TAG}.json 2> gpurun_out/rehearse2_${TAG}.err; rc=$?
+      cat gpurun_out/rehearse2_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/rehearse2_${TAG}.err; return $rc ;;
+    prof)
+      echo "== rocprof kernel-trace stats"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --steps $STEPS --warmup 5 --frames $FRAMES --no-cpu-baseline $BENCH_ARGS > gpurun_out/prof_${TAG}.log 2>&1; rc=$?
+      tail -2 gpurun_out/prof_${TAG}.log; return $rc ;;
+    pmc)
+      echo "== rocprof pmc FETCH_SIZE / WRITE_SIZE"
+      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_${TAG} -o run -- python3 bench.py --steps 5 --warmup 2 --frames $FRAMES --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc_fetch_${TAG}.log 2>&1 && \
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_${TAG} -o run -- python3 bench.py --steps 5 --warmup 2 --frames $FRAMES --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc_write_${TAG}.log 2>&1 ;;
+    configs)
+      echo "== bench_configs"
+      timeout -k 10 400 python tools/bench_configs.py $CONFIGS_ARGS > gpurun_out/configs_${TAG}.jsonl 2> gpurun_out/configs_${TAG}.err; rc=$?
+      cat gpurun_out/configs_${TAG}.jsonl; [ $rc -eq 0 ] || tail -20 gpurun_out/configs_${TAG}.err; return $rc ;;
+    percall)
+      echo "== per-call cost"
+      timeout -k 10 300 python tools/percall.py > gpurun_out/percall_${TAG}.json 2> gpurun_out/percall_${TAG}.err; rc=$?
+      tail -3 gpurun_out/percall_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/percall_${TAG}.err; return $rc ;;
+    *)
+      echo "unknown step $1"; return 2 ;;
+  esac
+}
+
+for s in "$@"; do
+  run_step "$s" || { echo "== step $s failed (rc=$?); stopping"; exit 1; }
+done
+echo "== done"
