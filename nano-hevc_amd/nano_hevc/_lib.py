@@ -138,8 +138,9 @@ def device_count() -> int:
     return n.value
 
 
-def check(rc: int, what: str = ""):
-    """Map an NH_E* code to the exception the reference raises in that case."""
+def check(rc: int, what: str = "", lib=None):
+    """Map an NH_E* code to the exception the reference raises in that case
+    (``lib``: the library that returned it, for its last-error text)."""
     if rc == NH_OK:
         return
     msg = f"{what}: " if what else ""
@@ -153,7 +154,7 @@ def check(rc: int, what: str = ""):
         raise ZeroDivisionError(msg + "integer division or modulo by zero")
     if rc == NH_ENODEV:
         raise NanoHevcUnavailable(msg + "no HIP device visible: nano_hevc (MI355X) has no CPU fallback")
-    err = load().nh_last_error().decode(errors="replace")
+    err = (lib or load()).nh_last_error().decode(errors="replace")
     if rc == NH_EARG:
         raise ValueError(msg + "bad argument: " + err)
     raise RuntimeError(msg + f"HIP error {rc}: {err}")

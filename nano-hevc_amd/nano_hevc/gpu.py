@@ -125,7 +125,7 @@ def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = T
     L = _lib.load() if int(variant) in PRODUCT_VARIANTS else _lib.load_ab()   # the A/B forms live in the A/B build
     check(L.nh_fwd8x8_quant_planes_variant(res.data_ptr(), out.data_ptr(), arr, len(sets), int(qp),
                                            int(bool(is_intra)), int(variant), C.c_void_p(_stream(stream, res.device))),
-          "fwd8x8_quant")
+          "fwd8x8_quant", L)
     return out
 
 

@@ -8,6 +8,7 @@
 #   bench      bench.py (default line: N=1, cfg 2 hot path, cpu_baseline)
 #   bench4     bench.py --config 4 (CTU-sharded config 4, N=1)
 #   rehearse2  bench.py --gpus 2 on the one GPU (gloo, both ranks on device 0)
+#   rehearse4  the same for --config 4, with the gathered-recon check
 #   prof       rocprofv3 --kernel-trace --stats of bench.py
 #   pmc        the FETCH_SIZE and WRITE_SIZE passes of bench.py (MI355X_MICROARCH.md §HBM)
 #   configs    tools/bench_configs.py (configs 3/4/5 + frame driver)
@@ -44,6 +45,10 @@ run_step() {
       echo "== bench --gpus 2 rehearsal (gloo, one device)"
       NH_DIST_BACKEND=gloo NH_FORCE_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --frames 32 $BENCH_ARGS > gpurun_out/rehearse2_${TAG}.json 2> gpurun_out/rehearse2_${TAG}.err; rc=$?
       cat gpurun_out/rehearse2_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/rehearse2_${TAG}.err; return $rc ;;
+    rehearse4)
+      echo "== bench --config 4 --gpus 2 rehearsal (gloo, one device, --check)"
+      NH_DIST_BACKEND=gloo NH_FORCE_DEVICE=0 timeout -k 10 400 python bench.py --config 4 --gpus 2 --steps 3 --warmup 1 --frames 4 --check $BENCH_ARGS > gpurun_out/rehearse4_${TAG}.json 2> gpurun_out/rehearse4_${TAG}.err; rc=$?
+      cat gpurun_out/rehearse4_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/rehearse4_${TAG}.err; return $rc ;;
     prof)
       echo "== rocprof kernel-trace stats"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run -- python3 bench.py --steps $STEPS --warmup 5 --frames $FRAMES --no-cpu-baseline $BENCH_ARGS > gpurun_out/prof_${TAG}.log 2>&1; rc=$?
