@@ -5,6 +5,7 @@ travels to the GPU box):
 
     python tests/golden/make_fullsize.py [/root/reference] [--procs 8]
     python tests/golden/make_fullsize.py --only-closed4     # add config 4 closed loop (3 processes, ~minutes)
+    python tests/golden/make_fullsize.py --only-extra       # add the 4K YUV420 config-2 levels and the 8K config-5 chroma
 
 Inputs are regenerated from seeds by ``fullsize_inputs`` (numpy only, imported
 by tests/test_fullsize_reference_gpu.py as well), outputs are produced by the
@@ -107,6 +108,12 @@ def _cfg5_band(args):
     return r0, r1, lvl, rec
 
 
+def _cfg2_band(args):
+    src, qp, r0, r1 = args
+    MG, _, T, Q, _ = _REF
+    return r0, r1, MG.ref_plane_cfg2(T, Q, src[r0 * 8:r1 * 8], qp)
+
+
 def _cfg4_closed_plane(args):
     src, ctb, pid, seed, qp, luma = args
     MG, I, T, Q, _ = _REF
@@ -129,6 +136,31 @@ def main():
     out = {"generator": "tests/golden/make_fullsize.py", "inputs": "tests/golden/fullsize_inputs.py",
            "numpy": np.__version__, "reference": "Luodian/nano-hevc @ /root/reference"}
     dst = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else os.path.join(HERE, "fullsize.json")
+    if "--only-extra" in sys.argv:   # add config 2 (4K YUV420) and config 5 chroma to an existing fullsize.json
+        with open(dst) as f:
+            out = json.load(f)
+        with mp.get_context("fork").Pool(procs, initializer=_init, initargs=(ref,)) as pool:
+            t0 = time.time()
+            for k, src in enumerate(FI.cfg2_frame()):      # the metric's own workload: one 4K YUV420 frame
+                lvl = np.zeros_like(src)
+                for r0, r1, l in pool.imap_unordered(_cfg2_band, [(src, FI.CFG2_QP, a, b) for a, b in
+                                                                  _bands(src.shape[0] // 8, 4 * procs)]):
+                    lvl[r0 * 8:r1 * 8] = l
+                out[f"cfg2_4k_p{k}"] = {"lvl": sha(lvl)}
+            print("cfg2", time.time() - t0, flush=True)
+            t0 = time.time()
+            for k, src in enumerate(FI.cfg5_chroma(), 1):   # 8K U, V planes (3840 x 2160)
+                lvl = np.zeros(src.shape, np.int32)
+                rec = np.zeros(src.shape, np.int16)
+                for r0, r1, l, r in pool.imap_unordered(_cfg5_band, [(src, FI.CFG5_QP, a, b) for a, b in
+                                                                     _bands(src.shape[0] // 32, 4 * procs)]):
+                    lvl[r0 * 32:r1 * 32] = l[r0 * 32:r1 * 32]
+                    rec[r0 * 32:r1 * 32] = r[r0 * 32:r1 * 32]
+                out[f"cfg5_{'uv'[k - 1]}"] = {"lvl": sha(lvl), "rec": sha(rec)}
+            print("cfg5 chroma", time.time() - t0, flush=True)
+        with open(dst, "w") as f:
+            json.dump(out, f, indent=1, sort_keys=True)
+        return
     if "--only-closed4" in sys.argv:   # add config 4 closed loop to an existing fullsize.json
         with open(dst) as f:
             out = json.load(f)

@@ -5,9 +5,10 @@ tests/golden/fullsize.json holds sha256 hashes of what the reference's
 functions, composed as DESIGN.md §3.3-3.5 / §3.7 define the drivers, produce
 on the frames of tests/golden/fullsize_inputs.py (generated in the build
 container by tests/golden/make_fullsize.py; the reference never travels here):
-config 3 on a 1080p YUV420 frame in open and closed loop, config 4 on a 4K
-YUV420 frame in open and closed loop, config 5 on an 8K luma plane (int8-MFMA
-and butterfly kernels).
+config 2 (the headline 8x8 DCT+quant) on a 4K YUV420 residual frame, config 3
+on a 1080p YUV420 frame in open and closed loop, config 4 on a 4K YUV420 frame
+in open and closed loop, config 5 on the three planes of an 8K YUV420 frame
+(int8-MFMA and butterfly kernels).
 """
 import hashlib
 import json
@@ -98,6 +99,34 @@ def test_cfg4_4k_equals_reference(ref, torch_dev):
         assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
         assert sha(tuy[0] if k == 0 else tuc[k - 1]) == e["tu"], k
         off += ph * pw
+
+
+def test_cfg2_4k_yuv420_equals_reference(ref, torch_dev):
+    """The metric's own workload: every 8x8 block of a 4K YUV420 residual frame
+    through forward_transform + quantize_block (transform.py:154-196,
+    quant.py:126-137), all three planes hashed against the reference."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = FI.cfg2_frame()
+    h, w = planes[0].shape
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    out = gpu.fwd8x8_quant(torch.from_numpy(buf).cuda(), gpu.yuv420_plane_sets(1, w, h), qp=FI.CFG2_QP)
+    out = out.cpu().numpy()
+    off = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        assert sha(out[off:off + ph * pw].reshape(ph, pw)) == ref[f"cfg2_4k_p{k}"]["lvl"], k
+        off += ph * pw
+
+
+@pytest.mark.parametrize("variant", [1, 0])   # int8 MFMA, butterfly
+def test_cfg5_8k_chroma_equals_reference(ref, torch_dev, variant):
+    torch = torch_dev
+    from nano_hevc import gpu
+    for name, src in zip("uv", FI.cfg5_chroma()):
+        l, r = gpu.tc32_plane(torch.from_numpy(src).cuda(), FI.CFG5_QP, variant)
+        assert sha(l.cpu().numpy()) == ref[f"cfg5_{name}"]["lvl"], name
+        assert sha(r.cpu().numpy()) == ref[f"cfg5_{name}"]["rec"], name
 
 
 @pytest.mark.parametrize("variant", [1, 0])   # int8 MFMA, butterfly

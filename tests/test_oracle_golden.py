@@ -256,6 +256,11 @@ def test_oracle_at_full_size_equals_reference():
         assert (sha(l), sha(r), sha(t)) == tuple(ref[f"cfg4_p{k}"][x] for x in ("lvl", "rec", "tu")), k
     l, r = O.tc32_plane(FI.cfg5_plane(), FI.CFG5_QP)
     assert (sha(l), sha(r)) == (ref["cfg5_y"]["lvl"], ref["cfg5_y"]["rec"])
+    for name, src in zip("uv", FI.cfg5_chroma()):   # 8K chroma planes
+        l, r = O.tc32_plane(src, FI.CFG5_QP)
+        assert (sha(l), sha(r)) == (ref[f"cfg5_{name}"]["lvl"], ref[f"cfg5_{name}"]["rec"]), name
+    for k, src in enumerate(FI.cfg2_frame()):   # the headline config on one 4K YUV420 frame
+        assert sha(O.fwd8x8_quant_plane(src, FI.CFG2_QP)) == ref[f"cfg2_4k_p{k}"]["lvl"], k
     for k, src in enumerate(FI.cfg4_frame()):   # config 4 in closed loop
         l, r, t = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, FI.CFG4_SEED, FI.CFG4_QP, k == 0)
         assert (sha(l), sha(r), sha(t)) == tuple(ref[f"closed4_p{k}"][x] for x in ("lvl", "rec", "tu")), k
