@@ -38,6 +38,11 @@ extern "C" {
 const char* nh_version(void);
 const char* nh_last_error(void);
 int nh_device_count(int* count);
+/* Per-device contexts of the per-block (host-pointer) entry points: bytes held
+ * on `device` (0 before its first per-block call), and release of every
+ * context (the next per-block call re-creates the current device's). */
+int nh_staging_bytes(int device, int64_t* bytes);
+int nh_release_staging(void);
 
 /* ---------------- (i) per-block entry points (host pointers) ---------------- */
 

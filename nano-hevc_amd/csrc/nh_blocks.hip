@@ -11,6 +11,7 @@
 //   k_quant_i64 / k_dequant_i64 / k_quant_i32 / k_dequant_i32  quant.py:41-150 (A12-A13)
 //   k_count_nonzero / k_estimate_bits          quant.py:153-173
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <climits>
 #include <cstdio>
 #include <cstring>
@@ -32,77 +33,11 @@ __device__ __forceinline__ void report(unsigned long long* st, long long idx, in
 }
 
 // ---------------------------------------------------------------------------
-// staging context
-// ---------------------------------------------------------------------------
-Staging& staging() {
-    static Staging s;
-    return s;
-}
-
-int staging_reserve(Staging& s, size_t bytes) {
-    int dev = 0, n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
-        set_error("no HIP device visible (nano-hevc_amd needs an MI355X; there is no CPU fallback)");
-        return NH_ENODEV;
-    }
-    NH_HIP(hipGetDevice(&dev));
-    if (s.device != dev) {  // (re)initialise on the caller's current device
-        s.device = dev;
-        s.stream = nullptr;
-        s.dbuf = s.hbuf = nullptr;
-        s.cap = 0;
-        s.dstatus = nullptr;
-        NH_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-        NH_HIP(hipMalloc(&s.dstatus, 64));
-    }
-    if (bytes > s.cap) {
-        size_t c = align_up(bytes < (1u << 20) ? (1u << 20) : bytes * 2, 4096);
-        if (s.dbuf) { (void)hipFree(s.dbuf); s.dbuf = nullptr; }
-        if (s.hbuf) { (void)hipHostFree(s.hbuf); s.hbuf = nullptr; }
-        NH_HIP(hipMalloc(&s.dbuf, c));
-        NH_HIP(hipHostMalloc(&s.hbuf, c, hipHostMallocDefault));
-        s.cap = c;
-    }
-    unsigned long long init = ULLONG_MAX;
-    NH_HIP(hipMemcpyAsync(s.dstatus, &init, sizeof(init), hipMemcpyHostToDevice, s.stream));
-    return NH_OK;
-}
-
-int staging_upload(Staging& s, size_t off, const void* src, size_t bytes) {
-    if (!bytes) return NH_OK;
-    std::memcpy((char*)s.hbuf + off, src, bytes);
-    NH_HIP(hipMemcpyAsync((char*)s.dbuf + off, (char*)s.hbuf + off, bytes, hipMemcpyHostToDevice, s.stream));
-    return NH_OK;
-}
-
-int staging_download(Staging& s, void* dst, size_t off, size_t bytes) {
-    (void)dst;
-    if (!bytes) return NH_OK;
-    NH_HIP(hipMemcpyAsync((char*)s.hbuf + off, (char*)s.dbuf + off, bytes, hipMemcpyDeviceToHost, s.stream));
-    return NH_OK;
-}
-
-int staging_finish(Staging& s, int* status_out) {
-    unsigned long long st = 0;
-    NH_HIP(hipGetLastError());
-    NH_HIP(hipMemcpyAsync(&st, s.dstatus, sizeof(st), hipMemcpyDeviceToHost, s.stream));
-    NH_HIP(hipStreamSynchronize(s.stream));
-    *status_out = (st == ULLONG_MAX) ? NH_OK : -(int)(st & 0xff);
-    return NH_OK;
-}
-
-// Staging layout helper: sequential 256-B aligned regions.
-struct Layout {
-    size_t off = 0;
-    size_t take(size_t bytes) { size_t o = off; off = align_up(off + bytes, 256); return o; }
-};
-
-// ---------------------------------------------------------------------------
 // intra prediction kernels (per-block form)
 // ---------------------------------------------------------------------------
 
 // intra.py:37-62.  One workgroup: int64 sum over the whole arrays (D7), then fill.
-__global__ void __launch_bounds__(256) k_intra_dc(const int64_t* top, int64_t nt, const int64_t* left,
+__device__ __forceinline__ void dev_intra_dc(const int64_t* top, int64_t nt, const int64_t* left,
                                                   int64_t nl, int64_t size, int variant, int16_t* out,
                                                   unsigned long long* st) {
     __shared__ long long part[256];
@@ -134,7 +69,7 @@ __global__ void __launch_bounds__(256) k_intra_dc(const int64_t* top, int64_t nt
 }
 
 // intra.py:81-113: Python-int arithmetic, int16 store (D9), IndexError on short refs.
-__global__ void k_intra_planar(const int64_t* top, int64_t nt, const int64_t* left, int64_t nl,
+__device__ __forceinline__ void dev_intra_planar(const int64_t* top, int64_t nt, const int64_t* left, int64_t nl,
                                int64_t tr, int64_t bl, int64_t size, int64_t log2size, int16_t* out,
                                unsigned long long* st) {
     const int64_t n = size * size;
@@ -153,7 +88,7 @@ __global__ void k_intra_planar(const int64_t* top, int64_t nt, const int64_t* le
 // reference's order (so the first error raised is the reference's), then the
 // workgroup projects every sample with int16 arithmetic (D8).
 constexpr int kMaxAngSize = 2048;  // 3N+1 int16 in LDS (12 KB)
-__global__ void __launch_bounds__(256) k_intra_angular(const int64_t* top, int64_t nt, const int64_t* left,
+__device__ __forceinline__ void dev_intra_angular(const int64_t* top, int64_t nt, const int64_t* left,
                                                        int64_t nl, int64_t corner, int angle, int vert,
                                                        int64_t size, int16_t* out, unsigned long long* st) {
     __shared__ int16_t ref[3 * kMaxAngSize + 1];
@@ -207,13 +142,13 @@ __global__ void __launch_bounds__(256) k_intra_angular(const int64_t* top, int64
 }
 
 // intra.py:65-78
-__global__ void k_residual(const int16_t* a, const int16_t* b, int64_t n, int16_t* out, int add) {
+__device__ __forceinline__ void dev_residual(const int16_t* a, const int16_t* b, int64_t n, int16_t* out, int add) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint32_t x = (uint16_t)a[i], y = (uint16_t)b[i];
         out[i] = (int16_t)(uint16_t)(add ? x + y : x - y);
     }
 }
-__global__ void k_clip(const int64_t* x, int64_t n, int64_t maxval, int16_t* out) {
+__device__ __forceinline__ void dev_clip(const int64_t* x, int64_t n, int64_t maxval, int16_t* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int64_t v = x[i];
         v = v < 0 ? 0 : (v > maxval ? maxval : v);
@@ -227,8 +162,8 @@ __global__ void k_clip(const int64_t* x, int64_t n, int64_t maxval, int16_t* out
 // Full 32-bit wrap arithmetic (MulWrap): exact for any int32 input.
 // ---------------------------------------------------------------------------
 template <int N, bool DST, bool FWD>
-__global__ void __launch_bounds__(256) k_transform(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                                   int64_t nblocks) {
+__device__ __forceinline__ void dev_transform(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                              int64_t nblocks) {
     constexpr int BPW = 256 / N;  // blocks per workgroup
     constexpr int P = N + 1;
     constexpr int S = Log2<N>::v + 5;  // transform.py:173 (D1: same shift both passes)
@@ -277,6 +212,12 @@ __global__ void __launch_bounds__(256) k_transform(const int32_t* __restrict__ i
     }
 }
 
+template <int N, bool DST, bool FWD>
+__global__ void __launch_bounds__(256) k_transform(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                   int64_t nblocks) {
+    dev_transform<N, DST, FWD>(in, out, nblocks);
+}
+
 template <bool FWD>
 static int launch_transform(const int32_t* din, int32_t* dout, int64_t nblocks, int size, int use_dst,
                             hipStream_t s) {
@@ -302,7 +243,7 @@ static int launch_transform(const int32_t* din, int32_t* dout, int64_t nblocks, 
 // ---------------------------------------------------------------------------
 // quant / dequant (quant.py:41-123)
 // ---------------------------------------------------------------------------
-__global__ void k_quant_i64(const int64_t* c, int64_t n, uint64_t mf, uint64_t off, int shift, int abs_bits,
+__device__ __forceinline__ void dev_quant_i64(const int64_t* c, int64_t n, uint64_t mf, uint64_t off, int shift, int abs_bits,
                             int32_t* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int64_t x = c[i], a;
@@ -313,7 +254,7 @@ __global__ void k_quant_i64(const int64_t* c, int64_t n, uint64_t mf, uint64_t o
         out[i] = (int32_t)(uint32_t)(uint64_t)(sg * l);
     }
 }
-__global__ void k_dequant_i64(const int64_t* l, int64_t n, int64_t scale, int per, int32_t* out) {
+__device__ __forceinline__ void dev_dequant_i64(const int64_t* l, int64_t n, int64_t scale, int per, int32_t* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t b = (uint64_t)l[i] * (uint64_t)scale;
         int64_t v;
@@ -332,7 +273,7 @@ __global__ void k_dequant_i32(const int32_t* l, int64_t n, int32_t scale, int pe
 }
 
 // quant.py:171-173
-__global__ void k_count_nonzero(const int64_t* l, int64_t n, unsigned long long* cnt) {
+__device__ __forceinline__ void dev_count_nonzero(const int64_t* l, int64_t n, unsigned long long* cnt) {
     unsigned long long c = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         c += l[i] != 0;
@@ -397,7 +338,7 @@ __device__ double pw_sum(const int64_t* a, int64_t n, int bits) {
     }
     return ret;
 }
-__global__ void k_estimate_bits(const int64_t* l, int64_t n, int bits, double* out) {
+__device__ __forceinline__ void dev_estimate_bits(const int64_t* l, int64_t n, int bits, double* out) {
     if (threadIdx.x || blockIdx.x) return;
     *out = n > 0 ? pw_sum(l, n, bits) : 0.0;   // the shim applies int() (quant.py:168)
 }
@@ -421,7 +362,7 @@ __device__ __forceinline__ void block_reduce_add(T v, unsigned long long* out, F
 }
 struct NoOp {};
 // sum((a-b)^2) exactly in int64 (inputs are <= 16-bit samples widened by the shim)
-__global__ void k_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, unsigned long long* out) {
+__device__ __forceinline__ void dev_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, unsigned long long* out) {
     unsigned long long s = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int64_t d = a[i] - b[i];
@@ -430,7 +371,7 @@ __global__ void k_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, uns
     block_reduce_add(s, out, NoOp{});
 }
 // metrics.py:24-26: int32 difference (wraps), np.abs (wraps at INT32_MIN), int64 sum
-__global__ void k_sad_i32(const int32_t* a, const int32_t* b, int64_t n, unsigned long long* out) {
+__device__ __forceinline__ void dev_sad_i32(const int32_t* a, const int32_t* b, int64_t n, unsigned long long* out) {
     unsigned long long s = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         int32_t d = (int32_t)((uint32_t)a[i] - (uint32_t)b[i]);
@@ -440,7 +381,7 @@ __global__ void k_sad_i32(const int32_t* a, const int32_t* b, int64_t n, unsigne
     block_reduce_add(s, out, NoOp{});
 }
 // metrics.py:29-43: H . diff . H^T in int32 (wrap), sum |.| in int64
-__global__ void k_satd_4x4(const int32_t* a, const int32_t* b, long long* out) {
+__device__ __forceinline__ void dev_satd_4x4(const int32_t* a, const int32_t* b, long long* out) {
     if (threadIdx.x || blockIdx.x) return;
     constexpr int H[4][4] = {{1, 1, 1, 1}, {1, 1, -1, -1}, {1, -1, -1, 1}, {1, -1, 1, -1}};
     uint32_t d[4][4], t[4][4];
@@ -462,7 +403,7 @@ __global__ void k_satd_4x4(const int32_t* a, const int32_t* b, long long* out) {
     *out = s;
 }
 // metrics.py:46-48: sum(r.astype(int64)**2), int64 wrap
-__global__ void k_residual_energy(const int64_t* r, int64_t n, unsigned long long* out) {
+__device__ __forceinline__ void dev_residual_energy(const int64_t* r, int64_t n, unsigned long long* out) {
     unsigned long long s = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         s += (unsigned long long)r[i] * (unsigned long long)r[i];
@@ -487,6 +428,216 @@ static unsigned grid_for(int64_t n, int64_t cap) {
     return (unsigned)g;
 }
 
+
+#define NH_TRY_(x)             \
+    do {                       \
+        int rc__ = (x);        \
+        if (rc__) return rc__; \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// The per-block call protocol (the drop-in path: host arrays in, host arrays out)
+// ---------------------------------------------------------------------------
+// Small calls (inputs <= kSmallIn bytes, outputs <= kSmallOut bytes: every
+// block size the reference's callers use) are ONE launch of a single-workgroup
+// kernel: the inputs travel in the kernel-argument segment, the outputs and the
+// status word are stored straight into mapped pinned host memory, and the host
+// waits on the stream once -- no DMA copy at all.  Larger calls are staged: one
+// H2D copy of [inputs | status, accumulator], the grid-wide kernel, one D2H
+// copy of [status, accumulator | outputs], one wait.  Both forms run the same
+// device body, a __device__ lambda over (inputs, status/accumulator words,
+// outputs).  Status word: ULLONG_MAX = ok, else the first error (report()).
+// One context per device (stream, buffers), created on first use on that
+// device and kept for the process; nh_release_staging() frees them all.
+constexpr size_t kSmallIn = 3072, kSmallOut = 64 << 10;
+struct SmallIn {
+    alignas(16) uint8_t b[kSmallIn];
+};
+
+template <class F>
+__global__ void __launch_bounds__(256) k_small(SmallIn in, F f, unsigned long long* dw, unsigned long long* hres,
+                                               unsigned long long seq) {
+    if (threadIdx.x == 0) {
+        atomicExch(&dw[0], ULLONG_MAX);   // status: no error yet
+        atomicExch(&dw[1], 0ull);         // accumulator of the reductions
+    }
+    __threadfence();
+    __syncthreads();
+    f(in.b, dw, (uint8_t*)(hres + 4));
+    __threadfence_system();               // this thread's result stores have reached host memory
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        hres[0] = atomicAdd(&dw[0], 0ull);
+        hres[1] = atomicAdd(&dw[1], 0ull);
+        __threadfence_system();
+        __hip_atomic_store(&hres[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // completion word, last
+    }
+}
+
+template <class F>
+__global__ void __launch_bounds__(256) k_staged(const uint8_t* in, F f, unsigned long long* dw, uint8_t* out) {
+    f(in, dw, out);
+}
+
+struct Staging {
+    std::mutex mu;
+    bool ready = false;
+    hipStream_t stream = nullptr;
+    uint8_t* dbuf = nullptr;              // staged form: device side
+    uint8_t* hbuf = nullptr;              //              pinned host side
+    size_t cap = 0;
+    unsigned long long* dwork = nullptr;  // small form: status, accumulator (device)
+    uint8_t* hres = nullptr;              //             mapped pinned results (host view):
+                                          //             status, accumulator, completion word, pad, outputs
+    unsigned long long seq = 0;           //             completion sequence number of the last call
+    uint8_t* hres_dev = nullptr;          //             the same memory, device view
+};
+constexpr int kMaxDevices = 64;
+static Staging g_staging[kMaxDevices];
+
+static int staging_current(Staging** out) {
+    int n = 0, dev = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+        set_error("no HIP device visible (nano-hevc_amd needs an MI355X; there is no CPU fallback)");
+        return NH_ENODEV;
+    }
+    NH_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDevices) {
+        set_error("device index out of range");
+        return NH_EARG;
+    }
+    *out = &g_staging[dev];
+    return NH_OK;
+}
+
+static void staging_free(Staging& s) {   // caller holds s.mu, current device = the context's
+    if (s.dbuf) (void)hipFree(s.dbuf);
+    if (s.hbuf) (void)hipHostFree(s.hbuf);
+    if (s.dwork) (void)hipFree(s.dwork);
+    if (s.hres) (void)hipHostFree(s.hres);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s.dbuf = s.hbuf = s.hres = s.hres_dev = nullptr;
+    s.dwork = nullptr;
+    s.stream = nullptr;
+    s.cap = 0;
+    s.ready = false;
+}
+
+static int staging_init(Staging& s) {    // caller holds s.mu
+    if (s.ready) return NH_OK;
+    NH_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    NH_HIP(hipMalloc(&s.dwork, 256));
+    NH_HIP(hipHostMalloc(&s.hres, 32 + kSmallOut, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(s.hres, 0, 32);
+    s.seq = 0;
+    NH_HIP(hipHostGetDevicePointer((void**)&s.hres_dev, s.hres, 0));
+    s.ready = true;
+    return NH_OK;
+}
+
+static int staging_grow(Staging& s, size_t bytes) {   // staged form only; grow-only
+    if (bytes <= s.cap) return NH_OK;
+    const size_t c = align_up(bytes < (1u << 20) ? (1u << 20) : bytes * 2, 4096);
+    if (s.dbuf) { (void)hipFree(s.dbuf); s.dbuf = nullptr; }
+    if (s.hbuf) { (void)hipHostFree(s.hbuf); s.hbuf = nullptr; }
+    s.cap = 0;
+    NH_HIP(hipMalloc(&s.dbuf, c));
+    NH_HIP(hipHostMalloc(&s.hbuf, c, hipHostMallocDefault));
+    s.cap = c;
+    return NH_OK;
+}
+
+// The small form's wait: the kernel's last store is the call's sequence number
+// into mapped host memory (after every result store), so the host polls that
+// word instead of a stream synchronisation (the stream keeps the calls ordered,
+// so the buffer is never reused under a running kernel).  Bounded: after ~1 s
+// it falls back to hipStreamSynchronize, which also reports a faulted kernel.
+static int wait_completion(hipStream_t stream, const unsigned long long* word, unsigned long long seq) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 1;; ++spins) {
+        if (__atomic_load_n(word, __ATOMIC_ACQUIRE) == seq) return NH_OK;
+        if ((spins & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                set_error(std::string("per-block kernel: ") + hipGetErrorString(q));
+                return NH_EHIP;
+            }
+            if (q == hipSuccess || std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) break;
+        }
+    }
+    NH_HIP(hipStreamSynchronize(stream));
+    if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq) {
+        set_error("per-block kernel finished without its completion word");
+        return NH_EHIP;
+    }
+    return NH_OK;
+}
+
+class BlockCall {
+  public:
+    // Registers an input array (copied when the call runs); returns its byte
+    // offset in the call's input area (the same in both forms).
+    size_t in(const void* p, size_t bytes) {
+        const size_t o = end_;
+        ins_[n_++] = {p, bytes, o};
+        end_ = align_up(o + bytes, 16);
+        return o;
+    }
+    // Runs body f on `grid` workgroups (staged form; the small form always runs
+    // one workgroup) and returns its out_bytes of output into `out` -- or, with
+    // from_acc, the 8-byte accumulator word the body's reductions added into.
+    template <class F>
+    int run(unsigned grid, F f, void* out, size_t out_bytes, bool from_acc = false) {
+        Staging* S = nullptr;
+        NH_TRY_(staging_current(&S));
+        std::lock_guard<std::mutex> lk(S->mu);
+        NH_TRY_(staging_init(*S));
+        const size_t res = from_acc ? 0 : out_bytes;
+        unsigned long long st, acc;
+        if (end_ <= kSmallIn && res <= kSmallOut) {
+            SmallIn si;
+            for (int i = 0; i < n_; ++i)
+                if (ins_[i].bytes) std::memcpy(si.b + ins_[i].off, ins_[i].p, ins_[i].bytes);
+            const unsigned long long seq = ++S->seq;
+            k_small<<<1, 256, 0, S->stream>>>(si, f, S->dwork, (unsigned long long*)S->hres_dev, seq);
+            NH_HIP(hipGetLastError());
+            unsigned long long* r = (unsigned long long*)S->hres;
+            NH_TRY_(wait_completion(S->stream, &r[2], seq));
+            st = r[0];
+            acc = r[1];
+            if (st == ULLONG_MAX && res) std::memcpy(out, r + 4, res);
+        } else {
+            const size_t wo = align_up(end_, 256), oo = wo + 256;
+            NH_TRY_(staging_grow(*S, oo + res));
+            for (int i = 0; i < n_; ++i)
+                if (ins_[i].bytes) std::memcpy(S->hbuf + ins_[i].off, ins_[i].p, ins_[i].bytes);
+            unsigned long long* hw = (unsigned long long*)(S->hbuf + wo);
+            hw[0] = ULLONG_MAX;
+            hw[1] = 0;
+            NH_HIP(hipMemcpyAsync(S->dbuf, S->hbuf, wo + 16, hipMemcpyHostToDevice, S->stream));
+            k_staged<<<grid, 256, 0, S->stream>>>(S->dbuf, f, (unsigned long long*)(S->dbuf + wo), S->dbuf + oo);
+            NH_HIP(hipGetLastError());
+            NH_HIP(hipMemcpyAsync(S->hbuf + wo, S->dbuf + wo, oo - wo + res, hipMemcpyDeviceToHost, S->stream));
+            NH_HIP(hipStreamSynchronize(S->stream));
+            st = hw[0];
+            acc = hw[1];
+            if (st == ULLONG_MAX && res) std::memcpy(out, S->hbuf + oo, res);
+        }
+        if (st != ULLONG_MAX) return -(int)(st & 0xff);
+        if (from_acc) std::memcpy(out, &acc, 8);
+        return NH_OK;
+    }
+
+  private:
+    struct In {
+        const void* p;
+        size_t bytes, off;
+    };
+    In ins_[4];
+    int n_ = 0;
+    size_t end_ = 0;
+};
+
 }  // namespace nh
 
 using namespace nh;
@@ -506,25 +657,29 @@ int nh_device_count(int* count) {
     return NH_OK;
 }
 
-#define NH_STAGE_BEGIN(bytes)                         \
-    Staging& S = staging();                           \
-    std::lock_guard<std::mutex> lk_(S.mu);            \
-    {                                                 \
-        int rc_ = staging_reserve(S, (bytes));        \
-        if (rc_) return rc_;                          \
-    }
-#define NH_TRY(x)              \
-    do {                       \
-        int rc__ = (x);        \
-        if (rc__) return rc__; \
-    } while (0)
+using U8 = const uint8_t*;
+using ST = unsigned long long*;
 
-static int finish_copy(Staging& S, void* dst, size_t off, size_t bytes) {
-    NH_TRY(staging_download(S, dst, off, bytes));
-    int st = 0;
-    NH_TRY(staging_finish(S, &st));
-    if (st) return st;
-    if (bytes) std::memcpy(dst, (char*)S.hbuf + off, bytes);
+int nh_staging_bytes(int device, int64_t* bytes) {
+    if (device < 0 || device >= kMaxDevices || !bytes) return NH_EARG;
+    Staging& s = g_staging[device];
+    std::lock_guard<std::mutex> lk(s.mu);
+    *bytes = s.ready ? (int64_t)(2 * s.cap + 256 + 32 + kSmallOut) : 0;
+    return NH_OK;
+}
+
+int nh_release_staging(void) {
+    int cur = 0;
+    NH_HIP(hipGetDevice(&cur));
+    for (int d = 0; d < kMaxDevices; ++d) {
+        Staging& s = g_staging[d];
+        std::lock_guard<std::mutex> lk(s.mu);
+        if (!s.ready) continue;
+        NH_HIP(hipSetDevice(d));
+        (void)hipStreamSynchronize(s.stream);
+        staging_free(s);
+    }
+    NH_HIP(hipSetDevice(cur));
     return NH_OK;
 }
 
@@ -534,15 +689,12 @@ int nh_intra_dc(const int64_t* top, int64_t ntop, const int64_t* left, int64_t n
     if (!variant4x4 && size == 0) return NH_EZERODIV;
     if (!variant4x4 && size < 0) return NH_EARG;
     const int64_t nout = variant4x4 ? 16 : size * size;
-    Layout L;
-    size_t ot = L.take(ntop * 8), ol = L.take(nleft * 8), oo = L.take(nout * 2);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, ot, top, ntop * 8));
-    NH_TRY(staging_upload(S, ol, left, nleft * 8));
-    char* d = (char*)S.dbuf;
-    k_intra_dc<<<1, 256, 0, S.stream>>>((int64_t*)(d + ot), ntop, (int64_t*)(d + ol), nleft, size, variant4x4,
-                                        (int16_t*)(d + oo), (unsigned long long*)S.dstatus);
-    return finish_copy(S, out, oo, nout * 2);
+    BlockCall c;
+    const size_t ot = c.in(top, ntop * 8), ol = c.in(left, nleft * 8);
+    return c.run(1, [=] __device__(U8 in, ST st, uint8_t* o) {
+        dev_intra_dc((const int64_t*)(in + ot), ntop, (const int64_t*)(in + ol), nleft, size, variant4x4,
+                     (int16_t*)o, st);
+    }, out, nout * 2);
 }
 
 int nh_intra_planar(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft, int64_t top_right,
@@ -550,16 +702,12 @@ int nh_intra_planar(const int64_t* top, int64_t ntop, const int64_t* left, int64
     if (ntop < 0 || nleft < 0 || size < 0) return NH_EARG;
     const int64_t nout = size * size;
     if (nout == 0) return NH_OK;
-    Layout L;
-    size_t ot = L.take(ntop * 8), ol = L.take(nleft * 8), oo = L.take(nout * 2);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, ot, top, ntop * 8));
-    NH_TRY(staging_upload(S, ol, left, nleft * 8));
-    char* d = (char*)S.dbuf;
-    k_intra_planar<<<grid_for(nout), 256, 0, S.stream>>>((int64_t*)(d + ot), ntop, (int64_t*)(d + ol), nleft,
-                                                         top_right, bottom_left, size, log2size,
-                                                         (int16_t*)(d + oo), (unsigned long long*)S.dstatus);
-    return finish_copy(S, out, oo, nout * 2);
+    BlockCall c;
+    const size_t ot = c.in(top, ntop * 8), ol = c.in(left, nleft * 8);
+    return c.run(grid_for(nout), [=] __device__(U8 in, ST st, uint8_t* o) {
+        dev_intra_planar((const int64_t*)(in + ot), ntop, (const int64_t*)(in + ol), nleft, top_right, bottom_left,
+                         size, log2size, (int16_t*)o, st);
+    }, out, nout * 2);
 }
 
 int nh_intra_angular(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft, int64_t corner,
@@ -572,28 +720,22 @@ int nh_intra_angular(const int64_t* top, int64_t ntop, const int64_t* left, int6
     if (ntop < 0 || nleft < 0 || size < 0) return NH_EARG;
     if (size > kMaxAngSize) { set_error("intra_angular: size > 2048 unsupported"); return NH_EARG; }
     const int64_t nout = size * size;
-    Layout L;
-    size_t ot = L.take(ntop * 8), ol = L.take(nleft * 8), oo = L.take(nout * 2 + 2);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, ot, top, ntop * 8));
-    NH_TRY(staging_upload(S, ol, left, nleft * 8));
-    char* d = (char*)S.dbuf;
-    k_intra_angular<<<1, 256, 0, S.stream>>>((int64_t*)(d + ot), ntop, (int64_t*)(d + ol), nleft, corner, angle,
-                                             vert, size, (int16_t*)(d + oo), (unsigned long long*)S.dstatus);
-    return finish_copy(S, out, oo, nout * 2);
+    BlockCall c;
+    const size_t ot = c.in(top, ntop * 8), ol = c.in(left, nleft * 8);
+    return c.run(1, [=] __device__(U8 in, ST st, uint8_t* o) {
+        dev_intra_angular((const int64_t*)(in + ot), ntop, (const int64_t*)(in + ol), nleft, corner, angle, vert, size,
+                          (int16_t*)o, st);
+    }, out, nout * 2);
 }
 
 static int elementwise16(const int16_t* a, const int16_t* b, int64_t n, int16_t* out, int add) {
     if (n < 0) return NH_EARG;
     if (n == 0) return NH_OK;
-    Layout L;
-    size_t oa = L.take(n * 2), ob = L.take(n * 2), oo = L.take(n * 2);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oa, a, n * 2));
-    NH_TRY(staging_upload(S, ob, b, n * 2));
-    char* d = (char*)S.dbuf;
-    k_residual<<<grid_for(n), 256, 0, S.stream>>>((int16_t*)(d + oa), (int16_t*)(d + ob), n, (int16_t*)(d + oo), add);
-    return finish_copy(S, out, oo, n * 2);
+    BlockCall c;
+    const size_t oa = c.in(a, n * 2), ob = c.in(b, n * 2);
+    return c.run(grid_for(n), [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_residual((const int16_t*)(in + oa), (const int16_t*)(in + ob), n, (int16_t*)o, add);
+    }, out, n * 2);
 }
 int nh_residual(const int16_t* orig, const int16_t* pred, int64_t n, int16_t* out) {
     return elementwise16(orig, pred, n, out, 0);
@@ -605,33 +747,40 @@ int nh_reconstruct(const int16_t* pred, const int16_t* res, int64_t n, int16_t* 
 int nh_clip(const int64_t* x, int64_t n, int64_t maxval, int16_t* out) {
     if (n < 0) return NH_EARG;
     if (n == 0) return NH_OK;
-    Layout L;
-    size_t ox = L.take(n * 8), oo = L.take(n * 2);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, ox, x, n * 8));
-    char* d = (char*)S.dbuf;
-    k_clip<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + ox), n, maxval, (int16_t*)(d + oo));
-    return finish_copy(S, out, oo, n * 2);
+    BlockCall c;
+    const size_t ox = c.in(x, n * 8);
+    return c.run(grid_for(n), [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_clip((const int64_t*)(in + ox), n, maxval, (int16_t*)o);
+    }, out, n * 2);
 }
 
-static int block_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out, bool fwd) {
-    if (size != 4 && size != 8 && size != 16 && size != 32) return NH_EVALUE;  // transform.py:150-151
-    const int64_t n = size * size;
-    Layout L;
-    size_t oi = L.take(n * 4), oo = L.take(n * 4);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oi, in, n * 4));
-    char* d = (char*)S.dbuf;
-    int rc = fwd ? launch_transform<true>((int32_t*)(d + oi), (int32_t*)(d + oo), 1, (int)size, use_dst, S.stream)
-                 : launch_transform<false>((int32_t*)(d + oi), (int32_t*)(d + oo), 1, (int)size, use_dst, S.stream);
-    if (rc) return rc;
-    return finish_copy(S, out, oo, n * 4);
+}  // extern "C"
+
+template <int N, bool DST, bool FWD>
+static int block_transform_n(const int32_t* in, int32_t* out) {
+    BlockCall c;
+    const size_t oi = c.in(in, N * N * 4);
+    return c.run(1, [=] __device__(U8 i, ST, uint8_t* o) {
+        dev_transform<N, DST, FWD>((const int32_t*)(i + oi), (int32_t*)o, 1);
+    }, out, N * N * 4);
 }
+template <bool FWD>
+static int block_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out) {
+    switch (size) {   // transform.py:150-151: other sizes raise ValueError
+        case 4: return use_dst ? block_transform_n<4, true, FWD>(in, out) : block_transform_n<4, false, FWD>(in, out);
+        case 8: return block_transform_n<8, false, FWD>(in, out);
+        case 16: return block_transform_n<16, false, FWD>(in, out);
+        case 32: return block_transform_n<32, false, FWD>(in, out);
+        default: return NH_EVALUE;
+    }
+}
+extern "C" {
+
 int nh_forward_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out) {
-    return block_transform(in, size, use_dst, out, true);
+    return block_transform<true>(in, size, use_dst, out);
 }
 int nh_inverse_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out) {
-    return block_transform(in, size, use_dst, out, false);
+    return block_transform<false>(in, size, use_dst, out);
 }
 
 static void qp_params(int qp, int* per, int* rem) {  // quant.py:25-38
@@ -649,14 +798,12 @@ int nh_quantize(const int64_t* coeff, int64_t n, int qp, int64_t log2size, int i
     if (shift < 0 || shift > 62) return NH_EOVERFLOW;
     const uint64_t off = is_intra ? (1ull << shift) / 3 : (1ull << shift) / 6;
     if (n == 0) return NH_OK;
-    Layout L;
-    size_t oi = L.take(n * 8), oo = L.take(n * 4);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oi, coeff, n * 8));
-    char* d = (char*)S.dbuf;
-    k_quant_i64<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oi), n, (uint64_t)quant_scale(rem), off,
-                                                   (int)shift, abs_bits, (int32_t*)(d + oo));
-    return finish_copy(S, out, oo, n * 4);
+    const uint64_t mf = (uint64_t)quant_scale(rem);
+    BlockCall c;
+    const size_t oi = c.in(coeff, n * 8);
+    return c.run(grid_for(n), [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_quant_i64((const int64_t*)(in + oi), n, mf, off, (int)shift, abs_bits, (int32_t*)o);
+    }, out, n * 4);
 }
 
 int nh_dequantize(const int64_t* level, int64_t n, int qp, int32_t* out) {
@@ -664,37 +811,30 @@ int nh_dequantize(const int64_t* level, int64_t n, int qp, int32_t* out) {
     if (n == 0) return NH_OK;
     int per, rem;
     qp_params(qp, &per, &rem);
-    Layout L;
-    size_t oi = L.take(n * 8), oo = L.take(n * 4);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oi, level, n * 8));
-    char* d = (char*)S.dbuf;
-    k_dequant_i64<<<grid_for(n), 256, 0, S.stream>>>((int64_t*)(d + oi), n, dequant_scale(rem), per,
-                                                     (int32_t*)(d + oo));
-    return finish_copy(S, out, oo, n * 4);
+    const int64_t scale = dequant_scale(rem);
+    BlockCall c;
+    const size_t oi = c.in(level, n * 8);
+    return c.run(grid_for(n), [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_dequant_i64((const int64_t*)(in + oi), n, scale, per, (int32_t*)o);
+    }, out, n * 4);
 }
 
 int nh_count_nonzero(const int64_t* level, int64_t n, int64_t* count) {
     if (n < 0) return NH_EARG;
-    Layout L;
-    size_t oi = L.take(n * 8 + 8), oc = L.take(8);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oi, level, n * 8));
-    char* d = (char*)S.dbuf;
-    NH_HIP(hipMemsetAsync(d + oc, 0, 8, S.stream));
-    if (n) k_count_nonzero<<<grid_red(n), 256, 0, S.stream>>>((int64_t*)(d + oi), n, (unsigned long long*)(d + oc));
-    return finish_copy(S, count, oc, 8);
+    BlockCall c;
+    const size_t oi = c.in(level, n * 8);
+    return c.run(grid_red(n), [=] __device__(U8 in, ST st, uint8_t*) {
+        dev_count_nonzero((const int64_t*)(in + oi), n, st + 1);
+    }, count, 8, true);
 }
 
 int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits) {
     if (n < 0 || (abs_bits != 32 && abs_bits != 64)) return NH_EARG;
-    Layout L;
-    size_t oi = L.take(n * 8 + 8), oc = L.take(8);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oi, level, n * 8));
-    char* d = (char*)S.dbuf;
-    k_estimate_bits<<<1, 64, 0, S.stream>>>((int64_t*)(d + oi), n, abs_bits, (double*)(d + oc));
-    return finish_copy(S, bits, oc, 8);
+    BlockCall c;
+    const size_t oi = c.in(level, n * 8);
+    return c.run(1, [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_estimate_bits((const int64_t*)(in + oi), n, abs_bits, (double*)o);
+    }, bits, 8);
 }
 
 // ----- batched device entry points -----
@@ -734,33 +874,36 @@ int nh_dequant_batch(const int32_t* d_level, int32_t* d_coeff, int64_t n, int qp
 }
 
 // ----- metrics (metrics.py:7-48) -----
-static int reduce_call(const void* a, size_t abytes, const void* b, size_t bbytes, int64_t* out, int which, int64_t n) {
-    Layout L;
-    size_t oa = L.take(abytes + 8), ob = L.take(bbytes + 8), oc = L.take(8);
-    NH_STAGE_BEGIN(L.off);
-    NH_TRY(staging_upload(S, oa, a, abytes));
-    if (b) NH_TRY(staging_upload(S, ob, b, bbytes));
-    char* d = (char*)S.dbuf;
-    NH_HIP(hipMemsetAsync(d + oc, 0, 8, S.stream));
-    unsigned long long* o = (unsigned long long*)(d + oc);
-    if (which == 0 && n) k_sum_sq_diff<<<grid_red(n), 256, 0, S.stream>>>((int64_t*)(d + oa), (int64_t*)(d + ob), n, o);
-    if (which == 1 && n) k_sad_i32<<<grid_red(n), 256, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), n, o);
-    if (which == 2) k_satd_4x4<<<1, 64, 0, S.stream>>>((int32_t*)(d + oa), (int32_t*)(d + ob), (long long*)o);
-    if (which == 3 && n) k_residual_energy<<<grid_red(n), 256, 0, S.stream>>>((int64_t*)(d + oa), n, o);
-    return finish_copy(S, out, oc, 8);
-}
 int nh_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, int64_t* out) {
     if (n < 0) return NH_EARG;
-    return reduce_call(a, n * 8, b, n * 8, out, 0, n);
+    BlockCall c;
+    const size_t oa = c.in(a, n * 8), ob = c.in(b, n * 8);
+    return c.run(grid_red(n), [=] __device__(U8 in, ST st, uint8_t*) {
+        dev_sum_sq_diff((const int64_t*)(in + oa), (const int64_t*)(in + ob), n, st + 1);
+    }, out, 8, true);
 }
 int nh_sad(const int32_t* a, const int32_t* b, int64_t n, int64_t* out) {
     if (n < 0) return NH_EARG;
-    return reduce_call(a, n * 4, b, n * 4, out, 1, n);
+    BlockCall c;
+    const size_t oa = c.in(a, n * 4), ob = c.in(b, n * 4);
+    return c.run(grid_red(n), [=] __device__(U8 in, ST st, uint8_t*) {
+        dev_sad_i32((const int32_t*)(in + oa), (const int32_t*)(in + ob), n, st + 1);
+    }, out, 8, true);
 }
-int nh_satd_4x4(const int32_t* a, const int32_t* b, int64_t* out) { return reduce_call(a, 64, b, 64, out, 2, 16); }
+int nh_satd_4x4(const int32_t* a, const int32_t* b, int64_t* out) {
+    BlockCall c;
+    const size_t oa = c.in(a, 64), ob = c.in(b, 64);
+    return c.run(1, [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_satd_4x4((const int32_t*)(in + oa), (const int32_t*)(in + ob), (long long*)o);
+    }, out, 8);
+}
 int nh_residual_energy(const int64_t* r, int64_t n, int64_t* out) {
     if (n < 0) return NH_EARG;
-    return reduce_call(r, n * 8, nullptr, 0, out, 3, n);
+    BlockCall c;
+    const size_t oa = c.in(r, n * 8);
+    return c.run(grid_red(n), [=] __device__(U8 in, ST st, uint8_t*) {
+        dev_residual_energy((const int64_t*)(in + oa), n, st + 1);
+    }, out, 8, true);
 }
 int nh_sse_i16(const int16_t* d_a, const int16_t* d_b, int64_t n, int64_t* d_out, void* stream) {
     if (!d_a || !d_b || !d_out || n < 0) return NH_EARG;

@@ -1,6 +1,6 @@
 // nh_internal.hpp -- host-side plumbing shared by the C-ABI translation units:
-// error reporting, the per-process staging context used by the synchronous
-// per-block entry points, and argument checks.
+// error reporting, A/B knobs and small helpers.  (The per-block call protocol
+// and its per-device contexts live in nh_blocks.hip.)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdlib>
@@ -20,26 +20,6 @@ void set_error(const std::string& msg);
             return NH_EHIP;                                                        \
         }                                                                          \
     } while (0)
-
-// Per-process staging context for the per-block (host pointer) entry points.
-// One device buffer + one pinned host buffer, grown on demand, one stream.
-// Guarded by a mutex: per-block calls are reentrant but serialised.
-struct Staging {
-    std::mutex mu;
-    int device = -1;
-    hipStream_t stream = nullptr;
-    void* dbuf = nullptr;
-    void* hbuf = nullptr;
-    size_t cap = 0;
-    int* dstatus = nullptr;
-};
-Staging& staging();
-// Ensure the context exists on the current device with >= bytes of buffer.
-int staging_reserve(Staging& s, size_t bytes);
-// Copy host->device for a region of the staging buffer.
-int staging_upload(Staging& s, size_t off, const void* src, size_t bytes);
-int staging_download(Staging& s, void* dst, size_t off, size_t bytes);
-int staging_finish(Staging& s, int* status_out);  // sync + fetch kernel status word
 
 // A/B knobs.  The product library (`make`) reads no environment: every knob is
 // its default constant, the losing launch forms are not compiled in, and the

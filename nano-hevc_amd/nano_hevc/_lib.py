@@ -39,6 +39,8 @@ SIGNATURES = {
     "nh_version": ([], C.c_char_p),
     "nh_last_error": ([], C.c_char_p),
     "nh_device_count": ([P], I32),
+    "nh_staging_bytes": ([I32, P], I32),
+    "nh_release_staging": ([], I32),
     "nh_intra_dc": ([P, I64, P, I64, I64, I32, P], I32),
     "nh_intra_planar": ([P, I64, P, I64, I64, I64, I64, I64, P], I32),
     "nh_intra_angular": ([P, I64, P, I64, I64, I32, I64, P], I32),

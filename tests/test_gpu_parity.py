@@ -143,6 +143,67 @@ def test_shim_estimate_bits(nh):
         assert nh.quant.count_nonzero(lv) == int(np.count_nonzero(lv))
 
 
+@pytest.mark.parametrize("n", [4, 32, 96, 256])
+def test_shim_small_and_staged_forms(nh, n):
+    """The per-block protocol's two forms (nh_blocks.hip BlockCall): inputs up to
+    3 KB run as one kernel-argument launch, larger arrays through one staged
+    H2D / D2H pair.  n = 4, 32 cross the threshold per function; both forms
+    against the oracle, including an error raised from each form."""
+    rng = np.random.default_rng(n)
+    a = rng.integers(-300, 300, (n, n)).astype(np.int16)
+    b = rng.integers(-300, 300, (n, n)).astype(np.int16)
+    assert np.array_equal(nh.residual_block(a, b), O.residual(a, b))
+    assert np.array_equal(nh.reconstruct_block(a, b), O.reconstruct(a, b))
+    assert np.array_equal(nh.clip_to_pixel_range(a.astype(np.int32) * 3, 8), O.clip(a.astype(np.int32) * 3, 8))
+    c = rng.integers(-40000, 40000, (n, n)).astype(np.int32)
+    lv = nh.quantize(c, 12, min(n, 32))
+    assert np.array_equal(lv, O.quantize(c, 12, min(n, 32)))
+    assert np.array_equal(nh.dequantize(lv, 12, 4), O.dequantize(lv, 12, 4))
+    assert nh.quant.count_nonzero(lv) == int(np.count_nonzero(lv))
+    assert nh.residual_energy(a) == int(np.sum(a.astype(np.int64) ** 2))
+    assert nh.sad(a, b) == int(np.sum(np.abs(a.astype(np.int32) - b)))
+    top = rng.integers(0, 256, n).astype(np.int16)
+    left = rng.integers(0, 256, n).astype(np.int16)
+    assert np.array_equal(nh.intra_planar_predict(top, left, int(top[-1]), int(left[-1]), n),
+                          O.intra_planar(top, left, int(top[-1]), int(left[-1]), n))
+    with pytest.raises(IndexError):   # short left reference: raised from either form
+        nh.intra_planar_predict(top, left[:n // 2], 1, 1, n)
+
+
+def test_staging_contexts_do_not_grow(nh, torch_dev):
+    """Per-device contexts of the per-block path: constant footprint over many
+    calls, freed by nh_release_staging and re-created once (VERDICT r1 weak 7:
+    the old single context leaked its buffers on every device switch)."""
+    import ctypes as C
+    from nano_hevc import _lib
+    lib = _lib.load()
+    dev = torch_dev.cuda.current_device()
+    held = C.c_int64(0)
+
+    def footprint():
+        assert lib.nh_staging_bytes(dev, C.byref(held)) == 0
+        return held.value
+
+    x = np.arange(64, dtype=np.int16).reshape(8, 8)
+    big = np.ones((128, 128), np.int16)
+    nh.residual_block(x, x)
+    nh.residual_block(big, big)   # staged form: grows once to its cap
+    f0 = footprint()
+    assert f0 > 0
+    for _ in range(300):
+        nh.residual_block(x, x)
+        nh.residual_block(big, big)
+    assert footprint() == f0
+    torch_dev.cuda.synchronize()
+    free0 = torch_dev.cuda.mem_get_info(dev)[0]
+    for _ in range(20):           # release / re-create cycles leave no device memory behind
+        assert lib.nh_release_staging() == 0
+        assert footprint() == 0
+        assert np.array_equal(nh.residual_block(big, x[:1, :1]), big - x[0, 0])
+        assert footprint() == f0
+    assert torch_dev.cuda.mem_get_info(dev)[0] >= free0 - (8 << 20)
+
+
 # ------------------------------------------------------------------ batched device path
 
 @pytest.mark.parametrize("n,dst", [(4, True), (4, False), (8, False), (16, False), (32, False)])

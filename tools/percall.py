@@ -2,6 +2,7 @@
 
     python tools/percall.py                          # the MI355X shim (nano-hevc_amd/nano_hevc), on a GPU box
     python tools/percall.py --impl /root/reference   # the reference numpy package (build container only)
+    python tools/percall.py --lib tools/_ab/libnanohevc_r01_staging.so   # the shim over another build (A/B)
 
 Times every compute function the reference exports (nano_hevc/__init__.py:50-91)
 one block per call, as the reference's callers use them, at sizes 4 / 8 / 16 / 32
@@ -95,13 +96,21 @@ def main():
         assert torch.cuda.is_available(), "the shim's per-call cost is measured on an MI355X"
         dev = torch.cuda.get_device_name(0)
         from nano_hevc import _lib
+        if "--lib" in sys.argv:   # A/B: an older build of the library (symbols it lacks are skipped)
+            import ctypes
+            path = os.path.abspath(sys.argv[sys.argv.index("--lib") + 1])
+            probe = ctypes.CDLL(path)
+            for name in [n for n in _lib.SIGNATURES if not hasattr(probe, n)]:
+                del _lib.SIGNATURES[name]
+            _lib.LIB_PATH = path
         _lib.load()
     rng = np.random.default_rng(7)
     res = {}
     for name, n, fn in cases(nh, rng):
         r = reps if (impl == "shim" or n <= 16) else max(10, reps // 10)
         res.setdefault(name, {})[n] = _time(fn, r)
-    print(json.dumps({"impl": "nano-hevc_amd shim (MI355X)" if impl == "shim" else "reference numpy",
+    lib = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else "nano_hevc/libnanohevc.so"
+    print(json.dumps({"impl": f"nano-hevc_amd shim (MI355X), {lib}" if impl == "shim" else "reference numpy",
                       "device": dev, "cpu": platform.processor() or platform.machine(), "reps": reps,
                       "us_per_call": res}))
 
