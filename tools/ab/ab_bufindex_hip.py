@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""tools/ab_bufindex.py with buffers from hipExtMallocWithFlags(flags) instead
+"""tools/ab/ab_bufindex.py with buffers from hipExtMallocWithFlags(flags) instead
 of torch's allocator (flags 0 default, 4 hipDeviceMallocContiguous): input =
 buffer 0, output = buffer j.  Median GB/s of 20 launches of the default
 launch per j."""
@@ -9,7 +9,7 @@ import os
 import statistics
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "nano-hevc_amd"))
 import torch  # noqa: E402
 

@@ -2,7 +2,7 @@
 """Hot kernel on buffers from hipExtMallocWithFlags (flags: 0 default,
 4 = hipDeviceMallocContiguous) instead of torch's allocator: does physically
 contiguous backing remove the per-process placement lottery seen with
-tools/ab_alloc.py?  One JSON line per process."""
+tools/ab/ab_alloc.py?  One JSON line per process."""
 import argparse
 import ctypes as C
 import json
@@ -10,7 +10,7 @@ import os
 import statistics
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "nano-hevc_amd"))
 import torch  # noqa: E402
 

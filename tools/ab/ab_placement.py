@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Why does the interleaved A/B (tools/ab_fwd8x8.py) time the default launch
+"""Why does the interleaved A/B (tools/ab/ab_fwd8x8.py) time the default launch
 faster than bench.py on the same box?  Time the bench's exact launch under
 controlled differences: a spacer allocation between input and output, bursts
 of K launches separated by a sync, and the input's generator.  One JSON line
@@ -10,7 +10,7 @@ import os
 import statistics
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "nano-hevc_amd"))
 import torch  # noqa: E402
 

@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """Launch the default hot kernel 5x with output = buffer 1 and 5x with
 output = buffer 5 (of 6 same-size torch buffers), for PMC passes that compare
-the two placements (tools/ab_bufindex.py showed output placement decides
+the two placements (tools/ab/ab_bufindex.py showed output placement decides
 5.9 vs 6.7 TB/s on some boxes).  Prints the per-launch ms of each group."""
 import json
 import os
 import statistics
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "nano-hevc_amd"))
 import torch  # noqa: E402
 

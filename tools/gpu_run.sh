@@ -12,7 +12,9 @@
 #   prof       rocprofv3 --kernel-trace --stats of bench.py
 #   pmc        the FETCH_SIZE and WRITE_SIZE passes of bench.py (MI355X_MICROARCH.md §HBM)
 #   configs    tools/bench_configs.py (configs 3/4/5 + frame driver)
-#   percall    tools/percall.py (drop-in per-call cost)
+#   percall    tools/percall.py (drop-in per-call cost); percall_ab: the same over tools/_ab/ (older build)
+#   pmc_sq     SQ wave-state pass (issue / wait fractions) of bench.py; CONFIG=4 for the config-4 bench
+#   kt_cfg     rocprofv3 kernel trace of tools/bench_configs.py $CONFIGS_ARGS (per-kernel times of configs 3/4/5)
 # Extra pytest args: PYTEST_K="-k expr"; bench args: BENCH_ARGS="...".
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -69,6 +71,12 @@ run_step() {
       echo "== per-call cost, previous build (tools/_ab/libnanohevc_r01_staging.so)"
       timeout -k 10 300 python tools/percall.py --lib tools/_ab/libnanohevc_r01_staging.so > gpurun_out/percall_r01lib_${TAG}.json 2> gpurun_out/percall_r01lib_${TAG}.err; rc=$?
       tail -3 gpurun_out/percall_r01lib_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/percall_r01lib_${TAG}.err; return $rc ;;
+    pmc_sq)
+      echo "== rocprof pmc SQ wave states (config ${CONFIG:-2})"
+      timeout -s KILL 180 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY --output-format csv -d gpurun_out/pmc_sq_${TAG} -o run -- python3 bench.py --config ${CONFIG:-2} --steps 3 --warmup 1 --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc_sq_${TAG}.log 2>&1 ;;
+    kt_cfg)
+      echo "== rocprof kernel trace of bench_configs $CONFIGS_ARGS"
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_cfg_${TAG} -o run -- python3 tools/bench_configs.py $CONFIGS_ARGS > gpurun_out/kt_cfg_${TAG}.log 2>&1 ;;
     *)
       echo "unknown step $1"; return 2 ;;
   esac
