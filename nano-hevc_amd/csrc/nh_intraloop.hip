@@ -1885,6 +1885,10 @@ extern "C" int64_t nh_tu_workspace_bytes(int w, int h, int ctb) {
 }
 
 namespace nh {
+// nh_ctu.hip: config 4 as one CTU-granular launch (NH_EVALUE: layout needs the per-size path)
+int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu, const nh_plane_set* set, int ctb,
+                    int plane_id, uint32_t seed, int is_luma, int row0, int row1, const QuantParams* q, int dqs,
+                    int dq_per, hipStream_t s);
 // nh_tc32.hip: config 4's 32x32 TUs on the int8 matrix cores
 int tc32_mfma_tree(const int16_t* src, int w, int h, int pitch, const QuantParams& qp, int dq_scale, int dq_per,
                    int32_t* lvl, int16_t* rec, uint8_t* tu, int bw, int n, const TreeArgs& ta, unsigned planes,
@@ -1909,6 +1913,17 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
     int per, rem;
     qp_split(qp, &per, &rem);
     const int dqs = dequant_scale(rem);
+    // One CTU-granular launch (k_ctu_open) unless the layout
+    // rules out its vector accesses; A/B build: NH_CFG4_FORM=1 forces the
+    // per-size launches below.
+    static const int form = NH_KNOB("NH_CFG4_FORM", 0);
+    if (form == 0) {
+        QuantParams q4[4];
+        for (int k = 0; k < 4; ++k) q4[k] = qparams(qp, k + 2, true);
+        const int rc = ctu_open_launch(d_src, d_lvl, d_recon, d_tu, set, ctb, plane_id, seed, is_luma, row0, row1, q4,
+                                       dqs, per, s);
+        if (rc != NH_EVALUE) return rc;
+    }
     const int yb = row0 * ctb, ye = row1 * ctb < h ? row1 * ctb : h;
     TreeArgs ta{ctb, plane_id, yb, seed};
     ta.ppg = set->planes_per_group;

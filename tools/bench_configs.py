@@ -80,9 +80,13 @@ def main():
     ap.add_argument("--configs", default="3,4,4b,5,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
     ap.add_argument("--closed-frames", type=int, default=64)
+    ap.add_argument("--ab", action="store_true", help="run on the A/B library (libnanohevc_ab.so: NH_* knobs read)")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
+    if args.ab:
+        _lib.use_ab()
     _lib.load()
+    knobs = {k: v for k, v in os.environ.items() if k.startswith("NH_")}
     torch.cuda.set_device(0)
     cfgs = {int(c) if c.isdigit() else c for c in args.configs.split(",")}
 
@@ -144,7 +148,10 @@ def main():
                           "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "frames_per_s": nf / ms * 1e3,
                           "samples_per_s": samples / ms * 1e3,
                           "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
-                          "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}), flush=True)
+                          "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H]), "knobs": knobs,
+                          "out_digest": [int(lv.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item()),
+                                         int((lv.to(torch.int64) * torch.arange(lv.numel(), device="cuda") % 1000003)
+                                             .sum().item())]}), flush=True)
 
     if "closed4" in cfgs:   # config 4 in closed loop: 64 4K YUV420 frames, 2 concurrent launches (CTU-row wavefronts)
         W, H, nf = 3840, 2160, args.closed4_frames

@@ -15,7 +15,7 @@
 #   percall    tools/percall.py (drop-in per-call cost); percall_ab: the same over tools/_ab/ (older build)
 #   pmc_sq     SQ wave-state pass (issue / wait fractions) of bench.py; CONFIG=4 for the config-4 bench
 #   kt_cfg     rocprofv3 kernel trace of tools/bench_configs.py $CONFIGS_ARGS (per-kernel times of configs 3/4/5)
-# Extra pytest args: PYTEST_K="-k expr"; bench args: BENCH_ARGS="...".
+# pytest selection: PYTEST_K="expr" (passed as -k expr); bench args: BENCH_ARGS="...".
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -29,7 +29,7 @@ run_step() {
   case "$1" in
     tests)
       echo "== pytest -m gpu"
-      timeout -k 10 900 $PT tests -m gpu $PYTEST_K > gpurun_out/pytest_gpu_${TAG}.log 2>&1; rc=$?
+      timeout -k 10 900 $PT tests -m gpu ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu_${TAG}.log 2>&1; rc=$?
       tail -5 gpurun_out/pytest_gpu_${TAG}.log; return $rc ;;
     smoke)
       echo "== smoke"
