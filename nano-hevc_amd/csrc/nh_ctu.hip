@@ -18,10 +18,11 @@
 //   2. classifies its units: lane u descends the quadtree to its unit's leaf
 //      (<= 3 hashes), writes the TU map entry, and the TU origins are compacted
 //      into per-size LDS lists with wave ballots;
-//   3. codes the TUs size by size: a 32x32 TU on the int8 matrix cores (the
-//      config-5 chain, one wave per TU), smaller TUs 64/N at a time, lane l
-//      taking column / row l mod N of TU l / N, transposes through an LDS
-//      tile of the strip (every TU at its own place, so TUs never collide).
+//   3. codes the TUs of the workgroup's 4 strips pooled by size, 64/N at a
+//      time: lane l takes column / row l mod N of TU l / N (32-point to 4-point
+//      butterflies; the 32x32 TUs alternatively on the int8 matrix cores, one
+//      per wave -- A/B only, not faster here), transposes through an LDS tile
+//      of the strip (every TU at its own place, so TUs never collide).
 // No workgroup barriers (a wave only touches its own LDS slices, and LDS
 // executes one wave's instructions in order), no global atomics, no per-size
 // relaunch, the source read once.  Levels and recon rows are stored straight
@@ -272,7 +273,7 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
 // TUs of all 4 strips are pooled per size, so a batch of 64/N TUs fills its
 // lanes (a strip alone holds ~half a batch per size), and the batches are
 // claimed by the 4 waves in descending cost (32x32 chains first).
-template <int CTB, bool LUMA, int WAVES>
+template <int CTB, bool LUMA, int WAVES, bool MFMA32>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a) {
     using G = Strip<CTB>;
     constexpr int SW = G::SW, UW = G::UW, IP = G::IP;
@@ -359,7 +360,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     __syncthreads();
 
     // ---- 3. batches, claimed in descending cost: 32x32 chains, then 16, 8, 4 ----
-    const int n32 = CTB == 32 ? cnt[3] : 0;
+    const int n32 = CTB == 32 ? (MFMA32 ? cnt[3] : (cnt[3] + 1) / 2) : 0;
     const int n16 = CTB >= 16 ? (cnt[2] + 3) / 4 : 0, n8 = CTB >= 8 ? (cnt[1] + 7) / 8 : 0, n4 = (cnt[0] + 15) / 16;
     const int total = n32 + n16 + n8 + n4;
     for (;;) {
@@ -369,8 +370,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         if (item >= total) break;
         if constexpr (CTB == 32) {
             if (item < n32) {
-                const int e = s_list[3][item], sw = e >> 6;
-                ctu_chain32(a, s_img + sw * G::IMG + 4, s_cf + sw * G::CF, s_org[2 * sw], s_org[2 * sw + 1], lvl, rec);
+                if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores
+                    const int e = s_list[3][item], sw = e >> 6;
+                    ctu_chain32(a, s_img + sw * G::IMG + 4, s_cf + sw * G::CF, s_org[2 * sw], s_org[2 * sw + 1], lvl,
+                                rec);
+                } else {                  // two TUs per wave, 32-point butterflies
+                    ctu_chain<32, false, CTB>(a, s_img, s_cf, s_list[3], cnt[3], 2 * item, s_org, lvl, rec);
+                }
                 continue;
             }
         }
@@ -442,24 +448,34 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     if (strips <= 0 || planes <= 0) return NH_OK;
     if ((strips + 3) / 4 > INT32_MAX) return NH_EARG;
     const dim3 grid((unsigned)((strips + 3) / 4), (unsigned)planes);
-    // CTB 32 holds the int8-MFMA chain: the compiler's allocation (228 registers,
-    // 2 waves/SIMD) capped at 3 waves/SIMD = 168 VGPRs without spills (4 waves
-    // spills); A/B build: NH_CTU_WAVES = 1 (compiler) / 3 / 4.
-    static const int cw = NH_KNOB("NH_CTU_WAVES", 3);
-#define NH_CTU(C, W)                                                                \
-    if (is_luma) k_ctu_open<C, true, W><<<grid, 256, 0, s>>>(a);                    \
-    else k_ctu_open<C, false, W><<<grid, 256, 0, s>>>(a);
+    // 32x32 TUs: 32-point butterflies, two TUs per wave (128 VGPRs, 4 waves/SIMD)
+    // by default; the int8-MFMA chain (one TU per wave, capped at 3 waves/SIMD =
+    // 168 VGPRs without spills; uncapped 228 registers) measured equal in
+    // rocprof (584.7 vs 586.6 us per 16 luma planes), so the
+    // north star's rule keeps the butterfly.  A/B build: NH_CTU_T32 = 1 (MFMA) /
+    // 0, NH_CTU_WAVES = 1 (compiler) / 3 / 4.
+    static const int cw = NH_KNOB("NH_CTU_WAVES", 0);
+    static const int t32 = NH_KNOB("NH_CTU_T32", 0);
+#define NH_CTU(C, W, M)                                                             \
+    if (is_luma) k_ctu_open<C, true, W, M><<<grid, 256, 0, s>>>(a);                 \
+    else k_ctu_open<C, false, W, M><<<grid, 256, 0, s>>>(a);
     switch (ctb) {
-        case 4: NH_CTU(4, 1) break;
-        case 8: NH_CTU(8, 1) break;
-        case 16: NH_CTU(16, 1) break;
+        case 4: NH_CTU(4, 1, false) break;
+        case 8: NH_CTU(8, 1, false) break;
+        case 16: NH_CTU(16, 1, false) break;
         case 32:
 #if NH_AB
-            if (cw == 1) { NH_CTU(32, 1) break; }
-            if (cw == 4) { NH_CTU(32, 4) break; }
+            if (t32 == 1) {
+                if (cw == 1) { NH_CTU(32, 1, true) break; }
+                if (cw == 4) { NH_CTU(32, 4, true) break; }
+                NH_CTU(32, 3, true) break;
+            }
+            if (cw == 3) { NH_CTU(32, 3, false) break; }
+            if (cw == 4) { NH_CTU(32, 4, false) break; }
 #endif
             (void)cw;
-            NH_CTU(32, 3) break;
+            (void)t32;
+            NH_CTU(32, 1, false) break;
         default: return NH_EVALUE;
     }
 #undef NH_CTU
