@@ -25,9 +25,10 @@ holds the whole synthetic input stream (a TU reads the source row above its
 band, block.py:38-50) and reconstructs only its bands.
 
 N > 1, both configs: after the compute-only phase, a gather-inclusive phase
-runs the path's one exchange step -- an RCCL gather to rank 0 (config 2: the
-int16 levels; config 4: the reconstructed bands as uint8, clip_to_pixel_range
-guarantees [0, 255]) -- on a side stream, the gather of step k overlapped with
+runs the path's one exchange step -- an RCCL gather to rank 0 (config 2: a
+--gather-frames sample of the int16 levels, 8 of 128 frames by default;
+config 4: all reconstructed bands as uint8, clip_to_pixel_range guarantees
+[0, 255]) -- on a side stream, the gather of step k overlapped with
 the compute of step k+1 (double-buffered outputs).  Reported as
 ``gather_inclusive`` with the bytes into rank 0 and the achieved xGMI rate.
 
@@ -84,6 +85,9 @@ def parse_args(argv=None):
     ap.add_argument("--variant", type=int, default=4341, help="config 2 launch variant (nanohevc.h); 4341 = default")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (1-thread + all-threads legs)")
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed steps of the gather-inclusive phase")
+    ap.add_argument("--gather-frames", type=int, default=8,
+                    help="config 2, N>1: frames' worth of int16 levels each rank ships to rank 0 per gathered step "
+                         "(a bounded sample of its output; the whole output would be 3.2 GB per rank at 128 frames)")
     ap.add_argument("--check", action="store_true", help="config 4, N>1: rank 0 compares the gathered recon with "
                                                           "an unsharded run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -330,16 +334,20 @@ def run_cfg2(args, dist, world, rank, dev):
     gather = None
     if dist and args.gather_steps > 0:
         outs.append(torch.zeros_like(outs[0]))
-        og = OverlappedGather(dist, dev, [padded // 4] * world, torch.int64)
-        gt = run_phase_gather(step_into, lambda s: outs[s].view(torch.int64), og, args.gather_steps, dist, stream)
+        frac = min(1.0, args.gather_frames / args.frames)
+        words = min(padded, -(-int(padded * frac) // 4) * 4) // 4   # int64 words sent per rank per step
+        og = OverlappedGather(dist, dev, [words] * world, torch.int64)
+        gt = run_phase_gather(step_into, lambda s: outs[s].view(torch.int64)[:words], og, args.gather_steps, dist,
+                              stream)
         (gt,), _ = reduce_max_sum(dist, dev, (gt,), ())
-        into_root = 2 * sum(sizes[1:])
+        into_root = 8 * words * (world - 1)
         gather = {"value": blocks_all * args.gather_steps / gt, "unit": "blocks/s", "steps": args.gather_steps,
                   "ms_per_step": gt / args.gather_steps * 1e3, "bytes_into_root_per_step": into_root,
                   "into_root_GBps": into_root * args.gather_steps / gt / 1e9, "overlapped": True,
-                  "backend": dist.get_backend(),
-                  "note": "compute + RCCL gather of every rank's int16 levels to rank 0 on a side stream, "
-                          "gather(k) under compute(k+1); bounded by rank 0's inbound xGMI (SURVEY.md §8e E-2)"}
+                  "backend": dist.get_backend(), "levels_fraction_gathered": frac,
+                  "note": f"compute + RCCL gather to rank 0 of a {args.gather_frames}-frame sample of every rank's "
+                          "int16 levels per step (the head of its output), on a side stream, gather(k) under "
+                          "compute(k+1); the exchange is bounded by rank 0's inbound xGMI (SURVEY.md §8e E-2)"}
 
     if rank != 0:
         return None
