@@ -33,6 +33,7 @@
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 #include "nh_mfma.hpp"
+#include "nh_packed.hpp"
 #include "nh_tree.hpp"
 
 namespace nh {
@@ -50,6 +51,7 @@ struct CtuArgs {
     uint32_t seed;
     QuantParams q[4];                // log2 N = 2..5
     int32_t dqs, dq_per;
+    int32_t wide_only;               // A/B build only (NH_CTU_NARROW=0): every workgroup on the 32-bit chain
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
@@ -69,6 +71,10 @@ __device__ __forceinline__ uint64_t sq2(int32_t a, int32_t b) {
 template <int CTB> struct Strip {
     static constexpr int SW = 1024 / CTB, UW = SW / 4, IP = SW + 8, CP = SW + 1;
     static constexpr int IMG = (CTB + 1) * IP, CF = CTB * CP;
+    // narrow workgroups: an int16 tile aliasing the int32 one, rows of TP int16
+    // (an odd number of dwords: the pair reads of a row pass are conflict-free)
+    static constexpr int TP = SW + 2, T16 = CTB * TP;
+    static_assert((TP / 2) % 2 == 1 && T16 * 2 <= CF * 4, "int16 tile layout");
 };
 
 // One batch of 64/N TUs of size N from the workgroup's size-N list: lane l
@@ -187,6 +193,147 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
     }
 }
 
+// The same chain for a NARROW workgroup (every sample of its strips and their
+// neighbours in [0, 255]): int16 pairs end to end.  Source
+// column, planar prediction (v_pk_mad_u16: numerators < 2^15) and residual as
+// row pairs, residual energies with v_dot2 in 32 bits (<= N^2 * 255^2), the
+// transforms of nh_packed.hpp, and an int16 coefficient tile: each pass stores
+// its outputs with 16-bit writes at the slots the next pass reads as pairs --
+// natural order into the forward row pass, inv_slot order (line = column) into
+// both inverse passes, so no pass permutes.  Same results as ctu_chain for
+// such TUs (bounds: tools/packed_bounds.py).
+template <int N, bool DST, int CTB>
+__device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_img, int16_t* s_t16, const uint16_t* list,
+                                             int cnt, int b0, const int* s_org, int32_t* __restrict__ lvl,
+                                             int16_t* __restrict__ rec) {
+    using G = Strip<CTB>;
+    constexpr int L2 = Log2<N>::v, S = L2 + 5, IP = G::IP, TP = G::TP, H = N / 2;
+    constexpr int32_t BIAS = 1 << (S - 1);
+    const ChainQ cq = make_chainq(a.q[L2 - 2], a.dqs, a.dq_per);
+    const int lane = threadIdx.x & 63, j = lane / N, t = lane % N;
+    const bool on = b0 + j < cnt;
+    const int e = list[on ? b0 + j : b0], sw = e >> 6, u = e & 63;   // idle lanes shadow the batch's first TU
+    const int lx = 4 * (u % G::UW), ly = 4 * (u / G::UW);
+    const int16_t* img = s_img + sw * G::IMG + ly * IP + 4 + lx;   // img[r * IP + c]: sample (ly + r - 1, lx + c)
+    int16_t* tl = s_t16 + sw * G::T16 + ly * TP + lx;              // tl[line * TP + slot]
+    const int gx0 = s_org[2 * sw] + lx, gy0 = s_org[2 * sw + 1] + ly;
+    const int32_t topt = img[t];                  // top[t]   (block.py:38-43)
+    const int32_t leftt = img[(1 + t) * IP - 1];  // left[t]  (block.py:45-50)
+    const int32_t tr = img[N - 1];                // top[-1]  (__main__.py:168)
+    const int32_t bl = img[N * IP - 1];           // left[-1]
+    int32_t sum = topt + leftt;                   // DC (intra.py:46-62)
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    const int32_t dc = (sum + N) >> (L2 + 1);
+    const pk16 dc2 = pk_splat(dc);
+    // column t: source rows (2m, 2m+1) and planar (intra.py:81-113)
+    // num(i) = (N-1-t) left[i] + [(t+1) tr + (N-1-i) top[t] + (i+1) bl + N]
+    pk16 o2[H];
+    pku16 pl2[H];
+    {
+        const int32_t b = (t + 1) * tr + (N - 1) * topt + bl + N, st = bl - topt;
+        pku16 bs = {(unsigned short)b, (unsigned short)(b + st)};
+        const pku16 st2 = {(unsigned short)(2 * st), (unsigned short)(2 * st)};
+        const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
+        const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            o2[m] = pk_pair(img[(1 + 2 * m) * IP + t], img[(2 + 2 * m) * IP + t]);
+            const pku16 lf = {(unsigned short)img[(1 + 2 * m) * IP - 1], (unsigned short)img[(2 + 2 * m) * IP - 1]};
+            pl2[m] = (lf * wl + bs) >> sh;
+            bs += st2;
+        }
+    }
+    int32_t ed = 0, ep = 0;
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+        const pk16 d0 = o2[m] - dc2, d1 = o2[m] - __builtin_bit_cast(pk16, pl2[m]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+    }
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) {
+        ed += __shfl_xor(ed, m, 64);
+        ep += __shfl_xor(ep, m, 64);
+    }
+    const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
+    pk16 r2[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) r2[m] = o2[m] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[m]));
+    // forward pass 1 (transform.py:179-185), column t -> line i, slot t
+    int32_t y[N];
+    fwd1d_pk<N, DST>(r2, y, BIAS);
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(y[i] >> S);
+    }
+    wave_sync();
+    // forward pass 2 (transform.py:188-194), row t; quantize_block, levels out, dequantize_block
+    // -> line k (column), slot inv_slot(t)
+    const int st = inv_slot<N, DST>(t);
+    {
+        pk16 P[H];
+#pragma unroll
+        for (int m = 0; m < H; ++m) P[m] = *(const pk16*)&tl[t * TP + 2 * m];
+        fwd1d_pk<N, DST>(P, y, BIAS);
+    }
+    if (on) {
+        int32_t* lrow = lvl + (int64_t)(gy0 + t) * a.pitch + gx0;
+#pragma unroll
+        for (int k0 = 0; k0 < N; k0 += 4) {
+            int32_t L4[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                L4[q] = quant_s(y[k0 + q] >> S, cq.qs, cq.h_v, cq.hneg_v);
+                tl[(k0 + q) * TP + st] = (int16_t)dequant_s(L4[q], cq);
+            }
+            *(int4*)(lrow + k0) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+        }
+    }
+    wave_sync();
+    // inverse pass 1 (transform.py:221-227), column t -> line i (row), slot inv_slot(t)
+    int32_t x[N];
+    {
+        pk16 Y[H];
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = *(const pk16*)&tl[t * TP + 2 * m];
+        inv1d_pk<N, DST>(Y, x, BIAS);
+    }
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(x[i] >> S);
+    }
+    wave_sync();
+    // inverse pass 2 (transform.py:230-236), row t; reconstruct + clip (intra.py:70-78), recon out
+    {
+        pk16 Y[H];
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = *(const pk16*)&tl[t * TP + 2 * m];
+        inv1d_pk<N, DST>(Y, x, BIAS);
+    }
+    if (on) {
+        // planar in row layout: num(k) = (N-1-t) top[k] + [(N-1-k) left[t] + (k+1) tr + (t+1) bl + N]
+        const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, st2v = tr - leftt;
+        pku16 bs = {(unsigned short)b, (unsigned short)(b + st2v)};
+        const pku16 stp = {(unsigned short)(2 * st2v), (unsigned short)(2 * st2v)};
+        const pku16 wt = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
+        const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
+        const pk16 zero = {0, 0}, maxv = {255, 255};
+        uint32_t pk[H];
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            const pku16 tp = __builtin_bit_cast(pku16, *(const pk16*)&img[2 * m]);
+            const pk16 pred = use_dc ? dc2 : __builtin_bit_cast(pk16, (pku16)((tp * wt + bs) >> sh));
+            bs += stp;
+            const pk16 rc = pred + pk_pair(x[2 * m] >> S, x[2 * m + 1] >> S);
+            pk[m] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_max(rc, zero), maxv));
+        }
+        int16_t* rrow = rec + (int64_t)(gy0 + t) * a.pitch + gx0;
+#pragma unroll
+        for (int m = 0; m < H; m += 2) *(uint2*)(rrow + 2 * m) = make_uint2(pk[m], pk[m + 1]);
+    }
+}
+
 // A 32x32 TU (a whole CTU of a CTB-32 strip) on the int8 matrix cores: the
 // chain of k_tc32_mfma (nh_tc32.hip) with the block, its
 // neighbours and the dequantized tile in the strip's LDS image / tile.
@@ -280,7 +427,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     __shared__ __attribute__((aligned(16))) int16_t s_img[4 * G::IMG];
     __shared__ int32_t s_cf[4 * G::CF];
     __shared__ uint16_t s_list[4][256];
-    __shared__ int s_cnt[4][4], s_org[8], s_next;
+    __shared__ int s_cnt[4][4], s_org[8], s_next, s_wide[4];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int strip = blockIdx.x * 4 + wv;
     const bool valid = strip < a.strips_x * a.nrows;
@@ -295,29 +442,37 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     int16_t* img = s_img + wv * G::IMG;
 
     // ---- 1. each wave: its strip, the row above and the column left, into LDS (8-B loads) ----
+    uint32_t hi_bits = 0;   // any sample outside [0, 255]: the workgroup takes the 32-bit chain
     if (valid) {
 #pragma unroll
         for (int g0 = 0; g0 < CTB * UW; g0 += 64) {
             const int g = g0 + lane, ry = g / UW, gx = g % UW, x = sx0 + 4 * gx, y = sy0 + ry;
             uint2 v = make_uint2(0u, 0u);   // outside the plane: no TU reads it
             if (x < w && y < h) v = *(const uint2*)(src + (int64_t)y * pitch + x);
+            hi_bits |= v.x | v.y;
             *(uint2*)&img[(1 + ry) * IP + 4 + 4 * gx] = v;
         }
         if (lane < UW) {
             const int x = sx0 + 4 * lane;
             uint2 v = make_uint2(0x00800080u, 0x00800080u);   // 128 above the frame (block.py:41)
             if (sy0 > 0 && x < w) v = *(const uint2*)(src + (int64_t)(sy0 - 1) * pitch + x);
+            hi_bits |= v.x | v.y;
             *(uint2*)&img[4 + 4 * lane] = v;
         }
         if (lane < CTB) {
             const int y = sy0 + lane;
-            img[(1 + lane) * IP + 3] =
-                sx0 == 0 ? (int16_t)128 : (y < h ? src[(int64_t)y * pitch + sx0 - 1] : (int16_t)0);
+            const int16_t v = sx0 == 0 ? (int16_t)128 : (y < h ? src[(int64_t)y * pitch + sx0 - 1] : (int16_t)0);
+            hi_bits |= (uint16_t)v;
+            img[(1 + lane) * IP + 3] = v;
         }
         if (lane == 0) {
             s_org[2 * wv] = sx0;
             s_org[2 * wv + 1] = sy0;
         }
+    }
+    {
+        const uint64_t wide = __ballot((hi_bits & 0xff00ff00u) != 0);
+        if (lane == 0) s_wide[wv] = wide != 0;
     }
 
     // ---- 2. classify the strip's 64 units: leaf size / origin (<= 3 hashes), TU map ----
@@ -360,9 +515,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     __syncthreads();
 
     // ---- 3. batches, claimed in descending cost: 32x32 chains, then 16, 8, 4 ----
+    // NARROW (every sample of the 4 strips and their neighbours 8-bit): the
+    // packed 16-bit chain; otherwise the 32-bit chain (any int16 input).
+    const bool narrow =
+        __builtin_amdgcn_readfirstlane((s_wide[0] | s_wide[1] | s_wide[2] | s_wide[3] | a.wide_only) == 0);
+    int16_t* s_t16 = (int16_t*)s_cf;
     const int n32 = CTB == 32 ? (MFMA32 ? cnt[3] : (cnt[3] + 1) / 2) : 0;
     const int n16 = CTB >= 16 ? (cnt[2] + 3) / 4 : 0, n8 = CTB >= 8 ? (cnt[1] + 7) / 8 : 0, n4 = (cnt[0] + 15) / 16;
     const int total = n32 + n16 + n8 + n4;
+#define NH_CHAIN(N, DST, L, B)                                                          \
+    if (narrow) ctu_chain_pk<N, DST, CTB>(a, s_img, s_t16, s_list[L], cnt[L], B, s_org, lvl, rec); \
+    else ctu_chain<N, DST, CTB>(a, s_img, s_cf, s_list[L], cnt[L], B, s_org, lvl, rec);
     for (;;) {
         int item = 0;
         if (lane == 0) item = atomicAdd(&s_next, 1);
@@ -370,12 +533,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         if (item >= total) break;
         if constexpr (CTB == 32) {
             if (item < n32) {
-                if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores
+                if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores (A/B form)
                     const int e = s_list[3][item], sw = e >> 6;
                     ctu_chain32(a, s_img + sw * G::IMG + 4, s_cf + sw * G::CF, s_org[2 * sw], s_org[2 * sw + 1], lvl,
                                 rec);
                 } else {                  // two TUs per wave, 32-point butterflies
-                    ctu_chain<32, false, CTB>(a, s_img, s_cf, s_list[3], cnt[3], 2 * item, s_org, lvl, rec);
+                    NH_CHAIN(32, false, 3, 2 * item)
                 }
                 continue;
             }
@@ -383,20 +546,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         item -= n32;
         if constexpr (CTB >= 16) {
             if (item < n16) {
-                ctu_chain<16, false, CTB>(a, s_img, s_cf, s_list[2], cnt[2], 4 * item, s_org, lvl, rec);
+                NH_CHAIN(16, false, 2, 4 * item)
                 continue;
             }
         }
         item -= n16;
         if constexpr (CTB >= 8) {
             if (item < n8) {
-                ctu_chain<8, false, CTB>(a, s_img, s_cf, s_list[1], cnt[1], 8 * item, s_org, lvl, rec);
+                NH_CHAIN(8, false, 1, 8 * item)
                 continue;
             }
         }
         item -= n8;
-        ctu_chain<4, LUMA, CTB>(a, s_img, s_cf, s_list[0], cnt[0], 16 * item, s_org, lvl, rec);
+        NH_CHAIN(4, LUMA, 0, 16 * item)
     }
+#undef NH_CHAIN
 }
 
 static int ensure_basis_ctu() {
@@ -453,9 +617,10 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // 168 VGPRs without spills; uncapped 228 registers) measured equal in
     // rocprof (584.7 vs 586.6 us per 16 luma planes), so the
     // north star's rule keeps the butterfly.  A/B build: NH_CTU_T32 = 1 (MFMA) /
-    // 0, NH_CTU_WAVES = 1 (compiler) / 3 / 4.
+    // 0, NH_CTU_WAVES = 1 (compiler) / 3 / 4 / 5, NH_CTU_NARROW = 0 (no packed chain).
     static const int cw = NH_KNOB("NH_CTU_WAVES", 0);
     static const int t32 = NH_KNOB("NH_CTU_T32", 0);
+    a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
 #define NH_CTU(C, W, M)                                                             \
     if (is_luma) k_ctu_open<C, true, W, M><<<grid, 256, 0, s>>>(a);                 \
     else k_ctu_open<C, false, W, M><<<grid, 256, 0, s>>>(a);
@@ -472,6 +637,7 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
             }
             if (cw == 3) { NH_CTU(32, 3, false) break; }
             if (cw == 4) { NH_CTU(32, 4, false) break; }
+            if (cw == 5) { NH_CTU(32, 5, false) break; }
 #endif
             (void)cw;
             (void)t32;

@@ -584,6 +584,29 @@ def test_tu_pipeline_int16_extremes(nh, torch_dev):
         assert np.array_equal(l.cpu().numpy(), el) and np.array_equal(r.cpu().numpy(), er)
 
 
+@pytest.mark.parametrize("qp", [0, 22, 51])
+def test_tu_pipeline_narrow_extremes_and_mixed(nh, torch_dev, qp):
+    """Config 4's packed 16-bit chain (narrow workgroups) at its
+    range limits -- samples only 0 / 255, so residuals reach +-255 -- and planes
+    where a few samples leave [0, 255] (those workgroups take the 32-bit chain,
+    their neighbours the packed one), against the oracle at QP 0 / 22 / 51."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(90 + qp)
+    h, w = 200, 264
+    two = (rng.integers(0, 2, size=(h, w)) * 255).astype(np.int16)
+    mixed = np.clip(128 + rng.integers(-60, 61, size=(h, w)), 0, 255).astype(np.int16)
+    for y, x, v in ((5, 7, 256), (70, 130, -1), (150, 40, 4000), (199, 263, -300), (31, 100, 511)):
+        mixed[y, x] = v
+    for src in (two, mixed):
+        for luma, ctb in ((True, 32), (False, 16)):
+            l, r, t = gpu.tu_pipeline_plane(torch.from_numpy(src).cuda(), ctb, int(not luma), 13, qp, luma)
+            el, er, et = O.tu_pipeline_plane(src, ctb, int(not luma), 13, qp, luma)
+            assert np.array_equal(t.cpu().numpy(), et)
+            assert np.array_equal(l.cpu().numpy(), el), (luma, qp)
+            assert np.array_equal(r.cpu().numpy(), er), (luma, qp)
+
+
 # ------------------------------------------------------------------ f-4: fused level-side epilogue
 
 def _ref_level_helpers(lv, sets):

@@ -1,0 +1,93 @@
+"""Range proof for the packed 16-bit config-4 chain.
+
+Narrow workgroups: every source sample and neighbour in [0, 255], so the
+residual is in [-255, 255].  This enumerates, for every TU kind (DST4, DCT
+4/8/16/32), every QP 0..51 and intra/inter rounding, a bound on every operand
+the packed chain holds in an int16 lane (butterfly E/O stages, pass outputs,
+dequantized coefficients) and on every int32 dot-product sum, from the L1 norms
+of the reference matrices (transform.py:20-135) and the monotone quantizer /
+dequantizer (quant.py:41-123).  Prints the table and fails if any bound
+reaches int16 / int32 limits.
+"""
+import numpy as np
+
+TAB = [64, 90, 90, 90, 89, 88, 87, 85, 83, 82, 80, 78, 75, 73, 70, 67,
+       64, 61, 57, 54, 50, 46, 43, 38, 36, 31, 25, 22, 18, 13, 9, 4, 0]
+
+
+def dct32(k, n):
+    if k == 0:
+        return 64
+    m = ((2 * n + 1) * k) % 128
+    return TAB[m] if m <= 32 else -TAB[64 - m] if m <= 64 else -TAB[m - 64] if m <= 96 else TAB[128 - m]
+
+
+def mat(n, dst):
+    if dst:
+        return np.array([[29, 55, 74, 84], [74, 74, 0, -74], [84, -29, -74, 55], [55, -84, 74, -29]], np.int64)
+    return np.array([[dct32(k * (32 // n), j) for j in range(n)] for k in range(n)], np.int64)
+
+
+QS = [26214, 23302, 20560, 18396, 16384, 14564]
+DQ = [40, 45, 51, 57, 64, 72]
+
+
+def quant(c, qp, l2, intra):
+    per, rem = qp // 6, qp % 6
+    sh = 14 + per + l2
+    off = (1 << sh) // (3 if intra else 6)
+    return (c * QS[rem] + off) >> sh
+
+
+def dequant(l, qp):
+    per, rem = qp // 6, qp % 6
+    b = l * DQ[rem]
+    return (b + (1 << (3 - per))) >> (4 - per) if per < 4 else b << (per - 4)
+
+
+def shift_bound(acc, s):   # |(acc + 2^(s-1)) >> s| for |acc| <= bound
+    return (acc + (1 << (s - 1))) >> s
+
+
+def butterfly_operand(x, n, dst):
+    """largest int16 operand of the packed forward butterfly on inputs |x| <= x:
+    stage d of an n-point DCT holds sums of 2^d inputs (up to the 2-point pair)."""
+    return x if dst else x * (n // 2)
+
+
+def main():
+    worst16, worst32 = 0, 0
+    rows = []
+    for n, dst in ((4, True), (4, False), (8, False), (16, False), (32, False)):
+        T = mat(n, dst)
+        l2 = int(np.log2(n))
+        s = l2 + 5
+        rowl1 = int(np.abs(T).sum(1).max())
+        coll1 = int(np.abs(T).sum(0).max())
+        x0 = 255
+        f1_op = butterfly_operand(x0, n, dst)
+        f1 = shift_bound(x0 * rowl1, s)
+        f2_op = butterfly_operand(f1, n, dst)
+        c = shift_bound(f1 * rowl1, s)
+        dqmax = 0
+        for qp in range(52):
+            for intra in (True, False):
+                dqmax = max(dqmax, dequant(quant(c, qp, l2, intra), qp))
+        i1 = shift_bound(dqmax * coll1, s)
+        i2 = shift_bound(i1 * coll1, s)
+        ops16 = [f1_op, f1, f2_op, c, dqmax, i1, i2 + 255]
+        sums32 = [x0 * rowl1 + (1 << s), f1 * rowl1 + (1 << s), dqmax * coll1 + (1 << s), i1 * coll1 + (1 << s),
+                  n * n * 255 * 255]
+        worst16 = max(worst16, max(ops16))
+        worst32 = max(worst32, max(sums32))
+        rows.append((("DST" if dst else "DCT") + str(n), f1_op, f1, f2_op, c, dqmax, i1, i2, max(sums32)))
+    print("%-6s %8s %6s %8s %6s %6s %6s %6s %12s" % ("kind", "fwd1 op", "pass1", "fwd2 op", "coeff", "dq", "inv1",
+                                                     "rres", "max int32"))
+    for r in rows:
+        print("%-6s %8d %6d %8d %6d %6d %6d %6d %12d" % r)
+    print("largest int16 operand %d (limit 32767), largest int32 sum %d (limit 2^31-1)" % (worst16, worst32))
+    assert worst16 <= 32767 and worst32 < 2 ** 31
+
+
+if __name__ == "__main__":
+    main()
