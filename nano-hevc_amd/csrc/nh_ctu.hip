@@ -30,6 +30,8 @@
 // Exactness of the 24-bit multiplies and the 32-bit quantizer: DESIGN.md §4.3,
 // §4.4 (the residual is int16).
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <type_traits>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 #include "nh_mfma.hpp"
@@ -39,6 +41,36 @@
 namespace nh {
 
 __constant__ Basis c_basis_ctu;
+
+// f16 DCT32 bases of the narrow 32x32 chain (ctu_chain32_h), every entry
+// T[k][n] * 2^-10 (exact in f16), pre-arranged so that each lane's MFMA operand
+// is one 16-byte load (crow: the accumulator row order, nh_mfma.hpp).
+struct BasisH {
+    uint16_t b1[32][32];         // [k][y] = T[k][y]                       pass 1, B operand (lane k)
+    uint16_t a2[32][2][2][8];    // [l][h][s][j] = T[l][crow(8s + j, h)]   pass 2, A operand (lane l)
+    uint16_t b3[32][32];         // [y][k] = T[k][y]                       inverse pass 1, B operand (lane y)
+    uint16_t a4[32][2][2][8];    // [x][h][s][j] = T[crow(8s + j, h)][x]   inverse pass 2, A operand (lane x)
+};
+__constant__ BasisH c_basis_h;
+
+static BasisH make_basis_h() {
+    auto h = [](int v) { return __builtin_bit_cast(uint16_t, (_Float16)((float)v / 1024.0f)); };
+    auto cr = [](int g, int hh) { return (g & 3) + 8 * (g >> 2) + 4 * hh; };
+    BasisH b;
+    for (int k = 0; k < 32; ++k)
+        for (int n = 0; n < 32; ++n) {
+            b.b1[k][n] = h(dct32(k, n));
+            b.b3[n][k] = h(dct32(k, n));
+        }
+    for (int r = 0; r < 32; ++r)
+        for (int hh = 0; hh < 2; ++hh)
+            for (int st = 0; st < 2; ++st)
+                for (int j = 0; j < 8; ++j) {
+                    b.a2[r][hh][st][j] = h(dct32(r, cr(8 * st + j, hh)));
+                    b.a4[r][hh][st][j] = h(dct32(cr(8 * st + j, hh), r));
+                }
+    return b;
+}
 
 struct CtuArgs {
     const int16_t* src;
@@ -52,9 +84,20 @@ struct CtuArgs {
     QuantParams q[4];                // log2 N = 2..5
     int32_t dqs, dq_per;
     int32_t wide_only;               // A/B build only (NH_CTU_NARROW=0): every workgroup on the 32-bit chain
+    int32_t probe;                   // A/B build only (NH_CTU_PROBE): 1 = no batches, 2 = no global loads (wrong outputs)
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
+
+// The lane id as an opaque value: lane-derived addresses and constants of a
+// chain are then computed inside each batch, not hoisted out of the batch loop
+// and held live across it (which multiplied the register pressure by the
+// number of chain kinds in the loop).
+__device__ __forceinline__ int opaque_lane() {
+    int l = threadIdx.x & 63;
+    asm volatile("" : "+v"(l));
+    return l;
+}
 
 __device__ __forceinline__ int32_t sext16(int32_t v) { return (int16_t)(uint16_t)(uint32_t)v; }
 
@@ -73,7 +116,9 @@ template <int CTB> struct Strip {
     static constexpr int IMG = (CTB + 1) * IP, CF = CTB * CP;
     // narrow workgroups: an int16 tile aliasing the int32 one, rows of TP int16
     // (an odd number of dwords: the pair reads of a row pass are conflict-free)
-    static constexpr int TP = SW + 2, T16 = CTB * TP;
+    static constexpr int TP = SW + 2;
+    // (CTB 32: room for the f16 transpose tile of ctu_chain32_h, 32 rows of QH = 40 halves)
+    static constexpr int QH = 40, T16 = CTB == 32 ? 32 * QH : CTB * TP;
     static_assert((TP / 2) % 2 == 1 && T16 * 2 <= CF * 4, "int16 tile layout");
 };
 
@@ -87,7 +132,7 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
     using G = Strip<CTB>;
     constexpr int L2 = Log2<N>::v, S = L2 + 5, IP = G::IP, CP = G::CP;
     const ChainQ cq = make_chainq(a.q[L2 - 2], a.dqs, a.dq_per);
-    const int lane = threadIdx.x & 63, j = lane / N, t = lane % N;
+    const int lane = opaque_lane(), j = lane / N, t = lane % N;
     const bool on = b0 + j < cnt;
     const int e = list[on ? b0 + j : b0], sw = e >> 6, u = e & 63;   // idle lanes shadow the batch's first TU
     const int lx = 4 * (u % G::UW), ly = 4 * (u / G::UW);
@@ -210,7 +255,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
     constexpr int L2 = Log2<N>::v, S = L2 + 5, IP = G::IP, TP = G::TP, H = N / 2;
     constexpr int32_t BIAS = 1 << (S - 1);
     const ChainQ cq = make_chainq(a.q[L2 - 2], a.dqs, a.dq_per);
-    const int lane = threadIdx.x & 63, j = lane / N, t = lane % N;
+    const int lane = opaque_lane(), j = lane / N, t = lane % N;
     const bool on = b0 + j < cnt;
     const int e = list[on ? b0 + j : b0], sw = e >> 6, u = e & 63;   // idle lanes shadow the batch's first TU
     const int lx = 4 * (u % G::UW), ly = 4 * (u / G::UW);
@@ -341,7 +386,7 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
                                             int32_t* __restrict__ lvl, int16_t* __restrict__ rec) {
     constexpr int IP = Strip<32>::IP, CP = Strip<32>::CP;   // img[r * IP + c]: sample (r - 1, c), c = -1: left; cf[r * CP + c]
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
-    const int l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
+    const int l = opaque_lane(), r = l & 31, hh = l >> 5;
     const int32_t my_nb = hh == 0 ? img[r] : img[(1 + r) * IP - 1];
     int32_t s = my_nb;
 #pragma unroll
@@ -416,68 +461,270 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
     }
 }
 
-// A workgroup = 4 strips (one per wave for loading and classification); the
+// A 32x32 TU of a NARROW group on the f16 matrix cores: one
+// TU per wave, the four transform passes as v_mfma_f32_32x32x16_f16 pairs.
+// Exact: every operand is an integer of at most 11 bits (residual + 1536 for
+// pass 1, pass outputs <= 510, dequantized <= 180, inverse pass-1 outputs
+// <= 327) against the basis scaled by 2^-10, every product is exact in fp32
+// and every partial sum is a multiple of 2^-10 below 2^14 (tools/
+// packed_bounds.py: at most 3,667,968 * 2^-10), so the fp32 accumulators hold
+// the reference's integer sums exactly; the rounding constant is the
+// accumulator's initial 0.5 (transform.py:185) and floor() is the arithmetic
+// shift.  Lane (r, hh): pass 1 and inverse pass 1 take the data as the A
+// operand (lane = the free index), passes 2 and 4 take the previous
+// accumulator as the B operand in accumulator row order (the bases
+// pre-permuted to match), and one LDS transpose sits after dequantization.
+// Same results as ctu_chain / ctu_chain_pk on these TUs.
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f16x_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ h8_t ld_h8(const uint16_t* p) { return __builtin_bit_cast(h8_t, *(const uint4*)p); }
+__device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
+}
+__device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s) {   // registers 8s .. 8s+7, floored, as f16
+    uint4 u;
+    u.x = pk_floor_h(acc[8 * s + 0], acc[8 * s + 1]);
+    u.y = pk_floor_h(acc[8 * s + 2], acc[8 * s + 3]);
+    u.z = pk_floor_h(acc[8 * s + 4], acc[8 * s + 5]);
+    u.w = pk_floor_h(acc[8 * s + 6], acc[8 * s + 7]);
+    return __builtin_bit_cast(h8_t, u);
+}
+__device__ __forceinline__ f16x_t splat16(float v) {
+    f16x_t r;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) r[g] = v;
+    return r;
+}
+
+__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, int gx0, int gy0,
+                                              int32_t* __restrict__ lvl, int16_t* __restrict__ rec) {
+    constexpr int IP = Strip<32>::IP, QH = Strip<32>::QH;   // img[r * IP + c]: sample (r - 1, c), c = -1: left
+    const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
+    const int l = opaque_lane(), r = l & 31, hh = l >> 5;
+    const int32_t topr = img[r], leftr = img[(1 + r) * IP - 1], tr = img[31], bl = img[32 * IP - 1];
+    int32_t sdc = hh ? leftr : topr;   // DC (intra.py:46-62): lane halves hold top / left
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sdc += __shfl_xor(sdc, o, 64);
+    const int32_t dc = (sdc + 32) >> 6;
+    const pk16 dc2 = pk_splat(dc);
+    // column x = r, rows y = 8hh + 16c + j (the pass-1 A operand), as row pairs p = 4c + q
+    pk16 o2[8];
+    pku16 pl2[8];
+    {
+        const pku16 wl = {(unsigned short)(31 - r), (unsigned short)(31 - r)}, sh = {6, 6};
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int y = 8 * hh + 16 * (p >> 2) + 2 * (p & 3);
+            o2[p] = pk_pair(img[(1 + y) * IP + r], img[(2 + y) * IP + r]);
+            const int32_t b = (r + 1) * tr + (31 - y) * topr + (y + 1) * bl + 32;   // planar, intra.py:81-113
+            const pku16 bs = {(unsigned short)b, (unsigned short)(b + bl - topr)};
+            const pku16 lf = {(unsigned short)img[(1 + y) * IP - 1], (unsigned short)img[(2 + y) * IP - 1]};
+            pl2[p] = (lf * wl + bs) >> sh;
+        }
+    }
+    int32_t ed = 0, ep = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const pk16 d0 = o2[p] - dc2, d1 = o2[p] - __builtin_bit_cast(pk16, pl2[p]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ed += __shfl_xor(ed, o, 64);
+        ep += __shfl_xor(ep, o, 64);
+    }
+    const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+    // residual (intra.py:65-67) + 1536 as f16 bits: 0x6600 + n for |n| < 512
+    uint32_t hx[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const pk16 rr = o2[p] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[p]));
+        hx[p] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, rr) + (pku16){0x6600, 0x6600});
+    }
+    // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x]; the 1536 offset removed by the bias (row 0 only:
+    // every other DCT32 row sums to 0)
+    f16x_t acc = splat16(r == 0 ? 0.5f - 3072.0f : 0.5f);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
+                                                 ld_h8(&c_basis_h.b1[r][8 * hh]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
+                                                 ld_h8(&c_basis_h.b1[r][16 + 8 * hh]), acc, 0, 0, 0);
+    // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
+    f16x_t acc2 = splat16(0.5f);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a2[r][hh][0][0]), acc_h8(acc, 0), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a2[r][hh][1][0]), acc_h8(acc, 1), acc2, 0, 0, 0);
+    // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
+    int32_t* lrow = lvl + (int64_t)(gy0 + r) * a.pitch + gx0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int32_t L4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int g = 4 * q + e;
+            L4[e] = quant_s((int32_t)__builtin_floorf(acc2[g]), cq.qs, cq.h_v, cq.hneg_v);
+            qt[crow(g, hh) * QH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
+        }
+        *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+    }
+    wave_sync();
+    // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
+    f16x_t acc3 = splat16(0.5f);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&c_basis_h.b3[r][8 * hh]), acc3,
+                                                  0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 16 + 8 * hh),
+                                                  ld_h8(&c_basis_h.b3[r][16 + 8 * hh]), acc3, 0, 0, 0);
+    // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
+    f16x_t acc4 = splat16(0.5f);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a4[r][hh][0][0]), acc_h8(acc3, 0), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a4[r][hh][1][0]), acc_h8(acc3, 1), acc4, 0, 0, 0);
+    // reconstruct + clip (intra.py:70-78), row y = r
+    int16_t* rrow = rec + (int64_t)(gy0 + r) * a.pitch + gx0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        int32_t R4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int x = 8 * q + 4 * hh + e;
+            const int32_t p = use_dc ? dc
+                                     : ((31 - x) * leftr + (x + 1) * tr + (31 - r) * (int32_t)img[x] + (r + 1) * bl + 32) >> 6;
+            const int32_t v = p + (int32_t)__builtin_floorf(acc4[4 * q + e]);
+            R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
+        }
+        *(uint2*)(rrow + 8 * q + 4 * hh) =
+            make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
+    }
+}
+
+// Shared memory of one workgroup = 4 strips.  Narrow kernels keep the
+// coefficient tile in int16 (half the LDS: more workgroups per CU).
+template <int CTB, bool NARROW> struct CtuSmem {
+    using G = Strip<CTB>;
+    static constexpr int TILE32 = NARROW ? (4 * G::T16 + 1) / 2 : 4 * G::CF;
+    __attribute__((aligned(16))) int16_t img[4 * G::IMG];
+    __attribute__((aligned(16))) int32_t tile[TILE32];
+    uint16_t list[4][256];
+    int cnt[4][4], org[8], next, wide[4];
+};
+
+// One group of 4 strips (one per wave for loading and classification); the
 // TUs of all 4 strips are pooled per size, so a batch of 64/N TUs fills its
 // lanes (a strip alone holds ~half a batch per size), and the batches are
 // claimed by the 4 waves in descending cost (32x32 chains first).
-template <int CTB, bool LUMA, int WAVES, bool MFMA32>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a) {
+// NARROW: the packed 16-bit chain.  A group with any sample (strip, row above,
+// column left) outside [0, 255] is not coded here: its strips are marked in
+// the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
+// !NARROW: the 32-bit chain, any int16 input.
+// A strip's source samples in flight: issued by strip_issue, written to the
+// LDS image by strip_store (the split lets the persistent kernel keep the next
+// group's loads in flight under the current group's chains).
+template <int CTB> struct StripLoad {
+    static constexpr int NV = (CTB * Strip<CTB>::UW + 63) / 64;
+    uint2 v[NV];
+    uint2 top;
+    int32_t left;
+};
+
+template <int CTB>
+__device__ __forceinline__ int strip_of(const CtuArgs& a, int grp, int wv, int& sx0, int& sy0) {
+    const int strip = grp * 4 + wv;
+    sx0 = (strip % a.strips_x) * Strip<CTB>::SW;
+    sy0 = (a.row0 + strip / a.strips_x) * CTB;
+    return strip < a.strips_x * a.nrows;
+}
+__device__ __forceinline__ int64_t plane_off(const CtuArgs& a, int pz) {
+    const int gz = pz / a.ppg, cz = pz - gz * a.ppg;
+    return (int64_t)gz * a.group_stride + (int64_t)cz * a.plane_stride;
+}
+
+template <int CTB>
+__device__ __forceinline__ void strip_issue(const CtuArgs& a, int grp, int pz, StripLoad<CTB>& ld) {
     using G = Strip<CTB>;
-    constexpr int SW = G::SW, UW = G::UW, IP = G::IP;
-    __shared__ __attribute__((aligned(16))) int16_t s_img[4 * G::IMG];
-    __shared__ int32_t s_cf[4 * G::CF];
-    __shared__ uint16_t s_list[4][256];
-    __shared__ int s_cnt[4][4], s_org[8], s_next, s_wide[4];
+    constexpr int UW = G::UW;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int strip = blockIdx.x * 4 + wv;
-    const bool valid = strip < a.strips_x * a.nrows;
-    const int pz = blockIdx.y, gz = pz / a.ppg, cz = pz - gz * a.ppg;
-    const int64_t poff = (int64_t)gz * a.group_stride + (int64_t)cz * a.plane_stride;
-    const int16_t* __restrict__ src = a.src + poff;
+    int sx0, sy0;
+    const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
+    const int16_t* __restrict__ src = a.src + plane_off(a, pz);
+    const int w = a.w, h = a.h, pitch = a.pitch;
+#pragma unroll
+    for (int i = 0; i < ld.NV; ++i) {
+        const int g = 64 * i + lane, ry = g / UW, gx = g % UW, x = sx0 + 4 * gx, y = sy0 + ry;
+        ld.v[i] = make_uint2(0u, 0u);   // outside the plane: no TU reads it
+        if (valid && g < CTB * UW && x < w && y < h && (!NH_AB || a.probe != 2))
+            ld.v[i] = *(const uint2*)(src + (int64_t)y * pitch + x);
+    }
+    ld.top = make_uint2(0x00800080u, 0x00800080u);   // 128 above the frame (block.py:41)
+    {
+        const int x = sx0 + 4 * lane;
+        if (valid && lane < UW && sy0 > 0 && x < w) ld.top = *(const uint2*)(src + (int64_t)(sy0 - 1) * pitch + x);
+    }
+    ld.left = 128;   // left of the frame (block.py:48)
+    {
+        const int y = sy0 + lane;
+        if (valid && lane < CTB && sx0 > 0) ld.left = y < h ? src[(int64_t)y * pitch + sx0 - 1] : 0;
+    }
+}
+
+// Writes the strip image; returns whether any of its samples is outside [0, 255].
+template <int CTB>
+__device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* img, bool valid) {
+    using G = Strip<CTB>;
+    constexpr int UW = G::UW, IP = G::IP;
+    const int lane = threadIdx.x & 63;
+    uint32_t hi_bits = 0;
+#pragma unroll
+    for (int i = 0; i < ld.NV; ++i) {
+        const int g = 64 * i + lane, ry = g / UW, gx = g % UW;
+        if (g < CTB * UW) {
+            hi_bits |= ld.v[i].x | ld.v[i].y;
+            *(uint2*)&img[(1 + ry) * IP + 4 + 4 * gx] = ld.v[i];
+        }
+    }
+    if (lane < UW) {
+        hi_bits |= ld.top.x | ld.top.y;
+        *(uint2*)&img[4 + 4 * lane] = ld.top;
+    }
+    if (lane < CTB) {
+        hi_bits |= (uint16_t)ld.left;
+        img[(1 + lane) * IP + 3] = (int16_t)ld.left;
+    }
+    return valid && (hi_bits & 0xff00ff00u) != 0;
+}
+
+// MFMA32: the 32x32 TUs on the matrix cores, one per batch (narrow: f16,
+// ctu_chain32_h; wide: int8, ctu_chain32 -- A/B forms); otherwise two per
+// batch on 32-point butterflies.
+//
+// One group of 4 strips (one per wave for loading and classification); the
+// TUs of all 4 strips are pooled per size, so a batch of 64/N TUs fills its
+// lanes (a strip alone holds ~half a batch per size), and the batches are
+// claimed by the 4 waves in descending cost (32x32 chains first).  The
+// group's loads (ld) were issued by the caller; the classification runs
+// while they are in flight.
+// NARROW: the packed 16-bit chain.  A group with any sample (strip, row above,
+// column left) outside [0, 255] is not coded here: its strips are marked in
+// the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
+// !NARROW: the 32-bit chain, any int16 input.
+// Returns with the workgroup's waves in the batch loop's exit (no barrier).
+template <int CTB, bool LUMA, bool NARROW, bool MFMA32, class Prefetch>
+__device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, CtuSmem<CTB, NARROW>& sm,
+                                          StripLoad<CTB>& ld, Prefetch&& prefetch) {
+    using G = Strip<CTB>;
+    constexpr int UW = G::UW;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int sx0, sy0;
+    const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
+    const int64_t poff = plane_off(a, pz);
     int32_t* lvl = a.lvl + poff;
     int16_t* rec = a.rec + poff;
-    const int pid = a.plane_id + cz;
-    const int w = a.w, h = a.h, pitch = a.pitch;
-    const int sx0 = (strip % a.strips_x) * SW, sy0 = (a.row0 + strip / a.strips_x) * CTB;
-    int16_t* img = s_img + wv * G::IMG;
+    const int pid = a.plane_id + (pz % a.ppg);
+    const int w = a.w, h = a.h;
+    int16_t* img = sm.img + wv * G::IMG;
 
-    // ---- 1. each wave: its strip, the row above and the column left, into LDS (8-B loads) ----
-    uint32_t hi_bits = 0;   // any sample outside [0, 255]: the workgroup takes the 32-bit chain
-    if (valid) {
-#pragma unroll
-        for (int g0 = 0; g0 < CTB * UW; g0 += 64) {
-            const int g = g0 + lane, ry = g / UW, gx = g % UW, x = sx0 + 4 * gx, y = sy0 + ry;
-            uint2 v = make_uint2(0u, 0u);   // outside the plane: no TU reads it
-            if (x < w && y < h) v = *(const uint2*)(src + (int64_t)y * pitch + x);
-            hi_bits |= v.x | v.y;
-            *(uint2*)&img[(1 + ry) * IP + 4 + 4 * gx] = v;
-        }
-        if (lane < UW) {
-            const int x = sx0 + 4 * lane;
-            uint2 v = make_uint2(0x00800080u, 0x00800080u);   // 128 above the frame (block.py:41)
-            if (sy0 > 0 && x < w) v = *(const uint2*)(src + (int64_t)(sy0 - 1) * pitch + x);
-            hi_bits |= v.x | v.y;
-            *(uint2*)&img[4 + 4 * lane] = v;
-        }
-        if (lane < CTB) {
-            const int y = sy0 + lane;
-            const int16_t v = sx0 == 0 ? (int16_t)128 : (y < h ? src[(int64_t)y * pitch + sx0 - 1] : (int16_t)0);
-            hi_bits |= (uint16_t)v;
-            img[(1 + lane) * IP + 3] = v;
-        }
-        if (lane == 0) {
-            s_org[2 * wv] = sx0;
-            s_org[2 * wv + 1] = sy0;
-        }
-    }
-    {
-        const uint64_t wide = __ballot((hi_bits & 0xff00ff00u) != 0);
-        if (lane == 0) s_wide[wv] = wide != 0;
-    }
-
-    // ---- 2. classify the strip's 64 units: leaf size / origin (<= 3 hashes), TU map ----
+    // ---- 1. classify the strip's 64 units (loads in flight): leaf size / origin (<= 3 hashes), TU map ----
     bool org = false;
     int ls = 0;
+    const int64_t tu_org = (int64_t)pz * a.tu_plane + (int64_t)(sy0 >> 2) * (w >> 2) + (sx0 >> 2);
     if (valid) {
         const int ux = lane % UW, uy = lane / UW, x = sx0 + 4 * ux, y = sy0 + 4 * uy;
         const bool in = x < w && y < h;
@@ -495,10 +742,29 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         m[k] = __ballot(org && ls == k + 2);
-        if (lane == 0) s_cnt[wv][k] = __popcll(m[k]);
+        if (lane == 0) sm.cnt[wv][k] = __popcll(m[k]);
     }
-    if (threadIdx.x == 0) s_next = 0;
+    // ---- 2. the strip image: its samples, the row above and the column left, into LDS ----
+    {
+        const bool wide = strip_store<CTB>(ld, img, valid);
+        if constexpr (NARROW) {
+            const uint64_t wb = __ballot(wide);
+            if (lane == 0) sm.wide[wv] = wb != 0;
+        }
+        if (lane == 0) {
+            sm.org[2 * wv] = sx0;
+            sm.org[2 * wv + 1] = sy0;
+        }
+    }
+    prefetch();   // the next group's loads into ld (persistent kernel)
+    if (threadIdx.x == 0) sm.next = 0;
     __syncthreads();
+    if constexpr (NARROW) {
+        if (__builtin_amdgcn_readfirstlane(sm.wide[0] | sm.wide[1] | sm.wide[2] | sm.wide[3] | a.wide_only)) {
+            if (valid && lane == 0) a.tu[tu_org] = (uint8_t)(ls | 0x80);   // unit 0 = the strip's origin
+            return;
+        }
+    }
     // pool the strips' TUs per size: entry = strip << 6 | unit
     int cnt[4];
 #pragma unroll
@@ -507,37 +773,39 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         cnt[k] = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            off += q < wv ? s_cnt[q][k] : 0;
-            cnt[k] += s_cnt[q][k];
+            off += q < wv ? sm.cnt[q][k] : 0;
+            cnt[k] += sm.cnt[q][k];
         }
-        if (org && ls == k + 2) s_list[k][off + __popcll(m[k] & ((1ull << lane) - 1))] = (uint16_t)(wv << 6 | lane);
+        if (org && ls == k + 2) sm.list[k][off + __popcll(m[k] & ((1ull << lane) - 1))] = (uint16_t)(wv << 6 | lane);
     }
     __syncthreads();
 
     // ---- 3. batches, claimed in descending cost: 32x32 chains, then 16, 8, 4 ----
-    // NARROW (every sample of the 4 strips and their neighbours 8-bit): the
-    // packed 16-bit chain; otherwise the 32-bit chain (any int16 input).
-    const bool narrow =
-        __builtin_amdgcn_readfirstlane((s_wide[0] | s_wide[1] | s_wide[2] | s_wide[3] | a.wide_only) == 0);
-    int16_t* s_t16 = (int16_t*)s_cf;
+    if (NH_AB && a.probe == 1) return;
     const int n32 = CTB == 32 ? (MFMA32 ? cnt[3] : (cnt[3] + 1) / 2) : 0;
     const int n16 = CTB >= 16 ? (cnt[2] + 3) / 4 : 0, n8 = CTB >= 8 ? (cnt[1] + 7) / 8 : 0, n4 = (cnt[0] + 15) / 16;
     const int total = n32 + n16 + n8 + n4;
-#define NH_CHAIN(N, DST, L, B)                                                          \
-    if (narrow) ctu_chain_pk<N, DST, CTB>(a, s_img, s_t16, s_list[L], cnt[L], B, s_org, lvl, rec); \
-    else ctu_chain<N, DST, CTB>(a, s_img, s_cf, s_list[L], cnt[L], B, s_org, lvl, rec);
+#define NH_CHAIN(N, DST, L, B)                                                                              \
+    if constexpr (NARROW)                                                                                   \
+        ctu_chain_pk<N, DST, CTB>(a, sm.img, (int16_t*)sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec);   \
+    else                                                                                                    \
+        ctu_chain<N, DST, CTB>(a, sm.img, sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec);
     for (;;) {
         int item = 0;
-        if (lane == 0) item = atomicAdd(&s_next, 1);
+        if (lane == 0) item = atomicAdd(&sm.next, 1);
         item = __builtin_amdgcn_readfirstlane(__shfl(item, 0, 64));
         if (item >= total) break;
         if constexpr (CTB == 32) {
             if (item < n32) {
-                if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores (A/B form)
-                    const int e = s_list[3][item], sw = e >> 6;
-                    ctu_chain32(a, s_img + sw * G::IMG + 4, s_cf + sw * G::CF, s_org[2 * sw], s_org[2 * sw + 1], lvl,
-                                rec);
-                } else {                  // two TUs per wave, 32-point butterflies
+                if constexpr (NARROW && MFMA32) {   // one TU per wave on the f16 matrix cores
+                    const int e = sm.list[3][item], sw = e >> 6;
+                    ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.org[2 * sw],
+                                  sm.org[2 * sw + 1], lvl, rec);
+                } else if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores (A/B form)
+                    const int e = sm.list[3][item], sw = e >> 6;
+                    ctu_chain32(a, sm.img + sw * G::IMG + 4, sm.tile + sw * G::CF, sm.org[2 * sw], sm.org[2 * sw + 1],
+                                lvl, rec);
+                } else {                          // two TUs per wave, 32-point butterflies
                     NH_CHAIN(32, false, 3, 2 * item)
                 }
                 continue;
@@ -563,6 +831,71 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
 #undef NH_CHAIN
 }
 
+// The config-4 kernel proper, packed chain, 32x32 TUs on packed butterflies
+// (MFMA32: on the f16 matrix cores, A/B form).  PERSIST: a grid of
+// resident workgroups walking the (group, plane) items with stride gridDim.x,
+// each group's loads issued during the previous group's chains.
+template <int CTB, bool LUMA, bool MFMA32 = false, bool PERSIST = false>
+__global__ void __launch_bounds__(256) k_ctu_open(CtuArgs a, int items) {
+    __shared__ CtuSmem<CTB, true> sm;
+    const int groups = items / (int)gridDim.y;
+    if constexpr (!PERSIST) {
+        StripLoad<CTB> ld;
+        strip_issue<CTB>(a, blockIdx.x, blockIdx.y, ld);
+        ctu_group<CTB, LUMA, true, MFMA32>(a, blockIdx.x, blockIdx.y, sm, ld, [] {});
+    } else {
+        (void)groups;
+        StripLoad<CTB> ld;
+        int it = blockIdx.x;
+        const int ngroups = a.strips_x * a.nrows;
+        const int gcount = (ngroups + 3) / 4;
+        if (it < items) strip_issue<CTB>(a, it % gcount, it / gcount, ld);
+        for (; it < items; it += gridDim.x) {
+            const int nx = it + gridDim.x;
+            ctu_group<CTB, LUMA, true, MFMA32>(a, it % gcount, it / gcount, sm, ld, [&] {
+                if (nx < items) strip_issue<CTB>(a, nx % gcount, nx / gcount, ld);
+            });
+            __syncthreads();   // every wave done with this group's LDS
+        }
+    }
+}
+
+// The wide fix-up: workgroup b scans the origin bytes of groups [16 b, 16 b + 16)
+// and codes the marked ones with the 32-bit chain (restoring their TU bytes).
+// For 8-bit content nothing is marked and every workgroup exits at once.
+constexpr int kWideGroups = 16;
+template <int CTB, bool LUMA, bool MFMA32>
+__global__ void __launch_bounds__(256) k_ctu_wide(CtuArgs a) {
+    __shared__ CtuSmem<CTB, false> sm;
+    __shared__ unsigned long long s_mask;
+    using G = Strip<CTB>;
+    const int g0 = blockIdx.x * kWideGroups, pz = blockIdx.y;
+    if (threadIdx.x < kWideGroups) {
+        const int nstrips = a.strips_x * a.nrows;
+        bool marked = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int strip = 4 * (g0 + (int)threadIdx.x) + k;
+            if (strip < nstrips) {
+                const int sx0 = (strip % a.strips_x) * G::SW, sy0 = (a.row0 + strip / a.strips_x) * CTB;
+                marked |= (a.tu[(int64_t)pz * a.tu_plane + (int64_t)(sy0 >> 2) * (a.w >> 2) + (sx0 >> 2)] & 0x80) != 0;
+            }
+        }
+        const uint64_t mk = __ballot(marked);
+        if (threadIdx.x == 0) s_mask = mk;
+    }
+    __syncthreads();
+    uint64_t mask = s_mask;
+    while (mask) {
+        const int b = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        StripLoad<CTB> ld;
+        strip_issue<CTB>(a, g0 + b, pz, ld);
+        ctu_group<CTB, LUMA, false, MFMA32>(a, g0 + b, pz, sm, ld, [] {});
+        __syncthreads();
+    }
+}
+
 static int ensure_basis_ctu() {
     static unsigned long long ready = 0;   // one bit per device
     int dev = 0;
@@ -571,6 +904,8 @@ static int ensure_basis_ctu() {
     if (!(ready >> dev & 1ull)) {
         const Basis b = make_basis();
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_ctu), &b, sizeof(b)));
+        const BasisH bh = make_basis_h();
+        NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_h), &bh, sizeof(bh)));
         ready |= 1ull << dev;
     }
     return NH_OK;
@@ -611,40 +946,71 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     const int64_t strips = (int64_t)a.strips_x * a.nrows;
     if (strips <= 0 || planes <= 0) return NH_OK;
     if ((strips + 3) / 4 > INT32_MAX) return NH_EARG;
-    const dim3 grid((unsigned)((strips + 3) / 4), (unsigned)planes);
-    // 32x32 TUs: 32-point butterflies, two TUs per wave (128 VGPRs, 4 waves/SIMD)
-    // by default; the int8-MFMA chain (one TU per wave, capped at 3 waves/SIMD =
-    // 168 VGPRs without spills; uncapped 228 registers) measured equal in
-    // rocprof (584.7 vs 586.6 us per 16 luma planes), so the
-    // north star's rule keeps the butterfly.  A/B build: NH_CTU_T32 = 1 (MFMA) /
-    // 0, NH_CTU_WAVES = 1 (compiler) / 3 / 4 / 5, NH_CTU_NARROW = 0 (no packed chain).
-    static const int cw = NH_KNOB("NH_CTU_WAVES", 0);
-    static const int t32 = NH_KNOB("NH_CTU_T32", 0);
+    const int64_t groups = (strips + 3) / 4;
+    if (groups * planes > INT32_MAX) return NH_EARG;
+    const int items = (int)(groups * planes);
+    const dim3 grid((unsigned)groups, (unsigned)planes), grid_wide((unsigned)((groups + kWideGroups - 1) / kWideGroups), (unsigned)planes);
+    // Narrow groups (8-bit content) are coded by k_ctu_open with the packed
+    // chain, their 32x32 TUs on the f16 matrix cores (rocprof: 428.5 vs 459.9
+    // us per 16 luma planes for the packed butterflies); the
+    // groups it marks (any sample outside [0, 255]) by k_ctu_wide with the
+    // 32-bit chain.  A/B build: NH_CTU_T32 = 0 (narrow 32x32 TUs on packed
+    // butterflies) / 1 (wide 32x32 TUs on int8 MFMA), NH_CTU_PERSIST = 1
+    // (resident grid, loads one group ahead), NH_CTU_NARROW = 0 (every group on
+    // the 32-bit path), NH_CTU_PROBE = 1 / 2 (no batches / no global loads).
+    static const int t32 = NH_KNOB("NH_CTU_T32", 2);
+    static const int persist = NH_KNOB("NH_CTU_PERSIST", 0);
     a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
-#define NH_CTU(C, W, M)                                                             \
-    if (is_luma) k_ctu_open<C, true, W, M><<<grid, 256, 0, s>>>(a);                 \
-    else k_ctu_open<C, false, W, M><<<grid, 256, 0, s>>>(a);
-    switch (ctb) {
-        case 4: NH_CTU(4, 1, false) break;
-        case 8: NH_CTU(8, 1, false) break;
-        case 16: NH_CTU(16, 1, false) break;
-        case 32:
-#if NH_AB
-            if (t32 == 1) {
-                if (cw == 1) { NH_CTU(32, 1, true) break; }
-                if (cw == 4) { NH_CTU(32, 4, true) break; }
-                NH_CTU(32, 3, true) break;
+    a.probe = NH_KNOB("NH_CTU_PROBE", 0);
+    auto launch_open = [&](auto kern) -> int {
+        if (NH_AB != 0 && persist) {
+            static int cus = 0;
+            if (!cus) {
+                int dev = 0;
+                NH_HIP(hipGetDevice(&dev));
+                NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             }
-            if (cw == 3) { NH_CTU(32, 3, false) break; }
-            if (cw == 4) { NH_CTU(32, 4, false) break; }
-            if (cw == 5) { NH_CTU(32, 5, false) break; }
-#endif
-            (void)cw;
-            (void)t32;
-            NH_CTU(32, 1, false) break;
+            int per_cu = 0;
+            NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+            const int res = std::max(1, cus * per_cu);
+            kern<<<dim3((unsigned)std::min(items, res), 1), 256, 0, s>>>(a, items);
+        } else {
+            kern<<<grid, 256, 0, s>>>(a, items);
+        }
+        return NH_OK;
+    };
+    // CTB 32 luma: 32x32 TUs on the matrix cores unless the A/B build says otherwise
+    auto launch_ctb = [&](auto ctb_c, auto luma_c) -> int {
+        constexpr int C = decltype(ctb_c)::value;
+        constexpr bool L = decltype(luma_c)::value;
+        constexpr bool M32 = C == 32 && L;
+        int rc3;
+        if constexpr (NH_AB != 0) {
+            const bool m = M32 && t32 != 0;
+            if (m) rc3 = persist ? launch_open(k_ctu_open<C, L, M32, true>) : launch_open(k_ctu_open<C, L, M32, false>);
+            else rc3 = persist ? launch_open(k_ctu_open<C, L, false, true>) : launch_open(k_ctu_open<C, L, false, false>);
+            if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
+            else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
+        } else {
+            rc3 = launch_open(k_ctu_open<C, L, M32, false>);
+            k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
+        }
+        return rc3;
+    };
+    using std::integral_constant;
+    int rc2 = NH_OK;
+    switch (ctb) {
+        case 4: rc2 = is_luma ? launch_ctb(integral_constant<int, 4>{}, std::true_type{})
+                              : launch_ctb(integral_constant<int, 4>{}, std::false_type{}); break;
+        case 8: rc2 = is_luma ? launch_ctb(integral_constant<int, 8>{}, std::true_type{})
+                              : launch_ctb(integral_constant<int, 8>{}, std::false_type{}); break;
+        case 16: rc2 = is_luma ? launch_ctb(integral_constant<int, 16>{}, std::true_type{})
+                               : launch_ctb(integral_constant<int, 16>{}, std::false_type{}); break;
+        case 32: rc2 = is_luma ? launch_ctb(integral_constant<int, 32>{}, std::true_type{})
+                               : launch_ctb(integral_constant<int, 32>{}, std::false_type{}); break;
         default: return NH_EVALUE;
     }
-#undef NH_CTU
+    if (rc2) return rc2;
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
