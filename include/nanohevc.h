@@ -210,13 +210,16 @@ int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane_set* set, 
 
 /* Config 5: every full 32x32 block of an int16 source plane through the
  * config-4 chain at N=32.  variant 0 = butterfly
- * (k_tu_process<32>), 1 = int8 matrix cores (v_mfma_i32_32x32x32_i8 with
- * exact int8 part splitting).  Identical outputs.  pitch % 8 == 0. */
+ * (k_tu_process<32>), 1 = matrix cores: blocks whose samples and neighbours
+ * are 8-bit on f16 MFMA (exact), the others on int8 MFMA
+ * (v_mfma_i32_32x32x32_i8 with exact int8 part splitting), 2 = int8 MFMA for
+ * every block (A/B).  Identical outputs.  pitch % 8 == 0. */
 int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl,
                   int16_t* d_recon, int variant, void* stream);
 /* Config 5 over every plane of up to NH_MAX_PLANE_SETS plane sets (a stream of
- * frames): variant 1 = one int8-MFMA launch per set (blockIdx.y = plane),
- * variant 0 = the butterfly, one launch per plane (A/B).  Levels / recon use
+ * frames): variant 1 = one f16-MFMA launch + one int8 fix-up launch per set
+ * (blockIdx.y = plane), 2 = one int8-MFMA launch per set, 0 = the butterfly,
+ * one launch per plane (A/B).  Levels / recon use
  * the source layout.  Same per-plane results as nh_tc32_plane. */
 int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
                    int16_t* d_recon, int variant, void* stream);

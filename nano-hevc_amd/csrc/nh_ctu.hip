@@ -11,22 +11,21 @@
 //
 // Layout of the work.  One wave owns a STRIP of 1024 samples: CTB rows x
 // 1024/CTB columns (one 32x32 luma CTU, four 16x16 chroma CTUs side by side,
-// ...), i.e. 64 4x4 units, one per lane.  The wave
-//   1. loads the strip, the row above it and the column left of it into an
-//      LDS image with 8-byte coalesced loads (every TU neighbour is then an
-//      LDS read);
-//   2. classifies its units: lane u descends the quadtree to its unit's leaf
-//      (<= 3 hashes), writes the TU map entry, and the TU origins are compacted
-//      into per-size LDS lists with wave ballots;
-//   3. codes the TUs of the workgroup's 4 strips pooled by size, 64/N at a
-//      time: lane l takes column / row l mod N of TU l / N (32-point to 4-point
-//      butterflies; the 32x32 TUs alternatively on the int8 matrix cores, one
-//      per wave -- A/B only, not faster here), transposes through an LDS tile
-//      of the strip (every TU at its own place, so TUs never collide).
-// No workgroup barriers (a wave only touches its own LDS slices, and LDS
-// executes one wave's instructions in order), no global atomics, no per-size
-// relaunch, the source read once.  Levels and recon rows are stored straight
-// from the registers (N contiguous int32 / int16 per lane).
+// ...), i.e. 64 4x4 units, one per lane; a workgroup codes a GROUP of 4 strips.
+// Each wave
+//   1. issues the loads of its strip, the row above it and the column left of
+//      it, classifies its units while they are in flight (lane u descends the
+//      quadtree to its unit's leaf, <= 3 hashes, and writes the TU map), then
+//      stores the strip image in LDS (every TU neighbour is an LDS read);
+//   2. the TU origins of the 4 strips are pooled into per-size LDS lists;
+//   3. the waves claim batches of 64/N TUs of one size (lane l: column / row
+//      l mod N of TU l / N), 32x32 TUs first.
+// Two kernels per plane set: k_ctu_open codes the groups whose samples are all
+// 8-bit with the packed 16-bit chain (nh_packed.hpp) and their
+// 32x32 TUs on exact f16 matrix cores (§4.4d); the groups it marks in the TU
+// map k_ctu_wide codes with the 32-bit chain (any int16 input).  No global
+// atomics, no per-size relaunch, the source read once.  Levels and recon rows
+// are stored straight from the registers.
 // Exactness of the 24-bit multiplies and the 32-bit quantizer: DESIGN.md §4.3,
 // §4.4 (the residual is int16).
 #include <hip/hip_runtime.h>
@@ -467,7 +466,7 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
 // pass 1, pass outputs <= 510, dequantized <= 180, inverse pass-1 outputs
 // <= 327) against the basis scaled by 2^-10, every product is exact in fp32
 // and every partial sum is a multiple of 2^-10 below 2^14 (tools/
-// packed_bounds.py: at most 3,667,968 * 2^-10), so the fp32 accumulators hold
+// packed_bounds.py: at most 6,813,696 * 2^-10), so the fp32 accumulators hold
 // the reference's integer sums exactly; the rounding constant is the
 // accumulator's initial 0.5 (transform.py:185) and floor() is the arithmetic
 // shift.  Lane (r, hh): pass 1 and inverse pass 1 take the data as the A
@@ -638,10 +637,11 @@ __device__ __forceinline__ int64_t plane_off(const CtuArgs& a, int pz) {
 }
 
 template <int CTB>
-__device__ __forceinline__ void strip_issue(const CtuArgs& a, int grp, int pz, StripLoad<CTB>& ld) {
+__device__ __forceinline__ void strip_issue(const CtuArgs& a, int grp, int pz, StripLoad<CTB>& ld, int wv = -1) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63;
+    if (wv < 0) wv = threadIdx.x >> 6;
     int sx0, sy0;
     const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
     const int16_t* __restrict__ src = a.src + plane_off(a, pz);
@@ -896,6 +896,49 @@ __global__ void __launch_bounds__(256) k_ctu_wide(CtuArgs a) {
     }
 }
 
+// Config 5 for narrow blocks: one wave per full 32x32
+// block of the plane (the strip machinery with strips_x = w / 32 blocks per
+// row), the block image as a CTB-32 strip in LDS, ctu_chain32_h.  A wave whose
+// block or neighbours leave [0, 255] codes nothing and writes the marker
+// -32768 at its block's recon origin (recon is always in [0, 255]); the int8
+// chain (k_tc32_mfma, nh_tc32.hip) then codes exactly the marked blocks.
+constexpr int16_t kWideMark = (int16_t)0x8000;
+// K blocks per wave (consecutive in raster order), block k+1's loads issued
+// before block k's chain.  K = 1 in the product: K = 4 measured slower (0.177
+// vs 0.159 ms per 8K frame; 114 registers, 4 waves/SIMD), DESIGN.md §4.5.
+template <int K>
+__global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
+    using G = Strip<32>;
+    __shared__ __attribute__((aligned(16))) int16_t s_img[4][G::IMG];
+    __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * G::QH];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b0 = (blockIdx.x * 4 + wv) * K;
+    if (b0 >= nblk) return;   // whole wave
+    const int pz = blockIdx.y;
+    const int64_t poff = plane_off(a, pz);
+    StripLoad<32> ld;
+    // strip_issue addresses strip 4 * grp + wave: block b is grp = b / 4 with this wave's slot b % 4
+    auto issue = [&](int b) { strip_issue<32>(a, b >> 2, pz, ld, b & 3); };
+    issue(b0);
+    for (int k = 0; k < K; ++k) {
+        const int b = b0 + k;
+        if (b >= nblk) break;
+        const int sx0 = (b % a.strips_x) * 32, sy0 = (b / a.strips_x) * 32;
+        const bool wide = __any(strip_store<32>(ld, s_img[wv], true));
+        if (k + 1 < K && b + 1 < nblk) issue(b + 1);
+        wave_sync();
+        if (wide) {
+            if (lane == 0) a.rec[poff + (int64_t)sy0 * a.pitch + sx0] = kWideMark;
+        } else {
+            ctu_chain32_h(a, s_img[wv] + 4, s_q[wv], sx0, sy0, a.lvl + poff, a.rec + poff);
+        }
+        wave_sync();   // this wave's LDS reads of block k before block k+1's image writes
+    }
+}
+
+int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
+                       int dqs, int dq_per, hipStream_t s);
+
 static int ensure_basis_ctu() {
     static unsigned long long ready = 0;   // one bit per device
     int dev = 0;
@@ -1011,6 +1054,34 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         default: return NH_EVALUE;
     }
     if (rc2) return rc2;
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+// Config 5's narrow launch over one plane set (full 32x32 blocks only).
+int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
+                       int dqs, int dq_per, hipStream_t s) {
+    const int rc = ensure_basis_ctu();
+    if (rc) return rc;
+    CtuArgs a{};
+    a.src = src + S.base;
+    a.lvl = lvl + S.base;
+    a.rec = rec + S.base;
+    a.group_stride = S.group_stride;
+    a.plane_stride = S.plane_stride;
+    a.w = S.width;
+    a.h = S.height;
+    a.pitch = S.pitch;
+    a.ppg = S.planes_per_group;
+    a.strips_x = S.width / 32;
+    a.nrows = S.height / 32;
+    a.q[3] = q;
+    a.dqs = dqs;
+    a.dq_per = dq_per;
+    const int nblk = a.strips_x * a.nrows, planes = S.planes_per_group * S.num_groups;
+    if (!nblk || !planes) return NH_OK;
+    constexpr int K = 1;
+    k_tc32_h<K><<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, 0, s>>>(a, nblk);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

@@ -40,7 +40,9 @@ constexpr int kOP = 40;  // LDS row pitch (elements) of the per-wave tiles: 16-B
 // proceeds where the seeded quadtree's leaf is exactly 32x32 (tu_leaf); it
 // then also writes its 8x8 entries of the TU map.  Same per-TU chain as
 // k_tu_process<32>.
-template <bool TREE>
+// FIXUP (config 5, grid mode): code only the blocks k_tc32_h marked wide
+// (recon origin == -32768, nh_ctu.hip), every other wave exits at once.
+template <bool TREE, bool FIXUP = false>
 __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                    int nbx, int nblk, QuantParams qp, int dq_scale, int dq_per,
                                                    int32_t* lvl, int16_t* recon, TreeArgs ta, uint8_t* tu_log2) {
@@ -63,6 +65,9 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
         }
     }
     const int x0 = (b % nbx) * 32, y0 = (b / nbx) * 32 + (TREE ? ta.y_base : 0);
+    if constexpr (FIXUP) {
+        if (recon[(int64_t)y0 * pitch + x0] != (int16_t)0x8000) return;
+    }
     if constexpr (TREE) {
         if (x0 + 32 > w || y0 + 32 > h || tu_leaf(w, h, ta.ctb, ta.plane_id, ta.seed, x0, y0) != 32) return;
         tu_log2[(int64_t)(y0 / 4 + (l >> 3)) * (w / 4) + x0 / 4 + (l & 7)] = 5;
@@ -196,8 +201,10 @@ static int ensure_basis(hipStream_t s) {
 
 using namespace nh;
 
-// butterfly variant lives in nh_intraloop.hip
+// butterfly variant lives in nh_intraloop.hip; the narrow f16 launch in nh_ctu.hip
 namespace nh {
+int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
+                       int dqs, int dq_per, hipStream_t s);
 int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
                    hipStream_t s);
 }
@@ -213,21 +220,10 @@ extern "C" int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int 
     const int nbx = w / 32, nblk = nbx * (h / 32);
     if (!nblk) return NH_OK;
     if (variant == 0) return tc32_butterfly(d_src, w, h, pitch, qp, d_lvl, d_recon, s);
-    if (variant != 1) return NH_EARG;
-    int rc = ensure_basis(s);
-    if (rc) return rc;
-    int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
-    const int per = q / 6, rem = q % 6;
-    QuantParams p;
-    p.shift = 14 + per + 5;
-    p.mf = quant_scale(rem);
-    p.off = (uint32_t)((1ull << p.shift) / 3);
-    k_tc32_mfma<false><<<(nblk + 3) / 4, 256, 0, s>>>(d_src, w, h, pitch, nbx, nblk, p, dequant_scale(rem), per,
-                                                      d_lvl, d_recon, TreeArgs{}, nullptr);
-    NH_HIP(hipGetLastError());
-    return NH_OK;
+    if (variant != 1 && variant != 2) return NH_EARG;
+    nh_plane_set one{0, 0, 0, w, h, pitch, 1, 1, 0};
+    return nh_tc32_planes(d_src, &one, 1, qp, d_lvl, d_recon, variant, stream);
 }
-
 extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
                               int16_t* d_recon, int variant, void* stream) {
     if (!d_src || !d_lvl || !d_recon || !sets || nsets < 0 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
@@ -244,7 +240,7 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
             return NH_EARG;
         }
     }
-    if (variant != 0 && variant != 1) return NH_EARG;
+    if (variant < 0 || variant > 2) return NH_EARG;
     hipStream_t s = as_stream(stream);
     int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
     const int per = q / 6, rem = q % 6;
@@ -252,7 +248,7 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
     p.shift = 14 + per + 5;
     p.mf = quant_scale(rem);
     p.off = (uint32_t)((1ull << p.shift) / 3);
-    if (variant == 1) {
+    if (variant != 0) {
         int rc = ensure_basis(s);
         if (rc) return rc;
     }
@@ -274,9 +270,18 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
         ta.ppg = S.planes_per_group;
         ta.group_stride = S.group_stride;
         ta.plane_stride = S.plane_stride;
-        k_tc32_mfma<false><<<dim3((nblk + 3) / 4, planes), 256, 0, s>>>(
-            d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p, dequant_scale(rem), per, d_lvl + S.base,
-            d_recon + S.base, ta, nullptr);
+        const dim3 grid((nblk + 3) / 4, planes);
+        if (variant == 1) {   // narrow blocks on the f16 matrix cores, then the marked wide ones on int8
+            int rc = tc32_narrow_launch(d_src, d_lvl, d_recon, S, p, dequant_scale(rem), per, s);
+            if (rc) return rc;
+            k_tc32_mfma<false, true><<<grid, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
+                                                          dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base,
+                                                          ta, nullptr);
+        } else {              // int8 matrix cores only (A/B)
+            k_tc32_mfma<false><<<grid, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
+                                                    dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base, ta,
+                                                    nullptr);
+        }
         NH_HIP(hipGetLastError());
     }
     return NH_OK;

@@ -9,7 +9,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
   intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
-  tc32_plane          -- config 5: 32x32 chain, butterfly or int8-MFMA variant
+  tc32_plane          -- config 5: 32x32 chain, butterfly or matrix-core variants
   tc32_planes         -- config 5 over a frame stream (one MFMA launch per plane set)
   tu_pipeline_closed  -- config 4 in closed loop (CTU-row wavefront, TUs in z-order)
   tu_pipeline_closed_yuv420 -- the same over a YUV420 stream, luma and chroma wavefronts concurrent
@@ -409,7 +409,8 @@ def tu_pipeline_closed_yuv420(src, luma: PlaneSet, chroma: PlaneSet, seed: int, 
 
 def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=None):
     """Config 5 on one int16 plane (H, W), W % 8 == 0: every full
-    32x32 block through the chain.  variant 0 = butterfly, 1 = int8 MFMA.
+    32x32 block through the chain.  variant 0 = butterfly, 1 = matrix cores (f16
+    for 8-bit blocks, int8 otherwise), 2 = int8 MFMA only (A/B).
     Returns (levels int32 (H, W), recon int16 (H, W))."""
     torch = _torch()
     _need(src, torch.int16, "tc32_plane")
@@ -423,7 +424,8 @@ def tc32_plane(src, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=N
 
 def tc32_planes(src, sets, qp: int = 32, variant: int = 1, lvl=None, rec=None, stream=None):
     """Config 5 over every plane of ``sets`` (e.g. yuv420_plane_sets of a frame
-    stream): one int8-MFMA launch per plane set (variant 1) or the butterfly
+    stream): per plane set one f16-MFMA launch plus an int8 fix-up for non-8-bit
+    blocks (variant 1), one int8-MFMA launch (2), or the butterfly
     per plane (variant 0).  Returns (levels int32, recon int16), source layout."""
     torch = _torch()
     _need(src, torch.int16, "tc32_planes(src)")

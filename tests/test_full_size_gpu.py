@@ -124,7 +124,7 @@ def test_cfg5_8k_luma_mfma_and_butterfly(torch_dev):
     el, er = O.tc32_plane(src, 4)
     full = (slice(0, 4320 // 32 * 32), slice(0, 7680 // 32 * 32))
     p_ref = psnr(src[full], er[full])
-    for v in (1, 0):   # int8 MFMA, butterfly
+    for v in (1, 2, 0):   # f16 MFMA (8-bit blocks), int8 MFMA, butterfly
         l, r = gpu.tc32_plane(d, 4, v)
         r = r.cpu().numpy()
         assert np.array_equal(l.cpu().numpy(), el), v

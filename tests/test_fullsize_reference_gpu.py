@@ -119,7 +119,7 @@ def test_cfg2_4k_yuv420_equals_reference(ref, torch_dev):
         off += ph * pw
 
 
-@pytest.mark.parametrize("variant", [1, 0])   # int8 MFMA, butterfly
+@pytest.mark.parametrize("variant", [1, 2, 0])   # f16 MFMA (8-bit blocks), int8 MFMA, butterfly
 def test_cfg5_8k_chroma_equals_reference(ref, torch_dev, variant):
     torch = torch_dev
     from nano_hevc import gpu
@@ -129,7 +129,7 @@ def test_cfg5_8k_chroma_equals_reference(ref, torch_dev, variant):
         assert sha(r.cpu().numpy()) == ref[f"cfg5_{name}"]["rec"], name
 
 
-@pytest.mark.parametrize("variant", [1, 0])   # int8 MFMA, butterfly
+@pytest.mark.parametrize("variant", [1, 2, 0])   # f16 MFMA (8-bit blocks), int8 MFMA, butterfly
 def test_cfg5_8k_luma_equals_reference(ref, torch_dev, variant):
     torch = torch_dev
     from nano_hevc import gpu

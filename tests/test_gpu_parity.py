@@ -504,7 +504,7 @@ def test_probe_mfma_i8_lane_maps(nh, torch_dev):
     assert np.array_equal(dd.cpu().numpy(), a.astype(np.int32) @ b.astype(np.int32))
 
 
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2])
 def test_tc32_golden(nh, torch_dev, golden, variant):
     """Config 5 vs the reference-composed golden plane, incl. the reference's Y-PSNR."""
     torch = torch_dev
@@ -520,7 +520,8 @@ def test_tc32_golden(nh, torch_dev, golden, variant):
 
 @pytest.mark.parametrize("kind", ["natural", "noise", "int16"])
 def test_tc32_mfma_equals_butterfly_and_oracle(nh, torch_dev, kind):
-    """int16-extreme planes force the 3-part int8 split in every MFMA stage."""
+    """int16-extreme planes force the 3-part int8 split in every MFMA stage (and
+    variant 1's wide fix-up); 8-bit planes take variant 1's f16 chain."""
     torch = torch_dev
     from nano_hevc import gpu
     rng = np.random.default_rng(len(kind))
@@ -535,13 +536,13 @@ def test_tc32_mfma_equals_butterfly_and_oracle(nh, torch_dev, kind):
     d = torch.from_numpy(src).cuda()
     for qp in (0, 30, 51):
         el, er = O.tc32_plane(src, qp)
-        for v in (0, 1):
+        for v in (0, 1, 2):
             l, r = gpu.tc32_plane(d, qp, v)
             assert np.array_equal(l.cpu().numpy(), el), (kind, qp, v)
             assert np.array_equal(r.cpu().numpy(), er), (kind, qp, v)
 
 
-@pytest.mark.parametrize("variant", [1, 0])
+@pytest.mark.parametrize("variant", [1, 2, 0])
 def test_tc32_planes_stream_equals_per_plane_and_oracle(nh, torch_dev, variant):
     """Config 5 batched over a ragged YUV420 frame stream (one MFMA launch per
     plane set) == the per-plane entry point == the oracle, every plane."""
@@ -553,6 +554,7 @@ def test_tc32_planes_stream_equals_per_plane_and_oracle(nh, torch_dev, variant):
     fe = gpu.yuv420_frame_elems(w, h)
     buf = rng.integers(0, 256, size=nf * fe).astype(np.int16)
     buf[fe:2 * fe] = rng.integers(-32768, 32768, size=fe)   # frame 1: int16 extremes (3-part split)
+    buf[2 * fe + 5 * w + 40] = 300                          # frame 2: one wide block among 8-bit ones
     d = torch.from_numpy(buf).cuda()
     lvl = torch.full(d.shape, -7, dtype=torch.int32, device="cuda")   # untouched outside full blocks
     rec = torch.full(d.shape, -7, dtype=torch.int16, device="cuda")

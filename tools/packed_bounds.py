@@ -87,6 +87,21 @@ def main():
         print("%-6s %8d %6d %8d %6d %6d %6d %6d %12d" % r)
     print("largest int16 operand %d (limit 32767), largest int32 sum %d (limit 2^31-1)" % (worst16, worst32))
     assert worst16 <= 32767 and worst32 < 2 ** 31
+    # f16 matrix-core 32x32 chain: operands integers of <= 11 bits,
+    # every |partial sum| < 2^24 units of 2^-10 (pass 1 carries the +1536 offset)
+    T = mat(32, False)
+    rs, rl1, cl1 = T.sum(1), int(np.abs(T).sum(1).max()), int(np.abs(T).sum(0).max())
+    x0 = 255
+    p1 = max(abs(1536 * int(rs[k])) + sum(abs(int(t)) * (1536 + x0) for t in T[k]) for k in range(32))
+    f1 = shift_bound(x0 * rl1, 10)
+    c = shift_bound(f1 * rl1, 10)
+    dq = max(dequant(quant(c, qp, 5, intra), qp) for qp in range(52) for intra in (True, False))
+    i1 = shift_bound(dq * cl1, 10)
+    sums = {"pass1": p1, "pass2": f1 * rl1, "inv1": dq * cl1, "inv2": i1 * cl1}
+    ops = {"residual+1536": 1536 + x0, "pass1 out": f1, "dequant": dq, "inv1 out": i1}
+    print("f16 32x32 chain: operands", ops, "(exact in f16 below 2048), |sums|", sums, "(limit 2^24)")
+    assert max(ops.values()) < 2048 and max(sums.values()) < 2 ** 24
+    assert all(int(r) == 0 for r in rs[1:]) and int(rs[0]) == 2048
 
 
 if __name__ == "__main__":
