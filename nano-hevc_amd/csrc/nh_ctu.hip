@@ -83,7 +83,7 @@ struct CtuArgs {
     QuantParams q[4];                // log2 N = 2..5
     int32_t dqs, dq_per;
     int32_t wide_only;               // A/B build only (NH_CTU_NARROW=0): every workgroup on the 32-bit chain
-    int32_t probe;                   // A/B build only (NH_CTU_PROBE): 1 = no batches, 2 = no global loads (wrong outputs)
+    int32_t probe;                   // A/B build only (NH_CTU_PROBE, bits): 1 = no batches, 2 = no global loads (wrong outputs)
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
@@ -477,6 +477,15 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef float f16x_t __attribute__((ext_vector_type(16)));
 
+// The bases live in LDS (one copy per workgroup, copy_basis_h): as global loads
+// every operand load after a store would wait for the wave's outstanding stores
+// (vmcnt counts both on gfx9), draining each chain's level stores.
+__device__ __forceinline__ void copy_basis_h(BasisH& dst) {
+    const uint4* s4 = (const uint4*)&c_basis_h;
+    uint4* d4 = (uint4*)&dst;
+    constexpr int n = (int)(sizeof(BasisH) / 16);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d4[i] = s4[i];
+}
 __device__ __forceinline__ h8_t ld_h8(const uint16_t* p) { return __builtin_bit_cast(h8_t, *(const uint4*)p); }
 __device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
@@ -496,7 +505,8 @@ __device__ __forceinline__ f16x_t splat16(float v) {
     return r;
 }
 
-__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, int gx0, int gy0,
+__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, const BasisH& bs,
+                                              int gx0, int gy0,
                                               int32_t* __restrict__ lvl, int16_t* __restrict__ rec) {
     constexpr int IP = Strip<32>::IP, QH = Strip<32>::QH;   // img[r * IP + c]: sample (r - 1, c), c = -1: left
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
@@ -546,13 +556,13 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     // every other DCT32 row sums to 0)
     f16x_t acc = splat16(r == 0 ? 0.5f - 3072.0f : 0.5f);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
-                                                 ld_h8(&c_basis_h.b1[r][8 * hh]), acc, 0, 0, 0);
+                                                 ld_h8(&bs.b1[r][8 * hh]), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
-                                                 ld_h8(&c_basis_h.b1[r][16 + 8 * hh]), acc, 0, 0, 0);
+                                                 ld_h8(&bs.b1[r][16 + 8 * hh]), acc, 0, 0, 0);
     // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
     f16x_t acc2 = splat16(0.5f);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a2[r][hh][0][0]), acc_h8(acc, 0), acc2, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a2[r][hh][1][0]), acc_h8(acc, 1), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a2[r][hh][0][0]), acc_h8(acc, 0), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a2[r][hh][1][0]), acc_h8(acc, 1), acc2, 0, 0, 0);
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
     int32_t* lrow = lvl + (int64_t)(gy0 + r) * a.pitch + gx0;
 #pragma unroll
@@ -569,14 +579,14 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     wave_sync();
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
     f16x_t acc3 = splat16(0.5f);
-    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&c_basis_h.b3[r][8 * hh]), acc3,
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.b3[r][8 * hh]), acc3,
                                                   0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 16 + 8 * hh),
-                                                  ld_h8(&c_basis_h.b3[r][16 + 8 * hh]), acc3, 0, 0, 0);
+                                                  ld_h8(&bs.b3[r][16 + 8 * hh]), acc3, 0, 0, 0);
     // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
     f16x_t acc4 = splat16(0.5f);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a4[r][hh][0][0]), acc_h8(acc3, 0), acc4, 0, 0, 0);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&c_basis_h.a4[r][hh][1][0]), acc_h8(acc3, 1), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a4[r][hh][0][0]), acc_h8(acc3, 0), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a4[r][hh][1][0]), acc_h8(acc3, 1), acc4, 0, 0, 0);
     // reconstruct + clip (intra.py:70-78), row y = r
     int16_t* rrow = rec + (int64_t)(gy0 + r) * a.pitch + gx0;
 #pragma unroll
@@ -597,13 +607,15 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 
 // Shared memory of one workgroup = 4 strips.  Narrow kernels keep the
 // coefficient tile in int16 (half the LDS: more workgroups per CU).
-template <int CTB, bool NARROW> struct CtuSmem {
+template <int CTB, bool NARROW, bool BASIS = false> struct CtuSmem {
     using G = Strip<CTB>;
+    struct Empty {};
     static constexpr int TILE32 = NARROW ? (4 * G::T16 + 1) / 2 : 4 * G::CF;
     __attribute__((aligned(16))) int16_t img[4 * G::IMG];
     __attribute__((aligned(16))) int32_t tile[TILE32];
     uint16_t list[4][256];
     int cnt[4][4], org[8], next, wide[4];
+    std::conditional_t<BASIS, BasisH, Empty> basis;   // ctu_chain32_h's f16 bases
 };
 
 // One group of 4 strips (one per wave for loading and classification); the
@@ -614,6 +626,69 @@ template <int CTB, bool NARROW> struct CtuSmem {
 // column left) outside [0, 255] is not coded here: its strips are marked in
 // the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
 // !NARROW: the 32-bit chain, any int16 input.
+// The seeded quadtree of a strip's CTUs, node-parallel: lane i evaluates node i
+// (CTU i / NPC, node i % NPC: level d, Morton index within the level) -- ONE
+// split hash per lane instead of up to log2(CTB / 4) per unit along its path --
+// and the split bits come back as a wave mask.  A node reaching past the plane
+// splits without a hash, as in tu_leaf (nh_tree.hpp).
+template <int CTB> struct QuadNodes {
+    static constexpr int L = CTB == 32 ? 3 : CTB == 16 ? 2 : CTB == 8 ? 1 : 0;   // split levels
+    static constexpr int NPC = ((1 << (2 * L)) - 1) / 3;                         // nodes per CTU
+    static constexpr int CPS = 1024 / (CTB * CTB);                                // CTUs per strip
+    static_assert(NPC * CPS <= 64, "one node per lane");
+};
+__device__ __forceinline__ int level_base(int d) { return ((1 << (2 * d)) - 1) / 3; }
+
+template <int CTB>
+__device__ __forceinline__ uint64_t strip_splits(uint32_t seed, int pid, int sx0, int sy0, int w, int h) {
+    using Q = QuadNodes<CTB>;
+    if constexpr (Q::L == 0) {
+        return 0;
+    } else {
+        const int i = opaque_lane();
+        bool sp = false;
+        if (i < Q::NPC * Q::CPS) {
+            const int c = i / Q::NPC, k = i - c * Q::NPC;
+            const int d = k >= level_base(2) ? 2 : k >= level_base(1) ? 1 : 0;
+            const int m = k - level_base(d);
+            int nx = sx0 + c * CTB, ny = sy0;
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {   // Morton digits, most significant first
+                if (j < d) {
+                    const int dig = (m >> (2 * (d - 1 - j))) & 3;
+                    nx += (dig & 1) * (CTB >> (j + 1));
+                    ny += (dig >> 1) * (CTB >> (j + 1));
+                }
+            }
+            const int ns = CTB >> d;
+            sp = nx + ns > w || ny + ns > h || tu_split(seed, pid, nx, ny, ns);
+        }
+        return __ballot(sp);
+    }
+}
+
+// Leaf of unit (ux, uy) of the strip from the split mask: returns log2 of its
+// size and its origin (cx, cy).  Same leaf as tu_leaf.
+template <int CTB>
+__device__ __forceinline__ int unit_leaf(uint64_t split, int ux, int uy, int sx0, int sy0, int& cx, int& cy) {
+    using Q = QuadNodes<CTB>;
+    constexpr int UPC = CTB / 4;   // units per CTU side
+    const int c = ux / UPC, lx = ux - c * UPC, ly = uy;
+    cx = sx0 + c * CTB;
+    cy = sy0;
+    int m = 0, s = CTB;
+#pragma unroll
+    for (int d = 0; d < Q::L; ++d) {
+        if (!((split >> (c * Q::NPC + level_base(d) + m)) & 1)) break;
+        s >>= 1;
+        const int qx = (lx * 4) & s ? 1 : 0, qy = (ly * 4) & s ? 1 : 0;   // quadrant at this level
+        cx += qx * s;
+        cy += qy * s;
+        m = 4 * m + 2 * qy + qx;
+    }
+    return s == 4 ? 2 : s == 8 ? 3 : s == 16 ? 4 : 5;
+}
+
 // A strip's source samples in flight: issued by strip_issue, written to the
 // LDS image by strip_store (the split lets the persistent kernel keep the next
 // group's loads in flight under the current group's chains).
@@ -640,7 +715,7 @@ template <int CTB>
 __device__ __forceinline__ void strip_issue(const CtuArgs& a, int grp, int pz, StripLoad<CTB>& ld, int wv = -1) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
-    const int lane = threadIdx.x & 63;
+    const int lane = opaque_lane();
     if (wv < 0) wv = threadIdx.x >> 6;
     int sx0, sy0;
     const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
@@ -650,7 +725,7 @@ __device__ __forceinline__ void strip_issue(const CtuArgs& a, int grp, int pz, S
     for (int i = 0; i < ld.NV; ++i) {
         const int g = 64 * i + lane, ry = g / UW, gx = g % UW, x = sx0 + 4 * gx, y = sy0 + ry;
         ld.v[i] = make_uint2(0u, 0u);   // outside the plane: no TU reads it
-        if (valid && g < CTB * UW && x < w && y < h && (!NH_AB || a.probe != 2))
+        if (valid && g < CTB * UW && x < w && y < h && (!NH_AB || (a.probe & 2) == 0))
             ld.v[i] = *(const uint2*)(src + (int64_t)y * pitch + x);
     }
     ld.top = make_uint2(0x00800080u, 0x00800080u);   // 128 above the frame (block.py:41)
@@ -670,7 +745,7 @@ template <int CTB>
 __device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* img, bool valid) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW, IP = G::IP;
-    const int lane = threadIdx.x & 63;
+    const int lane = opaque_lane();
     uint32_t hi_bits = 0;
 #pragma unroll
     for (int i = 0; i < ld.NV; ++i) {
@@ -707,11 +782,11 @@ __device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* i
 // !NARROW: the 32-bit chain, any int16 input.
 // Returns with the workgroup's waves in the batch loop's exit (no barrier).
 template <int CTB, bool LUMA, bool NARROW, bool MFMA32, class Prefetch>
-__device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, CtuSmem<CTB, NARROW>& sm,
+__device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, CtuSmem<CTB, NARROW, NARROW && MFMA32>& sm,
                                           StripLoad<CTB>& ld, Prefetch&& prefetch) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6, lane = opaque_lane();
     int sx0, sy0;
     const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
     const int64_t poff = plane_off(a, pz);
@@ -721,20 +796,16 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
     const int w = a.w, h = a.h;
     int16_t* img = sm.img + wv * G::IMG;
 
-    // ---- 1. classify the strip's 64 units (loads in flight): leaf size / origin (<= 3 hashes), TU map ----
+    // ---- 1. classify the strip's 64 units (loads in flight): leaf size / origin, TU map ----
     bool org = false;
     int ls = 0;
     const int64_t tu_org = (int64_t)pz * a.tu_plane + (int64_t)(sy0 >> 2) * (w >> 2) + (sx0 >> 2);
     if (valid) {
+        const uint64_t split = strip_splits<CTB>(a.seed, pid, sx0, sy0, w, h);
         const int ux = lane % UW, uy = lane / UW, x = sx0 + 4 * ux, y = sy0 + 4 * uy;
         const bool in = x < w && y < h;
-        int s = CTB, cx = sx0 + (4 * ux / CTB) * CTB, cy = sy0;
-        while (s > 4 && (cx + s > w || cy + s > h || tu_split(a.seed, pid, cx, cy, s))) {
-            s >>= 1;
-            cx += x >= cx + s ? s : 0;
-            cy += y >= cy + s ? s : 0;
-        }
-        ls = s == 4 ? 2 : s == 8 ? 3 : s == 16 ? 4 : 5;
+        int cx, cy;
+        ls = unit_leaf<CTB>(split, ux, uy, sx0, sy0, cx, cy);
         if (in) a.tu[(int64_t)pz * a.tu_plane + (int64_t)(y >> 2) * (w >> 2) + (x >> 2)] = (uint8_t)ls;
         org = in && cx == x && cy == y;
     }
@@ -781,7 +852,7 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
     __syncthreads();
 
     // ---- 3. batches, claimed in descending cost: 32x32 chains, then 16, 8, 4 ----
-    if (NH_AB && a.probe == 1) return;
+    if (NH_AB && (a.probe & 1)) return;
     const int n32 = CTB == 32 ? (MFMA32 ? cnt[3] : (cnt[3] + 1) / 2) : 0;
     const int n16 = CTB >= 16 ? (cnt[2] + 3) / 4 : 0, n8 = CTB >= 8 ? (cnt[1] + 7) / 8 : 0, n4 = (cnt[0] + 15) / 16;
     const int total = n32 + n16 + n8 + n4;
@@ -799,7 +870,7 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
             if (item < n32) {
                 if constexpr (NARROW && MFMA32) {   // one TU per wave on the f16 matrix cores
                     const int e = sm.list[3][item], sw = e >> 6;
-                    ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.org[2 * sw],
+                    ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.basis, sm.org[2 * sw],
                                   sm.org[2 * sw + 1], lvl, rec);
                 } else if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores (A/B form)
                     const int e = sm.list[3][item], sw = e >> 6;
@@ -835,25 +906,41 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
 // (MFMA32: on the f16 matrix cores, A/B form).  PERSIST: a grid of
 // resident workgroups walking the (group, plane) items with stride gridDim.x,
 // each group's loads issued during the previous group's chains.
-template <int CTB, bool LUMA, bool MFMA32 = false, bool PERSIST = false>
-__global__ void __launch_bounds__(256) k_ctu_open(CtuArgs a, int items) {
-    __shared__ CtuSmem<CTB, true> sm;
-    const int groups = items / (int)gridDim.y;
-    if constexpr (!PERSIST) {
+template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_ctu_open(CtuArgs a, int items) {
+    __shared__ CtuSmem<CTB, true, MFMA32> sm;
+    if constexpr (PERSIST == 0) {
+        // the bases' loads issued with the strip's and written to LDS after the
+        // strip image (one wait for both; ctu_group's barrier orders them before use)
+        static_assert(sizeof(BasisH) == 256 * 32, "two 16-byte pieces per thread");
+        uint4 bq[2];
+        if constexpr (MFMA32) {
+            const uint4* s4 = (const uint4*)&c_basis_h;
+            bq[0] = s4[threadIdx.x];
+            bq[1] = s4[threadIdx.x + 256];
+        }
         StripLoad<CTB> ld;
         strip_issue<CTB>(a, blockIdx.x, blockIdx.y, ld);
-        ctu_group<CTB, LUMA, true, MFMA32>(a, blockIdx.x, blockIdx.y, sm, ld, [] {});
+        ctu_group<CTB, LUMA, true, MFMA32>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
+            if constexpr (MFMA32) {
+                uint4* d4 = (uint4*)&sm.basis;
+                d4[threadIdx.x] = bq[0];
+                d4[threadIdx.x + 256] = bq[1];
+            }
+        });
     } else {
-        (void)groups;
+        if constexpr (MFMA32) copy_basis_h(sm.basis);   // ordered before use by ctu_group's barrier
+        // PERSIST = 1: the next group's loads in flight under this group's chains;
+        // PERSIST = 2: no prefetch (only the per-workgroup start-up amortised)
         StripLoad<CTB> ld;
         int it = blockIdx.x;
-        const int ngroups = a.strips_x * a.nrows;
-        const int gcount = (ngroups + 3) / 4;
-        if (it < items) strip_issue<CTB>(a, it % gcount, it / gcount, ld);
+        const int gcount = (a.strips_x * a.nrows + 3) / 4;
+        if (PERSIST == 1 && it < items) strip_issue<CTB>(a, it % gcount, it / gcount, ld);
         for (; it < items; it += gridDim.x) {
             const int nx = it + gridDim.x;
+            if constexpr (PERSIST == 2) strip_issue<CTB>(a, it % gcount, it / gcount, ld);
             ctu_group<CTB, LUMA, true, MFMA32>(a, it % gcount, it / gcount, sm, ld, [&] {
-                if (nx < items) strip_issue<CTB>(a, nx % gcount, nx / gcount, ld);
+                if (PERSIST == 1 && nx < items) strip_issue<CTB>(a, nx % gcount, nx / gcount, ld);
             });
             __syncthreads();   // every wave done with this group's LDS
         }
@@ -911,8 +998,11 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
     using G = Strip<32>;
     __shared__ __attribute__((aligned(16))) int16_t s_img[4][G::IMG];
     __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * G::QH];
+    __shared__ BasisH s_basis;
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int b0 = (blockIdx.x * 4 + wv) * K;
+    copy_basis_h(s_basis);
+    __syncthreads();
     if (b0 >= nblk) return;   // whole wave
     const int pz = blockIdx.y;
     const int64_t poff = plane_off(a, pz);
@@ -930,7 +1020,7 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
         if (wide) {
             if (lane == 0) a.rec[poff + (int64_t)sy0 * a.pitch + sx0] = kWideMark;
         } else {
-            ctu_chain32_h(a, s_img[wv] + 4, s_q[wv], sx0, sy0, a.lvl + poff, a.rec + poff);
+            ctu_chain32_h(a, s_img[wv] + 4, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff);
         }
         wave_sync();   // this wave's LDS reads of block k before block k+1's image writes
     }
@@ -998,8 +1088,8 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // us per 16 luma planes for the packed butterflies); the
     // groups it marks (any sample outside [0, 255]) by k_ctu_wide with the
     // 32-bit chain.  A/B build: NH_CTU_T32 = 0 (narrow 32x32 TUs on packed
-    // butterflies) / 1 (wide 32x32 TUs on int8 MFMA), NH_CTU_PERSIST = 1
-    // (resident grid, loads one group ahead), NH_CTU_NARROW = 0 (every group on
+    // butterflies) / 1 (wide 32x32 TUs on int8 MFMA), NH_CTU_PERSIST = 1 / 2
+    // (resident grid, loads one group ahead / without prefetch), NH_CTU_NARROW = 0 (every group on
     // the 32-bit path), NH_CTU_PROBE = 1 / 2 (no batches / no global loads).
     static const int t32 = NH_KNOB("NH_CTU_T32", 2);
     static const int persist = NH_KNOB("NH_CTU_PERSIST", 0);
@@ -1030,12 +1120,16 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         int rc3;
         if constexpr (NH_AB != 0) {
             const bool m = M32 && t32 != 0;
-            if (m) rc3 = persist ? launch_open(k_ctu_open<C, L, M32, true>) : launch_open(k_ctu_open<C, L, M32, false>);
-            else rc3 = persist ? launch_open(k_ctu_open<C, L, false, true>) : launch_open(k_ctu_open<C, L, false, false>);
+            if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>)
+                         : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>)
+                                        : launch_open(k_ctu_open<C, L, M32, 0>);
+            else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>)
+                       : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>)
+                                      : launch_open(k_ctu_open<C, L, false, 0>);
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else {
-            rc3 = launch_open(k_ctu_open<C, L, M32, false>);
+            rc3 = launch_open(k_ctu_open<C, L, M32, 0>);
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         }
         return rc3;

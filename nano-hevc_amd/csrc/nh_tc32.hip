@@ -129,6 +129,11 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
     // ---- forward pass 2: coeff^T = T . temp^T  (B from the accumulator, k permuted) ----
     const v4i_t F2 = load_perm16(&c_basis.t[r][0], hh);         // A[j][k] = T[j][k]
     acc = mfma_auto<false>(V, F2);
+    // the inverse bases before the level stores: a load issued after a store
+    // waits for it (vmcnt counts both on gfx9)
+    const v4i_t F3 = load_row16(&c_basis.tt[r][0], 16 * hh);    // B[k][i] = T[k][i]
+    const v4i_t F4 = load_perm16(&c_basis.tt[r][0], hh);        // A[j][k] = T[k][j]
+    asm volatile("" ::: "memory");
     // ---- quant / dequant, levels out (lane = row i, registers = columns crow(g)) ----
     int32_t* lrow = lvl + (int64_t)(y0 + r) * pitch + x0;
 #pragma unroll
@@ -146,12 +151,10 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
     // ---- inverse pass 1: temp2^T = dq^T . T   (A = dq^T via the LDS transpose) ----
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) X[jj] = s_dq[wv][16 * hh + jj][r];
-    const v4i_t F3 = load_row16(&c_basis.tt[r][0], 16 * hh);    // B[k][i] = T[k][i]
     acc = mfma_auto<true>(X, F3);
 #pragma unroll
     for (int g = 0; g < 16; ++g) V[g] = rshift_round<10>((uint32_t)acc[g]);   // transform.py:227
     // ---- inverse pass 2: res^T = T^T . temp2^T ----
-    const v4i_t F4 = load_perm16(&c_basis.tt[r][0], hh);        // A[j][k] = T[k][j]
     acc = mfma_auto<false>(V, F4);
     // ---- reconstruct + clip (intra.py:70-78), recon out ----
     int16_t* rrow = recon + (int64_t)(y0 + r) * pitch + x0;
