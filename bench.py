@@ -499,7 +499,11 @@ def run_cfg4(args, dist, world, rank, dev):
                    "frames_per_gpu": args.frames, "frames_per_s": value / (W * H + 2 * cw * ch),
                    "samples_per_step_rank0": my_samples, "parallelism": f"ctu-band{world} (rotated)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "bytes_per_sample": BYTES_PER_SAMPLE_CFG4,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(f"cfg4_4k_yuv420_f{args.frames}_n{world}"),
+                     "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower "
+                                     "bound for 8-B/lane row reads, <= 2x that if every request were 128 B), writes "
+                                     "exact; profiles/pmc_traffic.json",
+                     "bytes_per_sample": BYTES_PER_SAMPLE_CFG4,
                      "kernel_ms_avg": kern_ms},
         "cpu_baseline": None,
     }
