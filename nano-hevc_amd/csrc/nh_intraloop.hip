@@ -8,11 +8,13 @@
 // (the test-side CPU restatement, oh_intra_rdo_plane / oh_tu_pipeline_plane) and the golden
 // planes generated from the reference functions pin them.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 #include "nh_tree.hpp"
+#include "nh_packed.hpp"
 
 namespace nh {
 
@@ -1666,12 +1668,140 @@ __device__ __forceinline__ void tu_closed_batch(const Closed4Args& a, const int1
     __syncthreads();
 }
 
-template <int WAVES>
+// tu_closed_batch for a stream whose every source sample is 8-bit (the
+// reconstruction is clipped to [0, 255], so neighbours are too): the packed
+// 16-bit chain of DESIGN.md §4.4c (nh_packed.hpp; bounds: tools/packed_bounds.py)
+// with an int16 view of the tile (rows of TP = 34: pair reads conflict-free).
+// Same results as tu_closed_batch on such input.
+__device__ __forceinline__ int opaque_lane64() {
+    int l = threadIdx.x & 63;
+    asm volatile("" : "+v"(l));
+    return l;
+}
+template <int N, bool DST>
+__device__ __forceinline__ void tu_closed_batch_pk(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
+                                                   uint8_t* tu, int x0c, int y0c, int cnt, const int* slx,
+                                                   const int* sly, int16_t (*rc)[33], int16_t* t16, const ChainQ& cq) {
+    constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
+    constexpr int32_t BIAS = 1 << (S - 1);
+    const int lane = opaque_lane64(), j = lane / N, t = lane % N;
+    const bool on = j < cnt;
+    const int lx = on ? slx[j] : slx[0], ly = on ? sly[j] : sly[0], x = x0c + lx, y = y0c + ly;
+    int16_t* tl = t16 + ly * TP + lx;   // tl[line * TP + slot]
+    const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
+    const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
+    int32_t sum = topt + leftt;                                // DC (intra.py:46-62)
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    const int32_t dc = (sum + N) >> (L2 + 1);
+    const pk16 dc2 = pk_splat(dc);
+    pk16 o2[H];
+    pku16 pl2[H];
+    {
+        const int32_t b = (t + 1) * tr + (N - 1) * topt + bl + N, st = bl - topt;
+        pku16 bs = {(unsigned short)b, (unsigned short)(b + st)};
+        const pku16 st2 = {(unsigned short)(2 * st), (unsigned short)(2 * st)};
+        const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
+        const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
+        const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
+            const pku16 lf = {(unsigned short)rc[ly + 1 + 2 * m][lx], (unsigned short)rc[ly + 2 + 2 * m][lx]};
+            pl2[m] = (lf * wl + bs) >> sh;
+            bs += st2;
+        }
+    }
+    int32_t ed = 0, ep = 0;
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+        const pk16 d0 = o2[m] - dc2, d1 = o2[m] - __builtin_bit_cast(pk16, pl2[m]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+    }
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) {
+        ed += __shfl_xor(ed, m, 64);
+        ep += __shfl_xor(ep, m, 64);
+    }
+    const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
+    pk16 r2[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) r2[m] = o2[m] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[m]));
+    int32_t yv[N];
+    fwd1d_pk<N, DST>(r2, yv, BIAS);   // forward pass 1 (transform.py:179-185): column t -> line i, slot t
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(yv[i] >> S);
+    }
+    __syncthreads();
+    const int st = inv_slot<N, DST>(t);
+    {
+        pk16 P[H];   // forward pass 2 (transform.py:188-194): row t
+#pragma unroll
+        for (int m = 0; m < H; ++m) P[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        fwd1d_pk<N, DST>(P, yv, BIAS);
+    }
+    __syncthreads();
+    if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
+        int32_t* lrow = lvl + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const int32_t l = quant_s(yv[k] >> S, cq.qs, cq.h_v, cq.hneg_v);
+            lrow[k] = l;
+            tl[k * TP + st] = (int16_t)dequant_s(l, cq);
+        }
+    }
+    __syncthreads();
+    int32_t xv[N];
+    {
+        pk16 Y[H];   // inverse pass 1 (transform.py:221-227): column t -> line i, slot inv_slot(t)
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        inv1d_pk<N, DST>(Y, xv, BIAS);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(xv[i] >> S);
+    }
+    __syncthreads();
+    {
+        pk16 Y[H];   // inverse pass 2 (transform.py:230-236): row t
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        inv1d_pk<N, DST>(Y, xv, BIAS);
+    }
+    if (on) {   // reconstruct + clip (intra.py:70-78); planar in row layout
+        const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, stv = tr - leftt;
+        int16_t* rrow = rec + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int k = 0; k < N; ++k) {
+            const int32_t p = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + k] + b + k * stv) >> (L2 + 1);
+            int32_t q = p + (xv[k] >> S);
+            q = q < 0 ? 0 : (q > 255 ? 255 : q);
+            rrow[k] = (int16_t)q;
+            // the TU's own samples: no TU of this batch reads them
+            rc[ly + 1 + t][lx + 1 + k] = (int16_t)q;
+        }
+        if (t < N / 4) {
+            const int w4 = a.w / 4;
+            for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
+        }
+    }
+    __syncthreads();
+}
+
+// NARROW: the packed chain; the launch pairs it with the 32-bit form and the
+// stream's wide flag (work[2], set by k_closed_any_wide) makes exactly one of
+// the two code the stream -- the other returns before taking a ticket.
+template <int WAVES, bool NARROW = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed(Closed4Args a) {
     __shared__ int16_t rc[33][33];
     __shared__ int32_t tile[32][33];
     __shared__ int owner_of[64], done_of[64], slx[16], sly[16];
     __shared__ int row_s, stall_s;
+    if ((__builtin_nontemporal_load(&a.work[2]) != 0) == NARROW) return;   // the other form codes this stream
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
     ChainQ cq[4];
@@ -1775,9 +1905,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                         sly[k] = oy * 4;                                                                     \
                     }                                                                                        \
                     __syncthreads();                                                                         \
-                    for (int c0 = 0; c0 < cnt; c0 += 64 / NN)                                                \
-                        tu_closed_batch<NN, DST>(a, src, lvl, rec, tu, x0c, y0c, min(cnt - c0, 64 / NN),     \
-                                                 slx + c0, sly + c0, rc, tile, Q);                           \
+                    for (int c0 = 0; c0 < cnt; c0 += 64 / NN) {                                             \
+                        if constexpr (NARROW)                                                                \
+                            tu_closed_batch_pk<NN, DST>(a, src, lvl, rec, tu, x0c, y0c, min(cnt - c0, 64 / NN), \
+                                                        slx + c0, sly + c0, rc, (int16_t*)&tile[0][0], Q);   \
+                        else                                                                                 \
+                            tu_closed_batch<NN, DST>(a, src, lvl, rec, tu, x0c, y0c, min(cnt - c0, 64 / NN), \
+                                                     slx + c0, sly + c0, rc, tile, Q);                       \
+                    }                                                                                        \
                 }
                 NH_BATCH(32, false, cq[3]);
                 NH_BATCH(16, false, cq[2]);
@@ -1967,6 +2102,22 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
     return NH_OK;
 }
 
+// Sets work[2] when any source sample of the plane set is outside [0, 255]
+// (the closed-loop stream then takes the 32-bit chain).
+__global__ void __launch_bounds__(256) k_closed_any_wide(const int16_t* __restrict__ src, int64_t group_stride,
+                                                         int64_t plane_stride, int ppg, int w, int h, int pitch,
+                                                         int32_t* work) {
+    const int pz = blockIdx.y, gz = pz / ppg, cz = pz - gz * ppg;
+    const int16_t* p = src + (int64_t)gz * group_stride + (int64_t)cz * plane_stride;
+    const int64_t n = (int64_t)w * h;
+    uint32_t bits = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const int yy = (int)(i / w), xx = (int)(i - (int64_t)yy * w);
+        bits |= (uint16_t)p[(int64_t)yy * pitch + xx];
+    }
+    if (__ballot((bits & 0xff00u) != 0) && (threadIdx.x & 63) == 0) atomicOr(&work[2], 1);
+}
+
 static int closed4_layout(const nh_plane_set* set, int ctb, int64_t& lines0, int64_t& lw, int64_t& nplanes) {
     if (!set || (ctb != 4 && ctb != 8 && ctb != 16 && ctb != 32)) return NH_EARG;
     if (set->width < 4 || set->height < 0 || set->pitch < set->width || set->planes_per_group < 1 ||
@@ -1974,7 +2125,7 @@ static int closed4_layout(const nh_plane_set* set, int ctb, int64_t& lines0, int
         return NH_EARG;
     nplanes = (int64_t)set->planes_per_group * set->num_groups;
     if (nplanes > 65535) return NH_EARG;
-    lines0 = 2;   // ticket, status; then 64-bit words (8-B aligned)
+    lines0 = 4;   // ticket, status, wide flag, pad; then 64-bit words (8-B aligned)
     lw = (set->width + 1) / 2;
     return NH_OK;
 }
@@ -2034,6 +2185,30 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x waves/SIMD)
     const int64_t cap = cw == 3 ? 3072 : 2048;
     const unsigned waves = (unsigned)(rows < cap ? rows : cap);
+    // the stream's wide flag, then the packed-chain form (codes the stream iff no
+    // sample is outside [0, 255]) and the 32-bit form (iff one is); A/B knob
+    // NH_TU_CLOSED_NARROW = 0: the 32-bit form for every stream
+    static const int narrow_ok = NH_KNOB("NH_TU_CLOSED_NARROW", 1);
+    if (narrow_ok) {
+        const int64_t n = (int64_t)set->width * set->height;
+        const unsigned gx = (unsigned)std::min<int64_t>(256, (n + 255 * 8) / (256 * 8));
+        k_closed_any_wide<<<dim3(gx, (unsigned)np), 256, 0, s>>>(d_src + set->base, set->group_stride, set->plane_stride,
+                                                              set->planes_per_group, set->width, set->height,
+                                                              set->pitch, (int32_t*)d_work);
+    } else {
+        NH_HIP(hipMemsetAsync((int32_t*)d_work + 2, 0xff, 4, s));
+    }
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        NH_HIP(hipGetDevice(&dev));
+        NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    int per_cu = 0;
+    NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tu_closed<1, true>, 64, 0));
+    const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
+    const unsigned waves_n = (unsigned)(rows < cap_n ? rows : cap_n);
+    if (narrow_ok) k_tu_closed<1, true><<<waves_n, 64, 0, s>>>(a);
 #if NH_AB
     if (cw == 3) k_tu_closed<3><<<waves, 64, 0, s>>>(a);
     else
