@@ -57,3 +57,19 @@ def test_cfg4_band_views_tile_the_stream(world):
         assert packed.numel() == shard.cfg4_packed_elems(r, world, frames, W, H)
         seen[packed] += 1
     assert bool((seen == 1).all())
+
+
+def test_bench_inputs_travel_to_the_gpu_box():
+    """bench.py reads profiles/pmc_traffic.json for roofline.traffic: no
+    .gpurunignore pattern may keep it (or the built library) off the GPU box."""
+    import fnmatch
+    pats = [p.strip() for p in open(os.path.join(ROOT, ".gpurunignore")) if p.strip() and not p.startswith("#")]
+    for rel in ("profiles/pmc_traffic.json", "nano-hevc_amd/nano_hevc/libnanohevc.so", "bench.py"):
+        parts = rel.split("/")
+        for p in pats:
+            if p.startswith("./"):
+                anchored = p[2:].rstrip("/")
+                assert not (rel == anchored or rel.startswith(anchored + "/")), (rel, p)
+            else:
+                assert not any(fnmatch.fnmatch(x, p) for x in parts) and not fnmatch.fnmatch(rel, p), (rel, p)
+    assert os.path.exists(os.path.join(ROOT, "profiles", "pmc_traffic.json"))
