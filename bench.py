@@ -442,7 +442,18 @@ def run_cfg4(args, dist, world, rank, dev):
                                    tu=tuc, stream=stream)
 
     elapsed, kern_ms = timed_steps(lambda: step_into(0), args.steps, args.warmup, dist, stream)
-    (elapsed, kern_ms), (samples_all,) = reduce_max_sum(dist, dev, (elapsed, kern_ms), (my_samples,))
+    # TUs per size coded per step (blocks/s per TU size), from the TU maps
+    # (one byte per 4x4 unit = log2 of its TU's size; bit 7 marks a group recoded by the wide kernel)
+    tu_units = [0, 0, 0, 0]
+    for _, _, _, _, tuy, tuc in work:
+        for m in (tuy, tuc):
+            ls = (m & 0x7F).reshape(-1).to(torch.int64)
+            cnt = torch.bincount(ls, minlength=6)
+            for k in range(4):
+                tu_units[k] += int(cnt[k + 2])
+    tu_counts = [tu_units[k] // (1 << (2 * k)) for k in range(4)]   # a TU of 4*2^k samples square = 4^k units
+    (elapsed, kern_ms), sums = reduce_max_sum(dist, dev, (elapsed, kern_ms), [my_samples] + tu_counts)
+    samples_all, tu_all = sums[0], sums[1:]
     value = samples_all * args.steps / elapsed
 
     sizes = [shard.cfg4_packed_elems(r, world, nf, W, H) for r in range(world)]
@@ -497,7 +508,9 @@ def run_cfg4(args, dist, world, rank, dev):
         "config": {"workload": "config 4: 4K YUV420, seeded 4/8/16/32 TU quadtree per 32x32 CTU (16x16 chroma), "
                                "open-loop DC/planar choice, full chain, QP %d" % args.qp,
                    "frames_per_gpu": args.frames, "frames_per_s": value / (W * H + 2 * cw * ch),
-                   "samples_per_step_rank0": my_samples, "parallelism": f"ctu-band{world} (rotated)"},
+                   "samples_per_step_rank0": my_samples, "parallelism": f"ctu-band{world} (rotated)",
+                   "tu_blocks_per_step": {f"{4 << k}x{4 << k}": int(tu_all[k]) for k in range(4)},
+                   "tu_blocks_per_s": {f"{4 << k}x{4 << k}": tu_all[k] * args.steps / elapsed for k in range(4)}},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(f"cfg4_4k_yuv420_f{args.frames}_n{world}"),
                      "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower "

@@ -42,32 +42,24 @@ namespace nh {
 __constant__ Basis c_basis_ctu;
 
 // f16 DCT32 bases of the narrow 32x32 chain (ctu_chain32_h), every entry
-// T[k][n] * 2^-10 (exact in f16), pre-arranged so that each lane's MFMA operand
-// is one 16-byte load (crow: the accumulator row order, nh_mfma.hpp).
+// T[k][n] * 2^-10 (exact in f16), as the matrix and its transpose (4 KB: one
+// copy per workgroup in LDS).  Each lane's MFMA operand is one 16-byte piece of
+// a row (the data-side passes) or two 8-byte pieces of it in the accumulator
+// row order crow (passes 2 and 4, nh_mfma.hpp).
 struct BasisH {
-    uint16_t b1[32][32];         // [k][y] = T[k][y]                       pass 1, B operand (lane k)
-    uint16_t a2[32][2][2][8];    // [l][h][s][j] = T[l][crow(8s + j, h)]   pass 2, A operand (lane l)
-    uint16_t b3[32][32];         // [y][k] = T[k][y]                       inverse pass 1, B operand (lane y)
-    uint16_t a4[32][2][2][8];    // [x][h][s][j] = T[crow(8s + j, h)][x]   inverse pass 2, A operand (lane x)
+    uint16_t t[32][32];          // [k][n] = T[k][n]   pass 1 B operand (lane k); pass 2 A operand (lane l = k)
+    uint16_t tt[32][32];         // [n][k] = T[k][n]   inverse pass 1 B operand (lane n); inverse pass 2 A operand
 };
 __constant__ BasisH c_basis_h;
 
 static BasisH make_basis_h() {
     auto h = [](int v) { return __builtin_bit_cast(uint16_t, (_Float16)((float)v / 1024.0f)); };
-    auto cr = [](int g, int hh) { return (g & 3) + 8 * (g >> 2) + 4 * hh; };
     BasisH b;
     for (int k = 0; k < 32; ++k)
         for (int n = 0; n < 32; ++n) {
-            b.b1[k][n] = h(dct32(k, n));
-            b.b3[n][k] = h(dct32(k, n));
+            b.t[k][n] = h(dct32(k, n));
+            b.tt[n][k] = h(dct32(k, n));
         }
-    for (int r = 0; r < 32; ++r)
-        for (int hh = 0; hh < 2; ++hh)
-            for (int st = 0; st < 2; ++st)
-                for (int j = 0; j < 8; ++j) {
-                    b.a2[r][hh][st][j] = h(dct32(r, cr(8 * st + j, hh)));
-                    b.a4[r][hh][st][j] = h(dct32(cr(8 * st + j, hh), r));
-                }
     return b;
 }
 
@@ -487,6 +479,11 @@ __device__ __forceinline__ void copy_basis_h(BasisH& dst) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) d4[i] = s4[i];
 }
 __device__ __forceinline__ h8_t ld_h8(const uint16_t* p) { return __builtin_bit_cast(h8_t, *(const uint4*)p); }
+// Elements crow(8s + j, hh), j = 0..7, of a basis row: [16s + 4hh, +4) and [16s + 8 + 4hh, +4).
+__device__ __forceinline__ h8_t ld_crow_h8(const uint16_t* row, int s, int hh) {
+    const uint2 p = *(const uint2*)(row + 16 * s + 4 * hh), q = *(const uint2*)(row + 16 * s + 8 + 4 * hh);
+    return __builtin_bit_cast(h8_t, make_uint4(p.x, p.y, q.x, q.y));
+}
 __device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
 }
@@ -556,13 +553,13 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     // every other DCT32 row sums to 0)
     f16x_t acc = splat16(r == 0 ? 0.5f - 3072.0f : 0.5f);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
-                                                 ld_h8(&bs.b1[r][8 * hh]), acc, 0, 0, 0);
+                                                 ld_h8(&bs.t[r][8 * hh]), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
-                                                 ld_h8(&bs.b1[r][16 + 8 * hh]), acc, 0, 0, 0);
+                                                 ld_h8(&bs.t[r][16 + 8 * hh]), acc, 0, 0, 0);
     // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
     f16x_t acc2 = splat16(0.5f);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a2[r][hh][0][0]), acc_h8(acc, 0), acc2, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a2[r][hh][1][0]), acc_h8(acc, 1), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 0, hh), acc_h8(acc, 0), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 1, hh), acc_h8(acc, 1), acc2, 0, 0, 0);
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
     int32_t* lrow = lvl + (int64_t)(gy0 + r) * a.pitch + gx0;
 #pragma unroll
@@ -579,14 +576,14 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     wave_sync();
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
     f16x_t acc3 = splat16(0.5f);
-    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.b3[r][8 * hh]), acc3,
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.tt[r][8 * hh]), acc3,
                                                   0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 16 + 8 * hh),
-                                                  ld_h8(&bs.b3[r][16 + 8 * hh]), acc3, 0, 0, 0);
+                                                  ld_h8(&bs.tt[r][16 + 8 * hh]), acc3, 0, 0, 0);
     // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
     f16x_t acc4 = splat16(0.5f);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a4[r][hh][0][0]), acc_h8(acc3, 0), acc4, 0, 0, 0);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(&bs.a4[r][hh][1][0]), acc_h8(acc3, 1), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 0, hh), acc_h8(acc3, 0), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 1, hh), acc_h8(acc3, 1), acc4, 0, 0, 0);
     // reconstruct + clip (intra.py:70-78), row y = r
     int16_t* rrow = rec + (int64_t)(gy0 + r) * a.pitch + gx0;
 #pragma unroll
@@ -906,27 +903,20 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
 // (MFMA32: on the f16 matrix cores, A/B form).  PERSIST: a grid of
 // resident workgroups walking the (group, plane) items with stride gridDim.x,
 // each group's loads issued during the previous group's chains.
-template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) k_ctu_open(CtuArgs a, int items) {
+// WAVES: the occupancy floor (waves/SIMD) the registers are allocated for.
+template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
     __shared__ CtuSmem<CTB, true, MFMA32> sm;
     if constexpr (PERSIST == 0) {
         // the bases' loads issued with the strip's and written to LDS after the
         // strip image (one wait for both; ctu_group's barrier orders them before use)
-        static_assert(sizeof(BasisH) == 256 * 32, "two 16-byte pieces per thread");
-        uint4 bq[2];
-        if constexpr (MFMA32) {
-            const uint4* s4 = (const uint4*)&c_basis_h;
-            bq[0] = s4[threadIdx.x];
-            bq[1] = s4[threadIdx.x + 256];
-        }
+        static_assert(sizeof(BasisH) == 256 * 16, "one 16-byte piece per thread");
+        uint4 bq;
+        if constexpr (MFMA32) bq = ((const uint4*)&c_basis_h)[threadIdx.x];
         StripLoad<CTB> ld;
         strip_issue<CTB>(a, blockIdx.x, blockIdx.y, ld);
         ctu_group<CTB, LUMA, true, MFMA32>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
-            if constexpr (MFMA32) {
-                uint4* d4 = (uint4*)&sm.basis;
-                d4[threadIdx.x] = bq[0];
-                d4[threadIdx.x + 256] = bq[1];
-            }
+            if constexpr (MFMA32) ((uint4*)&sm.basis)[threadIdx.x] = bq;
         });
     } else {
         if constexpr (MFMA32) copy_basis_h(sm.basis);   // ordered before use by ctu_group's barrier
@@ -1093,6 +1083,12 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // the 32-bit path), NH_CTU_PROBE = 1 / 2 (no batches / no global loads).
     static const int t32 = NH_KNOB("NH_CTU_T32", 2);
     static const int persist = NH_KNOB("NH_CTU_PERSIST", 0);
+    // The luma f16-MFMA form stays at 5 waves/SIMD (90 VGPRs).  Its LDS (27 KB per
+    // workgroup with the 4 KB bases) would fit 6 workgroups per CU, but the
+    // 80-register cap spills 5 VGPRs: 466 vs 421 us per 16 luma planes
+    // (A/B build: NH_CTU_W32 = 6; profiles/r02/session5/).
+    constexpr int kW32 = 5;
+    static const int w32 = NH_KNOB("NH_CTU_W32", kW32);
     a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
     a.probe = NH_KNOB("NH_CTU_PROBE", 0);
     auto launch_open = [&](auto kern) -> int {
@@ -1122,14 +1118,15 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
             const bool m = M32 && t32 != 0;
             if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>)
                          : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>)
-                                        : launch_open(k_ctu_open<C, L, M32, 0>);
+                         : w32 == 6     ? launch_open(k_ctu_open<C, L, M32, 0, 6>)
+                                        : launch_open(k_ctu_open<C, L, M32, 0, kW32>);
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>)
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>)
                                       : launch_open(k_ctu_open<C, L, false, 0>);
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else {
-            rc3 = launch_open(k_ctu_open<C, L, M32, 0>);
+            rc3 = launch_open(k_ctu_open<C, L, M32, 0, 5>);
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         }
         return rc3;

@@ -1948,6 +1948,302 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     }
 }
 
+// ---------------------------------------------------------------------------
+// Config 4 closed loop, 8-bit streams: PLANE PAIRS.  The seeded quadtree of a
+// plane depends on its plane id, not on its frame, so the same CTU of two
+// frames has the same TUs and the same dataflow rounds.  A wave codes one CTU
+// row of two such planes (groups 2p and 2p + 1 of the set, same plane in the
+// group) in lock-step: each round's batch carries the ready TUs of both planes
+// (entry e < cnt: plane 0's TU e, else plane 1's TU e - cnt), so a round whose
+// TUs filled a quarter of the lanes for one plane fills half of them for two.
+// Every TU runs the same packed chain as tu_closed_batch_pk on its own plane's
+// LDS reconstruction and tile: same results.  The planes of a pair never
+// exchange data; each publishes and polls its own line words.
+struct PairPlanes {
+    const int16_t* src[2];
+    int32_t* lvl[2];
+    int16_t* rec[2];
+    uint8_t* tu[2];
+};
+
+template <int N, bool DST>
+__device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                                    int cnt, int total, int c0, const int* slx, const int* sly,
+                                                    int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq) {
+    constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
+    constexpr int32_t BIAS = 1 << (S - 1);
+    const int lane = opaque_lane64(), t = lane % N, e = c0 + lane / N;
+    const bool on = e < total;
+    const int p = on && e >= cnt ? 1 : 0, k = on ? e - p * cnt : 0;   // idle lanes shadow plane 0's first TU
+    const int lx = slx[k], ly = sly[k], x = x0c + lx, y = y0c + ly;
+    int16_t (*rc)[33] = rc2[p];
+    const int16_t* src = p ? pp.src[1] : pp.src[0];
+    int16_t* tl = t16 + p * (32 * TP) + ly * TP + lx;   // tl[line * TP + slot]
+    const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
+    const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
+    int32_t sum = topt + leftt;                                // DC (intra.py:46-62)
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    const int32_t dc = (sum + N) >> (L2 + 1);
+    const pk16 dc2 = pk_splat(dc);
+    pk16 o2[H];
+    pku16 pl2[H];
+    {
+        const int32_t b = (t + 1) * tr + (N - 1) * topt + bl + N, st = bl - topt;
+        pku16 bs = {(unsigned short)b, (unsigned short)(b + st)};
+        const pku16 st2 = {(unsigned short)(2 * st), (unsigned short)(2 * st)};
+        const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
+        const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
+        const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
+            const pku16 lf = {(unsigned short)rc[ly + 1 + 2 * m][lx], (unsigned short)rc[ly + 2 + 2 * m][lx]};
+            pl2[m] = (lf * wl + bs) >> sh;
+            bs += st2;
+        }
+    }
+    int32_t ed = 0, ep = 0;
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+        const pk16 d0 = o2[m] - dc2, d1 = o2[m] - __builtin_bit_cast(pk16, pl2[m]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+    }
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) {
+        ed += __shfl_xor(ed, m, 64);
+        ep += __shfl_xor(ep, m, 64);
+    }
+    const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
+    pk16 r2[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) r2[m] = o2[m] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[m]));
+    int32_t yv[N];
+    fwd1d_pk<N, DST>(r2, yv, BIAS);   // forward pass 1 (transform.py:179-185): column t -> line i, slot t
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(yv[i] >> S);
+    }
+    __syncthreads();
+    const int st = inv_slot<N, DST>(t);
+    {
+        pk16 P[H];   // forward pass 2 (transform.py:188-194): row t
+#pragma unroll
+        for (int m = 0; m < H; ++m) P[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        fwd1d_pk<N, DST>(P, yv, BIAS);
+    }
+    __syncthreads();
+    if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
+        int32_t* lrow = (p ? pp.lvl[1] : pp.lvl[0]) + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) {
+            const int32_t l = quant_s(yv[kk] >> S, cq.qs, cq.h_v, cq.hneg_v);
+            lrow[kk] = l;
+            tl[kk * TP + st] = (int16_t)dequant_s(l, cq);
+        }
+    }
+    __syncthreads();
+    int32_t xv[N];
+    {
+        pk16 Y[H];   // inverse pass 1 (transform.py:221-227): column t -> line i, slot inv_slot(t)
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        inv1d_pk<N, DST>(Y, xv, BIAS);
+    }
+    __syncthreads();
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(xv[i] >> S);
+    }
+    __syncthreads();
+    {
+        pk16 Y[H];   // inverse pass 2 (transform.py:230-236): row t
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        inv1d_pk<N, DST>(Y, xv, BIAS);
+    }
+    if (on) {   // reconstruct + clip (intra.py:70-78); planar in row layout
+        const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, stv = tr - leftt;
+        int16_t* rrow = (p ? pp.rec[1] : pp.rec[0]) + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) {
+            const int32_t pr = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + kk] + b + kk * stv) >> (L2 + 1);
+            int32_t q = pr + (xv[kk] >> S);
+            q = q < 0 ? 0 : (q > 255 ? 255 : q);
+            rrow[kk] = (int16_t)q;
+            rc[ly + 1 + t][lx + 1 + kk] = (int16_t)q;   // no TU of this batch reads the TU's own samples
+        }
+        if (t < N / 4) {
+            uint8_t* tu = p ? pp.tu[1] : pp.tu[0];
+            const int w4 = a.w / 4;
+            for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
+        }
+    }
+    __syncthreads();
+}
+
+// The pair form of k_tu_closed (NARROW streams only: the wide flag work[2]
+// makes it return when the 32-bit form codes the stream).  Tickets run
+// row-major over the pairs: ticket t = CTU row t / npairs of pair t % npairs;
+// pair q = (group pair q / ppg, plane q % ppg); a wave only waits on the same
+// pair's CTU row above, claimed before it.
+// The compiler's allocation (135 VGPRs, 3 waves/SIMD): 0.150 ms per 4K YUV420
+// frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
+constexpr int kPairWaves = 1;
+template <int WAVES>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
+    constexpr int TP = 34;
+    __shared__ int16_t rc[2][33][33];
+    __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * TP];
+    __shared__ int owner_of[64], done_of[64], slx[16], sly[16];
+    __shared__ int row_s, stall_s;
+    if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
+    const int lane = threadIdx.x;
+    const int ctb = a.ctb;
+    ChainQ cq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
+    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
+    const int ngroups = a.nplanes / a.ppg, npairs = ((ngroups + 1) / 2) * a.ppg;
+    const int total = a.crows * npairs;
+    // lanes [32 q, 32 q + 32) serve plane q of the pair for the line words and the left column (ctb <= 32)
+    const int hq = lane >> 5, hl = lane & 31;
+    for (;;) {
+        if (lane == 0) {
+            row_s = atomicAdd(&a.work[0], 1);
+            stall_s = 0;
+        }
+        __syncthreads();
+        const int tk = row_s;
+        if (tk >= total) break;
+        const int cy = tk / npairs, q = tk - cy * npairs;
+        const int c = q % a.ppg, g0 = 2 * (q / a.ppg);
+        const int two = g0 + 1 < ngroups ? 1 : 0;
+        PairPlanes pp;
+        uint64_t* line[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int g = g0 + (s & two);   // a lone plane: both slots name it (slot 1 never codes)
+            const int64_t off = (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
+            const int pl = g * a.ppg + c;
+            pp.src[s] = a.src + off;
+            pp.lvl[s] = a.lvl + off;
+            pp.rec[s] = a.rec + off;
+            pp.tu[s] = a.tu + (int64_t)pl * a.tu_plane;
+            line[s] = lines + (int64_t)pl * a.lw;
+        }
+        const int pid = a.plane_id + c, y0c = cy * ctb;
+        for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;   // recon starts as zeros (Frame.zeros)
+        __syncthreads();
+        if (hl < ctb) rc[hq][1 + hl][0] = 128;                             // x == 0: left = 128 (block.py:45-50)
+        for (int cx = 0; cx < a.ccols; ++cx) {
+            const int x0c = cx * ctb;
+            const int nw = (min(ctb, a.w - x0c) + 1) / 2;
+            // top row of this CTU: 128 at y == 0, else the CTU above's bottom row (tagged line words)
+            if (cy == 0) {
+                if (hl < ctb) rc[hq][0][1 + hl] = 128;
+            } else {
+                const bool need = hl < nw && hq <= two;
+                uint32_t val = 0;
+                int spins = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (need) {
+                        const uint64_t v = ld_sys64(line[hq] + x0c / 2 + hl);
+                        ok = (int)(v >> 32) == cy;
+                        val = (uint32_t)v;
+                    }
+                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
+                        if (lane == 0) atomicMax(&a.work[1], 1);
+                        stall_s = 1;
+                        break;
+                    }
+                }
+                if (need) {
+                    rc[hq][0][1 + 2 * hl] = (int16_t)(val & 0xffffu);
+                    if (2 * hl + 1 < ctb) rc[hq][0][2 + 2 * hl] = (int16_t)(val >> 16);
+                }
+            }
+            __syncthreads();
+            if (stall_s) break;
+            // the CTU's TUs in dataflow rounds (as k_tu_closed), found once for both planes
+            const int U = ctb / 4, UU = U * U;
+            int tn = 0, ox = 0, oy = 0;
+            bool pending = false;
+            if (lane < UU) {
+                const int ux = lane % U, uy = lane / U, x = x0c + 4 * ux, y = y0c + 4 * uy;
+                int own = lane;
+                if (x < a.w && y < a.h) {
+                    const int n = tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y), nu = n / 4;
+                    ox = ux - ux % nu;
+                    oy = uy - uy % nu;
+                    own = oy * U + ox;
+                    pending = ox == ux && oy == uy && x + n <= a.w && y + n <= a.h;
+                    tn = n;
+                }
+                owner_of[lane] = own;
+                done_of[lane] = 0;
+            }
+            __syncthreads();
+            for (int round = 0; round < UU && __ballot(pending); ++round) {
+                bool ready = pending;
+                if (pending) {
+                    const int nu = tn / 4;
+                    for (int k = 0; k < nu; ++k) {
+                        if (oy > 0 && !done_of[owner_of[(oy - 1) * U + ox + k]]) ready = false;
+                        if (ox > 0 && !done_of[owner_of[(oy + k) * U + ox - 1]]) ready = false;
+                    }
+                }
+                const uint64_t lt = (1ull << lane) - 1ull;
+#define NH_BATCH2(NN, DST, Q)                                                                                \
+                {                                                                                            \
+                    const uint64_t m = __ballot(ready && tn == NN);                                          \
+                    const int cnt = __popcll(m);                                                             \
+                    if (ready && tn == NN) {                                                                 \
+                        const int k = __popcll(m & lt);                                                      \
+                        slx[k] = ox * 4;                                                                     \
+                        sly[k] = oy * 4;                                                                     \
+                    }                                                                                        \
+                    __syncthreads();                                                                         \
+                    const int tot = cnt << two;                                                              \
+                    for (int c0 = 0; c0 < tot; c0 += 64 / NN)                                                \
+                        tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, slx, sly, rc, t16, Q);   \
+                }
+                NH_BATCH2(32, false, cq[3]);
+                NH_BATCH2(16, false, cq[2]);
+                NH_BATCH2(8, false, cq[1]);
+                if (a.is_luma) NH_BATCH2(4, true, cq[0]) else NH_BATCH2(4, false, cq[0])
+#undef NH_BATCH2
+                if (ready) {
+                    done_of[lane] = 1;
+                    pending = false;
+                }
+                __syncthreads();
+            }
+            // publish both bottom rows (the next CTU row polls them), then slide: right column -> left column
+            if (cy + 1 < a.crows && hl < nw && hq <= two) {
+                const uint32_t lo = (uint16_t)rc[hq][ctb][1 + 2 * hl];
+                const uint32_t hi = 2 * hl + 1 < ctb ? (uint16_t)rc[hq][ctb][2 + 2 * hl] : 0u;
+                st_sys64(line[hq] + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
+            }
+            __syncthreads();
+            int16_t keep = 0;
+            if (hl < ctb) keep = rc[hq][1 + hl][ctb];
+            __syncthreads();
+            for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
+            __syncthreads();
+            if (hl < ctb) rc[hq][1 + hl][0] = keep;
+            __syncthreads();
+        }
+        __syncthreads();
+        if (stall_s) break;
+    }
+}
+
 int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
                    hipStream_t s) {
     const int bw = w / 32, n = bw * (h / 32);
@@ -2204,11 +2500,26 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         NH_HIP(hipGetDevice(&dev));
         NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
-    int per_cu = 0;
-    NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tu_closed<1, true>, 64, 0));
-    const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
-    const unsigned waves_n = (unsigned)(rows < cap_n ? rows : cap_n);
-    if (narrow_ok) k_tu_closed<1, true><<<waves_n, 64, 0, s>>>(a);
+    // 8-bit streams: plane pairs (k_tu_closed_pair) when the set
+    // holds more than one group; A/B build: NH_TU_CLOSED_PAIR = 0 codes one plane
+    // per wave, = 4 the pair form capped at 4 waves/SIMD
+    static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
+    if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
+        int per_cu = 0;
+        auto kern = k_tu_closed_pair<kPairWaves>;
+#if NH_AB
+        if (pair_ok == 4) kern = k_tu_closed_pair<4>;   // A/B: capped at 4 waves/SIMD
+#endif
+        NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
+        const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
+        const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
+        kern<<<(unsigned)(prow < cap_n ? prow : cap_n), 64, 0, s>>>(a);
+    } else if (narrow_ok) {
+        int per_cu = 0;
+        NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_tu_closed<1, true>, 64, 0));
+        const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
+        k_tu_closed<1, true><<<(unsigned)(rows < cap_n ? rows : cap_n), 64, 0, s>>>(a);
+    }
 #if NH_AB
     if (cw == 3) k_tu_closed<3><<<waves, 64, 0, s>>>(a);
     else

@@ -873,6 +873,50 @@ def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
             off += ph * pw
 
 
+@pytest.mark.parametrize("conc", [False, True])
+@pytest.mark.parametrize("F,W,H,qp", [(1, 104, 72, 32), (2, 136, 104, 22), (3, 104, 72, 32), (5, 72, 40, 0),
+                                      (4, 136, 104, 51)])
+def test_tu_pipeline_closed_pairs_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
+    """8-bit YUV420 streams in closed loop: the plane-pair form (one wave codes
+    the same CTU row of frames 2p and 2p + 1, their TUs in shared batches) for
+    even and odd frame counts (a lone last plane), partial CTUs, QP 0 / 51 and
+    0 / 255 extremes; every plane equals the sequential oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(F * 1000 + W + qp)
+    fe = gpu.yuv420_frame_elems(W, H)
+    buf = np.empty(F * fe, np.int16)
+    off = 0
+    for f in range(F):
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            if f == 2:   # residuals at the extremes of the 8-bit range
+                p = 255 * rng.integers(0, 2, (ph, pw))
+            else:
+                p = np.clip(60 + (3 * xx + 2 * yy + 11 * f) % 150 + rng.integers(-30, 31, (ph, pw)), 0, 255)
+            buf[off:off + ph * pw] = p.reshape(-1)
+            off += ph * pw
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(F, W, H)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    if conc:
+        _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, 4242, qp, lvl=lvl, rec=rec)
+    else:
+        _, _, tuy = gpu.tu_pipeline_closed(d, sy, 32, 0, 4242, qp, True, lvl=lvl, rec=rec)
+        _, _, tuc = gpu.tu_pipeline_closed(d, suv, 16, 1, 4242, qp, False, lvl=lvl, rec=rec)
+    lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    off = 0
+    for f in range(F):
+        for k, (pw, ph) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er, et = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, 4242, qp, k == 0)
+            assert np.array_equal(lv[off:off + ph * pw].reshape(ph, pw), el), (f, k)
+            assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
+            assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
+            off += ph * pw
+
+
 @pytest.mark.parametrize("ctb", [4, 8, 16])
 def test_tu_pipeline_closed_small_ctb_vs_oracle(nh, torch_dev, ctb):
     """Closed-loop config 4 with CTBs below 32 (fewer units per CTU, more CTU rows)."""

@@ -177,12 +177,17 @@ def main():
                           "CTU-row wavefront on the device", "frames": nf,
                 "luma_chroma": "sequential" if args.closed4_seq else "concurrent", "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
                 "frames_per_s": nf / ms * 1e3, "samples_per_s": stream.numel() / ms * 1e3,
-                "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H])}
-        if args.check:
+                "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H]), "knobs": knobs,
+                "out_digest": [int(lv.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item())]}
+        if args.check:   # frames 0 and 1: the two planes of the first luma pair
             from oracle import oracle as O   # checker only
-            y = stream[:W * H].view(H, W).cpu().numpy()
-            el, er, _ = O.tu_pipeline_plane_closed(y, 32, 0, 1234, args.qp, True)
-            line["frame0_luma_equals_oracle"] = bool(np.array_equal(er, rc[:W * H].view(H, W).cpu().numpy()))
+            fe = gpu.yuv420_frame_elems(W, H)
+            for f in range(min(2, nf)):
+                y = stream[f * fe:f * fe + W * H].view(H, W).cpu().numpy()
+                el, er, _ = O.tu_pipeline_plane_closed(y, 32, 0, 1234, args.qp, True)
+                line[f"frame{f}_luma_equals_oracle"] = bool(
+                    np.array_equal(er, rc[f * fe:f * fe + W * H].view(H, W).cpu().numpy()) and
+                    np.array_equal(el, lv[f * fe:f * fe + W * H].view(H, W).cpu().numpy()))
         print(json.dumps(line), flush=True)
 
     if 5 in cfgs:
