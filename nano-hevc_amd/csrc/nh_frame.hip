@@ -483,17 +483,14 @@ __device__ __forceinline__ void decide_blk_u8(const EncArgs& a, const uint8_t* s
         }
     if (k.full) {
         const bool use_dc = edc <= epl;
-        int sse = 0;
+        // the recon is the chosen prediction (clip is the identity here), so its
+        // SSE against the source is that prediction's energy
+        const int sse = use_dc ? edc : epl;
 #pragma unroll
         for (int y = 0; y < N; ++y) {
             unsigned rv[N / 2];
 #pragma unroll
-            for (int q = 0; q < N / 2; ++q) {
-                const v2us v = use_dc ? dc2 : planar_row(y, q);
-                const v2s d = as_s(pair_u8(k.o[y][q >> 1], q & 1) - v);
-                sse = __builtin_amdgcn_sdot2(d, d, sse, false);
-                rv[q] = as_u(v);
-            }
+            for (int q = 0; q < N / 2; ++q) rv[q] = as_u(use_dc ? dc2 : planar_row(y, q));
             const int64_t i = off + (int64_t)(k.y0 + y) * a.pitch + k.x0;
             if (a.rec) {
                 if constexpr (N == 4) __builtin_nontemporal_store(v2u{rv[0], rv[1]}, (v2u*)(a.rec + i));
