@@ -75,7 +75,8 @@ struct CtuArgs {
     QuantParams q[4];                // log2 N = 2..5
     int32_t dqs, dq_per;
     int32_t wide_only;               // A/B build only (NH_CTU_NARROW=0): every workgroup on the 32-bit chain
-    int32_t probe;                   // A/B build only (NH_CTU_PROBE, bits): 1 = no batches, 2 = no global loads (wrong outputs)
+    int32_t probe;                   // A/B build only (NH_CTU_PROBE, bits): 1 = no batches, 2 = no global loads,
+                                     // 4 = return at once, 8 = no TU-map stores (wrong outputs)
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
@@ -803,7 +804,8 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
         const bool in = x < w && y < h;
         int cx, cy;
         ls = unit_leaf<CTB>(split, ux, uy, sx0, sy0, cx, cy);
-        if (in) a.tu[(int64_t)pz * a.tu_plane + (int64_t)(y >> 2) * (w >> 2) + (x >> 2)] = (uint8_t)ls;
+        if (in && (!NH_AB || (a.probe & 8) == 0))
+            a.tu[(int64_t)pz * a.tu_plane + (int64_t)(y >> 2) * (w >> 2) + (x >> 2)] = (uint8_t)ls;
         org = in && cx == x && cy == y;
     }
     uint64_t m[4];
@@ -907,6 +909,7 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
 template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
     __shared__ CtuSmem<CTB, true, MFMA32> sm;
+    if (NH_AB && (a.probe & 4)) return;   // A/B probe: the launch of the grid alone
     if constexpr (PERSIST == 0) {
         // the bases' loads issued with the strip's and written to LDS after the
         // strip image (one wait for both; ctu_group's barrier orders them before use)
