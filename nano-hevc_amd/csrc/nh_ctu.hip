@@ -81,6 +81,12 @@ struct CtuArgs {
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 
+// Level and recon rows out of the chains: plain stores.  Nontemporal ones (the
+// rows are never re-read here) took 127 vs 39 us per 4K YUV420 frame: 8-16 B
+// pieces of scattered rows (profiles/r02/session5/nt_ab.jsonl).
+__device__ __forceinline__ void st_lvl4(int32_t* p, int4 v) { *(int4*)p = v; }
+__device__ __forceinline__ void st_rec4(int16_t* p, uint2 v) { *(uint2*)p = v; }
+
 // The lane id as an opaque value: lane-derived addresses and constants of a
 // chain are then computed inside each batch, not hoisted out of the batch loop
 // and held live across it (which multiplied the register pressure by the
@@ -190,7 +196,7 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
                 L4[q] = quant_s(rshift_round<S>(r[k0 + q]), cq.qs, cq.h_v, cq.hneg_v);
                 cf[t * CP + k0 + q] = dequant_s(L4[q], cq);
             }
-            *(int4*)(lrow + k0) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+            st_lvl4(lrow + k0, make_int4(L4[0], L4[1], L4[2], L4[3]));
         }
     }
     wave_sync();
@@ -226,7 +232,7 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
         }
         int16_t* rrow = rec + (int64_t)(gy0 + t) * a.pitch + gx0;
 #pragma unroll
-        for (int k = 0; k < N / 2; k += 2) *(uint2*)(rrow + 2 * k) = make_uint2(pk[k], pk[k + 1]);
+        for (int k = 0; k < N / 2; k += 2) st_rec4(rrow + 2 * k, make_uint2(pk[k], pk[k + 1]));
     }
 }
 
@@ -324,7 +330,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
                 L4[q] = quant_s(y[k0 + q] >> S, cq.qs, cq.h_v, cq.hneg_v);
                 tl[(k0 + q) * TP + st] = (int16_t)dequant_s(L4[q], cq);
             }
-            *(int4*)(lrow + k0) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+            st_lvl4(lrow + k0, make_int4(L4[0], L4[1], L4[2], L4[3]));
         }
     }
     wave_sync();
@@ -367,7 +373,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
         }
         int16_t* rrow = rec + (int64_t)(gy0 + t) * a.pitch + gx0;
 #pragma unroll
-        for (int m = 0; m < H; m += 2) *(uint2*)(rrow + 2 * m) = make_uint2(pk[m], pk[m + 1]);
+        for (int m = 0; m < H; m += 2) st_rec4(rrow + 2 * m, make_uint2(pk[m], pk[m + 1]));
     }
 }
 
@@ -426,7 +432,7 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
             L4[e] = quant_s(rshift_round<10>((uint32_t)acc[g]), cq.qs, cq.h_v, cq.hneg_v);
             cf[r * CP + crow(g, hh)] = dequant_s(L4[e], cq);
         }
-        *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+        st_lvl4(lrow + 8 * q + 4 * hh, make_int4(L4[0], L4[1], L4[2], L4[3]));
     }
     wave_sync();
 #pragma unroll
@@ -448,8 +454,8 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
             const int32_t rc = sext16((use_dc ? dc : planar(r, jx)) + rr);
             R4[e] = rc < 0 ? 0 : (rc > 255 ? 255 : rc);
         }
-        *(uint2*)(rrow + 8 * q + 4 * hh) =
-            make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
+        st_rec4(rrow + 8 * q + 4 * hh,
+                make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16)));
     }
 }
 
@@ -572,7 +578,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             L4[e] = quant_s((int32_t)__builtin_floorf(acc2[g]), cq.qs, cq.h_v, cq.hneg_v);
             qt[crow(g, hh) * QH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
         }
-        *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+        st_lvl4(lrow + 8 * q + 4 * hh, make_int4(L4[0], L4[1], L4[2], L4[3]));
     }
     wave_sync();
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
@@ -598,8 +604,8 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             const int32_t v = p + (int32_t)__builtin_floorf(acc4[4 * q + e]);
             R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
         }
-        *(uint2*)(rrow + 8 * q + 4 * hh) =
-            make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
+        st_rec4(rrow + 8 * q + 4 * hh,
+                make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16)));
     }
 }
 
