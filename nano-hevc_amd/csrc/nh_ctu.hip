@@ -466,9 +466,11 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
 // <= 327) against the basis scaled by 2^-10, every product is exact in fp32
 // and every partial sum is a multiple of 2^-10 below 2^14 (tools/
 // packed_bounds.py: at most 6,813,696 * 2^-10), so the fp32 accumulators hold
-// the reference's integer sums exactly; the rounding constant is the
-// accumulator's initial 0.5 (transform.py:185) and floor() is the arithmetic
-// shift.  Lane (r, hh): pass 1 and inverse pass 1 take the data as the A
+// the reference's integer sums exactly; the accumulators start at 0 (an
+// inline constant: no registers hold an initial value) and the rounding
+// constant 0.5 (transform.py:185) -- for pass 1 also minus the 1536 offset of
+// row 0 -- is added before floor(), the arithmetic shift (still exact: the
+// sums stay below 2^23 * 2^-10).  Lane (r, hh): pass 1 and inverse pass 1 take the data as the A
 // operand (lane = the free index), passes 2 and 4 take the previous
 // accumulator as the B operand in accumulator row order (the bases
 // pre-permuted to match), and one LDS transpose sits after dequantization.
@@ -494,12 +496,12 @@ __device__ __forceinline__ h8_t ld_crow_h8(const uint16_t* row, int s, int hh) {
 __device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
 }
-__device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s) {   // registers 8s .. 8s+7, floored, as f16
+__device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s, float b) {   // registers 8s .. 8s+7 + b, floored, as f16
     uint4 u;
-    u.x = pk_floor_h(acc[8 * s + 0], acc[8 * s + 1]);
-    u.y = pk_floor_h(acc[8 * s + 2], acc[8 * s + 3]);
-    u.z = pk_floor_h(acc[8 * s + 4], acc[8 * s + 5]);
-    u.w = pk_floor_h(acc[8 * s + 6], acc[8 * s + 7]);
+    u.x = pk_floor_h(acc[8 * s + 0] + b, acc[8 * s + 1] + b);
+    u.y = pk_floor_h(acc[8 * s + 2] + b, acc[8 * s + 3] + b);
+    u.z = pk_floor_h(acc[8 * s + 4] + b, acc[8 * s + 5] + b);
+    u.w = pk_floor_h(acc[8 * s + 6] + b, acc[8 * s + 7] + b);
     return __builtin_bit_cast(h8_t, u);
 }
 __device__ __forceinline__ f16x_t splat16(float v) {
@@ -556,17 +558,18 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
         const pk16 rr = o2[p] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[p]));
         hx[p] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, rr) + (pku16){0x6600, 0x6600});
     }
-    // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x]; the 1536 offset removed by the bias (row 0 only:
-    // every other DCT32 row sums to 0)
-    f16x_t acc = splat16(r == 0 ? 0.5f - 3072.0f : 0.5f);
+    // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x]; the 1536 offset removed with the rounding bias
+    // b1 (row 0 only: every other DCT32 row sums to 0)
+    const float b1 = r == 0 ? 0.5f - 3072.0f : 0.5f;
+    f16x_t acc = splat16(0.0f);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
                                                  ld_h8(&bs.t[r][8 * hh]), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
                                                  ld_h8(&bs.t[r][16 + 8 * hh]), acc, 0, 0, 0);
     // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
-    f16x_t acc2 = splat16(0.5f);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 0, hh), acc_h8(acc, 0), acc2, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 1, hh), acc_h8(acc, 1), acc2, 0, 0, 0);
+    f16x_t acc2 = splat16(0.0f);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 0, hh), acc_h8(acc, 0, b1), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 1, hh), acc_h8(acc, 1, b1), acc2, 0, 0, 0);
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
     int32_t* lrow = lvl + (int64_t)(gy0 + r) * a.pitch + gx0;
 #pragma unroll
@@ -575,22 +578,22 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int g = 4 * q + e;
-            L4[e] = quant_s((int32_t)__builtin_floorf(acc2[g]), cq.qs, cq.h_v, cq.hneg_v);
+            L4[e] = quant_s((int32_t)__builtin_floorf(acc2[g] + 0.5f), cq.qs, cq.h_v, cq.hneg_v);
             qt[crow(g, hh) * QH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
         }
         st_lvl4(lrow + 8 * q + 4 * hh, make_int4(L4[0], L4[1], L4[2], L4[3]));
     }
     wave_sync();
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
-    f16x_t acc3 = splat16(0.5f);
+    f16x_t acc3 = splat16(0.0f);
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.tt[r][8 * hh]), acc3,
                                                   0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 16 + 8 * hh),
                                                   ld_h8(&bs.tt[r][16 + 8 * hh]), acc3, 0, 0, 0);
     // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
-    f16x_t acc4 = splat16(0.5f);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 0, hh), acc_h8(acc3, 0), acc4, 0, 0, 0);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 1, hh), acc_h8(acc3, 1), acc4, 0, 0, 0);
+    f16x_t acc4 = splat16(0.0f);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 0, hh), acc_h8(acc3, 0, 0.5f), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 1, hh), acc_h8(acc3, 1, 0.5f), acc4, 0, 0, 0);
     // reconstruct + clip (intra.py:70-78), row y = r
     int16_t* rrow = rec + (int64_t)(gy0 + r) * a.pitch + gx0;
 #pragma unroll
@@ -601,7 +604,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             const int x = 8 * q + 4 * hh + e;
             const int32_t p = use_dc ? dc
                                      : ((31 - x) * leftr + (x + 1) * tr + (31 - r) * (int32_t)img[x] + (r + 1) * bl + 32) >> 6;
-            const int32_t v = p + (int32_t)__builtin_floorf(acc4[4 * q + e]);
+            const int32_t v = p + (int32_t)__builtin_floorf(acc4[4 * q + e] + 0.5f);
             R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
         }
         st_rec4(rrow + 8 * q + 4 * hh,
@@ -1089,15 +1092,13 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // 32-bit chain.  A/B build: NH_CTU_T32 = 0 (narrow 32x32 TUs on packed
     // butterflies) / 1 (wide 32x32 TUs on int8 MFMA), NH_CTU_PERSIST = 1 / 2
     // (resident grid, loads one group ahead / without prefetch), NH_CTU_NARROW = 0 (every group on
-    // the 32-bit path), NH_CTU_PROBE = 1 / 2 (no batches / no global loads).
+    // the 32-bit path), NH_CTU_PROBE = bits 1 / 2 / 4 / 8 (no batches / no global loads /
+    // return at once / no TU-map stores).
     static const int t32 = NH_KNOB("NH_CTU_T32", 2);
     static const int persist = NH_KNOB("NH_CTU_PERSIST", 0);
-    // The luma f16-MFMA form stays at 5 waves/SIMD (90 VGPRs).  Its LDS (27 KB per
-    // workgroup with the 4 KB bases) would fit 6 workgroups per CU, but the
-    // 80-register cap spills 5 VGPRs: 466 vs 421 us per 16 luma planes
-    // (A/B build: NH_CTU_W32 = 6; profiles/r02/session5/).
-    constexpr int kW32 = 5;
-    static const int w32 = NH_KNOB("NH_CTU_W32", kW32);
+    // The luma f16-MFMA form runs at 6 waves/SIMD: 76 VGPRs with zero-initialised
+    // accumulators (90 with the rounding constant as their initial value) and
+    // 27 KB of LDS per workgroup with the 4 KB bases.
     a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
     a.probe = NH_KNOB("NH_CTU_PROBE", 0);
     auto launch_open = [&](auto kern) -> int {
@@ -1127,8 +1128,7 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
             const bool m = M32 && t32 != 0;
             if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>)
                          : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>)
-                         : w32 == 6     ? launch_open(k_ctu_open<C, L, M32, 0, 6>)
-                                        : launch_open(k_ctu_open<C, L, M32, 0, kW32>);
+                                        : launch_open(k_ctu_open<C, L, M32, 0>);
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>)
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>)
                                       : launch_open(k_ctu_open<C, L, false, 0>);

@@ -97,7 +97,10 @@ def main():
     c = shift_bound(f1 * rl1, 10)
     dq = max(dequant(quant(c, qp, 5, intra), qp) for qp in range(52) for intra in (True, False))
     i1 = shift_bound(dq * cl1, 10)
-    sums = {"pass1": p1, "pass2": f1 * rl1, "inv1": dq * cl1, "inv2": i1 * cl1}
+    # the accumulators start at 0; the rounding bias (0.5, pass 1 row 0: 0.5 - 3072) is added to
+    # the final sum before floor(): its magnitude in 2^-10 units joins the bound
+    bias = {"pass1": 3072 * 1024, "pass2": 512, "inv1": 512, "inv2": 512}
+    sums = {"pass1": p1 + bias["pass1"], "pass2": f1 * rl1 + 512, "inv1": dq * cl1 + 512, "inv2": i1 * cl1 + 512}
     ops = {"residual+1536": 1536 + x0, "pass1 out": f1, "dequant": dq, "inv1 out": i1}
     print("f16 32x32 chain: operands", ops, "(exact in f16 below 2048), |sums|", sums, "(limit 2^24)")
     assert max(ops.values()) < 2048 and max(sums.values()) < 2 ** 24
