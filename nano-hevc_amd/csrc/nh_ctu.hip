@@ -30,6 +30,7 @@
 // §4.4 (the residual is int16).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
@@ -1031,6 +1032,35 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, hipStream_t s);
 
+// Dynamic LDS that caps `kern` at `wgs` resident workgroups per CU: the
+// workgroup then reserves just over 1 / (wgs + 1) of the CU's LDS (static +
+// this pad; the pad is never touched).  These kernels run faster with fewer
+// resident workgroups.  Cached per kernel; 0 when the
+// device reports no per-CU LDS figure.  A/B build: NH_OCC_CAP = 0 disables it.
+template <class K>
+static unsigned lds_cap(K kern, int wgs) {
+    static const int on = NH_KNOB("NH_OCC_CAP", 1);
+    if (!on) return 0;
+    struct Entry { const void* k; int wgs, dev; unsigned pad; };
+    static Entry cache[32];
+    static int used = 0;
+    static std::mutex mu;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> g(mu);
+    for (int i = 0; i < used; ++i)
+        if (cache[i].k == (const void*)kern && cache[i].wgs == wgs && cache[i].dev == dev) return cache[i].pad;
+    int lds_cu = 0;
+    hipFuncAttributes fa{};
+    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+        hipFuncGetAttributes(&fa, (const void*)kern) != hipSuccess)
+        return 0;
+    const long need = (long)lds_cu / (wgs + 1) + 1 - (long)fa.sharedSizeBytes;   // wgs + 1 must not fit
+    const unsigned pad = need > 0 ? (unsigned)need : 0u;
+    if (used < 32) cache[used++] = Entry{(const void*)kern, wgs, dev, pad};
+    return pad;
+}
+
 static int ensure_basis_ctu() {
     static unsigned long long ready = 0;   // one bit per device
     int dev = 0;
@@ -1101,6 +1131,10 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // 27 KB of LDS per workgroup with the 4 KB bases.
     a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
     a.probe = NH_KNOB("NH_CTU_PROBE", 0);
+    // Occupancy caps: fewer resident workgroups run these
+    // kernels faster -- 3 per CU for luma (CTB 32), 4 for chroma.  A/B build:
+    // NH_OCC_CAP = 0 leaves them uncapped.
+    const int cap_wgs = ctb == 32 ? 3 : 4;
     auto launch_open = [&](auto kern) -> int {
         if (NH_AB != 0 && persist) {
             static int cus = 0;
@@ -1110,11 +1144,12 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
                 NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
             }
             int per_cu = 0;
-            NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0));
+            const unsigned pad = lds_cap(kern, cap_wgs);
+            NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, pad));
             const int res = std::max(1, cus * per_cu);
-            kern<<<dim3((unsigned)std::min(items, res), 1), 256, 0, s>>>(a, items);
+            kern<<<dim3((unsigned)std::min(items, res), 1), 256, pad, s>>>(a, items);
         } else {
-            kern<<<grid, 256, 0, s>>>(a, items);
+            kern<<<grid, 256, lds_cap(kern, cap_wgs), s>>>(a, items);
         }
         return NH_OK;
     };
@@ -1181,7 +1216,10 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     const int nblk = a.strips_x * a.nrows, planes = S.planes_per_group * S.num_groups;
     if (!nblk || !planes) return NH_OK;
     constexpr int K = 1;
-    k_tc32_h<K><<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, 0, s>>>(a, nblk);
+    // capped at 3 resident workgroups per CU: 0.137 vs 0.153 ms per 8K YUV420 frame
+    // uncapped (5 per CU; 2 per CU: 0.164), DESIGN.md §4.5
+    k_tc32_h<K><<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(k_tc32_h<K>, 3), s>>>(
+        a, nblk);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
