@@ -1032,35 +1032,6 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, hipStream_t s);
 
-// Dynamic LDS that caps `kern` at `wgs` resident workgroups per CU: the
-// workgroup then reserves just over 1 / (wgs + 1) of the CU's LDS (static +
-// this pad; the pad is never touched).  These kernels run faster with fewer
-// resident workgroups.  Cached per kernel; 0 when the
-// device reports no per-CU LDS figure.  A/B build: NH_OCC_CAP = 0 disables it.
-template <class K>
-static unsigned lds_cap(K kern, int wgs) {
-    static const int on = NH_KNOB("NH_OCC_CAP", 1);
-    if (!on) return 0;
-    struct Entry { const void* k; int wgs, dev; unsigned pad; };
-    static Entry cache[32];
-    static int used = 0;
-    static std::mutex mu;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    std::lock_guard<std::mutex> g(mu);
-    for (int i = 0; i < used; ++i)
-        if (cache[i].k == (const void*)kern && cache[i].wgs == wgs && cache[i].dev == dev) return cache[i].pad;
-    int lds_cu = 0;
-    hipFuncAttributes fa{};
-    if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
-        hipFuncGetAttributes(&fa, (const void*)kern) != hipSuccess)
-        return 0;
-    const long need = (long)lds_cu / (wgs + 1) + 1 - (long)fa.sharedSizeBytes;   // wgs + 1 must not fit
-    const unsigned pad = need > 0 ? (unsigned)need : 0u;
-    if (used < 32) cache[used++] = Entry{(const void*)kern, wgs, dev, pad};
-    return pad;
-}
-
 static int ensure_basis_ctu() {
     static unsigned long long ready = 0;   // one bit per device
     int dev = 0;

@@ -621,7 +621,7 @@ static void launch_small(int u, const EncArgs& a, dim3 grid, hipStream_t s) {
     if constexpr (std::is_same<T, uint8_t>::value && AL) {   // packed 16-bit path
         if (enc_tune().pipe) {
             if (N == 8 && u == 1 && enc_tune().waves == 4) k_encode_u8<N, 1, true, 4><<<grid, 256, 0, s>>>(a);
-            else if (u == 1) k_encode_u8<N, 1, true><<<grid, 256, 0, s>>>(a);
+            else if (u == 1) k_encode_u8<N, 1, true><<<grid, 256, lds_cap(k_encode_u8<N, 1, true>, NH_KNOB("NH_CAP_ENC", 0)), s>>>(a);
             else if (u == 2) k_encode_u8<N, 2, true><<<grid, 256, 0, s>>>(a);
             else k_encode_u8<N, 4, true><<<grid, 256, 0, s>>>(a);
         } else {

@@ -957,7 +957,10 @@ extern "C" int nh_fwd8x8_quant_planes_variant(const int16_t* d_res, int16_t* d_l
             k_fwd8x8_quant<1, 5><<<wg, 256, 0, s>>>(a);
         } else {
             a.xcd_chunk = wg / 8 ? wg / 8 : 1;
-            k_fwd8x8_quant<1, 5, 256, true><<<wg, 256, 0, s>>>(a);
+            // capped at 4 resident workgroups per CU (LDS reservation, lds_cap): +0.3-0.9 % in every
+            // placement regime; A/B build: NH_CAP_FWD8 = 0 uncapped
+            k_fwd8x8_quant<1, 5, 256, true>
+                <<<wg, 256, lds_cap(k_fwd8x8_quant<1, 5, 256, true>, NH_KNOB("NH_CAP_FWD8", 4)), s>>>(a);
         }
         NH_HIP(hipGetLastError());
         return NH_OK;

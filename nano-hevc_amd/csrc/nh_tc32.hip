@@ -281,7 +281,7 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
                                                           dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base,
                                                           ta, nullptr);
         } else {              // int8 matrix cores only (A/B)
-            k_tc32_mfma<false><<<grid, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
+            k_tc32_mfma<false><<<grid, 256, lds_cap(k_tc32_mfma<false>, NH_KNOB("NH_CAP_TC32", 0)), s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
                                                     dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base, ta,
                                                     nullptr);
         }
