@@ -667,7 +667,8 @@ int nh_widen_u8_i16(const uint8_t* d_in, int16_t* d_out, int64_t n, void* stream
     const hipStream_t s = as_stream(stream);
     if (((uintptr_t)d_in & 7) == 0 && ((uintptr_t)d_out & 15) == 0) {
         const int64_t chunks = n / 8, threads = chunks + (n - chunks * 8);
-        k_widen<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n, xcd_order());
+        k_widen<<<(unsigned)((threads + 255) / 256), 256, lds_cap(k_widen, NH_KNOB("NH_CAP_IO", 0)), s>>>(
+            d_in, d_out, chunks, n, xcd_order());
     } else {
         k_widen_scalar<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(d_in, d_out, n);
     }
@@ -681,7 +682,8 @@ int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* strea
     const hipStream_t s = as_stream(stream);
     if (((uintptr_t)d_in & 15) == 0 && ((uintptr_t)d_out & 7) == 0) {
         const int64_t chunks = n / 8, threads = chunks + (n - chunks * 8);
-        k_narrow<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(d_in, d_out, chunks, n, xcd_order());
+        k_narrow<<<(unsigned)((threads + 255) / 256), 256, lds_cap(k_narrow, NH_KNOB("NH_CAP_IO", 0)), s>>>(
+            d_in, d_out, chunks, n, xcd_order());
     } else {
         k_narrow_scalar<<<(unsigned)std::min<int64_t>((n + 255) / 256, 65536), 256, 0, s>>>(d_in, d_out, n);
     }
