@@ -613,16 +613,16 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     }
 }
 
-// Shared memory of one workgroup = 4 strips.  Narrow kernels keep the
-// coefficient tile in int16 (half the LDS: more workgroups per CU).
-template <int CTB, bool NARROW, bool BASIS = false> struct CtuSmem {
+// Shared memory of one workgroup = GS strips (a group).  Narrow kernels keep
+// the coefficient tile in int16 (half the LDS: more workgroups per CU).
+template <int CTB, bool NARROW, bool BASIS = false, int GS = 4> struct CtuSmem {
     using G = Strip<CTB>;
     struct Empty {};
-    static constexpr int TILE32 = NARROW ? (4 * G::T16 + 1) / 2 : 4 * G::CF;
-    __attribute__((aligned(16))) int16_t img[4 * G::IMG];
+    static constexpr int TILE32 = NARROW ? (GS * G::T16 + 1) / 2 : GS * G::CF;
+    __attribute__((aligned(16))) int16_t img[GS * G::IMG];
     __attribute__((aligned(16))) int32_t tile[TILE32];
-    uint16_t list[4][256];
-    int cnt[4][4], org[8], next, wide[4];
+    uint16_t list[4][64 * GS];   // per TU size: entry = strip << 6 | unit
+    int cnt[GS][4], org[2 * GS], next, wide[GS];
     std::conditional_t<BASIS, BasisH, Empty> basis;   // ctu_chain32_h's f16 bases
 };
 
@@ -707,9 +707,9 @@ template <int CTB> struct StripLoad {
     int32_t left;
 };
 
-template <int CTB>
+template <int CTB, int GS = 4>
 __device__ __forceinline__ int strip_of(const CtuArgs& a, int grp, int wv, int& sx0, int& sy0) {
-    const int strip = grp * 4 + wv;
+    const int strip = grp * GS + wv;
     sx0 = (strip % a.strips_x) * Strip<CTB>::SW;
     sy0 = (a.row0 + strip / a.strips_x) * CTB;
     return strip < a.strips_x * a.nrows;
@@ -719,14 +719,14 @@ __device__ __forceinline__ int64_t plane_off(const CtuArgs& a, int pz) {
     return (int64_t)gz * a.group_stride + (int64_t)cz * a.plane_stride;
 }
 
-template <int CTB>
+template <int CTB, int GS = 4>
 __device__ __forceinline__ void strip_issue(const CtuArgs& a, int grp, int pz, StripLoad<CTB>& ld, int wv = -1) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
     const int lane = opaque_lane();
     if (wv < 0) wv = threadIdx.x >> 6;
     int sx0, sy0;
-    const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
+    const bool valid = strip_of<CTB, GS>(a, grp, wv, sx0, sy0);
     const int16_t* __restrict__ src = a.src + plane_off(a, pz);
     const int w = a.w, h = a.h, pitch = a.pitch;
 #pragma unroll
@@ -789,14 +789,15 @@ __device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* i
 // the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
 // !NARROW: the 32-bit chain, any int16 input.
 // Returns with the workgroup's waves in the batch loop's exit (no barrier).
-template <int CTB, bool LUMA, bool NARROW, bool MFMA32, class Prefetch>
-__device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, CtuSmem<CTB, NARROW, NARROW && MFMA32>& sm,
-                                          StripLoad<CTB>& ld, Prefetch&& prefetch) {
+template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, class Prefetch>
+__device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
+                                          CtuSmem<CTB, NARROW, NARROW && MFMA32, GS>& sm, StripLoad<CTB>& ld,
+                                          Prefetch&& prefetch) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
     const int wv = threadIdx.x >> 6, lane = opaque_lane();
     int sx0, sy0;
-    const bool valid = strip_of<CTB>(a, grp, wv, sx0, sy0);
+    const bool valid = strip_of<CTB, GS>(a, grp, wv, sx0, sy0);
     const int64_t poff = plane_off(a, pz);
     int32_t* lvl = a.lvl + poff;
     int16_t* rec = a.rec + poff;
@@ -840,7 +841,10 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
     if (threadIdx.x == 0) sm.next = 0;
     __syncthreads();
     if constexpr (NARROW) {
-        if (__builtin_amdgcn_readfirstlane(sm.wide[0] | sm.wide[1] | sm.wide[2] | sm.wide[3] | a.wide_only)) {
+        int any_wide = a.wide_only;
+#pragma unroll
+        for (int q = 0; q < GS; ++q) any_wide |= sm.wide[q];
+        if (__builtin_amdgcn_readfirstlane(any_wide)) {
             if (valid && lane == 0) a.tu[tu_org] = (uint8_t)(ls | 0x80);   // unit 0 = the strip's origin
             return;
         }
@@ -852,7 +856,7 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
         int off = 0;
         cnt[k] = 0;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < GS; ++q) {
             off += q < wv ? sm.cnt[q][k] : 0;
             cnt[k] += sm.cnt[q][k];
         }
@@ -916,20 +920,25 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz, Ctu
 // resident workgroups walking the (group, plane) items with stride gridDim.x,
 // each group's loads issued during the previous group's chains.
 // WAVES: the occupancy floor (waves/SIMD) the registers are allocated for.
-template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
-    __shared__ CtuSmem<CTB, true, MFMA32> sm;
+template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4>
+__global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
+    __shared__ CtuSmem<CTB, true, MFMA32, GS> sm;
     if (NH_AB && (a.probe & 4)) return;   // A/B probe: the launch of the grid alone
     if constexpr (PERSIST == 0) {
         // the bases' loads issued with the strip's and written to LDS after the
         // strip image (one wait for both; ctu_group's barrier orders them before use)
-        static_assert(sizeof(BasisH) == 256 * 16, "one 16-byte piece per thread");
-        uint4 bq;
-        if constexpr (MFMA32) bq = ((const uint4*)&c_basis_h)[threadIdx.x];
+        static_assert(sizeof(BasisH) == 256 * 16 && GS >= 4, "one 16-byte piece per thread of the first 256");
+        uint4 bq{};
+        const bool bthr = threadIdx.x < 256;
+        if constexpr (MFMA32) {
+            if (bthr) bq = ((const uint4*)&c_basis_h)[threadIdx.x];
+        }
         StripLoad<CTB> ld;
-        strip_issue<CTB>(a, blockIdx.x, blockIdx.y, ld);
-        ctu_group<CTB, LUMA, true, MFMA32>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
-            if constexpr (MFMA32) ((uint4*)&sm.basis)[threadIdx.x] = bq;
+        strip_issue<CTB, GS>(a, blockIdx.x, blockIdx.y, ld);
+        ctu_group<CTB, LUMA, true, MFMA32, GS>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
+            if constexpr (MFMA32) {
+                if (bthr) ((uint4*)&sm.basis)[threadIdx.x] = bq;
+            }
         });
     } else {
         if constexpr (MFMA32) copy_basis_h(sm.basis);   // ordered before use by ctu_group's barrier
@@ -937,13 +946,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         // PERSIST = 2: no prefetch (only the per-workgroup start-up amortised)
         StripLoad<CTB> ld;
         int it = blockIdx.x;
-        const int gcount = (a.strips_x * a.nrows + 3) / 4;
-        if (PERSIST == 1 && it < items) strip_issue<CTB>(a, it % gcount, it / gcount, ld);
+        const int gcount = (a.strips_x * a.nrows + GS - 1) / GS;
+        if (PERSIST == 1 && it < items) strip_issue<CTB, GS>(a, it % gcount, it / gcount, ld);
         for (; it < items; it += gridDim.x) {
             const int nx = it + gridDim.x;
-            if constexpr (PERSIST == 2) strip_issue<CTB>(a, it % gcount, it / gcount, ld);
-            ctu_group<CTB, LUMA, true, MFMA32>(a, it % gcount, it / gcount, sm, ld, [&] {
-                if (PERSIST == 1 && nx < items) strip_issue<CTB>(a, nx % gcount, nx / gcount, ld);
+            if constexpr (PERSIST == 2) strip_issue<CTB, GS>(a, it % gcount, it / gcount, ld);
+            ctu_group<CTB, LUMA, true, MFMA32, GS>(a, it % gcount, it / gcount, sm, ld, [&] {
+                if (PERSIST == 1 && nx < items) strip_issue<CTB, GS>(a, nx % gcount, nx / gcount, ld);
             });
             __syncthreads();   // every wave done with this group's LDS
         }
@@ -981,7 +990,7 @@ __global__ void __launch_bounds__(256) k_ctu_wide(CtuArgs a) {
         mask &= mask - 1;
         StripLoad<CTB> ld;
         strip_issue<CTB>(a, g0 + b, pz, ld);
-        ctu_group<CTB, LUMA, false, MFMA32>(a, g0 + b, pz, sm, ld, [] {});
+        ctu_group<CTB, LUMA, false, MFMA32, 4>(a, g0 + b, pz, sm, ld, [] {});
         __syncthreads();
     }
 }
@@ -1081,11 +1090,9 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     a.dq_per = dq_per;
     const int64_t strips = (int64_t)a.strips_x * a.nrows;
     if (strips <= 0 || planes <= 0) return NH_OK;
-    if ((strips + 3) / 4 > INT32_MAX) return NH_EARG;
-    const int64_t groups = (strips + 3) / 4;
+    const int64_t groups = (strips + 3) / 4;   // k_ctu_wide's groups of 4 strips
     if (groups * planes > INT32_MAX) return NH_EARG;
-    const int items = (int)(groups * planes);
-    const dim3 grid((unsigned)groups, (unsigned)planes), grid_wide((unsigned)((groups + kWideGroups - 1) / kWideGroups), (unsigned)planes);
+    const dim3 grid_wide((unsigned)((groups + kWideGroups - 1) / kWideGroups), (unsigned)planes);
     // Narrow groups (8-bit content) are coded by k_ctu_open with the packed
     // chain, their 32x32 TUs on the f16 matrix cores (rocprof: 428.5 vs 459.9
     // us per 16 luma planes for the packed butterflies); the
@@ -1102,11 +1109,19 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // 27 KB of LDS per workgroup with the 4 KB bases.
     a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
     a.probe = NH_KNOB("NH_CTU_PROBE", 0);
-    // Occupancy caps: fewer resident workgroups run these
-    // kernels faster -- 3 per CU for luma (CTB 32), 4 for chroma.  A/B build:
-    // NH_OCC_CAP = 0 leaves them uncapped.
-    const int cap_wgs = ctb == 32 ? 3 : 4;
-    auto launch_open = [&](auto kern) -> int {
+    // Group size GS (strips pooled per workgroup of 64 GS threads) and the
+    // occupancy cap (resident workgroups per CU, lds_cap).
+    // A/B build: NH_CTU_GS = 4 / 6 / 8, NH_CTU_CAP = workgroups per CU,
+    // NH_OCC_CAP = 0 uncapped.
+    static const int gs_knob = NH_KNOB("NH_CTU_GS", 4), cap_knob = NH_KNOB("NH_CTU_CAP", 0);
+    auto launch_open = [&](auto kern, auto gs_c) -> int {
+        constexpr int GSZ = decltype(gs_c)::value;
+        const int64_t ngrp = (strips + GSZ - 1) / GSZ;
+        if (ngrp * planes > INT32_MAX) return NH_EARG;
+        const int items = (int)(ngrp * planes);
+        const dim3 grid((unsigned)ngrp, (unsigned)planes);
+        const int cap_wgs = cap_knob > 0 ? cap_knob
+                          : ctb == 32 ? (GSZ == 4 ? 3 : 2) : (GSZ == 4 ? 4 : GSZ == 6 ? 3 : 2);
         if (NH_AB != 0 && persist) {
             static int cus = 0;
             if (!cus) {
@@ -1116,11 +1131,11 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
             }
             int per_cu = 0;
             const unsigned pad = lds_cap(kern, cap_wgs);
-            NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, pad));
+            NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * GSZ, pad));
             const int res = std::max(1, cus * per_cu);
-            kern<<<dim3((unsigned)std::min(items, res), 1), 256, pad, s>>>(a, items);
+            kern<<<dim3((unsigned)std::min(items, res), 1), 64 * GSZ, pad, s>>>(a, items);
         } else {
-            kern<<<grid, 256, lds_cap(kern, cap_wgs), s>>>(a, items);
+            kern<<<grid, 64 * GSZ, lds_cap(kern, cap_wgs), s>>>(a, items);
         }
         return NH_OK;
     };
@@ -1130,18 +1145,23 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         constexpr bool L = decltype(luma_c)::value;
         constexpr bool M32 = C == 32 && L;
         int rc3;
+        using G4 = std::integral_constant<int, 4>;
         if constexpr (NH_AB != 0) {
             const bool m = M32 && t32 != 0;
-            if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>)
-                         : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>)
-                                        : launch_open(k_ctu_open<C, L, M32, 0>);
-            else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>)
-                       : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>)
-                                      : launch_open(k_ctu_open<C, L, false, 0>);
+            if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>, G4{})
+                         : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>, G4{})
+                         : gs_knob == 6 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 6>, std::integral_constant<int, 6>{})
+                         : gs_knob == 8 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 8>, std::integral_constant<int, 8>{})
+                                        : launch_open(k_ctu_open<C, L, M32, 0>, G4{});
+            else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>, G4{})
+                       : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>, G4{})
+                       : gs_knob == 6 ? launch_open(k_ctu_open<C, L, false, 0, 5, 6>, std::integral_constant<int, 6>{})
+                       : gs_knob == 8 ? launch_open(k_ctu_open<C, L, false, 0, 5, 8>, std::integral_constant<int, 8>{})
+                                      : launch_open(k_ctu_open<C, L, false, 0>, G4{});
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else {
-            rc3 = launch_open(k_ctu_open<C, L, M32, 0, 5>);
+            rc3 = launch_open(k_ctu_open<C, L, M32, 0, 5, 4>, G4{});
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         }
         return rc3;
