@@ -1206,11 +1206,16 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     a.dq_per = dq_per;
     const int nblk = a.strips_x * a.nrows, planes = S.planes_per_group * S.num_groups;
     if (!nblk || !planes) return NH_OK;
-    constexpr int K = 1;
     // capped at 3 resident workgroups per CU: 0.137 vs 0.153 ms per 8K YUV420 frame
-    // uncapped (5 per CU; 2 per CU: 0.164), DESIGN.md §4.5
-    k_tc32_h<K><<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(k_tc32_h<K>, 3), s>>>(
-        a, nblk);
+    // uncapped (5 per CU; 2 per CU: 0.164), DESIGN.md §4.5.  A/B build:
+    // NH_TC32H_K = blocks per wave (2 / 4), NH_TC32H_CAP = workgroups per CU.
+    static const int kk = NH_KNOB("NH_TC32H_K", 1), cap = NH_KNOB("NH_TC32H_CAP", 3);
+    auto launch = [&](auto kern, int K) {
+        kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, cap), s>>>(a, nblk);
+    };
+    if (NH_AB && kk == 2) launch(k_tc32_h<2>, 2);
+    else if (NH_AB && kk == 4) launch(k_tc32_h<4>, 4);
+    else launch(k_tc32_h<1>, 1);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
