@@ -56,15 +56,20 @@ inline unsigned lds_cap(K kern, int wgs) {
     static int used = 0;
     static std::mutex mu;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipGetDevice(&dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
     std::lock_guard<std::mutex> g(mu);
     for (int i = 0; i < used; ++i)
         if (cache[i].k == (const void*)kern && cache[i].wgs == wgs && cache[i].dev == dev) return cache[i].pad;
     int lds_cu = 0;
     hipFuncAttributes fa{};
     if (hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
-        hipFuncGetAttributes(&fa, (const void*)kern) != hipSuccess)
+        hipFuncGetAttributes(&fa, (const void*)kern) != hipSuccess) {
+        (void)hipGetLastError();   // uncapped; keep the failed query out of the launch's error check
         return 0;
+    }
     const long need = (long)lds_cu / (wgs + 1) + 1 - (long)fa.sharedSizeBytes;   // wgs + 1 must not fit
     const unsigned pad = need > 0 ? (unsigned)need : 0u;
     if (used < 32) cache[used++] = Entry{(const void*)kern, wgs, dev, pad};
