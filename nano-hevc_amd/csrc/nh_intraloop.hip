@@ -2279,9 +2279,16 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
     unsigned long long* sse = (unsigned long long*)d_sse;
     if (form == 0) {   // the packed-chain-only launch (3 waves/SIMD), then the fallback for groups with wide blocks
         // A/B build: NH_CAP_RDO = resident workgroups per CU (LDS reservation, lds_cap)
-        static const int cap_rdo = NH_KNOB("NH_CAP_RDO", 0);
+        static const int cap_rdo = NH_KNOB("NH_CAP_RDO", 0), w4 = NH_KNOB("NH_RDO_W4", 0);
+#if NH_AB   // A/B: the packed-only kernel capped at 128 VGPRs (4 waves/SIMD, 19 spilled)
+        if (w4)
+            k_intra_rdo8<4, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<4, true, 1>, cap_rdo), s>>>(
+                d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups);
+        else
+#endif
         k_intra_rdo8<1, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
             d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups);
+        (void)w4;
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
                                                         d_recon, sse, ngroups);
     }
