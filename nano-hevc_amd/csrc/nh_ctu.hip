@@ -88,13 +88,18 @@ __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 __device__ __forceinline__ void st_lvl4(int32_t* p, int4 v) { *(int4*)p = v; }
 __device__ __forceinline__ void st_rec4(int16_t* p, uint2 v) { *(uint2*)p = v; }
 
-// The lane id as an opaque value: lane-derived addresses and constants of a
-// chain are then computed inside each batch, not hoisted out of the batch loop
-// and held live across it (which multiplied the register pressure by the
-// number of chain kinds in the loop).
+// The lane id.  With NH_OPAQUE_LANE (A/B builds) it is opaque to the compiler
+// (an empty asm), so lane-derived addresses and constants of a chain are
+// recomputed inside each batch instead of hoisted out of the batch loop: 76
+// instead of 129 VGPRs for the luma kernel.  Since the kernels are capped at 3-4
+// resident waves per SIMD (lds_cap) the registers are free, and hoisting saves
+// VALU: 37.2 vs 38.1 us per 4K YUV420 frame, config 5 0.129 vs 0.138 ms per 8K
+// frame.
 __device__ __forceinline__ int opaque_lane() {
     int l = threadIdx.x & 63;
+#ifdef NH_OPAQUE_LANE
     asm volatile("" : "+v"(l));
+#endif
     return l;
 }
 
@@ -1152,16 +1157,17 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
                          : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>, G4{})
                          : gs_knob == 6 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 6>, std::integral_constant<int, 6>{})
                          : gs_knob == 8 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 8>, std::integral_constant<int, 8>{})
-                                        : launch_open(k_ctu_open<C, L, M32, 0>, G4{});
+                                        : launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4>, G4{});
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>, G4{})
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>, G4{})
                        : gs_knob == 6 ? launch_open(k_ctu_open<C, L, false, 0, 5, 6>, std::integral_constant<int, 6>{})
                        : gs_knob == 8 ? launch_open(k_ctu_open<C, L, false, 0, 5, 8>, std::integral_constant<int, 8>{})
-                                      : launch_open(k_ctu_open<C, L, false, 0>, G4{});
+                                      : launch_open(k_ctu_open<C, L, false, 0, C == 32 ? 3 : 4, 4>, G4{});
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else {
-            rc3 = launch_open(k_ctu_open<C, L, M32, 0, 5, 4>, G4{});
+            // register budget = the occupancy the cap allows (3 / 4 waves per SIMD)
+            rc3 = launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4>, G4{});
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         }
         return rc3;
