@@ -1675,7 +1675,9 @@ __device__ __forceinline__ void tu_closed_batch(const Closed4Args& a, const int1
 // Same results as tu_closed_batch on such input.
 __device__ __forceinline__ int opaque_lane64() {
     int l = threadIdx.x & 63;
+#ifndef NH_PLAIN_LANE64   // A/B builds: -DNH_PLAIN_LANE64 lets the compiler hoist lane-derived values
     asm volatile("" : "+v"(l));
+#endif
     return l;
 }
 template <int N, bool DST>
