@@ -502,12 +502,21 @@ __device__ __forceinline__ h8_t ld_crow_h8(const uint16_t* row, int s, int hh) {
 __device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
 }
+// Where the rounding bias enters: kBiasInit = the accumulators start at it
+// (16 more live registers per pass, no adds), else it is added before floor().
+#ifdef NH_ACC_INIT_BIAS
+constexpr bool kBiasInit = true;
+#else
+constexpr bool kBiasInit = false;
+#endif
+__device__ __forceinline__ float addb(float x, float b) { if constexpr (kBiasInit) return x; else return x + b; }
+__device__ __forceinline__ float initb(float b) { if constexpr (kBiasInit) return b; else return 0.0f; }
 __device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s, float b) {   // registers 8s .. 8s+7 + b, floored, as f16
     uint4 u;
-    u.x = pk_floor_h(acc[8 * s + 0] + b, acc[8 * s + 1] + b);
-    u.y = pk_floor_h(acc[8 * s + 2] + b, acc[8 * s + 3] + b);
-    u.z = pk_floor_h(acc[8 * s + 4] + b, acc[8 * s + 5] + b);
-    u.w = pk_floor_h(acc[8 * s + 6] + b, acc[8 * s + 7] + b);
+    u.x = pk_floor_h(addb(acc[8 * s + 0], b), addb(acc[8 * s + 1], b));
+    u.y = pk_floor_h(addb(acc[8 * s + 2], b), addb(acc[8 * s + 3], b));
+    u.z = pk_floor_h(addb(acc[8 * s + 4], b), addb(acc[8 * s + 5], b));
+    u.w = pk_floor_h(addb(acc[8 * s + 6], b), addb(acc[8 * s + 7], b));
     return __builtin_bit_cast(h8_t, u);
 }
 __device__ __forceinline__ f16x_t splat16(float v) {
@@ -567,13 +576,13 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x]; the 1536 offset removed with the rounding bias
     // b1 (row 0 only: every other DCT32 row sums to 0)
     const float b1 = r == 0 ? 0.5f - 3072.0f : 0.5f;
-    f16x_t acc = splat16(0.0f);
+    f16x_t acc = splat16(initb(b1));
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
                                                  ld_h8(&bs.t[r][8 * hh]), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
                                                  ld_h8(&bs.t[r][16 + 8 * hh]), acc, 0, 0, 0);
     // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
-    f16x_t acc2 = splat16(0.0f);
+    f16x_t acc2 = splat16(initb(0.5f));
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 0, hh), acc_h8(acc, 0, b1), acc2, 0, 0, 0);
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 1, hh), acc_h8(acc, 1, b1), acc2, 0, 0, 0);
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
@@ -584,20 +593,20 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int g = 4 * q + e;
-            L4[e] = quant_s((int32_t)__builtin_floorf(acc2[g] + 0.5f), cq.qs, cq.h_v, cq.hneg_v);
+            L4[e] = quant_s((int32_t)__builtin_floorf(addb(acc2[g], 0.5f)), cq.qs, cq.h_v, cq.hneg_v);
             qt[crow(g, hh) * QH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
         }
         st_lvl4(lrow + 8 * q + 4 * hh, make_int4(L4[0], L4[1], L4[2], L4[3]));
     }
     wave_sync();
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
-    f16x_t acc3 = splat16(0.0f);
+    f16x_t acc3 = splat16(initb(0.5f));
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.tt[r][8 * hh]), acc3,
                                                   0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 16 + 8 * hh),
                                                   ld_h8(&bs.tt[r][16 + 8 * hh]), acc3, 0, 0, 0);
     // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
-    f16x_t acc4 = splat16(0.0f);
+    f16x_t acc4 = splat16(initb(0.5f));
     acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 0, hh), acc_h8(acc3, 0, 0.5f), acc4, 0, 0, 0);
     acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 1, hh), acc_h8(acc3, 1, 0.5f), acc4, 0, 0, 0);
     // reconstruct + clip (intra.py:70-78), row y = r
@@ -610,7 +619,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             const int x = 8 * q + 4 * hh + e;
             const int32_t p = use_dc ? dc
                                      : ((31 - x) * leftr + (x + 1) * tr + (31 - r) * (int32_t)img[x] + (r + 1) * bl + 32) >> 6;
-            const int32_t v = p + (int32_t)__builtin_floorf(acc4[4 * q + e] + 0.5f);
+            const int32_t v = p + (int32_t)__builtin_floorf(addb(acc4[4 * q + e], 0.5f));
             R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
         }
         st_rec4(rrow + 8 * q + 4 * hh,
