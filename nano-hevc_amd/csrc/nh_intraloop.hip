@@ -825,6 +825,12 @@ struct ClosedArgs {
     int32_t max_bh;                 // largest block-row count of any set
     int32_t probe;                  // A/B build only (NH_CLOSED_PROBE=1): skip the chain (wrong outputs); 0 otherwise
 };
+// The tagged closed-loop kernel's forms: both chains per block (0), the packed
+// chain only, for streams whose every source sample is 8-bit (1), both chains
+// for the other streams (2).  Forms 1 / 2 read the stream's wide flag
+// (work[2 + total_rows], set by k_closed_any_wide) and return at once unless it
+// names them; the packed-only form needs fewer registers.
+enum { kClosedBoth = 0, kClosedNarrow = 1, kClosedWide = 2 };
 constexpr int kSpinLimit = 1 << 20;   // ~1 s of polling; a legitimate wait is a few block steps
 
 __device__ __forceinline__ int ld_sys(const int32_t* p) {
@@ -1016,8 +1022,11 @@ __device__ __forceinline__ void closed_ticket(const ClosedArgs& a, int t, int& s
     pl = (int)r;
 }
 
-template <int WAVES>
+template <int WAVES, int FORM = kClosedBoth>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8_closed_tag(ClosedArgs a) {
+    if constexpr (FORM != kClosedBoth) {
+        if ((__builtin_nontemporal_load(&a.work[2 + a.total_rows]) != 0) != (FORM == kClosedWide)) return;
+    }
     __shared__ RdoSlotLds L;
     __shared__ uint32_t refs[64][kRefStride];
     __shared__ uint32_t outP[32], outL[32];   // the winner's recon / level pairs, row-major
@@ -1111,7 +1120,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             } else
 #endif
             if (lane < kModes) {
-                key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
+                key = (rdo8_chain<FORM == kClosedNarrow>(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
             }
             unsigned long long best = key;
             for (int m = 32; m > 0; m >>= 1) {
@@ -2413,7 +2422,7 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
 // (the closed-loop stream then takes the 32-bit chain).
 __global__ void __launch_bounds__(256) k_closed_any_wide(const int16_t* __restrict__ src, int64_t group_stride,
                                                          int64_t plane_stride, int ppg, int w, int h, int pitch,
-                                                         int32_t* work) {
+                                                         int32_t* flag) {
     const int pz = blockIdx.y, gz = pz / ppg, cz = pz - gz * ppg;
     const int16_t* p = src + (int64_t)gz * group_stride + (int64_t)cz * plane_stride;
     const int64_t n = (int64_t)w * h;
@@ -2422,7 +2431,7 @@ __global__ void __launch_bounds__(256) k_closed_any_wide(const int16_t* __restri
         const int yy = (int)(i / w), xx = (int)(i - (int64_t)yy * w);
         bits |= (uint16_t)p[(int64_t)yy * pitch + xx];
     }
-    if (__ballot((bits & 0xff00u) != 0) && (threadIdx.x & 63) == 0) atomicOr(&work[2], 1);
+    if (__ballot((bits & 0xff00u) != 0) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
 static int closed4_layout(const nh_plane_set* set, int ctb, int64_t& lines0, int64_t& lw, int64_t& nplanes) {
@@ -2501,7 +2510,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         const unsigned gx = (unsigned)std::min<int64_t>(256, (n + 255 * 8) / (256 * 8));
         k_closed_any_wide<<<dim3(gx, (unsigned)np), 256, 0, s>>>(d_src + set->base, set->group_stride, set->plane_stride,
                                                               set->planes_per_group, set->width, set->height,
-                                                              set->pitch, (int32_t*)d_work);
+                                                              set->pitch, (int32_t*)d_work + 2);
     } else {
         NH_HIP(hipMemsetAsync((int32_t*)d_work + 2, 0xff, 4, s));
     }
@@ -2585,7 +2594,8 @@ static int closed_layout(const nh_plane_set* sets, int nsets, ClosedArgs& a, int
     }
     a.nsets = nsets;
     a.total_rows = (int32_t)rows;
-    a.lines0 = (2 + rows + 1) & ~1ll;   // 8-B aligned: the tagged form's 64-bit line words
+    a.lines0 = (2 + rows + 2) & ~1ll;   // 8-B aligned: the tagged form's 64-bit line words; word 2 + rows:
+                                        // the stream's wide flag (k_closed_any_wide)
     a.lines_total = lines;
     modes_total = modes;
     return NH_OK;
@@ -2652,12 +2662,38 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
                 else k_intra_rdo8_closed_pair<2><<<waves, 128, 0, s>>>(a);
             } else if (cw == 2) {
                 k_intra_rdo8_closed_tag<2><<<waves, 64, 0, s>>>(a);
+            } else if (cf == 3) {   // A/B: one kernel, either chain per block (round 1)
+                k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
             } else
 #endif
             {
                 (void)cf;
                 (void)cw;
-                k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
+                // the stream's wide flag, then the packed-only form (codes the stream iff every source
+                // sample is 8-bit: every neighbour is then too, the reconstruction being clipped) and the
+                // both-chains form (codes it otherwise); A/B build: NH_CLOSED_FORM = 3, one kernel
+                int32_t* flag = (int32_t*)d_work + 2 + a.total_rows;
+                for (int k = 0; k < nsets; ++k) {
+                    const nh_plane_set& p = sets[k];
+                    const int64_t np = (int64_t)p.planes_per_group * p.num_groups, n = (int64_t)p.width * p.height;
+                    if (np <= 0 || n <= 0) continue;
+                    const unsigned gx = (unsigned)std::min<int64_t>(256, (n + 255 * 8) / (256 * 8));
+                    k_closed_any_wide<<<dim3(gx, (unsigned)np), 256, 0, s>>>(d_src + p.base, p.group_stride,
+                                                                          p.plane_stride, p.planes_per_group, p.width,
+                                                                          p.height, p.pitch, flag);
+                }
+                static int cus = 0, per_cu = 0;
+                if (!cus) {
+                    int dev = 0;
+                    NH_HIP(hipGetDevice(&dev));
+                    NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+                    NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_intra_rdo8_closed_tag<1, kClosedNarrow>,
+                                                                        64, 0));
+                }
+                const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
+                k_intra_rdo8_closed_tag<1, kClosedNarrow>
+                    <<<(unsigned)(a.total_rows < cap_n ? a.total_rows : cap_n), 64, 0, s>>>(a);
+                k_intra_rdo8_closed_tag<1, kClosedWide><<<waves, 64, 0, s>>>(a);
             }
         }
     }
