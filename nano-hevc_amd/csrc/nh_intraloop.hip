@@ -2691,6 +2691,14 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
                                                                         64, 0));
                 }
                 const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
+#if NH_AB   // A/B: NH_CLOSED_W3 = 1 the packed-only form capped at 168 VGPRs (3 waves/SIMD, 33 spilled)
+                static const int w3 = NH_KNOB("NH_CLOSED_W3", 0);
+                if (w3) {
+                    const int64_t cap3 = 3ll * 4 * cus;
+                    k_intra_rdo8_closed_tag<3, kClosedNarrow>
+                        <<<(unsigned)(a.total_rows < cap3 ? a.total_rows : cap3), 64, 0, s>>>(a);
+                } else
+#endif
                 k_intra_rdo8_closed_tag<1, kClosedNarrow>
                     <<<(unsigned)(a.total_rows < cap_n ? a.total_rows : cap_n), 64, 0, s>>>(a);
                 k_intra_rdo8_closed_tag<1, kClosedWide><<<waves, 64, 0, s>>>(a);
