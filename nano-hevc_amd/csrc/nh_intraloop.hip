@@ -2532,8 +2532,11 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
 #endif
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
         const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
-        static const int wpc = NH_KNOB("NH_CLOSED4_WPC", 0);   // A/B build: resident waves per CU
-        const int64_t cap_n = (int64_t)(wpc > 0 ? wpc : std::max(1, per_cu)) * cus;
+        // A/B build: resident waves per CU, for both sets or per luma / chroma set
+        static const int wpc = NH_KNOB("NH_CLOSED4_WPC", 0), wpc_l = NH_KNOB("NH_CLOSED4_WPC_L", 0),
+                         wpc_c = NH_KNOB("NH_CLOSED4_WPC_C", 0);
+        const int wsel = is_luma ? (wpc_l > 0 ? wpc_l : wpc) : (wpc_c > 0 ? wpc_c : wpc);
+        const int64_t cap_n = (int64_t)(wsel > 0 ? wsel : std::max(1, per_cu)) * cus;
         kern<<<(unsigned)(prow < cap_n ? prow : cap_n), 64, 0, s>>>(a);
     } else if (narrow_ok) {
         int per_cu = 0;
