@@ -21,8 +21,8 @@ scaling.
 
 --config 4 (BASELINE.json configs[3]): 4K YUV420 frames, mixed 4/8/16/32 TUs
 per 32x32 CTU, CTU-row bands per rank as above; every rank
-holds the whole synthetic input stream (a TU reads the source row above its
-band, block.py:38-50) and reconstructs only its bands.
+synthesises and holds only its bands plus the one source row above each band
+(all a TU reads, block.py:38-50; shard.Cfg4Layout) and reconstructs them.
 
 N > 1, both configs: after the compute-only phase, a gather-inclusive phase
 runs the path's one exchange step -- an RCCL gather to rank 0 (config 2: a
@@ -124,12 +124,14 @@ def launch_or_check(args, argv):
     return None
 
 
-def init_dist(world):
-    """Process group for world > 1 (RCCL, one GPU per rank).  NH_DIST_BACKEND /
+def init_dist(world, force_group=False):
+    """Process group for world > 1 (RCCL, one GPU per rank); ``force_group``
+    also builds one at world 1 (tests/rccl_world1.py: the RCCL branch and the
+    device-tensor gather executed on a one-GPU box).  NH_DIST_BACKEND /
     NH_FORCE_DEVICE are rehearsal knobs of this script only (e.g. 2 gloo ranks
     sharing the one GPU of a test box)."""
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1:
+    if world == 1 and not force_group:
         torch.cuda.set_device(0)
         return None
     import torch.distributed as dist
@@ -378,36 +380,117 @@ def run_cfg2(args, dist, world, rank, dev):
 # ---------------------------------------------------------------------------
 # config 4: mixed 4/8/16/32 TUs per CTU, CTU-row bands, uint8 recon gather
 # ---------------------------------------------------------------------------
+def synth_rows(f, c, r0, r1, pw, seed, dev):
+    """Rows [r0, r1) of plane c (0 Y, 1 U, 2 V) of synthetic frame f: 8-bit
+    natural-ish content (gradient + hashed noise in [-15, 15]).  A pure function
+    of (seed, f, c, y, x), so a rank synthesises exactly the rows it holds and
+    every rank agrees on every sample."""
+    yy = torch.arange(r0, r1, device=dev, dtype=torch.int64).view(-1, 1)
+    xx = torch.arange(pw, device=dev, dtype=torch.int64).view(1, -1)
+    base = (50 + (3 * xx + 2 * yy + 13 * f) % 150 + (xx // 97) * 5) % 256
+    m = 0xFFFFFFFF
+    h = ((xx * 0x9E3779B1) ^ (yy * 0x85EBCA77) ^ ((3 * f + c + 1) * 0xC2B2AE3D) ^ ((seed * 0x27D4EB2F) & m)) & m
+    h = h ^ (h >> 15)
+    h = (h * 0x2C1B3C6D) & m
+    h = h ^ (h >> 12)
+    h = (h * 0x297A2D39) & m
+    h = h ^ (h >> 15)
+    return torch.clamp(base + h % 31 - 15, 0, 255).to(torch.int16)
+
+
 def synth_stream(nf, w, h, seed, dev):
-    """8-bit natural-ish content (gradient + seeded noise), identical on every rank."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(seed)
+    """The whole synthetic stream (frames [Y][U][V] back to back): what every
+    rank's bands are cut from (used by --check and the tests, not by the ranks)."""
     parts = []
     for f in range(nf):
-        for pw, ph in ((w, h), (w // 2, h // 2), (w // 2, h // 2)):
-            yy = torch.arange(ph, device=dev).view(ph, 1)
-            xx = torch.arange(pw, device=dev).view(1, pw)
-            base = (50 + (3 * xx + 2 * yy + 13 * f) % 150 + (xx // 97) * 5) % 256
-            noise = torch.randint(-15, 16, (ph, pw), device=dev, generator=g)
-            parts.append(torch.clamp(base + noise, 0, 255).to(torch.int16).reshape(-1))
+        for c, (pw, ph) in enumerate(((w, h), (w // 2, h // 2), (w // 2, h // 2))):
+            parts.append(synth_rows(f, c, 0, ph, pw, seed, dev).reshape(-1))
     return torch.cat(parts)
 
 
-def band_views(stream, rank, world, frames, width, height):
-    """This rank's reconstructed bands as strided views: per band, the Y / U / V
-    rows of the frames f0, f0 + world, ... (one view per plane)."""
+class Cfg4Rank:
+    """One rank's share of config 4 (shard.Cfg4Layout): a local buffer holding
+    only its bands' rows plus one source row above each band (block.py:38-50 is
+    all a TU reads), lvl / recon in the same layout, one luma and one chroma
+    plane set per band (rows of the full plane, so the CTU grid, the seeded
+    quadtree and the frame-border rule are the unsharded ones), and the packing
+    of its reconstructed bands for the gather."""
+
+    def __init__(self, rank, world, frames, width, height, dev, seed):
+        from nano_hevc import gpu, shard
+        self.gpu, self.dev, self.seed = gpu, dev, seed
+        self.lay = shard.cfg4_layout(rank, world, frames, width, height)
+        W, H = width, height
+        self.work = []
+        for b in self.lay.bands:
+            r0, r1 = b.ctu_rows()
+            tuy = torch.zeros((b.cnt, H // 4, W // 4), dtype=torch.uint8, device=dev)
+            tuc = torch.zeros((2 * b.cnt, H // 8, W // 8), dtype=torch.uint8, device=dev)
+            self.work.append((self.lay.luma_set(gpu, b), self.lay.chroma_set(gpu, b), r0, r1, tuy, tuc))
+        self.total = self.lay.total_elems
+        self.packed_elems = self.lay.packed_elems()
+
+    def synth_source(self):
+        """The rank's local source buffer, synthesised row range by row range."""
+        lay, W = self.lay, self.lay.width
+        src = torch.empty(max(1, self.total), dtype=torch.int16, device=self.dev)
+        for b in lay.bands:
+            for j in range(b.cnt):
+                f = b.f0 + j * lay.world
+                o = b.off + j * b.slot_elems
+                pieces = ((0, b.y0 - b.hy, b.y1, W, 0), (1, b.c0 - b.hc, b.c1, W // 2, b.u_off),
+                          (2, b.c0 - b.hc, b.c1, W // 2, b.u_off + b.chroma_elems))
+                for c, r0, r1, pw, po in pieces:
+                    n = (r1 - r0) * pw
+                    src[o + po:o + po + n] = synth_rows(f, c, r0, r1, pw, self.seed, self.dev).reshape(-1)
+        return src
+
+    def fill_source(self, stream):
+        src = torch.zeros(max(1, self.total), dtype=torch.int16, device=self.dev)
+        return self.lay.fill_from_stream(stream, src)
+
+    def new_lvl(self):
+        return torch.zeros(max(1, self.total), dtype=torch.int32, device=self.dev)
+
+    def new_rec(self):
+        return torch.zeros(max(1, self.total), dtype=torch.int16, device=self.dev)
+
+    def run(self, src, qp, lvl, rec, stream):
+        for sy, suv, r0, r1, tuy, tuc in self.work:
+            self.gpu.tu_pipeline_planes(src, sy, 32, 0, self.seed, qp, True, r0, r1, lvl=lvl, rec=rec, tu=tuy,
+                                        stream=stream)
+            self.gpu.tu_pipeline_planes(src, suv, 16, 1, self.seed, qp, False, r0, r1, lvl=lvl, rec=rec, tu=tuc,
+                                        stream=stream)
+
+    def send_of(self, rec, packed):
+        """Pack + narrow the reconstructed band rows (values in [0, 255]) into ``packed``."""
+        o = 0
+        for v in self.lay.local_views(rec):
+            n = v.numel()
+            packed[o:o + n].view(v.shape).copy_(v)
+            o += n
+        return packed
+
+    def tu_counts(self):
+        """TUs per size coded per step, from the TU maps (one byte per 4x4 unit =
+        log2 of its TU's size; bit 7 marks a group recoded by the wide kernel)."""
+        units = [0, 0, 0, 0]
+        for *_, tuy, tuc in self.work:
+            for m in (tuy, tuc):
+                cnt = torch.bincount((m & 0x7F).reshape(-1).to(torch.int64), minlength=6)
+                for k in range(4):
+                    units[k] += int(cnt[k + 2])
+        return [units[k] // (1 << (2 * k)) for k in range(4)]   # a TU of (4*2^k)^2 samples = 4^k units
+
+
+def unpack_to_stream(packed, rank, world, frames, width, height, stream):
+    """Rank ``rank``'s gathered bands (Cfg4Rank.send_of order) into a full stream."""
     from nano_hevc import shard
-    fe = width * height + 2 * (width // 2) * (height // 2)
-    cw, ch = width // 2, height // 2
-    out = []
-    for b, f0, cnt in shard.cfg4_plan(rank, world, frames):
-        y0, y1 = shard.ctu_bands(height, world)[b]
-        c0, c1 = y0 // 2, y1 // 2
-        for off, n in ((width * y0, width * (y1 - y0)), (width * height + cw * c0, cw * (c1 - c0)),
-                       (width * height + cw * ch + cw * c0, cw * (c1 - c0))):
-            if n:
-                out.append(stream.as_strided((cnt, n), (world * fe, 1), f0 * fe + off))
-    return out
+    o = 0
+    for v in shard.cfg4_layout(rank, world, frames, width, height).full_views(stream):
+        v.copy_(packed[o:o + v.numel()].view(v.shape))
+        o += v.numel()
+    return o
 
 
 def run_cfg4(args, dist, world, rank, dev):
@@ -417,62 +500,28 @@ def run_cfg4(args, dist, world, rank, dev):
     cw, ch = W // 2, H // 2
     fe = gpu.yuv420_frame_elems(W, H)
     nf = args.frames * world
-    src = synth_stream(nf, W, H, args.seed, dev)          # the whole input stream on every rank
-    lvl = torch.zeros(src.shape, dtype=torch.int32, device=dev)
-    recs = [torch.zeros(src.shape, dtype=torch.int16, device=dev)]
-    bands = shard.ctu_bands(H, world)
-    plan = shard.cfg4_plan(rank, world, nf)
-    work = []
-    for b, f0, cnt in plan:
-        y0, y1 = bands[b]
-        r0, r1 = y0 // 32, (y1 + 31) // 32
-        sy = gpu.plane_set(f0 * fe, W, H, W, 1, cnt, 0, world * fe)
-        suv = gpu.plane_set(f0 * fe + W * H, cw, ch, cw, 2, cnt, cw * ch, world * fe)
-        tuy = torch.zeros((cnt, H // 4, W // 4), dtype=torch.uint8, device=dev)
-        tuc = torch.zeros((2 * cnt, ch // 4, cw // 4), dtype=torch.uint8, device=dev)
-        work.append((sy, suv, r0, r1, tuy, tuc))
-    my_samples = shard.cfg4_packed_elems(rank, world, nf, W, H)
+    me = Cfg4Rank(rank, world, nf, W, H, dev, args.seed)
+    src = me.synth_source()          # only this rank's bands + one halo row each
+    lvl = me.new_lvl()
+    recs = [me.new_rec()]
     stream = torch.cuda.current_stream(dev)
 
     def step_into(slot):
-        for sy, suv, r0, r1, tuy, tuc in work:
-            gpu.tu_pipeline_planes(src, sy, 32, 0, args.seed, args.qp, True, r0, r1, lvl=lvl, rec=recs[slot], tu=tuy,
-                                   stream=stream)
-            gpu.tu_pipeline_planes(src, suv, 16, 1, args.seed, args.qp, False, r0, r1, lvl=lvl, rec=recs[slot],
-                                   tu=tuc, stream=stream)
+        me.run(src, args.qp, lvl, recs[slot], stream)
 
     elapsed, kern_ms = timed_steps(lambda: step_into(0), args.steps, args.warmup, dist, stream)
-    # TUs per size coded per step (blocks/s per TU size), from the TU maps
-    # (one byte per 4x4 unit = log2 of its TU's size; bit 7 marks a group recoded by the wide kernel)
-    tu_units = [0, 0, 0, 0]
-    for _, _, _, _, tuy, tuc in work:
-        for m in (tuy, tuc):
-            ls = (m & 0x7F).reshape(-1).to(torch.int64)
-            cnt = torch.bincount(ls, minlength=6)
-            for k in range(4):
-                tu_units[k] += int(cnt[k + 2])
-    tu_counts = [tu_units[k] // (1 << (2 * k)) for k in range(4)]   # a TU of 4*2^k samples square = 4^k units
-    (elapsed, kern_ms), sums = reduce_max_sum(dist, dev, (elapsed, kern_ms), [my_samples] + tu_counts)
+    my_samples = me.packed_elems
+    (elapsed, kern_ms), sums = reduce_max_sum(dist, dev, (elapsed, kern_ms), [my_samples] + me.tu_counts())
     samples_all, tu_all = sums[0], sums[1:]
     value = samples_all * args.steps / elapsed
 
     sizes = [shard.cfg4_packed_elems(r, world, nf, W, H) for r in range(world)]
     gather, check = None, None
     if dist and args.gather_steps > 0:
-        recs.append(torch.zeros_like(recs[0]))
+        recs.append(me.new_rec())
         packed = [torch.zeros(max(sizes), dtype=torch.uint8, device=dev) for _ in range(2)]
-        views = [band_views(r, rank, world, nf, W, H) for r in recs]
-
-        def send_of(slot):   # pack + narrow this rank's recon bands (values in [0, 255]) on the side stream
-            o = 0
-            for v in views[slot]:
-                n = v.numel()
-                packed[slot][o:o + n].view(v.shape).copy_(v)
-                o += n
-            return packed[slot]
-
         og = OverlappedGather(dist, dev, sizes, torch.uint8)
-        gt = run_phase_gather(step_into, send_of, og, args.gather_steps, dist, stream)
+        gt = run_phase_gather(step_into, lambda s: me.send_of(recs[s], packed[s]), og, args.gather_steps, dist, stream)
         (gt,), _ = reduce_max_sum(dist, dev, (gt,), ())
         into_root = sum(sizes[1:])
         gather = {"value": samples_all * args.gather_steps / gt, "unit": "samples/s", "steps": args.gather_steps,
@@ -483,18 +532,15 @@ def run_cfg4(args, dist, world, rank, dev):
                           "stream, gather(k) under compute(k+1)"}
         if args.check and rank == 0:   # reassemble the last gather and compare with an unsharded run
             torch.cuda.synchronize()
-            full = torch.zeros_like(recs[0])
+            full_src = synth_stream(nf, W, H, args.seed, dev)
+            full = torch.zeros_like(full_src)
             for r in range(world):
-                got = og.recv[r][:sizes[r]].to(dev)
-                o = 0
-                for v in band_views(full, r, world, nf, W, H):
-                    v.copy_(got[o:o + v.numel()].view(v.shape))
-                    o += v.numel()
-            ref_l = torch.zeros_like(lvl)
-            ref_r = torch.zeros_like(recs[0])
+                unpack_to_stream(og.recv[r][:sizes[r]].to(dev), r, world, nf, W, H, full)
+            ref_l = torch.zeros(full_src.shape, dtype=torch.int32, device=dev)
+            ref_r = torch.zeros_like(full_src)
             sy, suv = gpu.yuv420_plane_sets(nf, W, H)
-            gpu.tu_pipeline_planes(src, sy, 32, 0, args.seed, args.qp, True, lvl=ref_l, rec=ref_r)
-            gpu.tu_pipeline_planes(src, suv, 16, 1, args.seed, args.qp, False, lvl=ref_l, rec=ref_r)
+            gpu.tu_pipeline_planes(full_src, sy, 32, 0, args.seed, args.qp, True, lvl=ref_l, rec=ref_r)
+            gpu.tu_pipeline_planes(full_src, suv, 16, 1, args.seed, args.qp, False, lvl=ref_l, rec=ref_r)
             check = bool(torch.equal(full, ref_r))
 
     if rank != 0:
@@ -504,20 +550,16 @@ def run_cfg4(args, dist, world, rank, dev):
         "metric": METRIC_CFG4, "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "int32",
-        "data": "synthetic 8-bit 4K YUV420 frames (gradient + seeded noise, int16 samples), resident in HBM",
+        "data": "synthetic 8-bit 4K YUV420 frames (gradient + hashed noise, int16 samples), resident in HBM",
         "config": {"workload": "config 4: 4K YUV420, seeded 4/8/16/32 TU quadtree per 32x32 CTU (16x16 chroma), "
                                "open-loop DC/planar choice, full chain, QP %d" % args.qp,
                    "frames_per_gpu": args.frames, "frames_per_s": value / (W * H + 2 * cw * ch),
                    "samples_per_step_rank0": my_samples, "parallelism": f"ctu-band{world} (rotated)",
+                   "source_bytes_rank0": 2 * me.total, "source_bytes_stream": 2 * nf * fe,
+                   "source_fraction_rank0": me.total / (nf * fe),
                    "tu_blocks_per_step": {f"{4 << k}x{4 << k}": int(tu_all[k]) for k in range(4)},
                    "tu_blocks_per_s": {f"{4 << k}x{4 << k}": tu_all[k] * args.steps / elapsed for k in range(4)}},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(f"cfg4_4k_yuv420_f{args.frames}_n{world}"),
-                     "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower "
-                                     "bound for 8-B/lane row reads, <= 2x that if every request were 128 B), writes "
-                                     "exact; profiles/pmc_traffic.json",
-                     "bytes_per_sample": BYTES_PER_SAMPLE_CFG4,
-                     "kernel_ms_avg": kern_ms},
+        "roofline": cfg4_roofline(my_samples, kern_ms, args.frames, world),
         "cpu_baseline": None,
     }
     if gather:
@@ -525,36 +567,63 @@ def run_cfg4(args, dist, world, rank, dev):
     if check is not None:
         line["gathered_recon_equals_unsharded"] = check
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_cfg4(src, lvl, recs[0], args, fe)
+        line["cpu_baseline"] = cpu_baseline_cfg4(me, src, lvl, recs[0], args, fe)
     return line
 
 
-def cpu_baseline_cfg4(src, lvl, rec, args, fe):
-    """oracle tu_pipeline_plane (one thread) on whole frames of the same stream
-    until ~cpu_seconds; the GPU levels and recon of those frames checked bit-exact."""
+def cfg4_roofline(samples, kern_ms, frames, world):
+    """HBM view of the config-4 step (8 B/sample of algorithmic traffic)."""
+    achieved = samples * BYTES_PER_SAMPLE_CFG4 / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(f"cfg4_4k_yuv420_f{frames}_n{world}"),
+            "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower bound for "
+                            "8-B/lane row reads, <= 2x that if every request were 128 B), writes exact; "
+                            "profiles/pmc_traffic.json",
+            "bytes_per_sample": BYTES_PER_SAMPLE_CFG4, "kernel_ms_avg": kern_ms}
+
+
+def cpu_baseline_cfg4(me, src, lvl, rec, args, fe):
+    """oracle tu_pipeline_plane on whole frames of the same stream, first on one
+    thread, then CTU-row-banded over all of the job's host threads
+    (oh_tu_pipeline_plane_mt), each leg ~cpu_seconds/2; the GPU levels and
+    recon of every sampled frame are checked bit-exact.  N = 1 only: the rank's
+    one band is then the whole frame (slot = frame)."""
     from oracle import oracle as O   # checker + CPU baseline only
     O.lib()
+    b = me.lay.bands[0]
+    assert len(me.lay.bands) == 1 and b.slot_elems == fe and b.hy == 0
     W, H = W4K, H4K
     cw, ch = W // 2, H // 2
     planes = [(0, H, W, 32, 0, True), (W * H, ch, cw, 16, 1, False), (W * H + cw * ch, ch, cw, 16, 2, False)]
-    t_cpu, f, samples, exact = 0.0, 0, 0, True
-    while f < args.frames and (t_cpu < args.cpu_seconds or f == 0):
-        s = src[f * fe:(f + 1) * fe].cpu().numpy()
-        gl = lvl[f * fe:(f + 1) * fe].cpu().numpy()
-        gr = rec[f * fe:(f + 1) * fe].cpu().numpy()
-        for off, h, w, ctb, pid, luma in planes:
-            p = s[off:off + h * w].reshape(h, w)
-            t0 = time.perf_counter()
-            ol, orc, _ = O.tu_pipeline_plane(p, ctb, pid, args.seed, args.qp, luma)
-            t_cpu += time.perf_counter() - t0
-            samples += h * w
-            exact &= bool(np.array_equal(ol, gl[off:off + h * w].reshape(h, w)) and
-                          np.array_equal(orc, gr[off:off + h * w].reshape(h, w)))
-        f += 1
-    return {"value": samples / t_cpu, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": f"{f} whole 4K YUV420 frames ({samples} samples) through oracle/nh_oracle.c "
-                      f"oh_tu_pipeline_plane on 1 thread ({t_cpu:.1f} s)",
-            "cpu_model": cpu_model(), "gpu_outputs_bit_exact_on_sample": exact}
+    nthr = cpu_threads()
+    legs, exact = {}, True
+    for threads in (1, nthr):
+        t_cpu, f, samples = 0.0, 0, 0
+        while f < args.frames and (t_cpu < args.cpu_seconds / 2 or f == 0):
+            s = src[f * fe:(f + 1) * fe].cpu().numpy()
+            gl = lvl[f * fe:(f + 1) * fe].cpu().numpy()
+            gr = rec[f * fe:(f + 1) * fe].cpu().numpy()
+            for off, h, w, ctb, pid, luma in planes:
+                p = s[off:off + h * w].reshape(h, w)
+                t0 = time.perf_counter()
+                if threads == 1:
+                    ol, orc, _ = O.tu_pipeline_plane(p, ctb, pid, args.seed, args.qp, luma)
+                else:
+                    ol, orc, _ = O.tu_pipeline_plane_mt(p, ctb, pid, args.seed, args.qp, luma, threads)
+                t_cpu += time.perf_counter() - t0
+                samples += h * w
+                exact &= bool(np.array_equal(ol, gl[off:off + h * w].reshape(h, w)) and
+                              np.array_equal(orc, gr[off:off + h * w].reshape(h, w)))
+            f += 1
+        legs[threads] = (samples / t_cpu, f, samples, t_cpu)
+    v1, f1, s1, t1 = legs[1]
+    vn, fn, sn, tn = legs[nthr]
+    return {"value": vn, "unit": "samples/s", "cores": nthr, "kind": "port",
+            "sample": f"{fn} whole 4K YUV420 frames ({sn} samples) through oracle/nh_oracle.c "
+                      f"oh_tu_pipeline_plane_mt on {nthr} threads ({tn:.1f} s); single thread: {f1} frames, "
+                      f"{s1} samples, {t1:.1f} s",
+            "value_1thread": v1, "cpu_model": cpu_model(), "nproc_machine": os.cpu_count(),
+            "gpu_outputs_bit_exact_on_sample": exact}
 
 
 def launcher_selftest(world, rank):

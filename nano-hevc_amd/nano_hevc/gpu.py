@@ -110,6 +110,25 @@ def sets_fit(sets: Sequence[PlaneSet], numel: int, what: str):
             raise ValueError(f"{what}: a plane set reaches outside the buffer ({last} > {numel} elements)")
 
 
+def sets_fit_rows(sets: Sequence[PlaneSet], numel: int, row_lo: int, row_hi: int, what: str):
+    """Like sets_fit, for a launch that touches only rows [row_lo, row_hi) of each
+    plane (a band of CTU rows plus the source row above it): those rows must lie
+    inside the buffer; the set's base may then point before it (a band-local
+    buffer described as rows of the full plane, shard.Cfg4Layout)."""
+    for s in sets:
+        lo, hi = max(0, row_lo), min(s.height, row_hi)
+        if s.num_groups <= 0 or s.width <= 0 or hi <= lo:
+            continue
+        if s.plane_stride < 0 or s.group_stride < 0:
+            raise ValueError(f"{what}: negative plane strides")
+        first = s.base + lo * s.pitch
+        last = s.base + (s.num_groups - 1) * s.group_stride + (s.planes_per_group - 1) * s.plane_stride + \
+            (hi - 1) * s.pitch + s.width
+        if first < 0 or last > numel:
+            raise ValueError(f"{what}: rows [{lo}, {hi}) of a plane set reach outside the buffer "
+                             f"([{first}, {last}) vs {numel} elements)")
+
+
 def fwd8x8_quant(res, sets: Sequence[PlaneSet], qp: int = 32, is_intra: bool = True, out=None,
                  variant: int = DEFAULT_VARIANT, stream=None):
     """Forward 8x8 DCT (transform.py:154-196) + quantize_block (quant.py:126-137) on
@@ -280,12 +299,16 @@ def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_
 
 def tu_pipeline_planes(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,
                        row0: int = 0, row1: int = 1 << 30, lvl=None, rec=None, tu=None, stream=None):
-    """Config 4 over every plane of one plane set in one launch per TU size
-    (plane p = g*ppg + c gets plane id plane_id + c).  Returns (lvl int32,
-    recon int16 -- source layout --, tu uint8 (planes, h/4, w/4))."""
+    """Config 4 over every plane of one plane set in one launch (plane p =
+    g*ppg + c gets plane id plane_id + c), CTU rows [row0, row1).  ``lvl`` and
+    ``rec`` share the source's layout; the set may describe a band-local buffer
+    as rows of the full plane (shard.Cfg4Layout: only the band's rows and the
+    row above are read).  Returns (lvl int32, recon int16, tu uint8 (planes,
+    h/4, w/4), indexed by full-plane position))."""
     torch = _torch()
     _need(src, torch.int16, "tu_pipeline_planes(src)")
-    sets_fit([pset], src.numel(), "tu_pipeline_planes")
+    # the launch reads rows [row0*ctb - 1, row1*ctb) (its CTU rows + the source row above) and writes its CTU rows
+    sets_fit_rows([pset], src.numel(), int(row0) * ctb - 1, min(int(row1), 1 << 30) * ctb, "tu_pipeline_planes")
     planes = pset.planes_per_group * pset.num_groups
     if lvl is None:
         lvl = torch.zeros(src.shape, dtype=torch.int32, device=src.device)

@@ -160,10 +160,12 @@ def gather_to_root(local, layouts_total_elems: List[int], dist, group=None):
 
 
 # ---------------------------------------------------------------------------
-# Config 4 (mixed TUs): CTU-row bands of full frames.  The
-# TU chain reads the source row above its band (block.py:38-50), so every rank
-# holds the whole input stream and computes only its bands (rotation as
-# above); reconstructed bands are packed, gathered to rank 0 and unpacked.
+# Config 4 (mixed TUs): CTU-row bands of full frames.  A TU
+# reads the source row above it and the column to its left (block.py:38-50),
+# so a band needs its own rows plus ONE source row above it (the halo) and
+# nothing else.  Each rank holds only those rows (Cfg4Layout), computes its
+# bands (rotation as above), and its reconstructed bands are packed, gathered
+# to rank 0 and unpacked.
 # ---------------------------------------------------------------------------
 
 def cfg4_plan(rank: int, world: int, frames: int) -> List[Tuple[int, int, int]]:
@@ -178,49 +180,155 @@ def cfg4_plan(rank: int, world: int, frames: int) -> List[Tuple[int, int, int]]:
     return plan
 
 
-def _band_views(stream, f: int, y0: int, y1: int, width: int, height: int):
-    """Flat slices [Y rows y0..y1, U rows y0/2..y1/2, V rows ...] of frame f."""
-    cw, ch = width // 2, height // 2
-    fe = width * height + 2 * cw * ch
-    base = f * fe
-    c0, c1 = y0 // 2, y1 // 2
-    u = base + width * height
-    v = u + cw * ch
-    return [stream[base + width * y0:base + width * y1], stream[u + cw * c0:u + cw * c1],
-            stream[v + cw * c0:v + cw * c1]]
+@dataclass
+class Cfg4Band:
+    """One band of one rank in its local buffer: ``cnt`` frame slots (frames f0,
+    f0 + world, ...) of ``slot_elems`` elements each, a slot holding the band's
+    Y rows [y0 - hy, y1), then U and V rows [c0 - hc, c1) (hy / hc = 1: the
+    halo row above the band, 0 for the top band)."""
+    band: int
+    f0: int
+    cnt: int
+    y0: int
+    y1: int
+    hy: int
+    hc: int
+    off: int            # local element offset of the band's first slot
+    slot_elems: int
+    u_off: int          # offset of the U rows inside a slot (V follows at u_off + chroma_elems)
+    chroma_elems: int   # elements of one chroma plane's rows in a slot (halo included)
+
+    @property
+    def c0(self):
+        return self.y0 // 2
+
+    @property
+    def c1(self):
+        return self.y1 // 2
+
+    def ctu_rows(self, ctu: int = CTU_LUMA) -> Tuple[int, int]:
+        """CTU rows [r0, r1) of the band (luma CTB 32 and chroma CTB 16 number
+        the same rows in 4:2:0)."""
+        return self.y0 // ctu, (self.y1 + ctu - 1) // ctu
+
+
+@dataclass
+class Cfg4Layout:
+    """A rank's local config-4 buffer: its bands, nothing else of the stream."""
+    width: int
+    height: int
+    world: int
+    rank: int
+    frames: int
+    bands: List[Cfg4Band]
+    total_elems: int
+
+    def luma_set(self, gpu, b: Cfg4Band):
+        """nh_plane_set of the band's Y planes as rows of the FULL plane: the base
+        is the element where full-plane row 0 would sit (negative offsets are
+        fine: the kernels touch rows [y0 - 1, y1) only; gpu.tu_pipeline_planes
+        checks exactly those rows against the buffer)."""
+        w = self.width
+        return gpu.plane_set(b.off - (b.y0 - b.hy) * w, w, self.height, w, 1, b.cnt, 0, b.slot_elems)
+
+    def chroma_set(self, gpu, b: Cfg4Band):
+        cw = self.width // 2
+        return gpu.plane_set(b.off + b.u_off - (b.c0 - b.hc) * cw, cw, self.height // 2, cw, 2, b.cnt,
+                             b.chroma_elems, b.slot_elems)
+
+    def local_views(self, local):
+        """The band rows (halo excluded) of a local-layout tensor, as (cnt, n)
+        strided views: per band, Y then U then V (the order of full_views)."""
+        out = []
+        w, cw = self.width, self.width // 2
+        for b in self.bands:
+            for off, n in ((b.off + b.hy * w, w * (b.y1 - b.y0)),
+                           (b.off + b.u_off + b.hc * cw, cw * (b.c1 - b.c0)),
+                           (b.off + b.u_off + b.chroma_elems + b.hc * cw, cw * (b.c1 - b.c0))):
+                if n:
+                    out.append(local.as_strided((b.cnt, n), (b.slot_elems, 1), local.storage_offset() + off))
+        return out
+
+    def full_views(self, stream):
+        """The same band rows of a FULL-frame stream (frames [Y][U][V] back to
+        back), as (cnt, n) strided views in local_views' order."""
+        w, h = self.width, self.height
+        cw, ch = w // 2, h // 2
+        fe = w * h + 2 * cw * ch
+        out = []
+        for b in self.bands:
+            for off, n in ((w * b.y0, w * (b.y1 - b.y0)), (w * h + cw * b.c0, cw * (b.c1 - b.c0)),
+                           (w * h + cw * ch + cw * b.c0, cw * (b.c1 - b.c0))):
+                if n:
+                    out.append(stream.as_strided((b.cnt, n), (self.world * fe, 1),
+                                                 stream.storage_offset() + b.f0 * fe + off))
+        return out
+
+    def held_views(self, stream, local):
+        """Every row this rank holds (bands + halos) as pairs (view of a FULL
+        stream, view of the local buffer), (cnt, n) each."""
+        w, h = self.width, self.height
+        cw, ch = w // 2, h // 2
+        fe = w * h + 2 * cw * ch
+        out = []
+        for b in self.bands:
+            for foff, loff, n in ((w * (b.y0 - b.hy), 0, w * (b.y1 - b.y0 + b.hy)),
+                                  (w * h + cw * (b.c0 - b.hc), b.u_off, b.chroma_elems),
+                                  (w * h + cw * ch + cw * (b.c0 - b.hc), b.u_off + b.chroma_elems, b.chroma_elems)):
+                if n:
+                    out.append((stream.as_strided((b.cnt, n), (self.world * fe, 1),
+                                                  stream.storage_offset() + b.f0 * fe + foff),
+                                local.as_strided((b.cnt, n), (b.slot_elems, 1), local.storage_offset() + b.off + loff)))
+        return out
+
+    def fill_from_stream(self, stream, local):
+        """Copy every row this rank holds (bands + halos) out of a full stream."""
+        for full, loc in self.held_views(stream, local):
+            loc.copy_(full)
+        return local
+
+    def packed_elems(self) -> int:
+        cw = self.width // 2
+        return sum(b.cnt * (self.width * (b.y1 - b.y0) + 2 * cw * (b.c1 - b.c0)) for b in self.bands)
+
+
+def cfg4_layout(rank: int, world: int, frames: int, width: int = 3840, height: int = 2160) -> Cfg4Layout:
+    """Local buffer of ``rank``: for each band it codes, its frame slots of band
+    rows + one halo row per plane (none for the top band)."""
+    bands_y = ctu_bands(height, world)
+    cw = width // 2
+    out, off = [], 0
+    for b, f0, cnt in cfg4_plan(rank, world, frames):
+        y0, y1 = bands_y[b]
+        if y1 <= y0:
+            continue
+        hy = 1 if y0 > 0 else 0
+        c0, c1 = y0 // 2, y1 // 2
+        hc = 1 if c0 > 0 else 0
+        u_off = width * (y1 - y0 + hy)
+        ce = cw * (c1 - c0 + hc)
+        slot = u_off + 2 * ce
+        out.append(Cfg4Band(b, f0, cnt, y0, y1, hy, hc, off, slot, u_off, ce))
+        off += cnt * slot
+    return Cfg4Layout(width, height, world, rank, frames, out, off)
 
 
 def cfg4_pack(stream, rank: int, world: int, frames: int, width: int, height: int):
-    """This rank's reconstructed bands of a full-frame stream, packed band-major
-    (frames in plan order, Y then U then V rows of each) into one flat tensor."""
+    """This rank's reconstructed bands of a FULL-frame stream, packed in
+    Cfg4Layout.full_views order into one flat tensor."""
     import torch
-    bands = ctu_bands(height, world)
-    parts = []
-    for b, f0, cnt in cfg4_plan(rank, world, frames):
-        y0, y1 = bands[b]
-        for f in range(f0, frames, world):
-            parts += _band_views(stream, f, y0, y1, width, height)
-    return torch.cat(parts) if parts else stream[:0].clone()
+    views = cfg4_layout(rank, world, frames, width, height).full_views(stream)
+    return torch.cat([v.reshape(-1) for v in views]) if views else stream[:0].clone()
 
 
 def cfg4_unpack(packed, rank: int, world: int, frames: int, width: int, height: int, stream):
     """Inverse of cfg4_pack: write rank ``rank``'s bands into the full stream."""
-    bands = ctu_bands(height, world)
     o = 0
-    for b, f0, cnt in cfg4_plan(rank, world, frames):
-        y0, y1 = bands[b]
-        for f in range(f0, frames, world):
-            for view in _band_views(stream, f, y0, y1, width, height):
-                view.copy_(packed[o:o + view.numel()])
-                o += view.numel()
+    for view in cfg4_layout(rank, world, frames, width, height).full_views(stream):
+        view.copy_(packed[o:o + view.numel()].view(view.shape))
+        o += view.numel()
     return o
 
 
 def cfg4_packed_elems(rank: int, world: int, frames: int, width: int, height: int) -> int:
-    bands = ctu_bands(height, world)
-    cw = width // 2
-    n = 0
-    for b, f0, cnt in cfg4_plan(rank, world, frames):
-        y0, y1 = bands[b]
-        n += cnt * (width * (y1 - y0) + 2 * cw * (y1 // 2 - y0 // 2))
-    return n
+    return cfg4_layout(rank, world, frames, width, height).packed_elems()

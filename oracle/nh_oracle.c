@@ -534,6 +534,50 @@ void oh_tu_pipeline_plane(const int16_t* src, int w, int h, int pitch, int ctb,
                     lvl, recon, tu_log2);
 }
 
+/* Same walk split over nthreads POSIX threads by CTU row (SURVEY.md §8(d) D-4,
+ * the all-cores leg of config 4's CPU baseline).  Open loop: a CTU row reads
+ * only source samples (D12), so the rows are independent and the output equals
+ * oh_tu_pipeline_plane's. */
+typedef struct {
+    const int16_t* src; int w, h, pitch, ctb, plane_id; uint32_t seed; int qp, is_luma, row0, row1;
+    int32_t* lvl; int16_t* recon; uint8_t* tu_log2;
+} oh_tu_band;
+
+static void* oh_tu_band_run(void* p) {
+    const oh_tu_band* b = (const oh_tu_band*)p;
+    oh_tu_pipeline_plane(b->src, b->w, b->h, b->pitch, b->ctb, b->plane_id, b->seed, b->qp, b->is_luma, b->row0,
+                         b->row1, b->lvl, b->recon, b->tu_log2);
+    return NULL;
+}
+
+int oh_tu_pipeline_plane_mt(const int16_t* src, int w, int h, int pitch, int ctb, int plane_id, uint32_t seed,
+                            int qp, int is_luma, int row0, int row1, int32_t* lvl, int16_t* recon,
+                            uint8_t* tu_log2, int nthreads) {
+    enum { kMaxThreads = 256 };
+    int rows = (h + ctb - 1) / ctb;
+    if (row1 > rows) row1 = rows;
+    if (row0 < 0) row0 = 0;
+    if (row1 <= row0) return 0;
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > kMaxThreads) nthreads = kMaxThreads;
+    if (nthreads > row1 - row0) nthreads = row1 - row0;
+    if (!g_dct_init) dct_init();   /* lazy table init stays single-threaded */
+    pthread_t tid[kMaxThreads];
+    oh_tu_band band[kMaxThreads];
+    int spawned[kMaxThreads];
+    const int n = row1 - row0;
+    for (int t = 0; t < nthreads; ++t) {
+        oh_tu_band b = {src, w, h, pitch, ctb, plane_id, seed, qp, is_luma, row0 + n * t / nthreads,
+                        row0 + n * (t + 1) / nthreads, lvl, recon, tu_log2};
+        band[t] = b;
+        spawned[t] = t < nthreads - 1 && pthread_create(&tid[t], NULL, oh_tu_band_run, &band[t]) == 0;
+        if (!spawned[t]) oh_tu_band_run(&band[t]);
+    }
+    for (int t = 0; t < nthreads; ++t)
+        if (spawned[t]) pthread_join(tid[t], NULL);
+    return 0;
+}
+
 /* cfg 4 in closed loop: CTUs in raster order, TUs in z-order,
  * neighbours from the reconstruction built so far (zero-initialised,
  * frame.py:41-43) with the BlockView rules (block.py:38-50). */

@@ -52,6 +52,7 @@ def lib():
             "oh_intra_rdo_plane_closed": [P, i32, i32, i32, i32, P, P, P, P],
             "oh_tu_pipeline_plane": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P],
             "oh_tu_pipeline_plane_closed": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, P, P, P],
+            "oh_tu_pipeline_plane_mt": [P, i32, i32, i32, i32, i32, C.c_uint32, i32, i32, i32, i32, P, P, P, i32],
             "oh_tu_split": [C.c_uint32, i32, i32, i32, i32],
             "oh_tc32_plane": [P, i32, i32, i32, i32, P, P],
             "oh_encode_intra_plane": [P, i32, i32, i32, i32, P, P],
@@ -209,6 +210,18 @@ def tu_pipeline_plane(src, ctb, plane_id, seed, qp, is_luma, row0=0, row1=1 << 3
     tul = np.zeros((h // 4, w // 4), np.uint8)
     lib().oh_tu_pipeline_plane(_p(src), w, h, w, ctb, plane_id, seed, qp, int(is_luma), row0, row1,
                                _p(lvl), _p(rec), _p(tul))
+    return lvl, rec, tul
+
+
+def tu_pipeline_plane_mt(src, ctb, plane_id, seed, qp, is_luma, nthreads=1, row0=0, row1=1 << 30):
+    """tu_pipeline_plane on ``nthreads`` host threads (CTU rows banded; same output)."""
+    src = np.ascontiguousarray(src, np.int16)
+    h, w = src.shape
+    lvl = np.zeros(src.shape, np.int32)
+    rec = np.zeros(src.shape, np.int16)
+    tul = np.zeros((h // 4, w // 4), np.uint8)
+    _check(lib().oh_tu_pipeline_plane_mt(_p(src), w, h, w, ctb, plane_id, seed, qp, int(is_luma), row0, row1,
+                                         _p(lvl), _p(rec), _p(tul), int(nthreads)))
     return lvl, rec, tul
 
 

@@ -36,6 +36,8 @@ def test_cfg4_two_ranks_gathered_recon_equals_unsharded():
     assert d["n_gpus"] == 2
     assert d["gathered_recon_equals_unsharded"] is True
     assert d["gather_inclusive"]["bytes_into_root_per_step"] > 0
+    # the input is sharded: rank 0 holds its bands + one halo row per band and plane, ~1/2 of the stream
+    assert 0.5 <= d["config"]["source_fraction_rank0"] < 0.51
 
 
 def test_cfg2_two_ranks_report_the_whole_job():

@@ -15,12 +15,18 @@
 #   percall    tools/percall.py (drop-in per-call cost); percall_ab: the same over tools/_ab/ (older build)
 #   pmc_sq     SQ wave-state pass (issue / wait fractions) of bench.py; CONFIG=4 for the config-4 bench
 #   kt_cfg     rocprofv3 kernel trace of tools/bench_configs.py $CONFIGS_ARGS (per-kernel times of configs 3/4/5)
+#   rccl       tests/rccl_world1.py (the RCCL branch at world size 1; also in `tests`)
+#   valu_rate  tools/ab/_valu_rate: chip-wide issue rate per VALU opcode (build it first, see the .hip)
+#   counters   rocprofv3 -L (the counters this box offers)
+#   valu_kt / valu_pmc1 / valu_pmc2   the VALU roofline passes over bench_configs $VALU_CFGS
+#              (kernel trace; SQ wave/instruction counters; MFMA busy + GRBM clock) -> tools/pmc_valu.py
 # pytest selection: PYTEST_K="expr" (passed as -k expr); bench args: BENCH_ARGS="...".
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
+VALU_CFGS=${VALU_CFGS:-3,4b,5,closed,closed4}
 STEPS=${STEPS:-20}
 FRAMES=${FRAMES:-128}
 PT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
@@ -77,6 +83,30 @@ run_step() {
     kt_cfg)
       echo "== rocprof kernel trace of bench_configs $CONFIGS_ARGS"
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt_cfg_${TAG} -o run -- python3 tools/bench_configs.py $CONFIGS_ARGS > gpurun_out/kt_cfg_${TAG}.log 2>&1 ;;
+    rccl)
+      echo "== RCCL world-1 gather check"
+      timeout -k 10 240 python tests/rccl_world1.py > gpurun_out/rccl_${TAG}.json 2> gpurun_out/rccl_${TAG}.err; rc=$?
+      cat gpurun_out/rccl_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/rccl_${TAG}.err; return $rc ;;
+    valu_rate)
+      echo "== VALU issue rates"
+      timeout -k 10 120 tools/ab/_valu_rate > gpurun_out/valu_rate_${TAG}.jsonl 2> gpurun_out/valu_rate_${TAG}.err; rc=$?
+      tail -3 gpurun_out/valu_rate_${TAG}.jsonl; return $rc ;;
+    counters)
+      echo "== rocprofv3 -L"
+      timeout -s KILL 90 rocprofv3 -L > gpurun_out/counters_${TAG}.txt 2>&1; rc=$?
+      grep -c "" gpurun_out/counters_${TAG}.txt; return $rc ;;
+    valu_kt)
+      echo "== kernel trace of bench_configs ${VALU_CFGS}"
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/valu_kt_${TAG} -o run -- python3 tools/bench_configs.py --configs ${VALU_CFGS} --reps 3 > gpurun_out/valu_kt_${TAG}.log 2>&1; rc=$?
+      tail -3 gpurun_out/valu_kt_${TAG}.log; return $rc ;;
+    valu_pmc1)
+      echo "== SQ pass 1 over bench_configs ${VALU_CFGS}"
+      timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d gpurun_out/valu_pmc1_${TAG} -o run -- python3 tools/bench_configs.py --configs ${VALU_CFGS} --reps 3 > gpurun_out/valu_pmc1_${TAG}.log 2>&1; rc=$?
+      tail -3 gpurun_out/valu_pmc1_${TAG}.log; return $rc ;;
+    valu_pmc2)
+      echo "== SQ pass 2 over bench_configs ${VALU_CFGS}"
+      timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/valu_pmc2_${TAG} -o run -- python3 tools/bench_configs.py --configs ${VALU_CFGS} --reps 3 > gpurun_out/valu_pmc2_${TAG}.log 2>&1; rc=$?
+      tail -3 gpurun_out/valu_pmc2_${TAG}.log; return $rc ;;
     *)
       echo "unknown step $1"; return 2 ;;
   esac
