@@ -43,6 +43,11 @@ int nh_device_count(int* count);
  * context (the next per-block call re-creates the current device's). */
 int nh_staging_bytes(int device, int64_t* bytes);
 int nh_release_staging(void);
+/* Host-side phases of the calling thread's last per-block call, in ns:
+ * [0] marshal (inputs into the kernel-argument block or the staging buffer),
+ * [1] launch (the launch API calls), [2] wait (launch returned -> completion
+ * seen), [3] finish (outputs copied back).  Diagnostics (tools/percall.py). */
+int nh_last_call_times(int64_t* ns);
 
 /* ---------------- (i) per-block entry points (host pointers) ---------------- */
 
@@ -70,6 +75,11 @@ int nh_inverse_transform(const int32_t* in, int64_t size, int use_dst, int32_t* 
 /* quant.py:41-79 quantize: abs_bits = bit width in which np.abs wraps (8/16/32/64) */
 int nh_quantize(const int64_t* coeff, int64_t n, int qp, int64_t log2size, int is_intra,
                 int abs_bits, int32_t* out);
+/* quant.py:77-78 for FLOAT coefficients: out = (abs_coeff * MF + offset) >> shift
+ * in int64 (wrapping), abs_coeff = np.abs(coeff).astype(np.int64) from the
+ * shim, which then applies quant.py:79's (np.sign(coeff) * level).astype(np.int32). */
+int nh_quantize_abs(const int64_t* abs_coeff, int64_t n, int qp, int64_t log2size, int is_intra,
+                    int64_t* out);
 /* quant.py:82-123 dequantize (size unused, D4) */
 int nh_dequantize(const int64_t* level, int64_t n, int qp, int32_t* out);
 /* quant.py:171-173 count_nonzero */
@@ -85,6 +95,10 @@ int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits
  * nh_satd_4x4: H.diff.H^T in int32, sum |.| (metrics.py:29-43), 16 samples;
  * nh_residual_energy: sum(int64(r)^2) mod 2^64 (metrics.py:46-48). */
 int nh_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, int64_t* out);
+/* metrics.py:9-10 for samples of any dtype (float, wide ints): the float64 sum
+ * of (a-b)^2 over a, b already cast to float64 by the shim, in numpy's pairwise
+ * summation order (np.mean = this / n) -- bit-identical to the reference's. */
+int nh_sum_sq_diff_f64(const double* a, const double* b, int64_t n, double* out);
 int nh_sad(const int32_t* a, const int32_t* b, int64_t n, int64_t* out);
 int nh_satd_4x4(const int32_t* a, const int32_t* b, int64_t* out);
 int nh_residual_energy(const int64_t* r, int64_t n, int64_t* out);

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <climits>
+#include <type_traits>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -254,6 +255,15 @@ __device__ __forceinline__ void dev_quant_i64(const int64_t* c, int64_t n, uint6
         out[i] = (int32_t)(uint32_t)(uint64_t)(sg * l);
     }
 }
+// quant.py:77-78 on abs_coeff = np.abs(coeff).astype(np.int64) computed by the
+// shim for float coefficients: (abs_coeff * mf + offset) >> shift in int64
+// (numpy's wrapping int64 multiply); the shim applies sign * level and the
+// int32 cast with the reference's own float expression (quant.py:79).
+__device__ __forceinline__ void dev_quant_abs64(const int64_t* a, int64_t n, uint64_t mf, uint64_t off, int shift,
+                                                int64_t* out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (int64_t)((uint64_t)a[i] * mf + off) >> shift;
+}
 __device__ __forceinline__ void dev_dequant_i64(const int64_t* l, int64_t n, int64_t scale, int per, int32_t* out) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         uint64_t b = (uint64_t)l[i] * (uint64_t)scale;
@@ -296,8 +306,12 @@ __device__ double eb_term(int64_t v, int bits) {
     else { as = (int64_t)a; as1 = (int64_t)a1; }
     return log2((double)as1) + (double)((as > 0) * 2);
 }
-__device__ double pw_sum(const int64_t* a, int64_t n, int bits) {
-    // iterative form of numpy's pairwise_sum over eb_term(a[i])
+// numpy's pairwise_sum (loops_utils.h.src) over term(i), i in [0, n), iteratively:
+// below 8 terms a plain running sum from 0; up to 128 eight accumulators over
+// the multiple-of-8 prefix, combined ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then
+// the rest added in order; above 128 the halves n2 = n/2 - (n/2)%8 and n - n2.
+template <class Term>
+__device__ double pw_sum(int64_t n, Term term) {
     struct Fr { int64_t off, n; int stage; double left; };
     Fr stk[48];
     int sp = 0;
@@ -309,15 +323,15 @@ __device__ double pw_sum(const int64_t* a, int64_t n, int bits) {
             double res;
             if (f.n < 8) {
                 res = 0.;
-                for (int64_t i = 0; i < f.n; ++i) res += eb_term(a[f.off + i], bits);
+                for (int64_t i = 0; i < f.n; ++i) res += term(f.off + i);
             } else {
                 double r[8];
-                for (int j = 0; j < 8; ++j) r[j] = eb_term(a[f.off + j], bits);
+                for (int j = 0; j < 8; ++j) r[j] = term(f.off + j);
                 int64_t i;
                 for (i = 8; i < f.n - (f.n % 8); i += 8)
-                    for (int j = 0; j < 8; ++j) r[j] += eb_term(a[f.off + i + j], bits);
+                    for (int j = 0; j < 8; ++j) r[j] += term(f.off + i + j);
                 res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-                for (; i < f.n; ++i) res += eb_term(a[f.off + i], bits);
+                for (; i < f.n; ++i) res += term(f.off + i);
             }
             --sp;
             ret = res;
@@ -340,7 +354,7 @@ __device__ double pw_sum(const int64_t* a, int64_t n, int bits) {
 }
 __device__ __forceinline__ void dev_estimate_bits(const int64_t* l, int64_t n, int bits, double* out) {
     if (threadIdx.x || blockIdx.x) return;
-    *out = n > 0 ? pw_sum(l, n, bits) : 0.0;   // the shim applies int() (quant.py:168)
+    *out = n > 0 ? pw_sum(n, [=](int64_t i) { return eb_term(l[i], bits); }) : 0.0;   // the shim applies int() (quant.py:168)
 }
 
 // ---------------------------------------------------------------------------
@@ -369,6 +383,14 @@ __device__ __forceinline__ void dev_sum_sq_diff(const int64_t* a, const int64_t*
         s += (unsigned long long)(d * d);
     }
     block_reduce_add(s, out, NoOp{});
+}
+// metrics.py:9-10 for any sample dtype: the shim casts both arrays to float64
+// (the reference's .astype(np.float64)); np.mean(diff ** 2) is numpy's add
+// reduction -- pairwise_sum above -- of the squares divided by n on the host.
+// One thread walks the pairwise tree (the per-call arrays are block-sized).
+__device__ __forceinline__ void dev_sum_sq_diff_f64(const double* a, const double* b, int64_t n, double* out) {
+    if (threadIdx.x || blockIdx.x) return;
+    *out = n > 0 ? 0.0 + pw_sum(n, [=](int64_t i) { const double d = a[i] - b[i]; return d * d; }) : 0.0;
 }
 // metrics.py:24-26: int32 difference (wraps), np.abs (wraps at INT32_MIN), int64 sum
 __device__ __forceinline__ void dev_sad_i32(const int32_t* a, const int32_t* b, int64_t n, unsigned long long* out) {
@@ -450,12 +472,25 @@ static unsigned grid_for(int64_t n, int64_t cap) {
 // One context per device (stream, buffers), created on first use on that
 // device and kept for the process; nh_release_staging() frees them all.
 constexpr size_t kSmallIn = 3072, kSmallOut = 64 << 10;
+// The kernel-argument block is sized to the call's inputs (256 B / 1 KB / 3 KB):
+// the argument segment is written per launch, so a 4x4 call does not ship 3 KB.
+template <size_t SZ>
 struct SmallIn {
-    alignas(16) uint8_t b[kSmallIn];
+    alignas(16) uint8_t b[SZ];
 };
 
-template <class F>
-__global__ void __launch_bounds__(256) k_small(SmallIn in, F f, unsigned long long* dw, unsigned long long* hres,
+// Host-side phases of the last per-block call on this thread (ns): marshal
+// (inputs into the argument block), launch (the launch API), wait (launch
+// returned -> completion word seen), finish (outputs copied back).
+// nh_last_call_times() reads them (tools/percall.py --phases).
+static thread_local int64_t g_call_ns[4] = {0, 0, 0, 0};
+static inline int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+template <class F, size_t SZ>
+__global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned long long* dw, unsigned long long* hres,
                                                unsigned long long seq) {
     if (threadIdx.x == 0) {
         atomicExch(&dw[0], ULLONG_MAX);   // status: no error yet
@@ -588,6 +623,7 @@ class BlockCall {
     // from_acc, the 8-byte accumulator word the body's reductions added into.
     template <class F>
     int run(unsigned grid, F f, void* out, size_t out_bytes, bool from_acc = false) {
+        const int64_t t0 = now_ns();
         Staging* S = nullptr;
         NH_TRY_(staging_current(&S));
         std::lock_guard<std::mutex> lk(S->mu);
@@ -595,17 +631,32 @@ class BlockCall {
         const size_t res = from_acc ? 0 : out_bytes;
         unsigned long long st, acc;
         if (end_ <= kSmallIn && res <= kSmallOut) {
-            SmallIn si;
-            for (int i = 0; i < n_; ++i)
-                if (ins_[i].bytes) std::memcpy(si.b + ins_[i].off, ins_[i].p, ins_[i].bytes);
             const unsigned long long seq = ++S->seq;
-            k_small<<<1, 256, 0, S->stream>>>(si, f, S->dwork, (unsigned long long*)S->hres_dev, seq);
-            NH_HIP(hipGetLastError());
+            int64_t t1 = 0;
+            auto launch = [&](auto sz_c) -> int {
+                constexpr size_t SZ = decltype(sz_c)::value;
+                SmallIn<SZ> si;
+                for (int i = 0; i < n_; ++i)
+                    if (ins_[i].bytes) std::memcpy(si.b + ins_[i].off, ins_[i].p, ins_[i].bytes);
+                t1 = now_ns();
+                k_small<<<1, 256, 0, S->stream>>>(si, f, S->dwork, (unsigned long long*)S->hres_dev, seq);
+                NH_HIP(hipGetLastError());
+                return NH_OK;
+            };
+            if (end_ <= 256) NH_TRY_(launch(std::integral_constant<size_t, 256>{}));
+            else if (end_ <= 1024) NH_TRY_(launch(std::integral_constant<size_t, 1024>{}));
+            else NH_TRY_(launch(std::integral_constant<size_t, kSmallIn>{}));
+            const int64_t t2 = now_ns();
             unsigned long long* r = (unsigned long long*)S->hres;
             NH_TRY_(wait_completion(S->stream, &r[2], seq));
+            const int64_t t3 = now_ns();
             st = r[0];
             acc = r[1];
             if (st == ULLONG_MAX && res) std::memcpy(out, r + 4, res);
+            g_call_ns[0] = t1 - t0;
+            g_call_ns[1] = t2 - t1;
+            g_call_ns[2] = t3 - t2;
+            g_call_ns[3] = now_ns() - t3;
         } else {
             const size_t wo = align_up(end_, 256), oo = wo + 256;
             NH_TRY_(staging_grow(*S, oo + res));
@@ -614,14 +665,21 @@ class BlockCall {
             unsigned long long* hw = (unsigned long long*)(S->hbuf + wo);
             hw[0] = ULLONG_MAX;
             hw[1] = 0;
+            const int64_t t1 = now_ns();
             NH_HIP(hipMemcpyAsync(S->dbuf, S->hbuf, wo + 16, hipMemcpyHostToDevice, S->stream));
             k_staged<<<grid, 256, 0, S->stream>>>(S->dbuf, f, (unsigned long long*)(S->dbuf + wo), S->dbuf + oo);
             NH_HIP(hipGetLastError());
             NH_HIP(hipMemcpyAsync(S->hbuf + wo, S->dbuf + wo, oo - wo + res, hipMemcpyDeviceToHost, S->stream));
+            const int64_t t2 = now_ns();
             NH_HIP(hipStreamSynchronize(S->stream));
+            const int64_t t3 = now_ns();
             st = hw[0];
             acc = hw[1];
             if (st == ULLONG_MAX && res) std::memcpy(out, S->hbuf + oo, res);
+            g_call_ns[0] = t1 - t0;
+            g_call_ns[1] = t2 - t1;
+            g_call_ns[2] = t3 - t2;
+            g_call_ns[3] = now_ns() - t3;
         }
         if (st != ULLONG_MAX) return -(int)(st & 0xff);
         if (from_acc) std::memcpy(out, &acc, 8);
@@ -671,15 +729,33 @@ int nh_staging_bytes(int device, int64_t* bytes) {
 int nh_release_staging(void) {
     int cur = 0;
     NH_HIP(hipGetDevice(&cur));
+    int first_err = NH_OK;
     for (int d = 0; d < kMaxDevices; ++d) {
         Staging& s = g_staging[d];
         std::lock_guard<std::mutex> lk(s.mu);
         if (!s.ready) continue;
-        NH_HIP(hipSetDevice(d));
+        const hipError_t e = hipSetDevice(d);
+        if (e != hipSuccess) {   // skip this device, free the others, restore the caller's device, report
+            if (first_err == NH_OK) {
+                set_error(std::string("nh_release_staging: hipSetDevice: ") + hipGetErrorString(e));
+                first_err = NH_EHIP;
+            }
+            continue;
+        }
         (void)hipStreamSynchronize(s.stream);
         staging_free(s);
     }
-    NH_HIP(hipSetDevice(cur));
+    const hipError_t e = hipSetDevice(cur);
+    if (e != hipSuccess && first_err == NH_OK) {
+        set_error(std::string("nh_release_staging: hipSetDevice: ") + hipGetErrorString(e));
+        first_err = NH_EHIP;
+    }
+    return first_err;
+}
+
+int nh_last_call_times(int64_t* ns) {
+    if (!ns) return NH_EARG;
+    for (int i = 0; i < 4; ++i) ns[i] = g_call_ns[i];
     return NH_OK;
 }
 
@@ -806,6 +882,22 @@ int nh_quantize(const int64_t* coeff, int64_t n, int qp, int64_t log2size, int i
     }, out, n * 4);
 }
 
+int nh_quantize_abs(const int64_t* abs_coeff, int64_t n, int qp, int64_t log2size, int is_intra, int64_t* out) {
+    if (n < 0) return NH_EARG;
+    int per, rem;
+    qp_params(qp, &per, &rem);
+    const int64_t shift = 14 + per + log2size;  // quant.py:73 (D3)
+    if (shift < 0 || shift > 62) return NH_EOVERFLOW;
+    const uint64_t off = is_intra ? (1ull << shift) / 3 : (1ull << shift) / 6;
+    if (n == 0) return NH_OK;
+    const uint64_t mf = (uint64_t)quant_scale(rem);
+    BlockCall c;
+    const size_t oi = c.in(abs_coeff, n * 8);
+    return c.run(grid_for(n), [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_quant_abs64((const int64_t*)(in + oi), n, mf, off, (int)shift, (int64_t*)o);
+    }, out, n * 8);
+}
+
 int nh_dequantize(const int64_t* level, int64_t n, int qp, int32_t* out) {
     if (n < 0) return NH_EARG;
     if (n == 0) return NH_OK;
@@ -881,6 +973,14 @@ int nh_sum_sq_diff(const int64_t* a, const int64_t* b, int64_t n, int64_t* out) 
     return c.run(grid_red(n), [=] __device__(U8 in, ST st, uint8_t*) {
         dev_sum_sq_diff((const int64_t*)(in + oa), (const int64_t*)(in + ob), n, st + 1);
     }, out, 8, true);
+}
+int nh_sum_sq_diff_f64(const double* a, const double* b, int64_t n, double* out) {
+    if (n < 0) return NH_EARG;
+    BlockCall c;
+    const size_t oa = c.in(a, n * 8), ob = c.in(b, n * 8);
+    return c.run(1, [=] __device__(U8 in, ST, uint8_t* o) {
+        dev_sum_sq_diff_f64((const double*)(in + oa), (const double*)(in + ob), n, (double*)o);
+    }, out, 8);
 }
 int nh_sad(const int32_t* a, const int32_t* b, int64_t n, int64_t* out) {
     if (n < 0) return NH_EARG;

@@ -1055,19 +1055,18 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, hipStream_t s);
 
+// The bases in constant memory, once per device.  hipMemcpyToSymbol is
+// host-synchronous, so every kernel queued afterwards -- on any stream -- reads
+// the uploaded values.
 static int ensure_basis_ctu() {
-    static unsigned long long ready = 0;   // one bit per device
-    int dev = 0;
-    NH_HIP(hipGetDevice(&dev));
-    if (dev < 0 || dev >= 64) return NH_EARG;
-    if (!(ready >> dev & 1ull)) {
+    static PerDeviceOnce once;
+    return once.run([] {
         const Basis b = make_basis();
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_ctu), &b, sizeof(b)));
         const BasisH bh = make_basis_h();
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_h), &bh, sizeof(bh)));
-        ready |= 1ull << dev;
-    }
-    return NH_OK;
+        return (int)NH_OK;
+    });
 }
 
 // Launches k_ctu_open over CTU rows [row0, row1) of every plane of the set.
@@ -1137,13 +1136,8 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         const int cap_wgs = cap_knob > 0 ? cap_knob
                           : ctb == 32 ? (GSZ == 4 ? 3 : 2) : (GSZ == 4 ? 4 : GSZ == 6 ? 3 : 2);
         if (NH_AB != 0 && persist) {
-            static int cus = 0;
-            if (!cus) {
-                int dev = 0;
-                NH_HIP(hipGetDevice(&dev));
-                NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-            }
-            int per_cu = 0;
+            int cus = 0, per_cu = 0;
+            NH_TRY(device_cus(&cus));
             const unsigned pad = lds_cap(kern, cap_wgs);
             NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * GSZ, pad));
             const int res = std::max(1, cus * per_cu);

@@ -1227,19 +1227,15 @@ extern "C" int nh_fwd8x8_quant_planes_ex(const int16_t* d_res, int16_t* d_lvl, c
     if (rc) return rc;
     if (!wg) return NH_OK;
     hipStream_t s = as_stream(stream);
-    if (d_bits) {   // the term table, once per device (stream-ordered before first use)
-        static std::mutex mu;
-        static bool ready[64] = {};
-        int dev = 0;
-        NH_HIP(hipGetDevice(&dev));
-        std::lock_guard<std::mutex> lk(mu);
-        if (dev < 0 || dev >= 64) return NH_EARG;
-        if (!ready[dev]) {
+    if (d_bits) {   // the term table, once per device (synchronised: visible to every stream)
+        static PerDeviceOnce once;
+        rc = once.run([&] {
             k_init_eb_tab<<<(kEbTab + 255) / 256, 256, 0, s>>>();
             NH_HIP(hipGetLastError());
             NH_HIP(hipStreamSynchronize(s));
-            ready[dev] = true;
-        }
+            return (int)NH_OK;
+        });
+        if (rc) return rc;
     }
     EpiArgs e{d_nnz, d_bits};
     // occupancy targets: the largest without spills (bits: 104 VGPRs, nnz only: 75)

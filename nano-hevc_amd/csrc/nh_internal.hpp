@@ -76,6 +76,45 @@ inline unsigned lds_cap(K kern, int wgs) {
     return pad;
 }
 
+#define NH_TRY(x)              \
+    do {                       \
+        int rc__ = (x);        \
+        if (rc__) return rc__; \
+    } while (0)
+
+// Per-device one-time initialisation, thread-safe: init() runs at most once per
+// device (again only if it failed), under a lock, on the calling thread with
+// that device current.  init() must be host-synchronous (e.g. hipMemcpyToSymbol
+// or a launch it synchronises), so work queued afterwards on ANY stream sees it.
+struct PerDeviceOnce {
+    std::mutex mu;
+    bool done[64] = {};
+    template <class F>
+    int run(F init) {
+        int dev = 0;
+        NH_HIP(hipGetDevice(&dev));
+        if (dev < 0 || dev >= 64) return NH_EARG;
+        std::lock_guard<std::mutex> lk(mu);
+        if (done[dev]) return NH_OK;
+        const int rc = init();
+        if (rc == NH_OK) done[dev] = true;
+        return rc;
+    }
+};
+
+// Compute units of the current device, cached per device (thread-safe).
+inline int device_cus(int* out) {
+    static std::mutex mu;
+    static int cus[64] = {};
+    int dev = 0;
+    NH_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return NH_EARG;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!cus[dev]) NH_HIP(hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev));
+    *out = cus[dev];
+    return NH_OK;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 

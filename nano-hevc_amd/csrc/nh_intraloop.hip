@@ -2514,12 +2514,8 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     } else {
         NH_HIP(hipMemsetAsync((int32_t*)d_work + 2, 0xff, 4, s));
     }
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        NH_HIP(hipGetDevice(&dev));
-        NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    int cus = 0;
+    NH_TRY(device_cus(&cus));
     // 8-bit streams: plane pairs (k_tu_closed_pair) when the set
     // holds more than one group; A/B build: NH_TU_CLOSED_PAIR = 0 codes one plane
     // per wave, = 4 the pair form capped at 4 waves/SIMD
@@ -2685,14 +2681,10 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
                                                                           p.plane_stride, p.planes_per_group, p.width,
                                                                           p.height, p.pitch, flag);
                 }
-                static int cus = 0, per_cu = 0;
-                if (!cus) {
-                    int dev = 0;
-                    NH_HIP(hipGetDevice(&dev));
-                    NH_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-                    NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_intra_rdo8_closed_tag<1, kClosedNarrow>,
-                                                                        64, 0));
-                }
+                int cus = 0, per_cu = 0;
+                NH_TRY(device_cus(&cus));
+                NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_intra_rdo8_closed_tag<1, kClosedNarrow>,
+                                                                    64, 0));
                 const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
 #if NH_AB   // A/B: NH_CLOSED_W3 = 1 the packed-only form capped at 168 VGPRs (3 waves/SIMD, 33 spilled)
                 static const int w3 = NH_KNOB("NH_CLOSED_W3", 0);

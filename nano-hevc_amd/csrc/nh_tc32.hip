@@ -185,19 +185,15 @@ __global__ void k_probe_mfma_i8(const int8_t* A, const int8_t* B, int32_t* D) {
     for (int g = 0; g < 16; ++g) D[crow(g, hh) * 32 + r] = d[g];
 }
 
-static bool g_basis_ready = false;
+// The int8 basis in constant memory, once per device (host-synchronous upload).
 static int ensure_basis(hipStream_t s) {
     (void)s;
-    int dev = 0;
-    static int ready_dev = -1;
-    NH_HIP(hipGetDevice(&dev));
-    if (!g_basis_ready || ready_dev != dev) {
+    static PerDeviceOnce once;
+    return once.run([] {
         Basis b = make_basis();
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis), &b, sizeof(b)));
-        g_basis_ready = true;
-        ready_dev = dev;
-    }
-    return NH_OK;
+        return (int)NH_OK;
+    });
 }
 
 }  // namespace nh

@@ -41,6 +41,7 @@ SIGNATURES = {
     "nh_device_count": ([P], I32),
     "nh_staging_bytes": ([I32, P], I32),
     "nh_release_staging": ([], I32),
+    "nh_last_call_times": ([P], I32),
     "nh_intra_dc": ([P, I64, P, I64, I64, I32, P], I32),
     "nh_intra_planar": ([P, I64, P, I64, I64, I64, I64, I64, P], I32),
     "nh_intra_angular": ([P, I64, P, I64, I64, I32, I64, P], I32),
@@ -50,10 +51,12 @@ SIGNATURES = {
     "nh_forward_transform": ([P, I64, I32, P], I32),
     "nh_inverse_transform": ([P, I64, I32, P], I32),
     "nh_quantize": ([P, I64, I32, I64, I32, I32, P], I32),
+    "nh_quantize_abs": ([P, I64, I32, I64, I32, P], I32),
     "nh_dequantize": ([P, I64, I32, P], I32),
     "nh_count_nonzero": ([P, I64, P], I32),
     "nh_estimate_bits": ([P, I64, I32, P], I32),
     "nh_sum_sq_diff": ([P, P, I64, P], I32),
+    "nh_sum_sq_diff_f64": ([P, P, I64, P], I32),
     "nh_sad": ([P, P, I64, P], I32),
     "nh_satd_4x4": ([P, P, P], I32),
     "nh_residual_energy": ([P, I64, P], I32),
@@ -162,5 +165,13 @@ def check(rc: int, what: str = "", lib=None):
     raise RuntimeError(msg + f"HIP error {rc}: {err}")
 
 
+try:   # in-tree host glue (nano_hevc/_nhaddr.c, built by the Makefile): ~0.15 us per address
+    from ._nhaddr import addr as _addr
+except ImportError:  # pragma: no cover - numpy's ctypes route (1-4 us per address)
+    _addr = None
+
+
 def ptr(a: np.ndarray):
-    return a.ctypes.data_as(C.c_void_p)
+    """Data address of a C-contiguous host array for a c_void_p argument (the
+    array must stay referenced for the duration of the call)."""
+    return _addr(a) if _addr is not None else a.ctypes.data_as(C.c_void_p)

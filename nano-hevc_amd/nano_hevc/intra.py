@@ -4,7 +4,9 @@ Same names, signatures, output dtypes and exceptions; every sample is computed
 by the gfx950 kernels in libnanohevc.so (k_intra_dc / k_intra_planar /
 k_intra_angular / k_residual / k_clip in csrc/nh_blocks.hip).  The shim only
 converts inputs the way the reference itself does (``.astype(np.int16)``,
-``int(...)`` of array elements) before handing host buffers to the C ABI.
+``int(...)`` of array elements, ``int(x.sum())``, numpy's int16 element
+stores) before handing integer host buffers to the C ABI -- so float and bool
+sample arrays give the reference's results and raise its exceptions.
 """
 from __future__ import annotations
 
@@ -26,23 +28,51 @@ INTRA_PRED_ANGLE = [
 INV_ANGLE = {-2: -4096, -5: -1638, -9: -910, -13: -630, -17: -482, -21: -390, -26: -315, -32: -256}
 
 
+_I64_SAFE = 1 << 62   # host-converted values beyond this would leave the kernels' int64 arithmetic
+
+
 def _ints1d(x, what):
     """Integer 1-D view as int64 (lossless for every integer dtype but uint64 > 2^63)."""
     a = np.asarray(x)
     if a.dtype.kind not in "iub":
-        raise NotImplementedError(f"{what}: nano_hevc (MI355X) takes integer sample arrays, got {a.dtype}")
+        raise TypeError(f"{what}: expected an integer sample array, got {a.dtype}")
     return np.ascontiguousarray(a.ravel(), dtype=np.int64)
+
+
+def _int_kind(x) -> bool:
+    return np.asarray(x).dtype.kind in "iub"
+
+
+def _fit_i64(v: int) -> int:
+    """A Python int from the reference's int(...) of a float, handed to the int64
+    kernels.  Beyond +-2^62 the reference's int16 store overflows (OverflowError)
+    unless other huge values cancel it exactly; that case raises here too."""
+    if not -_I64_SAFE < v < _I64_SAFE:
+        raise OverflowError(f"Python integer {v} out of bounds for int16")
+    return v
+
+
+def _dc_sum(x, what):
+    """intra.py:42 / :61: int(x.sum()).  Integer arrays go to the kernel whole (it
+    sums them, D7); for float / complex / object arrays the shim evaluates the
+    reference's own int(x.sum()) (numpy's sum in that dtype, then int(): the
+    same truncation and the same ValueError / OverflowError / TypeError) and
+    hands the kernel that one integer."""
+    a = np.asarray(x)
+    if a.dtype.kind in "iub":
+        return np.ascontiguousarray(a.ravel(), dtype=np.int64)
+    return np.array([_fit_i64(int(a.sum()))], np.int64)
 
 
 def _corner(v, what):
     if isinstance(v, (float, np.floating)):
-        raise NotImplementedError(f"{what}: integer corner sample expected")
+        raise TypeError(f"{what}: integer corner sample expected")
     return operator.index(v)
 
 
 def intra_dc_predict_4x4(top, left):
     """intra.py:37-43: DC = (sum(top) + sum(left) + 4) >> 3, 4x4 int16."""
-    t, l = _ints1d(top, "top"), _ints1d(left, "left")
+    t, l = _dc_sum(top, "top"), _dc_sum(left, "left")
     out = np.empty((4, 4), np.int16)
     check(_lib.load().nh_intra_dc(ptr(t), t.size, ptr(l), l.size, 4, 1, ptr(out)), "intra_dc_predict_4x4")
     return out
@@ -55,7 +85,7 @@ def intra_dc_predict(top, left, size):
         raise ZeroDivisionError("integer division or modulo by zero")
     if size < 0:
         raise ValueError("negative dimensions are not allowed")
-    t, l = _ints1d(top, "top"), _ints1d(left, "left")
+    t, l = _dc_sum(top, "top"), _dc_sum(left, "left")
     out = np.empty((size, size), np.int16)
     check(_lib.load().nh_intra_dc(ptr(t), t.size, ptr(l), l.size, size, 0, ptr(out)), "intra_dc_predict")
     return out
@@ -84,13 +114,30 @@ def reconstruct_block(pred, residual):
 
 
 def clip_to_pixel_range(block, bit_depth: int = 8):
-    """intra.py:75-78: np.clip(block, 0, 2**bd - 1).astype(int16)."""
+    """intra.py:75-78: np.clip(block, 0, 2**bd - 1).astype(int16).
+
+    Integer (and bool) blocks go to the kernel as int64.  A float block is first
+    put through the reference's own np.clip in its dtype, then every value v is
+    handed over as the integer the reference's .astype(np.int16) starts from:
+    trunc(v) when |v| < 2^31, else 0 (numpy's float -> int16 cast goes through
+    int32: NaN and values outside int32 become 0); the kernel's clamp and int16
+    wrap then give the reference's sample exactly."""
     max_val = (1 << bit_depth) - 1
     a = np.asarray(block)
-    if a.dtype.kind not in "iu":
-        raise NotImplementedError(f"clip_to_pixel_range: integer blocks only, got {a.dtype}")
-    np.clip(np.empty(0, a.dtype), 0, max_val)   # numpy's own bound/dtype checks (raises like the reference)
-    x = np.ascontiguousarray(a, dtype=np.int64)
+    if a.dtype.kind in "iu":
+        np.clip(np.empty(0, a.dtype), 0, max_val)   # numpy's own bound/dtype checks (raises like the reference)
+        x = np.ascontiguousarray(a, dtype=np.int64)
+    elif a.dtype.kind == "b":
+        np.clip(a[:0], 0, max_val)
+        x = np.ascontiguousarray(a, dtype=np.int64)
+    else:
+        c = np.asarray(np.clip(a, 0, max_val))
+        if c.dtype.kind not in "f":
+            raise TypeError(f"clip_to_pixel_range: cannot cast {c.dtype} samples to int16 like the reference")
+        with np.errstate(invalid="ignore"):
+            t = np.trunc(c.astype(np.float64))
+            ok = np.abs(t) < 2.0 ** 31
+        x = np.ascontiguousarray(np.where(ok, t, 0.0).astype(np.int64))
     out = np.empty(a.shape, np.int16)
     check(_lib.load().nh_clip(ptr(x), x.size, min(max_val, 2**63 - 1), ptr(out)), "clip_to_pixel_range")
     return out
@@ -108,21 +155,103 @@ def _narrow_corner_ok(v, n, arrays):
             f"intra_planar_predict: {v.dtype} corner arithmetic may wrap for these samples; pass Python ints")
 
 
+def _planar_float_refs(top, left, size, corners):
+    """intra.py:107-111 for non-integer top/left: the loop reads int(left[y]) and
+    int(top[x]), in the order left[0], top[0..size-1], left[1], left[2], ... (a
+    repeated read raises nothing new); any float corner makes the first (h + v +
+    size) >> k raise TypeError right after left[0] and top[0] were read.  The
+    elements are converted here exactly as int() does (truncation; ValueError for
+    NaN, OverflowError for inf) up to the first IndexError, which the kernel
+    raises in the same place; the kernel then runs on those integers."""
+    ta, la = np.asarray(top), np.asarray(left)
+    tv = np.zeros(ta.size, np.int64)
+    lv = np.zeros(la.size, np.int64)
+    fl_t, fl_l = ta.ravel(), la.ravel()
+
+    def conv(arr, flat, vals, i):
+        if i >= flat.size:
+            return False                                       # IndexError: the kernel's (same position)
+        vals[i] = _fit_i64(int(arr[i]) if arr.ndim == 1 else int(flat[i]))
+        return True
+
+    if size <= 0:
+        return tv, lv
+    if not conv(la, fl_l, lv, 0):
+        return tv, lv
+    for x in range(size):
+        if not conv(ta, fl_t, tv, x):
+            return tv, lv
+        if x == 0 and any(isinstance(c, (float, np.floating)) for c in corners):
+            raise TypeError("unsupported operand type(s) for >>: 'float' and 'int'")
+    for y in range(1, size):
+        if not conv(la, fl_l, lv, y):
+            break
+    return tv, lv
+
+
 def intra_planar_predict(top, left, top_right, bottom_left, size):
     """intra.py:81-113: pred[y,x] = ((N-1-x)left[y] + (x+1)tr + (N-1-y)top[x] + (y+1)bl + N) >> (log2N+1)."""
     size = operator.index(size)
     if size < 0:
         raise ValueError("negative dimensions are not allowed")
     log2_size = int(np.log2(size))          # the reference's own parameter computation
-    t, l = _ints1d(top, "top"), _ints1d(left, "left")
-    n = min(size, t.size, l.size)
-    _narrow_corner_ok(top_right, size, [t[:n], l[:n]])
-    _narrow_corner_ok(bottom_left, size, [t[:n], l[:n]])
-    tr, bl = _corner(top_right, "top_right"), _corner(bottom_left, "bottom_left")
+    if _int_kind(top) and _int_kind(left):
+        t, l = _ints1d(top, "top"), _ints1d(left, "left")
+    else:
+        t, l = _planar_float_refs(top, left, size, (top_right, bottom_left))
+    if any(isinstance(c, (float, np.floating)) for c in (top_right, bottom_left)):
+        # float corners make h and v floats: the first (h + v + size) >> k raises
+        # TypeError (intra.py:111) right after left[0] / top[0] were read; an
+        # IndexError on those reads comes first, and the kernel raises it
+        if size > 0 and t.size and l.size:
+            raise TypeError("unsupported operand type(s) for >>: 'float' and 'int'")
+        tr = bl = 0
+    else:
+        n = min(size, t.size, l.size)
+        _narrow_corner_ok(top_right, size, [t[:n], l[:n]])
+        _narrow_corner_ok(bottom_left, size, [t[:n], l[:n]])
+        tr, bl = _corner(top_right, "top_right"), _corner(bottom_left, "bottom_left")
     out = np.empty((size, size), np.int16)
     check(_lib.load().nh_intra_planar(ptr(t), t.size, ptr(l), l.size, tr, bl, size, log2_size, ptr(out)),
           "intra_planar_predict")
     return out
+
+
+def _store16(v):
+    """The int16 element store of _build_ref_array (intra.py:173, :176, :178,
+    :186) for one value: numpy's own setitem (int() of a float: truncation,
+    ValueError for NaN, OverflowError outside int16)."""
+    z = np.zeros(1, np.int16)
+    z[0] = v
+    return int(z[0])
+
+
+def _angular_float_refs(top, left, top_left, mode, size):
+    """intra.py:159-188 for non-integer top/left or a float corner: every element
+    _build_ref_array stores is converted by numpy's own int16 setitem, in the
+    reference's order (corner, primary[1..2N] with replicate-last, then the
+    negative-angle projections of secondary), so the first error raised is the
+    reference's; the kernel then builds the reference array from those integers
+    (unread elements are 0)."""
+    angle = INTRA_PRED_ANGLE[mode - 2]
+    vert = mode >= 18
+    ta, la = np.asarray(top), np.asarray(left)
+    pa, sa = (ta, la) if vert else (la, ta)
+    pv, sv = np.zeros(pa.size, np.int64), np.zeros(sa.size, np.int64)
+    corner = _store16(top_left)
+    for i in range(1, 2 * size + 1):
+        k = i if i < len(pa) else -1
+        if k == -1 and len(pa) == 0:
+            raise IndexError("index -1 is out of bounds for axis 0 with size 0")
+        pv[k] = _store16(pa[k])
+    if angle < 0:
+        inv = INV_ANGLE[angle]
+        for i in range(-1, ((size * angle) >> 5) - 1, -1):
+            proj = ((i + 1) * inv + 128) >> 8
+            if proj < len(sa):
+                sv[proj] = _store16(sa[proj])
+    t, l = (pv, sv) if vert else (sv, pv)
+    return t, l, corner
 
 
 def intra_angular_predict(top, left, top_left, mode, size):
@@ -131,8 +260,11 @@ def intra_angular_predict(top, left, top_left, mode, size):
     if size < 0:
         raise ValueError("negative dimensions are not allowed")
     INTRA_PRED_ANGLE[mode - 2]              # IndexError/TypeError exactly as intra.py:142 (D10)
-    t, l = _ints1d(top, "top"), _ints1d(left, "left")
-    corner = _corner(top_left, "top_left")
+    if _int_kind(top) and _int_kind(left) and not isinstance(top_left, (float, np.floating)):
+        t, l = _ints1d(top, "top"), _ints1d(left, "left")
+        corner = _corner(top_left, "top_left")
+    else:
+        t, l, corner = _angular_float_refs(top, left, top_left, mode, size)
     out = np.empty((size, size), np.int16)
     check(_lib.load().nh_intra_angular(ptr(t), t.size, ptr(l), l.size, corner, int(mode), size, ptr(out)),
           "intra_angular_predict")

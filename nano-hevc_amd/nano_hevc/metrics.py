@@ -3,9 +3,10 @@
 The array reductions run on the GPU (k_sum_sq_diff / k_sad_i32 / k_satd_4x4 /
 k_residual_energy in csrc/nh_blocks.hip); only the final scalar formulas
 (mean, log10) are evaluated on the host, with the reference's expressions.
-``mse``/``psnr`` are exact for integer samples of <= 16 bits: the squared
-differences are integers, so numpy's float64 sum is exact whenever the total
-is below 2**53 (checked; larger totals raise instead of rounding differently).
+``mse``/``psnr``: integer samples of <= 16 bits take an exact int64 SSE (the
+squares are integers, so numpy's float64 sum is exact below 2**53, checked);
+every other dtype (float, wider ints) is cast to float64 by the shim as the
+reference does and summed on the GPU in numpy's pairwise order, bit-identical.
 """
 from __future__ import annotations
 
@@ -15,30 +16,45 @@ from . import _lib
 from ._lib import check, ptr
 
 
-def _samples(x, what):
-    a = np.asarray(x)
-    if a.dtype.kind not in "iub" or a.dtype.itemsize > 2:
-        raise NotImplementedError(f"{what}: integer samples of <= 16 bits only (got {a.dtype})")
-    return a
+def _small_int(a) -> bool:
+    return a.dtype.kind in "iub" and a.dtype.itemsize <= 2
 
 
-def _sum_sq_diff(original, reconstructed) -> int:
-    a = np.ascontiguousarray(_samples(original, "mse"), dtype=np.int64)
-    b = np.ascontiguousarray(_samples(reconstructed, "mse"), dtype=np.int64)
-    a, b = np.broadcast_arrays(a, b)
-    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+def _sum_sq_diff_int(a, b):
+    """Exact int64 SSE of <= 16-bit samples: every partial sum is an integer below
+    2^53 (checked), so numpy's float64 sum of the squares is exact in any order."""
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.int64)
     out = np.zeros(1, np.int64)
     check(_lib.load().nh_sum_sq_diff(ptr(a), ptr(b), a.size, ptr(out)), "mse")
-    s = int(out[0])
-    if s >= 2**53:
-        raise NotImplementedError("mse: float64 sum would round (total >= 2**53)")
-    return s, a.size
+    return int(out[0])
+
+
+def _sum_sq_diff_f64(a, b) -> float:
+    """metrics.py:9-10 for any other dtype: the reference's .astype(np.float64)
+    on the host, then the sum of squares on the GPU in numpy's pairwise order
+    (memory order of the operands, as numpy's reduction walks a contiguous
+    array)."""
+    x, y = a.astype(np.float64), b.astype(np.float64)
+    order = "F" if (x.flags.f_contiguous and not x.flags.c_contiguous and
+                    y.flags.f_contiguous and not y.flags.c_contiguous) else "C"
+    x = np.ascontiguousarray(np.ravel(x, order=order))
+    y = np.ascontiguousarray(np.ravel(y, order=order))
+    out = np.zeros(1, np.float64)
+    check(_lib.load().nh_sum_sq_diff_f64(ptr(x), ptr(y), x.size, ptr(out)), "mse")
+    return float(out[0])
 
 
 def mse(original, reconstructed) -> float:
     """metrics.py:7-10: mean((orig - recon)^2) in float64."""
-    s, n = _sum_sq_diff(original, reconstructed)
-    return float(np.float64(s) / np.float64(n))
+    a, b = np.asarray(original), np.asarray(reconstructed)
+    a, b = np.broadcast_arrays(a, b)
+    n = a.size
+    if _small_int(a) and _small_int(b):
+        s = _sum_sq_diff_int(a, b)
+        if s < 2**53:
+            return float(np.float64(s) / np.float64(n))
+    return float(np.float64(_sum_sq_diff_f64(a, b)) / np.float64(n))
 
 
 def psnr(original, reconstructed, peak: int = 255) -> float:

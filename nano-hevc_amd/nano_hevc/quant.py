@@ -24,13 +24,14 @@ def get_qp_params(qp: int) -> tuple[int, int]:
 
 
 def _abs_bits(dt) -> int:
-    """Width in which np.abs wraps for this dtype (quant.py:75)."""
+    """Width in which np.abs wraps for this integer dtype (quant.py:77); 0 for
+    the dtypes quantize() hands to nh_quantize_abs instead."""
     dt = np.dtype(dt)
     if dt.kind == "i":
         return dt.itemsize * 8
-    if dt.kind in "ub" and dt.itemsize < 8:
+    if dt.kind == "u" and dt.itemsize < 8:
         return 64
-    raise NotImplementedError(f"quantize: integer coefficients only (got {dt})")
+    return 0
 
 
 def quantize(coeff, qp: int, size: int, is_intra: bool = True) -> np.ndarray:
@@ -42,11 +43,22 @@ def quantize(coeff, qp: int, size: int, is_intra: bool = True) -> np.ndarray:
     offset = (1 << shift) // 3 if is_intra else (1 << shift) // 6   # noqa: F841
     c = np.asarray(coeff)
     ab = _abs_bits(c.dtype)
-    x = np.ascontiguousarray(c, dtype=np.int64)
-    out = np.empty(c.shape, np.int32)
-    check(_lib.load().nh_quantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), log2_size, int(bool(is_intra)),
-                                  ab, ptr(out)), "quantize")
-    return out
+    if ab:
+        x = np.ascontiguousarray(c, dtype=np.int64)
+        out = np.empty(c.shape, np.int32)
+        check(_lib.load().nh_quantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), log2_size, int(bool(is_intra)),
+                                      ab, ptr(out)), "quantize")
+        return out
+    # float (and uint64 / bool / other) coefficients: the reference's own host
+    # expressions around the kernel -- np.sign (raises for bool, like quant.py:76),
+    # np.abs(...).astype(np.int64), the level on the GPU, then
+    # (sign * level).astype(np.int32) in float64 (quant.py:79)
+    sign = np.sign(c)
+    abs_coeff = np.ascontiguousarray(np.abs(c).astype(np.int64))
+    level = np.empty(abs_coeff.shape, np.int64)
+    check(_lib.load().nh_quantize_abs(ptr(abs_coeff), abs_coeff.size, int(qp_per * 6 + qp_rem), log2_size,
+                                      int(bool(is_intra)), ptr(level)), "quantize")
+    return (sign * level).astype(np.int32)
 
 
 def dequantize(level, qp: int, size: int) -> np.ndarray:
@@ -86,7 +98,7 @@ def count_nonzero(level) -> int:
     """quant.py:171-173."""
     a = np.asarray(level)
     if a.dtype.kind not in "iub":
-        raise NotImplementedError(f"count_nonzero: integer levels only (got {a.dtype})")
+        a = a != 0          # np.count_nonzero's "nonzero" for float / complex / object (NaN counts)
     x = np.ascontiguousarray(a, dtype=np.int64)
     cnt = np.zeros(1, np.int64)
     check(_lib.load().nh_count_nonzero(ptr(x), x.size, ptr(cnt)), "count_nonzero")

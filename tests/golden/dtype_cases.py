@@ -1,0 +1,140 @@
+"""Non-integer inputs to the drop-in functions: float, bool,
+float32/float16 sample arrays, float corners, NaN / inf / out-of-range values.
+
+cases() rebuilds the same seeded calls every time; make_golden.py --only
+dtypes.npz records the REFERENCE's result (an array / scalar, or the name of
+the exception it raised) per case, and tests/test_dtypes_gpu.py runs the same
+calls on the MI355X drop-in and compares bit for bit.  Each case is
+(name, function name, args tuple, kwargs dict).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def cases():
+    rng = np.random.default_rng(90210)
+    out = []
+
+    def add(fn, *args, **kw):
+        out.append((f"{len(out):03d}_{fn}", fn, args, kw))
+
+    nan, inf = float("nan"), float("inf")
+    # ---- intra_dc_predict / _4x4 (intra.py:42, :61: int(x.sum()))
+    add("intra_dc_predict", np.array([100.5, 98, 100, 101]), np.array([103, 102, 101, 99.]), 4)
+    add("intra_dc_predict_4x4", np.array([100.5, 98, 100, 101]), np.array([103, 102, 101, 99.]))
+    for n in (4, 8, 16, 32):
+        t = rng.uniform(-20, 300, n)
+        l = rng.uniform(-20, 300, n)
+        add("intra_dc_predict", t, l, n)
+        add("intra_dc_predict", t.astype(np.float32), l.astype(np.float32), n)
+        add("intra_dc_predict", t.astype(np.float16), l.astype(np.int16), n)
+        add("intra_dc_predict", rng.random(n) > 0.5, rng.random(n) > 0.3, n)
+    add("intra_dc_predict", np.array([-3.9, -0.5, 2.2, 1.0]), np.array([-7.5, 0.0, 0.0, 0.0]), 4)
+    add("intra_dc_predict", np.array([nan, 1.0, 2.0, 3.0]), np.array([1.0, 2.0, 3.0, 4.0]), 4)
+    add("intra_dc_predict", np.array([inf, 1.0, 2.0, 3.0]), np.array([1.0, 2.0, 3.0, 4.0]), 4)
+    add("intra_dc_predict", np.array([1e6, 1.0, 2.0, 3.0]), np.array([1.0, 2.0, 3.0, 4.0]), 4)
+    add("intra_dc_predict_4x4", np.array([True, True, False, True]), np.array([True, False, False, True]))
+    # ---- intra_planar_predict (int(left[y]) / int(top[x]); float corners -> TypeError)
+    for n in (4, 8, 16, 32):
+        t = rng.uniform(0, 255, n + 1)
+        l = rng.uniform(0, 255, n + 1)
+        add("intra_planar_predict", t, l, int(t[-1]), int(l[-1]), n)
+        add("intra_planar_predict", t.astype(np.float32), l, 7, 250, n)
+        add("intra_planar_predict", rng.random(n) > 0.5, rng.random(n) > 0.5, 1, 0, n)
+    t = rng.uniform(0, 255, 8)
+    add("intra_planar_predict", t, t, 128.0, 128, 8)
+    add("intra_planar_predict", t, t, 128, np.float64(3.5), 8)
+    t2 = t.copy()
+    t2[5] = nan
+    add("intra_planar_predict", t2, t, 10, 20, 8)
+    add("intra_planar_predict", t, t2, 10, 20, 8)
+    add("intra_planar_predict", np.append(t[:4], nan), t[:5], 10, 20, 4)        # NaN past size: never read
+    t3 = t.copy()
+    t3[3] = -inf
+    add("intra_planar_predict", t3, t, 10, 20, 8)
+    add("intra_planar_predict", np.array([-5.7, 3.2, 250.9, 17.0]), np.array([1.5, -2.5, 8.0, 9.9]), 100, 3, 4)
+    # ---- intra_angular_predict (numpy's int16 element stores of _build_ref_array)
+    for n in (4, 8):
+        top = rng.uniform(0, 255, 2 * n + 1)
+        left = rng.uniform(0, 255, 2 * n + 1)
+        for mode in (2, 6, 10, 11, 14, 18, 21, 25, 26, 30, 34):
+            add("intra_angular_predict", top, left, float(top[0]), mode, n)
+        add("intra_angular_predict", top.astype(np.float32), left.astype(np.float16), 100, 18, n)
+        add("intra_angular_predict", top[:n + 1], left[:n - 1], 90, 14, n)           # short refs (D6)
+        add("intra_angular_predict", rng.random(2 * n + 1) > 0.5, rng.random(2 * n + 1) > 0.5, True, 22, n)
+    top = rng.uniform(0, 255, 9)
+    left = rng.uniform(0, 255, 9)
+    add("intra_angular_predict", top, left, nan, 26, 4)
+    add("intra_angular_predict", top, left, 1e6, 26, 4)
+    add("intra_angular_predict", top, left, 32767.9, 26, 4)
+    bad = top.copy()
+    bad[3] = nan
+    add("intra_angular_predict", bad, left, 10, 26, 4)
+    add("intra_angular_predict", bad, left, 10, 10, 4)     # horizontal: top is the secondary array
+    big = left.copy()
+    big[1] = 4e4
+    add("intra_angular_predict", top, big, 10, 18, 4)
+    add("intra_angular_predict", top, big, 10, 34, 4)      # vertical positive angle: left never read
+    # ---- residual_block / reconstruct_block (.astype(np.int16))
+    a = rng.uniform(-300, 300, (8, 8))
+    b = rng.uniform(-300, 300, (8, 8))
+    add("residual_block", a, b)
+    add("reconstruct_block", a.astype(np.float32), b)
+    add("residual_block", np.array([[7e4, -7e4, 4e9, nan]]), np.array([[1.5, 2.5, 3.5, 4.5]]))
+    add("reconstruct_block", rng.random((4, 4)) > 0.5, a[:4, :4])
+    # ---- clip_to_pixel_range (np.clip(...).astype(np.int16))
+    add("clip_to_pixel_range", np.array([[1.6, 300.]]))
+    add("clip_to_pixel_range", rng.uniform(-50, 400, (8, 8)))
+    add("clip_to_pixel_range", rng.uniform(-50, 400, (4, 4)).astype(np.float32))
+    add("clip_to_pixel_range", rng.uniform(-50, 400, (4, 4)).astype(np.float16))
+    add("clip_to_pixel_range", np.array([nan, inf, -inf, -0.5, 0.99, 254.999, 255.0, 1e300]))
+    add("clip_to_pixel_range", rng.uniform(-5000, 5000, (8, 8)), 10)
+    add("clip_to_pixel_range", np.array([7e4, 65535.9, 32768.5, 1e6, -1.0]), 16)
+    add("clip_to_pixel_range", np.array([7e4, 65535.9, 32768.5, 1e6, 4e9, 3e9, nan]), 20)
+    add("clip_to_pixel_range", np.array([7e4, 2.5e9, 4e9, 1e12, 1e19, inf]), 40)
+    add("clip_to_pixel_range", rng.random((4, 4)) > 0.5)
+    add("clip_to_pixel_range", rng.random((4, 4)) > 0.5, 16)
+    # ---- quantize / quantize_block / dequantize (quant.py:76-79, :114)
+    add("quantize", np.array([[100.7, -33.2]]), 22, 4)
+    for n in (4, 8, 16, 32):
+        c = rng.uniform(-2000, 2000, (n, n))
+        for qp in (0, 17, 22, 32, 51):
+            add("quantize", c, qp, n)
+        add("quantize", c, 30, n, False)
+        add("quantize_block", c.astype(np.float32), 27)
+        add("dequantize", rng.uniform(-300, 300, (n, n)), 22, n)
+        add("dequantize_block", rng.uniform(-300, 300, (n, n)).astype(np.float32), 40)
+    add("quantize", np.array([[nan, inf, -inf, -0.0, 0.4, -0.6]]), 22, 4)
+    add("quantize", np.array([[1e12, -1e12, 3e15, 2**62 * 1.0]]), 4, 8)
+    add("quantize", np.array([[1e12, -1e12, 3e15]]), 51, 32)
+    add("quantize", np.array([[True, False]]), 22, 4)
+    add("dequantize", np.array([[nan, 1e30, -2.5, 2.5]]), 22, 4)
+    add("dequantize", np.array([[True, False, True]]), 40, 4)
+    # ---- count_nonzero / is_all_zero
+    add("count_nonzero", np.array([0.0, nan, -0.0, 0.1, -1e-300]))
+    add("is_all_zero", np.array([0.0, -0.0]))
+    add("is_all_zero", np.array([0.0, nan]))
+    add("count_nonzero", np.array([True, False, True]))
+    # ---- metrics on floats / wide ints
+    x = rng.uniform(0, 255, (16, 16))
+    y = rng.uniform(0, 255, (16, 16))
+    for sh in ((4, 4), (8, 8), (16, 16), (5, 7), (100,), (300,), (1000,)):
+        n = int(np.prod(sh))
+        u = rng.uniform(-100, 400, n).reshape(sh)
+        v = rng.uniform(-100, 400, n).reshape(sh)
+        add("mse", u, v)
+        add("psnr", u, v)
+        add("psnr", u.astype(np.float32), v.astype(np.float32), 1023)
+    add("mse", x, x)
+    add("psnr", x, x)
+    add("mse", rng.integers(-2**40, 2**40, (8, 8)), rng.integers(-2**40, 2**40, (8, 8)))
+    add("psnr", rng.integers(-2**31, 2**31, 64, dtype=np.int64).astype(np.int32),
+        rng.integers(-2**31, 2**31, 64, dtype=np.int64).astype(np.int32))
+    add("mse", np.asfortranarray(x), np.asfortranarray(y))
+    add("mse", x, y[0])                                    # broadcasting
+    add("sad", x, y)
+    add("satd_4x4", x[:4, :4], y[:4, :4])
+    add("residual_energy", x - y)
+    add("psnr", rng.random((8, 8)) > 0.5, rng.random((8, 8)) > 0.5, 1)
+    return out

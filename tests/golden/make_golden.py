@@ -561,6 +561,28 @@ def plane_hash_1080p(T, Q):
     return hashlib.sha256(lvl.tobytes()).hexdigest()
 
 
+def gen_dtypes(I, Q, M):
+    """Non-integer inputs (tests/golden/dtype_cases.py): per case the reference's
+    result (out_*, with rtype_* its Python type) or its exception (err_* the
+    class name, errbase_* the builtin class it derives from)."""
+    sys.path.insert(0, HERE)
+    from dtype_cases import cases
+    mods = (I, Q, M)
+    out = {}
+    bases = (ZeroDivisionError, OverflowError, IndexError, ValueError, TypeError, AttributeError)
+    for name, fn, args, kw in cases():
+        f = next(getattr(m, fn) for m in mods if hasattr(m, fn))
+        try:
+            r = f(*args, **kw)
+        except Exception as e:
+            out["err_" + name] = np.array(type(e).__name__)
+            out["errbase_" + name] = np.array(next(b.__name__ for b in bases if isinstance(e, b)))
+            continue
+        out["out_" + name] = np.asarray(r)
+        out["rtype_" + name] = np.array(type(r).__name__)
+    return out
+
+
 def main():
     pos = [a for i, a in enumerate(sys.argv[1:], 1) if not a.startswith("--") and sys.argv[i - 1] != "--only"]
     ref = pos[0] if pos else "/root/reference"
@@ -569,7 +591,8 @@ def main():
     rng = np.random.default_rng(1234)
     if "--only" in sys.argv:   # regenerate one file (own rng), keep the others and their manifest entries
         name = sys.argv[sys.argv.index("--only") + 1]
-        gen = {"closed4.npz": lambda: gen_closed4(I, T, Q), "closed.npz": lambda: gen_closed(I, T, Q)}[name]
+        gen = {"closed4.npz": lambda: gen_closed4(I, T, Q), "closed.npz": lambda: gen_closed(I, T, Q),
+               "dtypes.npz": lambda: gen_dtypes(I, Q, M)}[name]
         p = os.path.join(HERE, name)
         np.savez_compressed(p, **gen())
         mp = os.path.join(HERE, "manifest.json")
@@ -591,6 +614,7 @@ def main():
         "encode.npz": gen_encode(ref),
         "closed.npz": gen_closed(I, T, Q),
         "closed4.npz": gen_closed4(I, T, Q),
+        "dtypes.npz": gen_dtypes(I, Q, M),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

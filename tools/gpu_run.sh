@@ -71,7 +71,7 @@ run_step() {
       cat gpurun_out/configs_${TAG}.jsonl; [ $rc -eq 0 ] || tail -20 gpurun_out/configs_${TAG}.err; return $rc ;;
     percall)
       echo "== per-call cost"
-      timeout -k 10 300 python tools/percall.py $PERCALL_ARGS > gpurun_out/percall_${TAG}.json 2> gpurun_out/percall_${TAG}.err; rc=$?
+      timeout -k 10 300 python tools/percall.py --phases $PERCALL_ARGS > gpurun_out/percall_${TAG}.json 2> gpurun_out/percall_${TAG}.err; rc=$?
       tail -3 gpurun_out/percall_${TAG}.json; [ $rc -eq 0 ] || tail -20 gpurun_out/percall_${TAG}.err; return $rc ;;
     percall_ab)
       echo "== per-call cost, previous build (tools/_ab/libnanohevc_r01_staging.so)"

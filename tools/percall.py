@@ -9,6 +9,13 @@ one block per call, as the reference's callers use them, at sizes 4 / 8 / 16 / 3
 where a size applies: median microseconds per call over ``--reps`` calls after
 warm-up.  Prints one JSON object {"impl": ..., "us_per_call": {name: {size: us}}}.
 Inputs are the same seeded arrays for both implementations.
+
+--phases (shim only): also splits each call's median into
+  python   -- the shim's numpy conversions + the Python/ctypes call overhead
+              (total minus the time spent inside the C function),
+  marshal / launch / wait / finish -- the C library's host phases of the call
+              (nh_last_call_times: inputs into the argument block, the launch
+              API, launch-return -> completion word seen, outputs copied back).
 """
 from __future__ import annotations
 
@@ -84,6 +91,55 @@ def cases(nh, rng):
     return out
 
 
+class _Timed:
+    """Proxy over the ctypes library: records the wall time of each C call."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self.last = 0.0
+
+    def __getattr__(self, name):
+        f = getattr(self._lib, name)
+        if not name.startswith("nh_") or name == "nh_last_call_times":
+            return f
+
+        def call(*a):
+            t0 = time.perf_counter()
+            r = f(*a)
+            self.last = time.perf_counter() - t0
+            return r
+        return call
+
+
+def phases(nh, fn, reps):
+    """Median split of one call (see --phases)."""
+    import ctypes
+    from nano_hevc import _lib
+    real = _lib.load()
+    prox = _Timed(real)
+    load0 = _lib.load
+    _lib.load = lambda: prox
+    ns = (ctypes.c_int64 * 4)()
+    rows = []
+    try:
+        for _ in range(5):
+            fn()
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            tot = time.perf_counter() - t0
+            real.nh_last_call_times(ns)
+            rows.append((tot, prox.last, ns[0] * 1e-9, ns[1] * 1e-9, ns[2] * 1e-9, ns[3] * 1e-9))
+    finally:
+        _lib.load = load0
+    med = [statistics.median(r[i] for r in rows) * 1e6 for i in range(6)]
+    c_internal = med[2] + med[3] + med[4] + med[5]
+    return {"total_with_proxy": round(med[0], 2), "in_c_call": round(med[1], 2),
+            "python_and_ctypes": round(med[0] - med[1], 2), "ctypes_entry_exit": round(med[1] - c_internal, 2),
+            "marshal": round(med[2], 2), "launch": round(med[3], 2), "wait": round(med[4], 2),
+            "finish": round(med[5], 2)}
+
+
 def main():
     impl = "shim"
     if "--impl" in sys.argv:
@@ -105,14 +161,17 @@ def main():
             _lib.LIB_PATH = path
         _lib.load()
     rng = np.random.default_rng(7)
-    res = {}
+    res, ph = {}, {}
+    want_phases = impl == "shim" and "--phases" in sys.argv
     for name, n, fn in cases(nh, rng):
         r = reps if (impl == "shim" or n <= 16) else max(10, reps // 10)
         res.setdefault(name, {})[n] = _time(fn, r)
+        if want_phases:
+            ph.setdefault(name, {})[n] = phases(nh, fn, r)
     lib = sys.argv[sys.argv.index("--lib") + 1] if "--lib" in sys.argv else "nano_hevc/libnanohevc.so"
     print(json.dumps({"impl": f"nano-hevc_amd shim (MI355X), {lib}" if impl == "shim" else "reference numpy",
                       "device": dev, "cpu": platform.processor() or platform.machine(), "reps": reps,
-                      "us_per_call": res}))
+                      "us_per_call": res, **({"phases_us": ph} if ph else {})}))
 
 
 if __name__ == "__main__":
