@@ -312,6 +312,7 @@ __device__ double eb_term(int64_t v, int bits) {
 // the rest added in order; above 128 the halves n2 = n/2 - (n/2)%8 and n - n2.
 template <class Term>
 __device__ double pw_sum(int64_t n, Term term) {
+#pragma clang fp contract(off)   // numpy rounds every add on its own: no fused multiply-adds with the terms
     struct Fr { int64_t off, n; int stage; double left; };
     Fr stk[48];
     int sp = 0;
@@ -390,7 +391,12 @@ __device__ __forceinline__ void dev_sum_sq_diff(const int64_t* a, const int64_t*
 // One thread walks the pairwise tree (the per-call arrays are block-sized).
 __device__ __forceinline__ void dev_sum_sq_diff_f64(const double* a, const double* b, int64_t n, double* out) {
     if (threadIdx.x || blockIdx.x) return;
-    *out = n > 0 ? 0.0 + pw_sum(n, [=](int64_t i) { const double d = a[i] - b[i]; return d * d; }) : 0.0;
+    // diff ** 2 is rounded before the sum adds it (contract(off) here and in pw_sum)
+    *out = n > 0 ? 0.0 + pw_sum(n, [=](int64_t i) {
+#pragma clang fp contract(off)
+        const double d = a[i] - b[i];
+        return d * d;
+    }) : 0.0;
 }
 // metrics.py:24-26: int32 difference (wraps), np.abs (wraps at INT32_MIN), int64 sum
 __device__ __forceinline__ void dev_sad_i32(const int32_t* a, const int32_t* b, int64_t n, unsigned long long* out) {
