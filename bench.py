@@ -571,15 +571,49 @@ def run_cfg4(args, dist, world, rank, dev):
     return line
 
 
+def load_valu(cfg_key: str):
+    """The VALU roofline inputs of a configuration, committed in
+    profiles/valu_roofline.json by tools/pmc_valu.py: per kernel of the step the
+    SQ_INSTS_VALU wave-instructions per launch (PMC) and the attainable issue
+    rate of its static VALU mix priced at the measured per-opcode rates."""
+    p = os.path.join(ROOT, "profiles", "valu_roofline.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get("configs", {}).get(cfg_key)
+    except Exception:
+        return None
+
+
 def cfg4_roofline(samples, kern_ms, frames, world):
-    """HBM view of the config-4 step (8 B/sample of algorithmic traffic)."""
-    achieved = samples * BYTES_PER_SAMPLE_CFG4 / (kern_ms * 1e-3) / 1e9
-    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(f"cfg4_4k_yuv420_f{frames}_n{world}"),
-            "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower bound for "
-                            "8-B/lane row reads, <= 2x that if every request were 128 B), writes exact; "
-                            "profiles/pmc_traffic.json",
-            "bytes_per_sample": BYTES_PER_SAMPLE_CFG4, "kernel_ms_avg": kern_ms}
+    """Config 4 is VALU-issue-bound: the roofline is the VALU
+    issue rate.  achieved = the step's VALU wave-instructions (PMC, per kernel of
+    the step, from profiles/valu_roofline.json) / the step's HIP-event time
+    measured here; peak = the attainable rate of the step's instruction mix
+    (harmonic combination of each kernel's attainable rate, weighted by its
+    instructions).  The HBM view (8 B/sample) rides along as ``hbm``."""
+    gbs = samples * BYTES_PER_SAMPLE_CFG4 / (kern_ms * 1e-3) / 1e9
+    hbm = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
+           "traffic": load_traffic(f"cfg4_4k_yuv420_f{frames}_n{world}"),
+           "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower bound for "
+                           "8-B/lane row reads, <= 2x that if every request were 128 B), writes exact; "
+                           "profiles/pmc_traffic.json",
+           "bytes_per_sample": BYTES_PER_SAMPLE_CFG4}
+    v = load_valu("cfg4_4k_yuv420")
+    if not v:
+        return dict(hbm, kernel_ms_avg=kern_ms)
+    nf = samples / (W4K * H4K * 3 // 2)        # frames' worth of samples this rank coded per step
+    ks = [k for k in v["kernels"].values() if k.get("valu_per_frame") and k.get("attainable_valu_winst_per_s")]
+    instr = sum(k["valu_per_frame"] * nf for k in ks)
+    t_att = sum(k["valu_per_frame"] * nf / k["attainable_valu_winst_per_s"] for k in ks)
+    peak = instr / t_att / 1e9
+    achieved = instr / (kern_ms * 1e-3) / 1e9
+    return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G VALU wave-instr/s",
+            "frac": achieved / peak, "traffic": hbm["traffic"], "valu_instr_per_step": instr,
+            "valu_instr_per_sample": instr * 64 / samples,
+            "peak_note": "attainable issue rate of the step's static VALU mix at the measured per-opcode rates "
+                         "(tools/valu_mix.py x tools/ab/valu_rate.hip; profiles/valu_roofline.json)",
+            "valu_source": v.get("source"), "kernel_ms_avg": kern_ms, "hbm": hbm}
 
 
 def cpu_baseline_cfg4(me, src, lvl, rec, args, fe):

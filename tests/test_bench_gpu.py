@@ -31,7 +31,11 @@ def _check_common(d, steps):
     assert d["n_gpus"] == 1 and d["steps"] == steps and d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["value"] > 0 and d["ms_per_step"] > 0 and "workload" in d["config"]
     rf = d["roofline"]
-    assert rf["bound"] in ("hbm", "mfma") and rf["unit"] in ("GB/s", "TFLOP/s") and rf["peak"] == 8000.0
+    assert rf["bound"] in ("hbm", "mfma", "valu")
+    if rf["bound"] == "valu":   # config 4: VALU issue against the attainable rate of its instruction mix
+        assert rf["unit"] == "G VALU wave-instr/s" and rf["valu_instr_per_step"] > 0 and rf["hbm"]["peak"] == 8000.0
+    else:
+        assert rf["unit"] in ("GB/s", "TFLOP/s") and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9 and 0 < rf["frac"] < 1
     assert rf["kernel_ms_avg"] <= d["ms_per_step"] * 1.05
     cb = d["cpu_baseline"]
@@ -53,6 +57,7 @@ def test_bench_config4_line():
     assert d["unit"] == "samples/s" and d["cpu_baseline"]["gpu_outputs_bit_exact_on_sample"] is True
     assert d["cpu_baseline"]["cores"] > 1 and d["cpu_baseline"]["value_1thread"] > 0
     assert d["config"]["source_fraction_rank0"] == 1.0
+    assert d["roofline"]["bound"] == "valu"
     tu = d["config"]["tu_blocks_per_step"]
     # every sample of the two frames lies in exactly one TU
     area = sum(n * (4 << k) ** 2 for k, n in enumerate(tu[f"{4 << k}x{4 << k}"] for k in range(4)))

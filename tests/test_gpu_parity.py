@@ -797,6 +797,45 @@ def test_tu_pipeline_planes_batched_vs_oracle(nh, torch_dev, W, H, rows):
         assert np.array_equal(tuy[f] if c == 0 else tuc[2 * f + c - 1], et), (f, c)
 
 
+@pytest.mark.parametrize("layout", ["pitch+2", "base+2"])
+@pytest.mark.parametrize("qp", [0, 22, 51])
+def test_tu_pipeline_layout_fallback_vs_oracle(nh, torch_dev, layout, qp):
+    """Layouts the CTU-granular kernel's vector accesses cannot take -- a pitch
+    that is not a multiple of 4 elements, or a plane base 2 elements off (source
+    / recon rows not 8-B aligned, level rows not 16-B aligned) -- make
+    ctu_open_launch return NH_EVALUE and nh_tu_pipeline_planes fall back to the
+    per-size launches (k_tu_process, 32x32 TUs on the butterfly).  That path
+    against the oracle: luma (CTB 32) and chroma (CTB 16), 8-bit and int16
+    content, two planes per set (group stride), partial CTUs."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(17 + qp)
+    W, H = 200, 136
+    pitch, base = (W + 2, 0) if layout == "pitch+2" else (W, 2)
+    gs = pitch * H + 6
+    eight = [np.clip(120 + rng.integers(-70, 71, (H, W)), 0, 255).astype(np.int16) for _ in range(2)]
+    wide = [rng.integers(-32768, 32768, (H, W)).astype(np.int16) for _ in range(2)]
+    for planes in (eight, wide):
+        buf = np.zeros(base + 2 * gs, np.int16)
+        for g, p in enumerate(planes):
+            for y in range(H):
+                o = base + g * gs + y * pitch
+                buf[o:o + W] = p[y]
+        d = torch.from_numpy(buf).cuda()
+        for luma, ctb, pid in ((True, 32, 0), (False, 16, 1)):
+            lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+            rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+            pset = gpu.plane_set(base, W, H, pitch, 1, 2, 0, gs)
+            _, _, tu = gpu.tu_pipeline_planes(d, pset, ctb, pid, 77, qp, luma, lvl=lvl, rec=rec)
+            lv, rc, tu = lvl.cpu().numpy(), rec.cpu().numpy(), tu.cpu().numpy()
+            for g, p in enumerate(planes):
+                el, er, et = O.tu_pipeline_plane(p, ctb, pid, 77, qp, luma)
+                rows = [slice(base + g * gs + y * pitch, base + g * gs + y * pitch + W) for y in range(H)]
+                assert np.array_equal(np.stack([lv[r] for r in rows]), el), (layout, luma, g)
+                assert np.array_equal(np.stack([rc[r] for r in rows]), er), (layout, luma, g)
+                assert np.array_equal(tu[g], et), (layout, luma, g)
+
+
 def test_fused8x8_stripe_form_needs_contiguous_rows(nh, torch_dev):
     """The stripe form (variant 33) walks a tile as one contiguous range: a plane
     whose pitch is not 8 * (width // 8) is refused, never silently mis-read."""

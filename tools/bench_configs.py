@@ -190,6 +190,22 @@ def main():
                     np.array_equal(el, lv[f * fe:f * fe + W * H].view(H, W).cpu().numpy()))
         print(json.dumps(line), flush=True)
 
+    if "5b" in cfgs:   # config 5 batched only (the product launch), for per-config profiler runs
+        W, H, nf = 7680, 4320, args.cfg5_frames
+        fe = gpu.yuv420_frame_elems(W, H)
+        stream5 = torch.cat([torch.cat([synth_plane(H, W, 7 + 3 * f).flatten(), synth_plane(H // 2, W // 2, 8 + 3 * f).flatten(),
+                                        synth_plane(H // 2, W // 2, 9 + 3 * f).flatten()]) for f in range(nf)])
+        sets5 = gpu.yuv420_plane_sets(nf, W, H)
+        lv5 = torch.zeros_like(stream5, dtype=torch.int32)
+        rc5 = torch.zeros_like(stream5)
+        ms = timed(lambda: gpu.tc32_planes(stream5, sets5, args.qp5, 1, lvl=lv5, rec=rc5), args.reps)
+        nblk = nf * sum((h // 32) * (w // 32) for w, h in ((W, H), (W // 2, H // 2), (W // 2, H // 2)))
+        print(json.dumps({"config": "cfg5 batched: 8K YUV420 frame stream, f16 MFMA launch + int8 fix-up per plane set",
+                          "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "blocks_per_s": nblk / ms * 1e3,
+                          "samples_per_s": nf * fe / ms * 1e3, "bytes_per_sample": 8,
+                          "achieved_GBps": nf * fe * 8 / ms / 1e6, "psnr_y_frame0": psnr_dev(stream5[:W * H], rc5[:W * H])}),
+              flush=True)
+
     if 5 in cfgs:
         W, H = 7680, 4320
         planes = [synth_plane(H, W, 7), synth_plane(H // 2, W // 2, 8), synth_plane(H // 2, W // 2, 9)]

@@ -26,7 +26,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-r03}
-VALU_CFGS=${VALU_CFGS:-3,4b,5,closed,closed4}
+VALU_CFGS=${VALU_CFGS:-3,4b,5b,closed,closed4}
 STEPS=${STEPS:-20}
 FRAMES=${FRAMES:-128}
 PT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
@@ -95,18 +95,16 @@ run_step() {
       echo "== rocprofv3 -L"
       timeout -s KILL 90 rocprofv3 -L > gpurun_out/counters_${TAG}.txt 2>&1; rc=$?
       grep -c "" gpurun_out/counters_${TAG}.txt; return $rc ;;
-    valu_kt)
-      echo "== kernel trace of bench_configs ${VALU_CFGS}"
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/valu_kt_${TAG} -o run -- python3 tools/bench_configs.py --configs ${VALU_CFGS} --reps 3 > gpurun_out/valu_kt_${TAG}.log 2>&1; rc=$?
-      tail -3 gpurun_out/valu_kt_${TAG}.log; return $rc ;;
-    valu_pmc1)
-      echo "== SQ pass 1 over bench_configs ${VALU_CFGS}"
-      timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d gpurun_out/valu_pmc1_${TAG} -o run -- python3 tools/bench_configs.py --configs ${VALU_CFGS} --reps 3 > gpurun_out/valu_pmc1_${TAG}.log 2>&1; rc=$?
-      tail -3 gpurun_out/valu_pmc1_${TAG}.log; return $rc ;;
-    valu_pmc2)
-      echo "== SQ pass 2 over bench_configs ${VALU_CFGS}"
-      timeout -s KILL 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/valu_pmc2_${TAG} -o run -- python3 tools/bench_configs.py --configs ${VALU_CFGS} --reps 3 > gpurun_out/valu_pmc2_${TAG}.log 2>&1; rc=$?
-      tail -3 gpurun_out/valu_pmc2_${TAG}.log; return $rc ;;
+    valu_kt|valu_pmc1|valu_pmc2)
+      # one profiler run per config (a config's kernels alone in each CSV)
+      for c in ${VALU_CFGS//,/ }; do
+        echo "== $1 over bench_configs --configs $c"
+        case "$1" in
+          valu_kt)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
+          valu_pmc1) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
+          valu_pmc2) timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
+        esac
+      done ;;
     *)
       echo "unknown step $1"; return 2 ;;
   esac

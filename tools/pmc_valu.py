@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""VALU roofline of the VALU-bound configs from committed profiles.
+
+    python tools/pmc_valu.py --tag r03a [--dir gpurun_out] [--out profiles/valu_roofline.json]
+
+Inputs, all written by `TAG=... tools/gpu_run.sh valu_rate valu_kt valu_pmc1 valu_pmc2`
+(one profiler run per config of tools/bench_configs.py, so every CSV holds one
+config's kernels):
+  * valu_rate_<tag>.jsonl: chip-wide issue rate of each VALU opcode class
+    (tools/ab/valu_rate.hip, 8 waves/SIMD, on the clock the chip holds);
+  * valu_kt_<tag>_<cfg>/: kernel trace (average duration, calls per kernel);
+  * valu_pmc1_<tag>_<cfg>/: SQ_INSTS_VALU, SQ_WAVES, SQ_WAVE_CYCLES,
+    SQ_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, SQ_WAIT_ANY, SQ_INSTS_SALU, SQ_INSTS_LDS
+    per dispatch;
+  * valu_pmc2_<tag>_<cfg>/: SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_ANY,
+    SQ_WAIT_INST_ANY, SQ_INSTS_VMEM_RD/WR, SQ_ACTIVE_INST_LDS, GRBM_GUI_ACTIVE,
+    GRBM_COUNT per dispatch;
+  * the static VALU mix of each kernel (tools/valu_mix.py, compiled here).
+
+Per kernel: achieved = SQ_INSTS_VALU per dispatch / average duration (chip-wide
+VALU wave-instructions per second); attainable = the kernel's static VALU mix
+priced at the measured per-opcode rates, N / sum(n_i / r_i); frac = achieved /
+attainable.  Per config: the same over one frame's worth of its kernels
+(instructions summed, attainable combined harmonically, time = the kernels'
+summed average durations per frame).  SQ ratios say where the rest goes:
+valu_active = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, wait_any = SQ_WAIT_ANY /
+SQ_WAVE_CYCLES, clock = GRBM_GUI_ACTIVE / duration.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# bench_configs config -> (profile key, anchor kernel, anchor dispatches per frame)
+CONFIGS = {
+    "3": ("cfg3_1080p_yuv420", "k_intra_rdo8<1, true, 1>", 3.0),
+    "closed": ("cfg3_closed_1080p_yuv420", "k_intra_rdo8_closed_tag<1, 1>", 1 / 64),
+    "4b": ("cfg4_4k_yuv420", "k_ctu_open<32", 1 / 16),
+    "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair", 2 / 64),
+    "5b": ("cfg5_8k_yuv420", "k_tc32_h<1>", 2 / 8),
+}
+
+
+def _find(d, pattern):
+    hits = sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
+    return hits[0] if hits else None
+
+
+def kernel_times(d):
+    p = _find(d, "*kernel_stats.csv")
+    out = {}
+    if p:
+        for r in csv.DictReader(open(p)):
+            if "nh::" in r["Name"]:
+                out[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+    return out, p
+
+
+def counters(d):
+    p = _find(d, "*counter_collection.csv")
+    per = collections.defaultdict(lambda: collections.defaultdict(list))
+    if p:
+        for r in csv.DictReader(open(p)):
+            if "nh::" in r["Kernel_Name"]:
+                per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    out = {}
+    for k, d2 in per.items():
+        e = {c: statistics.mean(v) for c, v in d2.items()}
+        e["_dispatches"] = max(len(v) for v in d2.values())
+        out[k] = e
+    return out, p
+
+
+def static_mix(rates_path):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "valu_mix.py"), "--rates", rates_path, "--kernels", "nh::"],
+                       capture_output=True, text=True, check=True)
+    return {d["kernel"]: d for d in (json.loads(x) for x in r.stdout.splitlines() if x.startswith("{"))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "valu_roofline.json"))
+    ap.add_argument("--configs", default=",".join(CONFIGS))
+    a = ap.parse_args()
+    rates_path = os.path.join(a.dir, f"valu_rate_{a.tag}.jsonl")
+    rates = [json.loads(x) for x in open(rates_path) if x.startswith("{")]
+    mix = static_mix(rates_path)
+    res = {"tag": a.tag, "rates_chip_winst_per_s": {r["op"]: r["chip_winst_per_s"] for r in rates},
+           "method": "achieved = SQ_INSTS_VALU per dispatch / kernel-trace average duration; attainable = static "
+                     "VALU mix (tools/valu_mix.py) priced at the measured per-opcode rates (tools/ab/valu_rate.hip)",
+           "configs": {}}
+    for c in a.configs.split(","):
+        key, anchor, anchor_pf = CONFIGS[c]
+        times, kt_path = kernel_times(os.path.join(a.dir, f"valu_kt_{a.tag}_{c}"))
+        c1, p1_path = counters(os.path.join(a.dir, f"valu_pmc1_{a.tag}_{c}"))
+        c2, p2_path = counters(os.path.join(a.dir, f"valu_pmc2_{a.tag}_{c}"))
+        if not times or not c1:
+            print(f"{c}: missing profiles", file=sys.stderr)
+            continue
+        f_pmc = next(v["_dispatches"] for k, v in c1.items() if anchor in k) / anchor_pf
+        f_kt = next(v["calls"] for k, v in times.items() if anchor in k) / anchor_pf
+        kernels, instr, t_att, t_ms = {}, 0.0, 0.0, 0.0
+        for name in sorted(set(times) | set(c1)):
+            t, p, q, m = times.get(name), c1.get(name, {}), c2.get(name, {}), mix.get(name)
+            e = {"calls_traced": t["calls"] if t else 0, "avg_ms": t["avg_ns"] / 1e6 if t else None,
+                 "dispatches_counted": p.get("_dispatches", 0)}
+            for k in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU",
+                      "SQ_WAIT_ANY", "SQ_INSTS_SALU", "SQ_INSTS_LDS"):
+                if k in p:
+                    e[k] = p[k]
+            for k in ("SQ_VALU_MFMA_BUSY_CYCLES", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_INSTS_VMEM_RD",
+                      "SQ_INSTS_VMEM_WR", "SQ_ACTIVE_INST_LDS", "GRBM_GUI_ACTIVE", "GRBM_COUNT"):
+                if k in q:
+                    e[k] = q[k]
+            wc = p.get("SQ_WAVE_CYCLES", 0)
+            if wc:
+                e["valu_active_of_wave_cycles"] = p.get("SQ_ACTIVE_INST_VALU", 0) / wc
+                e["wait_any_of_wave_cycles"] = p.get("SQ_WAIT_ANY", 0) / wc
+                if "SQ_WAIT_INST_ANY" in q:
+                    e["wait_inst_any_of_wave_cycles"] = q["SQ_WAIT_INST_ANY"] / wc
+                if "SQ_ACTIVE_INST_ANY" in q:
+                    e["active_any_of_wave_cycles"] = q["SQ_ACTIVE_INST_ANY"] / wc
+            if t and "GRBM_GUI_ACTIVE" in q:
+                e["clock_GHz_held"] = q["GRBM_GUI_ACTIVE"] / t["avg_ns"]
+            if m:
+                e["valu_static"] = m["valu_static"]
+                e["valu_by_rate_class"] = m["valu_by_rate_class"]
+                e["attainable_valu_winst_per_s"] = m.get("attainable_valu_winst_per_s")
+                e["attainable_vs_plain_32bit"] = m.get("attainable_vs_plain_32bit")
+            if t and "SQ_INSTS_VALU" in p:
+                e["achieved_valu_winst_per_s"] = p["SQ_INSTS_VALU"] / (t["avg_ns"] * 1e-9)
+                if e.get("attainable_valu_winst_per_s"):
+                    e["valu_frac"] = e["achieved_valu_winst_per_s"] / e["attainable_valu_winst_per_s"]
+            # one frame's worth of this kernel
+            if "SQ_INSTS_VALU" in p:
+                e["valu_per_frame"] = p["SQ_INSTS_VALU"] * p["_dispatches"] / f_pmc
+                instr += e["valu_per_frame"]
+                if e.get("attainable_valu_winst_per_s"):
+                    t_att += e["valu_per_frame"] / e["attainable_valu_winst_per_s"]
+            if t:
+                e["ms_per_frame"] = t["avg_ns"] * t["calls"] / f_kt / 1e6
+                t_ms += e["ms_per_frame"]
+            kernels[name] = e
+        ent = {"kernels": kernels, "frames_counted": f_pmc, "frames_traced": f_kt,
+               "valu_per_frame": instr, "kernel_ms_per_frame": t_ms,
+               "source": {"kernel_trace": os.path.relpath(kt_path, ROOT) if kt_path else None,
+                          "pmc1": os.path.relpath(p1_path, ROOT) if p1_path else None,
+                          "pmc2": os.path.relpath(p2_path, ROOT) if p2_path else None, "rates": os.path.relpath(rates_path, ROOT)}}
+        if t_ms and t_att:
+            ent["achieved_valu_winst_per_s"] = instr / (t_ms * 1e-3)
+            ent["attainable_valu_winst_per_s"] = instr / t_att
+            ent["valu_frac"] = ent["achieved_valu_winst_per_s"] / ent["attainable_valu_winst_per_s"]
+        res["configs"][key] = ent
+        print(f"{key:28s} frac {ent.get('valu_frac', float('nan')):.3f}  {t_ms:.4f} ms/frame (kernel sum)  "
+              f"VALU/frame {instr:.4g}", flush=True)
+        for name, e in kernels.items():
+            if e.get("valu_per_frame", 0) > 0.01 * instr:
+                print(f"    {e.get('valu_frac', float('nan')):6.3f} act {e.get('valu_active_of_wave_cycles', float('nan')):.3f} "
+                      f"wait {e.get('wait_any_of_wave_cycles', float('nan')):.3f} {name[:90]}")
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1, sort_keys=True)
+        f.write("\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
