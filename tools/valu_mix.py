@@ -151,8 +151,9 @@ def summarize(sym, cnt, rates):
     nv = sum(valu.values())
     res = {"kernel": sym, "units": dict(units), "valu_static": nv}
     by_class = collections.Counter()
-    for m, n in valu.items():
-        by_class[rate_class(m)] += n
+    for m, n in valu.items():   # a measured opcode prices itself; the rest take their class's measured opcode
+        b = base_mnemonic(m)
+        by_class[b if rates and b in rates else rate_class(m)] += n
     res["valu_by_rate_class"] = dict(by_class.most_common())
     res["valu_top"] = dict(valu.most_common(25))
     if rates and nv:
