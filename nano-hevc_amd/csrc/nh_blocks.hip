@@ -11,6 +11,7 @@
 //   k_quant_i64 / k_dequant_i64 / k_quant_i32 / k_dequant_i32  quant.py:41-150 (A12-A13)
 //   k_count_nonzero / k_estimate_bits          quant.py:153-173
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <type_traits>
@@ -537,8 +538,14 @@ constexpr int kMaxDevices = 64;
 static Staging g_staging[kMaxDevices];
 
 static int staging_current(Staging** out) {
-    int n = 0, dev = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    // the device count of the process is fixed: asked once (a successful answer is kept)
+    static std::atomic<int> ndev{-1};
+    int n = ndev.load(std::memory_order_relaxed), dev = 0;
+    if (n <= 0) {
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        if (n > 0) ndev.store(n, std::memory_order_relaxed);
+    }
+    if (n == 0) {
         set_error("no HIP device visible (nano-hevc_amd needs an MI355X; there is no CPU fallback)");
         return NH_ENODEV;
     }

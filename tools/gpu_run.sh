@@ -104,6 +104,7 @@ run_step() {
           valu_pmc1) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
           valu_pmc2) timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
         esac
+        python3 tools/trim_prof.py gpurun_out/$1_${TAG}_$c
       done ;;
     *)
       echo "unknown step $1"; return 2 ;;
