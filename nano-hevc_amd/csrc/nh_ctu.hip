@@ -78,6 +78,8 @@ struct CtuArgs {
     int32_t wide_only;               // A/B build only (NH_CTU_NARROW=0): every workgroup on the 32-bit chain
     int32_t probe;                   // A/B build only (NH_CTU_PROBE, bits): 1 = no batches, 2 = no global loads,
                                      // 4 = return at once, 8 = no TU-map stores (wrong outputs)
+    uint32_t* wide_flag;             // config 5: set to `epoch` when a block is left to the int8 fix-up
+    uint32_t epoch;
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
@@ -526,9 +528,16 @@ __device__ __forceinline__ f16x_t splat16(float v) {
     return r;
 }
 
+// TSTORE: the level and recon rows leave through an LDS tile `ot` (per wave,
+// kOutP int32 per row) so that every global store instruction writes whole
+// rows -- 8 rows of 128 B (levels), 16 rows of 64 B (recon) -- instead of 32-B
+// / 16-B pieces of 32 rows.
+constexpr int kOutP = 36, kRecP = 24;   // int32 per row: level tile, recon tile (48 halves; 16-B rows)
+template <bool TSTORE = false>
 __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, const BasisH& bs,
                                               int gx0, int gy0,
-                                              int32_t* __restrict__ lvl, int16_t* __restrict__ rec) {
+                                              int32_t* __restrict__ lvl, int16_t* __restrict__ rec,
+                                              int32_t* ot = nullptr) {
     constexpr int IP = Strip<32>::IP, QH = Strip<32>::QH;   // img[r * IP + c]: sample (r - 1, c), c = -1: left
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
     const int l = opaque_lane(), r = l & 31, hh = l >> 5;
@@ -596,9 +605,18 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             L4[e] = quant_s((int32_t)__builtin_floorf(addb(acc2[g], 0.5f)), cq.qs, cq.h_v, cq.hneg_v);
             qt[crow(g, hh) * QH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
         }
-        st_lvl4(lrow + 8 * q + 4 * hh, make_int4(L4[0], L4[1], L4[2], L4[3]));
+        if constexpr (TSTORE) *(int4*)&ot[r * kOutP + 8 * q + 4 * hh] = make_int4(L4[0], L4[1], L4[2], L4[3]);
+        else st_lvl4(lrow + 8 * q + 4 * hh, make_int4(L4[0], L4[1], L4[2], L4[3]));
     }
     wave_sync();
+    if constexpr (TSTORE) {   // 4 instructions of 8 whole 128-B level rows
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rr = (l >> 3) + 8 * i, c = 4 * (l & 7);
+            st_lvl4(lvl + (int64_t)(gy0 + rr) * a.pitch + gx0 + c, *(const int4*)&ot[rr * kOutP + c]);
+        }
+        wave_sync();   // the tile's reads before the recon tile reuses it
+    }
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
     f16x_t acc3 = splat16(initb(0.5f));
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.tt[r][8 * hh]), acc3,
@@ -622,8 +640,17 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             const int32_t v = p + (int32_t)__builtin_floorf(addb(acc4[4 * q + e], 0.5f));
             R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
         }
-        st_rec4(rrow + 8 * q + 4 * hh,
-                make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16)));
+        const uint2 pk = make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
+        if constexpr (TSTORE) *(uint2*)&ot[r * kRecP + 4 * q + 2 * hh] = pk;
+        else st_rec4(rrow + 8 * q + 4 * hh, pk);
+    }
+    if constexpr (TSTORE) {   // 2 instructions of 16 whole 64-B recon rows
+        wave_sync();
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int rr = (l >> 2) + 16 * i, c = 4 * (l & 3);
+            *(uint4*)(rec + (int64_t)(gy0 + rr) * a.pitch + gx0 + 2 * c) = *(const uint4*)&ot[rr * kRecP + c];
+        }
     }
 }
 
@@ -1019,23 +1046,35 @@ constexpr int16_t kWideMark = (int16_t)0x8000;
 // K blocks per wave (consecutive in raster order), block k+1's loads issued
 // before block k's chain.  K = 1 in the product: K = 4 measured slower (0.177
 // vs 0.159 ms per 8K frame; 114 registers, 4 waves/SIMD), DESIGN.md §4.5.
-template <int K>
+// XCD: the workgroup grid renumbered so that XCD x runs the x-th eighth of the
+// (plane, block) order (xcd_eighths, as the hot kernel; A/B).  TSTORE: the
+// chain's outputs leave in whole rows through an LDS tile (ctu_chain32_h).
+// The strip loads are issued before the bases are copied to LDS, so the copy
+// and its barrier run under the loads.
+template <int K, bool XCD = false, bool TSTORE = false>
 __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
     using G = Strip<32>;
     __shared__ __attribute__((aligned(16))) int16_t s_img[4][G::IMG];
     __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * G::QH];
     __shared__ BasisH s_basis;
+    __shared__ __attribute__((aligned(16))) int32_t s_out[TSTORE ? 4 : 1][TSTORE ? 32 * kOutP : 4];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b0 = (blockIdx.x * 4 + wv) * K;
-    copy_basis_h(s_basis);
-    __syncthreads();
-    if (b0 >= nblk) return;   // whole wave
-    const int pz = blockIdx.y;
-    const int64_t poff = plane_off(a, pz);
+    uint32_t bx = blockIdx.x, by = blockIdx.y;
+    if constexpr (XCD) {
+        const uint32_t id = xcd_eighths(by * gridDim.x + bx, gridDim.x * gridDim.y);
+        by = id / gridDim.x;
+        bx = id - by * gridDim.x;
+    }
+    const int b0 = ((int)bx * 4 + wv) * K;
+    const int pz = (int)by;
     StripLoad<32> ld;
     // strip_issue addresses strip 4 * grp + wave: block b is grp = b / 4 with this wave's slot b % 4
     auto issue = [&](int b) { strip_issue<32>(a, b >> 2, pz, ld, b & 3); };
-    issue(b0);
+    if (b0 < nblk) issue(b0);   // in flight under the bases' copy and the barrier
+    copy_basis_h(s_basis);
+    __syncthreads();
+    if (b0 >= nblk) return;   // whole wave
+    const int64_t poff = plane_off(a, pz);
     for (int k = 0; k < K; ++k) {
         const int b = b0 + k;
         if (b >= nblk) break;
@@ -1044,9 +1083,13 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
         if (k + 1 < K && b + 1 < nblk) issue(b + 1);
         wave_sync();
         if (wide) {
-            if (lane == 0) a.rec[poff + (int64_t)sy0 * a.pitch + sx0] = kWideMark;
+            if (lane == 0) {
+                a.rec[poff + (int64_t)sy0 * a.pitch + sx0] = kWideMark;
+                if (a.wide_flag) *a.wide_flag = a.epoch;   // the fix-up launch has work
+            }
         } else {
-            ctu_chain32_h(a, s_img[wv] + 4, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff);
+            ctu_chain32_h<TSTORE>(a, s_img[wv] + 4, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff,
+                                  TSTORE ? s_out[TSTORE ? wv : 0] : nullptr);
         }
         wave_sync();   // this wave's LDS reads of block k before block k+1's image writes
     }
@@ -1195,7 +1238,7 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
 
 // Config 5's narrow launch over one plane set (full 32x32 blocks only).
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
-                       int dqs, int dq_per, hipStream_t s) {
+                       int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s) {
     const int rc = ensure_basis_ctu();
     if (rc) return rc;
     CtuArgs a{};
@@ -1213,18 +1256,28 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     a.q[3] = q;
     a.dqs = dqs;
     a.dq_per = dq_per;
+    a.wide_flag = wide_flag;
+    a.epoch = epoch;
     const int nblk = a.strips_x * a.nrows, planes = S.planes_per_group * S.num_groups;
     if (!nblk || !planes) return NH_OK;
     // capped at 3 resident workgroups per CU: 0.137 vs 0.153 ms per 8K YUV420 frame
     // uncapped (5 per CU; 2 per CU: 0.164), DESIGN.md §4.5.  A/B build:
-    // NH_TC32H_K = blocks per wave (2 / 4), NH_TC32H_CAP = workgroups per CU.
-    static const int kk = NH_KNOB("NH_TC32H_K", 1), cap = NH_KNOB("NH_TC32H_CAP", 3);
+    // NH_TC32H_K = blocks per wave (2 / 4), NH_TC32H_CAP = workgroups per CU,
+    // NH_TC32H_FORM = bit 1 XCD-ordered grid, bit 2 whole-row output stores.
+    static const int kk = NH_KNOB("NH_TC32H_K", 1), cap = NH_KNOB("NH_TC32H_CAP", 3),
+                     form = NH_KNOB("NH_TC32H_FORM", 0);
     auto launch = [&](auto kern, int K) {
         kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, cap), s>>>(a, nblk);
     };
     if (NH_AB && kk == 2) launch(k_tc32_h<2>, 2);
     else if (NH_AB && kk == 4) launch(k_tc32_h<4>, 4);
+#if NH_AB
+    else if (form == 1) launch(k_tc32_h<1, true, false>, 1);
+    else if (form == 2) launch(k_tc32_h<1, false, true>, 1);
+    else if (form == 3) launch(k_tc32_h<1, true, true>, 1);
+#endif
     else launch(k_tc32_h<1>, 1);
+    (void)form;
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

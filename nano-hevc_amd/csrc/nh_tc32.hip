@@ -24,6 +24,8 @@
 //   B: lane l holds B[16(l>>5) + j][l&31]
 //   C/D: register g of lane l is D[(g&3) + 8(g>>2) + 4(l>>5)][l&31]
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <atomic>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 #include "nh_tree.hpp"
@@ -40,18 +42,20 @@ constexpr int kOP = 40;  // LDS row pitch (elements) of the per-wave tiles: 16-B
 // proceeds where the seeded quadtree's leaf is exactly 32x32 (tu_leaf); it
 // then also writes its 8x8 entries of the TU map.  Same per-TU chain as
 // k_tu_process<32>.
-// FIXUP (config 5, grid mode): code only the blocks k_tc32_h marked wide
-// (recon origin == -32768, nh_ctu.hip), every other wave exits at once.
-template <bool TREE, bool FIXUP = false>
-__global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ src, int w, int h, int pitch,
-                                                   int nbx, int nblk, QuantParams qp, int dq_scale, int dq_per,
-                                                   int32_t* lvl, int16_t* recon, TreeArgs ta, uint8_t* tu_log2) {
-    __shared__ int16_t s_orig[4][32][kOP];
-    __shared__ int32_t s_dq[4][32][kOP];
-    __shared__ int16_t s_top[4][32], s_left[4][32];
-    const int wv = threadIdx.x >> 6, l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
-    const int b = blockIdx.x * 4 + wv;
-    if (b >= nblk) return;                       // whole wave exits together
+// FIXUP (config 5): code only the blocks k_tc32_h marked wide (recon origin ==
+// -32768, nh_ctu.hip).  A small grid walks the blocks with stride gridDim.x * 4
+// waves, and returns at once unless k_tc32_h set *wide_flag to this launch's
+// epoch -- 8-bit content (no marked block) costs one small launch, not a wave
+// per block.
+
+// One 32x32 block b of the plane blockIdx.y: the chain of k_tc32_mfma, in this
+// wave's LDS tiles.
+template <bool TREE, bool FIXUP>
+__device__ __forceinline__ void tc32_block(const int16_t* __restrict__ src, int w, int h, int pitch, int nbx, int b,
+                                           QuantParams qp, int dq_scale, int dq_per, int32_t* lvl, int16_t* recon,
+                                           TreeArgs ta, uint8_t* tu_log2, int16_t (*s_orig_w)[kOP],
+                                           int32_t (*s_dq_w)[kOP], int16_t* s_top_w, int16_t* s_left_w) {
+    const int l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
     const ChainQ cq = make_chainq(qp, dq_scale, dq_per);   // 32-bit quant/dequant (int16 residual)
     {   // this workgroup's plane of the batch (blockIdx.y; ta.ppg >= 1)
         const int pz = blockIdx.y, gz = pz / ta.ppg, cz = pz - gz * ta.ppg;
@@ -78,31 +82,31 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
         const int row = l >> 1, half = l & 1;
         const int16_t* g = src + (int64_t)(y0 + row) * pitch + x0 + half * 16;
         v4i_t a0 = *(const v4i_t*)g, a1 = *(const v4i_t*)(g + 8);
-        *(v4i_t*)&s_orig[wv][row][half * 16] = a0;
-        *(v4i_t*)&s_orig[wv][row][half * 16 + 8] = a1;
-        if (hh == 0) s_top[wv][r] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + r];
-        else s_left[wv][r] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + r) * pitch + x0 - 1];
+        *(v4i_t*)&s_orig_w[row][half * 16] = a0;
+        *(v4i_t*)&s_orig_w[row][half * 16 + 8] = a1;
+        if (hh == 0) s_top_w[r] = y0 == 0 ? (int16_t)128 : src[(int64_t)(y0 - 1) * pitch + x0 + r];
+        else s_left_w[r] = x0 == 0 ? (int16_t)128 : src[(int64_t)(y0 + r) * pitch + x0 - 1];
     }
     // Each wave touches only its own LDS slices, and LDS executes one wave's
     // instructions in order: a wave barrier (no s_barrier) orders write -> read.
     __builtin_amdgcn_wave_barrier();
 
     // ---- DC (intra.py:46-62) and planar (intra.py:81-113) ----
-    const int32_t my_nb = hh == 0 ? s_top[wv][r] : s_left[wv][r];
+    const int32_t my_nb = hh == 0 ? s_top_w[r] : s_left_w[r];
     int32_t s = my_nb;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     const int32_t dc = (s + 32) >> 6;
-    const int32_t tr = s_top[wv][31], bl = s_left[wv][31];
+    const int32_t tr = s_top_w[31], bl = s_left_w[31];
     auto planar = [&](int y, int x) -> int32_t {
-        return ((31 - x) * s_left[wv][y] + (x + 1) * tr + (31 - y) * s_top[wv][x] + (y + 1) * bl + 32) >> 6;
+        return ((31 - x) * s_left_w[y] + (x + 1) * tr + (31 - y) * s_top_w[x] + (y + 1) * bl + 32) >> 6;
     };
     // this lane's operand slice of the block: column j = r, rows k = 16hh .. 16hh+15
     long long e_dc = 0, e_pl = 0;
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
         const int k = 16 * hh + jj;
-        const int32_t o = s_orig[wv][k][r];
+        const int32_t o = s_orig_w[k][r];
         const int32_t d1 = wrap16i(o - dc), d2 = wrap16i(o - planar(k, r));
         e_dc += (long long)d1 * d1;
         e_pl += (long long)d2 * d2;
@@ -117,7 +121,7 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
         const int k = 16 * hh + jj;
-        X[jj] = wrap16i((int32_t)s_orig[wv][k][r] - (use_dc ? dc : planar(k, r)));
+        X[jj] = wrap16i((int32_t)s_orig_w[k][r] - (use_dc ? dc : planar(k, r)));
     }
 
     // ---- forward pass 1: tempPre^T = X^T . T^T   (lane = i, registers = j) ----
@@ -143,14 +147,14 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
         for (int e = 0; e < 4; ++e) {
             const int g = 4 * q + e;
             L4[e] = quant_s(rshift_round<10>((uint32_t)acc[g]), cq.qs, cq.h_v, cq.hneg_v);
-            s_dq[wv][r][crow(g, hh)] = dequant_s(L4[e], cq);
+            s_dq_w[r][crow(g, hh)] = dequant_s(L4[e], cq);
         }
         *(v4i_t*)(lrow + 8 * q + 4 * hh) = v4i_t{L4[0], L4[1], L4[2], L4[3]};
     }
     __builtin_amdgcn_wave_barrier();
     // ---- inverse pass 1: temp2^T = dq^T . T   (A = dq^T via the LDS transpose) ----
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) X[jj] = s_dq[wv][16 * hh + jj][r];
+    for (int jj = 0; jj < 16; ++jj) X[jj] = s_dq_w[16 * hh + jj][r];
     acc = mfma_auto<true>(X, F3);
 #pragma unroll
     for (int g = 0; g < 16; ++g) V[g] = rshift_round<10>((uint32_t)acc[g]);   // transform.py:227
@@ -170,6 +174,28 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
         }
         *(uint2*)(rrow + 8 * q + 4 * hh) =
             make_uint2((uint16_t)R4[0] | ((uint32_t)(uint16_t)R4[1] << 16), (uint16_t)R4[2] | ((uint32_t)(uint16_t)R4[3] << 16));
+    }
+}
+
+template <bool TREE, bool FIXUP = false>
+__global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ src, int w, int h, int pitch,
+                                                   int nbx, int nblk, QuantParams qp, int dq_scale, int dq_per,
+                                                   int32_t* lvl, int16_t* recon, TreeArgs ta, uint8_t* tu_log2,
+                                                   const uint32_t* wide_flag = nullptr, uint32_t epoch = 0) {
+    __shared__ int16_t s_orig[4][32][kOP];
+    __shared__ int32_t s_dq[4][32][kOP];
+    __shared__ int16_t s_top[4][32], s_left[4][32];
+    const int wv = threadIdx.x >> 6;
+    if constexpr (FIXUP) {
+        if (*wide_flag != epoch) return;   // k_tc32_h left no block of this launch's planes to the fix-up
+        for (int b = blockIdx.x * 4 + wv; b < nblk; b += gridDim.x * 4)   // wave-uniform walk
+            tc32_block<TREE, true>(src, w, h, pitch, nbx, b, qp, dq_scale, dq_per, lvl, recon, ta, tu_log2, s_orig[wv],
+                                   s_dq[wv], s_top[wv], s_left[wv]);
+    } else {
+        const int b = blockIdx.x * 4 + wv;
+        if (b >= nblk) return;                       // whole wave exits together
+        tc32_block<TREE, false>(src, w, h, pitch, nbx, b, qp, dq_scale, dq_per, lvl, recon, ta, tu_log2, s_orig[wv],
+                                s_dq[wv], s_top[wv], s_left[wv]);
     }
 }
 
@@ -203,7 +229,31 @@ using namespace nh;
 // butterfly variant lives in nh_intraloop.hip; the narrow f16 launch in nh_ctu.hip
 namespace nh {
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
-                       int dqs, int dq_per, hipStream_t s);
+                       int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s);
+
+// Config 5's wide flags: a ring of words per device, one per f16 launch (slot =
+// epoch mod kFlagRing), so concurrent launches on other streams use other
+// slots.  k_tc32_h stores the launch's epoch into its slot when it leaves a
+// block to the int8 fix-up, which returns at once otherwise.
+constexpr uint32_t kFlagRing = 1024;
+static int wide_flag_slot(uint32_t** flag, uint32_t* epoch) {
+    static PerDeviceOnce once;
+    static uint32_t* ring[64] = {};
+    static std::atomic<uint32_t> next{1};
+    int dev = 0;
+    NH_HIP(hipGetDevice(&dev));
+    const int rc = once.run([&] {
+        NH_HIP(hipMalloc(&ring[dev], kFlagRing * sizeof(uint32_t)));
+        NH_HIP(hipMemset(ring[dev], 0, kFlagRing * sizeof(uint32_t)));   // epochs start at 1
+        return (int)NH_OK;
+    });
+    if (rc) return rc;
+    uint32_t e = next.fetch_add(1);
+    if (e == 0) e = next.fetch_add(1);   // 0 never names a launch (the ring's initial value)
+    *epoch = e;
+    *flag = ring[dev] + (e % kFlagRing);
+    return NH_OK;
+}
 int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
                    hipStream_t s);
 }
@@ -271,11 +321,18 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
         ta.plane_stride = S.plane_stride;
         const dim3 grid((nblk + 3) / 4, planes);
         if (variant == 1) {   // narrow blocks on the f16 matrix cores, then the marked wide ones on int8
-            int rc = tc32_narrow_launch(d_src, d_lvl, d_recon, S, p, dequant_scale(rem), per, s);
+            uint32_t* flag = nullptr;
+            uint32_t epoch = 0;
+            int rc = wide_flag_slot(&flag, &epoch);
             if (rc) return rc;
-            k_tc32_mfma<false, true><<<grid, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
+            rc = tc32_narrow_launch(d_src, d_lvl, d_recon, S, p, dequant_scale(rem), per, flag, epoch, s);
+            if (rc) return rc;
+            int cus = 0;
+            NH_TRY(device_cus(&cus));
+            const dim3 gfix((unsigned)std::min<int64_t>((nblk + 3) / 4, 2 * cus), (unsigned)planes);
+            k_tc32_mfma<false, true><<<gfix, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
                                                           dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base,
-                                                          ta, nullptr);
+                                                          ta, nullptr, flag, epoch);
         } else {              // int8 matrix cores only (A/B)
             k_tc32_mfma<false><<<grid, 256, lds_cap(k_tc32_mfma<false>, NH_KNOB("NH_CAP_TC32", 0)), s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
                                                     dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base, ta,

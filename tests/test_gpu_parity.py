@@ -542,6 +542,35 @@ def test_tc32_mfma_equals_butterfly_and_oracle(nh, torch_dev, kind):
             assert np.array_equal(r.cpu().numpy(), er), (kind, qp, v)
 
 
+def test_tc32_fixup_walks_every_marked_block(nh, torch_dev):
+    """Variant 1 on planes where every (or every other) 32x32 block is wide: the
+    int8 fix-up launch (a small grid walking the blocks, k_tc32_mfma<.., FIXUP>)
+    must code each marked block -- thousands per plane, many per wave -- exactly
+    as the int8-only launch (variant 2) does; the oracle checks a corner."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(77)
+    nf, w, h = 2, 3840, 2160
+    sets = gpu.yuv420_plane_sets(nf, w, h)
+    fe = gpu.yuv420_frame_elems(w, h)
+    buf = rng.integers(0, 256, size=nf * fe).astype(np.int16)
+    buf[:w * h] = rng.integers(-32768, 32768, size=w * h)          # frame 0 luma: every block wide
+    cb = buf[fe:fe + w * h].reshape(h, w)
+    cb[::64, ::64] = 999                                            # frame 1 luma: every other block row/col wide
+    d = torch.from_numpy(buf).cuda()
+    outs = []
+    for v in (1, 2):
+        lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+        rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+        gpu.tc32_planes(d, sets, 30, v, lvl=lvl, rec=rec)
+        outs.append((lvl, rec))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    corner = buf[:w * h].reshape(h, w)[:64, :96]
+    el, er = O.tc32_plane(corner.copy(), 30)
+    got = outs[0][1][:w * h].view(h, w)[:64, :96].cpu().numpy()
+    assert np.array_equal(got, er)
+
+
 @pytest.mark.parametrize("variant", [1, 2, 0])
 def test_tc32_planes_stream_equals_per_plane_and_oracle(nh, torch_dev, variant):
     """Config 5 batched over a ragged YUV420 frame stream (one MFMA launch per

@@ -203,7 +203,11 @@ def main():
         print(json.dumps({"config": "cfg5 batched: 8K YUV420 frame stream, f16 MFMA launch + int8 fix-up per plane set",
                           "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "blocks_per_s": nblk / ms * 1e3,
                           "samples_per_s": nf * fe / ms * 1e3, "bytes_per_sample": 8,
-                          "achieved_GBps": nf * fe * 8 / ms / 1e6, "psnr_y_frame0": psnr_dev(stream5[:W * H], rc5[:W * H])}),
+                          "achieved_GBps": nf * fe * 8 / ms / 1e6, "psnr_y_frame0": psnr_dev(stream5[:W * H], rc5[:W * H]),
+                          "knobs": knobs,
+                          "out_digest": [int(lv5.to(torch.int64).sum().item()), int(rc5.to(torch.int64).sum().item()),
+                                         int((lv5.to(torch.int64) * torch.arange(lv5.numel(), device="cuda") % 1000003)
+                                             .sum().item())]}),
               flush=True)
 
     if 5 in cfgs:
