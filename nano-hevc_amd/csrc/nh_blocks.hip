@@ -496,9 +496,32 @@ static inline int64_t now_ns() {
         .count();
 }
 
+// The small form's status / accumulator words live in LDS (one workgroup): no
+// device-memory reset and no agent-scope fence before the body.  After the body
+// every wave waits for its own output stores (s_waitcnt 0) before the barrier,
+// then one lane publishes status, accumulator and -- with a system-scope
+// release -- the completion word.  (NH_SMALL_OLD builds the previous form:
+// device-memory words reset under __threadfence(), a system fence per wave.)
 template <class F, size_t SZ>
 __global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned long long* dw, unsigned long long* hres,
                                                unsigned long long seq) {
+#ifndef NH_SMALL_OLD
+    (void)dw;
+    __shared__ unsigned long long s_w[2];
+    if (threadIdx.x == 0) {
+        s_w[0] = ULLONG_MAX;   // status: no error yet
+        s_w[1] = 0ull;         // accumulator of the reductions
+    }
+    __syncthreads();
+    f(in.b, s_w, (uint8_t*)(hres + 4));
+    __builtin_amdgcn_s_waitcnt(0);        // this wave's result stores acknowledged
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        hres[0] = s_w[0];
+        hres[1] = s_w[1];
+        __hip_atomic_store(&hres[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // completion word, last
+    }
+#else
     if (threadIdx.x == 0) {
         atomicExch(&dw[0], ULLONG_MAX);   // status: no error yet
         atomicExch(&dw[1], 0ull);         // accumulator of the reductions
@@ -514,6 +537,7 @@ __global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned lon
         __threadfence_system();
         __hip_atomic_store(&hres[2], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // completion word, last
     }
+#endif
 }
 
 template <class F>

@@ -1263,7 +1263,8 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     // capped at 3 resident workgroups per CU: 0.137 vs 0.153 ms per 8K YUV420 frame
     // uncapped (5 per CU; 2 per CU: 0.164), DESIGN.md §4.5.  A/B build:
     // NH_TC32H_K = blocks per wave (2 / 4), NH_TC32H_CAP = workgroups per CU,
-    // NH_TC32H_FORM = bit 1 XCD-ordered grid, bit 2 whole-row output stores.
+    // NH_TC32H_FORM = 1 XCD-ordered grid, 3 the same with whole-row stores,
+    // 4 row-piece stores from registers (the round-2 form).
     static const int kk = NH_KNOB("NH_TC32H_K", 1), cap = NH_KNOB("NH_TC32H_CAP", 3),
                      form = NH_KNOB("NH_TC32H_FORM", 0);
     auto launch = [&](auto kern, int K) {
@@ -1273,10 +1274,12 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     else if (NH_AB && kk == 4) launch(k_tc32_h<4>, 4);
 #if NH_AB
     else if (form == 1) launch(k_tc32_h<1, true, false>, 1);
-    else if (form == 2) launch(k_tc32_h<1, false, true>, 1);
+    else if (form == 4) launch(k_tc32_h<1, false, false>, 1);
     else if (form == 3) launch(k_tc32_h<1, true, true>, 1);
 #endif
-    else launch(k_tc32_h<1>, 1);
+    // whole-row output stores: 0.106 vs 0.125 ms per 8K YUV420 frame (forms 2 vs 0 of
+    // profiles/r03/cfg5/ab_tc32h_forms.jsonl; the XCD-ordered grid is slower, 0.132)
+    else launch(k_tc32_h<1, false, true>, 1);
     (void)form;
     NH_HIP(hipGetLastError());
     return NH_OK;
