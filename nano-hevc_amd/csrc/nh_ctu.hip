@@ -253,10 +253,14 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
 // natural order into the forward row pass, inv_slot order (line = column) into
 // both inverse passes, so no pass permutes.  Same results as ctu_chain for
 // such TUs (bounds: tools/packed_bounds.py).
-template <int N, bool DST, int CTB>
+// OST: levels and recon go to the group's LDS output images (olvl / orec: strip
+// sw's rows of SW at sw * CTB * SW), written out in whole rows after the
+// group's batches (strip_writeout).
+template <int N, bool DST, int CTB, bool OST = false>
 __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_img, int16_t* s_t16, const uint16_t* list,
                                              int cnt, int b0, const int* s_org, int32_t* __restrict__ lvl,
-                                             int16_t* __restrict__ rec) {
+                                             int16_t* __restrict__ rec, int32_t* olvl = nullptr,
+                                             int16_t* orec = nullptr) {
     using G = Strip<CTB>;
     constexpr int L2 = Log2<N>::v, S = L2 + 5, IP = G::IP, TP = G::TP, H = N / 2;
     constexpr int32_t BIAS = 1 << (S - 1);
@@ -329,7 +333,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
         fwd1d_pk<N, DST>(P, y, BIAS);
     }
     if (on) {
-        int32_t* lrow = lvl + (int64_t)(gy0 + t) * a.pitch + gx0;
+        int32_t* lrow = OST ? olvl + sw * (CTB * G::SW) + (ly + t) * G::SW + lx : lvl + (int64_t)(gy0 + t) * a.pitch + gx0;
 #pragma unroll
         for (int k0 = 0; k0 < N; k0 += 4) {
             int32_t L4[4];
@@ -379,7 +383,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
             const pk16 rc = pred + pk_pair(x[2 * m] >> S, x[2 * m + 1] >> S);
             pk[m] = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_max(rc, zero), maxv));
         }
-        int16_t* rrow = rec + (int64_t)(gy0 + t) * a.pitch + gx0;
+        int16_t* rrow = OST ? orec + sw * (CTB * G::SW) + (ly + t) * G::SW + lx : rec + (int64_t)(gy0 + t) * a.pitch + gx0;
 #pragma unroll
         for (int m = 0; m < H; m += 2) st_rec4(rrow + 2 * m, make_uint2(pk[m], pk[m + 1]));
     }
@@ -537,7 +541,8 @@ template <bool TSTORE = false>
 __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, const BasisH& bs,
                                               int gx0, int gy0,
                                               int32_t* __restrict__ lvl, int16_t* __restrict__ rec,
-                                              int32_t* ot = nullptr) {
+                                              int32_t* ot = nullptr, int64_t opitch = -1) {
+    const int64_t op = opitch >= 0 ? opitch : (int64_t)a.pitch;   // row pitch of lvl / rec (an LDS image's: OST)
     constexpr int IP = Strip<32>::IP, QH = Strip<32>::QH;   // img[r * IP + c]: sample (r - 1, c), c = -1: left
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
     const int l = opaque_lane(), r = l & 31, hh = l >> 5;
@@ -595,7 +600,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 0, hh), acc_h8(acc, 0, b1), acc2, 0, 0, 0);
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 1, hh), acc_h8(acc, 1, b1), acc2, 0, 0, 0);
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
-    int32_t* lrow = lvl + (int64_t)(gy0 + r) * a.pitch + gx0;
+    int32_t* lrow = lvl + (int64_t)(gy0 + r) * op + gx0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         int32_t L4[4];
@@ -613,7 +618,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int rr = (l >> 3) + 8 * i, c = 4 * (l & 7);
-            st_lvl4(lvl + (int64_t)(gy0 + rr) * a.pitch + gx0 + c, *(const int4*)&ot[rr * kOutP + c]);
+            st_lvl4(lvl + (int64_t)(gy0 + rr) * op + gx0 + c, *(const int4*)&ot[rr * kOutP + c]);
         }
         wave_sync();   // the tile's reads before the recon tile reuses it
     }
@@ -628,7 +633,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 0, hh), acc_h8(acc3, 0, 0.5f), acc4, 0, 0, 0);
     acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 1, hh), acc_h8(acc3, 1, 0.5f), acc4, 0, 0, 0);
     // reconstruct + clip (intra.py:70-78), row y = r
-    int16_t* rrow = rec + (int64_t)(gy0 + r) * a.pitch + gx0;
+    int16_t* rrow = rec + (int64_t)(gy0 + r) * op + gx0;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         int32_t R4[4];
@@ -649,14 +654,14 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int rr = (l >> 2) + 16 * i, c = 4 * (l & 3);
-            *(uint4*)(rec + (int64_t)(gy0 + rr) * a.pitch + gx0 + 2 * c) = *(const uint4*)&ot[rr * kRecP + c];
+            *(uint4*)(rec + (int64_t)(gy0 + rr) * op + gx0 + 2 * c) = *(const uint4*)&ot[rr * kRecP + c];
         }
     }
 }
 
 // Shared memory of one workgroup = GS strips (a group).  Narrow kernels keep
 // the coefficient tile in int16 (half the LDS: more workgroups per CU).
-template <int CTB, bool NARROW, bool BASIS = false, int GS = 4> struct CtuSmem {
+template <int CTB, bool NARROW, bool BASIS = false, int GS = 4, bool OST = false> struct CtuSmem {
     using G = Strip<CTB>;
     struct Empty {};
     static constexpr int TILE32 = NARROW ? (GS * G::T16 + 1) / 2 : GS * G::CF;
@@ -665,6 +670,9 @@ template <int CTB, bool NARROW, bool BASIS = false, int GS = 4> struct CtuSmem {
     uint16_t list[4][64 * GS];   // per TU size: entry = strip << 6 | unit
     int cnt[GS][4], org[2 * GS], next, wide[GS];
     std::conditional_t<BASIS, BasisH, Empty> basis;   // ctu_chain32_h's f16 bases
+    // OST: the group's level / recon images, strip-major rows of SW (whole-row stores at the end)
+    __attribute__((aligned(16))) int32_t olvl[OST ? GS * CTB * G::SW : 4];
+    __attribute__((aligned(16))) int16_t orec[OST ? GS * CTB * G::SW : 8];
 };
 
 // One group of 4 strips (one per wave for loading and classification); the
@@ -815,6 +823,32 @@ __device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* i
     return valid && (hi_bits & 0xff00ff00u) != 0;
 }
 
+// OST: a strip's level / recon rows from the group's LDS images to the plane in
+// whole rows -- a wave instruction writes 1 KiB of contiguous row segments
+// (16 B per lane) instead of 16-128 B pieces of N rows.
+template <int CTB>
+__device__ __forceinline__ void strip_writeout(const CtuArgs& a, int sx0, int sy0, const int32_t* ol, const int16_t* orr,
+                                               int32_t* lvl, int16_t* rec) {
+    constexpr int SW = Strip<CTB>::SW;
+    const int lane = threadIdx.x & 63, w = a.w, h = a.h;
+    const int64_t pitch = a.pitch;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // CTB * SW int32 = 256 pieces of 16 B
+        const int c = 64 * i + lane, r = c / (SW / 4), x = 4 * (c % (SW / 4));
+        if (sy0 + r < h && sx0 + x < w) st_lvl4(lvl + (int64_t)(sy0 + r) * pitch + sx0 + x, *(const int4*)&ol[r * SW + x]);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {   // CTB * SW int16 = 128 pieces of 16 B
+        const int c = 64 * i + lane, r = c / (SW / 8), x = 8 * (c % (SW / 8));
+        if (sy0 + r < h && sx0 + x < w) {
+            const uint4 v = *(const uint4*)&orr[r * SW + x];
+            int16_t* p = rec + (int64_t)(sy0 + r) * pitch + sx0 + x;
+            if (sx0 + x + 8 <= w) *(uint4*)p = v;
+            else st_rec4(p, make_uint2(v.x, v.y));   // w % 4 == 0: the last 4 samples of a row
+        }
+    }
+}
+
 // MFMA32: the 32x32 TUs on the matrix cores, one per batch (narrow: f16,
 // ctu_chain32_h; wide: int8, ctu_chain32 -- A/B forms); otherwise two per
 // batch on 32-point butterflies.
@@ -830,9 +864,9 @@ __device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* i
 // the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
 // !NARROW: the 32-bit chain, any int16 input.
 // Returns with the workgroup's waves in the batch loop's exit (no barrier).
-template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, class Prefetch>
+template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, bool OST = false, class Prefetch>
 __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
-                                          CtuSmem<CTB, NARROW, NARROW && MFMA32, GS>& sm, StripLoad<CTB>& ld,
+                                          CtuSmem<CTB, NARROW, NARROW && MFMA32, GS, OST>& sm, StripLoad<CTB>& ld,
                                           Prefetch&& prefetch) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
@@ -912,7 +946,8 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
     const int total = n32 + n16 + n8 + n4;
 #define NH_CHAIN(N, DST, L, B)                                                                              \
     if constexpr (NARROW)                                                                                   \
-        ctu_chain_pk<N, DST, CTB>(a, sm.img, (int16_t*)sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec);   \
+        ctu_chain_pk<N, DST, CTB, OST>(a, sm.img, (int16_t*)sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec, \
+                                       sm.olvl, sm.orec);                                                   \
     else                                                                                                    \
         ctu_chain<N, DST, CTB>(a, sm.img, sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec);
     for (;;) {
@@ -924,8 +959,12 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
             if (item < n32) {
                 if constexpr (NARROW && MFMA32) {   // one TU per wave on the f16 matrix cores
                     const int e = sm.list[3][item], sw = e >> 6;
-                    ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.basis, sm.org[2 * sw],
-                                  sm.org[2 * sw + 1], lvl, rec);
+                    if constexpr (OST)
+                        ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.basis, 0, 0,
+                                      sm.olvl + sw * (CTB * G::SW), sm.orec + sw * (CTB * G::SW), nullptr, G::SW);
+                    else
+                        ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.basis,
+                                      sm.org[2 * sw], sm.org[2 * sw + 1], lvl, rec);
                 } else if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores (A/B form)
                     const int e = sm.list[3][item], sw = e >> 6;
                     ctu_chain32(a, sm.img + sw * G::IMG + 4, sm.tile + sw * G::CF, sm.org[2 * sw], sm.org[2 * sw + 1],
@@ -954,6 +993,10 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
         NH_CHAIN(4, LUMA, 0, 16 * item)
     }
 #undef NH_CHAIN
+    if constexpr (OST) {   // every TU of the group is coded: each wave writes its strip out in whole rows
+        __syncthreads();
+        if (valid) strip_writeout<CTB>(a, sx0, sy0, sm.olvl + wv * (CTB * G::SW), sm.orec + wv * (CTB * G::SW), lvl, rec);
+    }
 }
 
 // The config-4 kernel proper, packed chain, 32x32 TUs on packed butterflies
@@ -961,9 +1004,9 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
 // resident workgroups walking the (group, plane) items with stride gridDim.x,
 // each group's loads issued during the previous group's chains.
 // WAVES: the occupancy floor (waves/SIMD) the registers are allocated for.
-template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4>
+template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4, bool OST = false>
 __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
-    __shared__ CtuSmem<CTB, true, MFMA32, GS> sm;
+    __shared__ CtuSmem<CTB, true, MFMA32, GS, OST> sm;
     if (NH_AB && (a.probe & 4)) return;   // A/B probe: the launch of the grid alone
     if constexpr (PERSIST == 0) {
         // the bases' loads issued with the strip's and written to LDS after the
@@ -976,7 +1019,7 @@ __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WA
         }
         StripLoad<CTB> ld;
         strip_issue<CTB, GS>(a, blockIdx.x, blockIdx.y, ld);
-        ctu_group<CTB, LUMA, true, MFMA32, GS>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
+        ctu_group<CTB, LUMA, true, MFMA32, GS, OST>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
             if constexpr (MFMA32) {
                 if (bthr) ((uint4*)&sm.basis)[threadIdx.x] = bq;
             }
@@ -992,7 +1035,7 @@ __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WA
         for (; it < items; it += gridDim.x) {
             const int nx = it + gridDim.x;
             if constexpr (PERSIST == 2) strip_issue<CTB, GS>(a, it % gcount, it / gcount, ld);
-            ctu_group<CTB, LUMA, true, MFMA32, GS>(a, it % gcount, it / gcount, sm, ld, [&] {
+            ctu_group<CTB, LUMA, true, MFMA32, GS, OST>(a, it % gcount, it / gcount, sm, ld, [&] {
                 if (PERSIST == 1 && nx < items) strip_issue<CTB, GS>(a, nx % gcount, nx / gcount, ld);
             });
             __syncthreads();   // every wave done with this group's LDS
@@ -1170,6 +1213,9 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // A/B build: NH_CTU_GS = 4 / 6 / 8, NH_CTU_CAP = workgroups per CU,
     // NH_OCC_CAP = 0 uncapped.
     static const int gs_knob = NH_KNOB("NH_CTU_GS", 4), cap_knob = NH_KNOB("NH_CTU_CAP", 0);
+    // A/B build: NH_CTU_OST = bit 1 luma / bit 2 chroma with whole-row output stores (LDS output images)
+    static const int ost_knob = NH_KNOB("NH_CTU_OST", 0);
+    (void)ost_knob;
     auto launch_open = [&](auto kern, auto gs_c) -> int {
         constexpr int GSZ = decltype(gs_c)::value;
         const int64_t ngrp = (strips + GSZ - 1) / GSZ;
@@ -1199,10 +1245,12 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         using G4 = std::integral_constant<int, 4>;
         if constexpr (NH_AB != 0) {
             const bool m = M32 && t32 != 0;
+            const bool ost_on = (ost_knob & (L ? 1 : 2)) != 0;
             if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>, G4{})
                          : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>, G4{})
                          : gs_knob == 6 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 6>, std::integral_constant<int, 6>{})
                          : gs_knob == 8 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 8>, std::integral_constant<int, 8>{})
+                         : ost_on       ? launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4, true>, G4{})
                                         : launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4>, G4{});
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>, G4{})
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>, G4{})
