@@ -1260,8 +1260,12 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else {
-            // register budget = the occupancy the cap allows (3 / 4 waves per SIMD)
-            rc3 = launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4>, G4{});
+            // register budget = the occupancy the cap allows (3 / 4 waves per SIMD); chroma
+            // (CTB 16) writes its outputs through LDS images in whole rows: 36.8-37.5 vs
+            // 37.7-38.3 us per 4K YUV420 frame, luma does not gain (40.0-40.5,
+            // profiles/r03/cfg4/ab_ctu_ost.jsonl)
+            if constexpr (C == 32) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4>, G4{});
+            else rc3 = launch_open(k_ctu_open<C, L, M32, 0, 4, 4, true>, G4{});
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         }
         return rc3;
@@ -1318,8 +1322,8 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     auto launch = [&](auto kern, int K) {
         kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, cap), s>>>(a, nblk);
     };
-    if (NH_AB && kk == 2) launch(k_tc32_h<2>, 2);
-    else if (NH_AB && kk == 4) launch(k_tc32_h<4>, 4);
+    if (NH_AB && kk == 2) launch(k_tc32_h<2, false, true>, 2);
+    else if (NH_AB && kk == 4) launch(k_tc32_h<4, false, true>, 4);
 #if NH_AB
     else if (form == 1) launch(k_tc32_h<1, true, false>, 1);
     else if (form == 4) launch(k_tc32_h<1, false, false>, 1);

@@ -39,6 +39,8 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# kernels of the measuring harness, not of a config (bench_configs' PSNR reduction)
+HARNESS = ("k_sse_i16",)
 
 # bench_configs config -> (profile key, anchor kernel, anchor dispatches per frame)
 CONFIGS = {
@@ -46,7 +48,7 @@ CONFIGS = {
     "closed": ("cfg3_closed_1080p_yuv420", "k_intra_rdo8_closed_tag<1, 1>", 1 / 64),
     "4b": ("cfg4_4k_yuv420", "k_ctu_open<32", 1 / 16),
     "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair", 2 / 64),
-    "5b": ("cfg5_8k_yuv420", "k_tc32_h<1>", 2 / 8),
+    "5b": ("cfg5_8k_yuv420", "k_tc32_h<1", 2 / 8),
 }
 
 
@@ -60,7 +62,7 @@ def kernel_times(d):
     out = {}
     if p:
         for r in csv.DictReader(open(p)):
-            if "nh::" in r["Name"]:
+            if "nh::" in r["Name"] and not any(k in r["Name"] for k in HARNESS):
                 out[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
     return out, p
 
@@ -70,7 +72,7 @@ def counters(d):
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     if p:
         for r in csv.DictReader(open(p)):
-            if "nh::" in r["Kernel_Name"]:
+            if "nh::" in r["Kernel_Name"] and not any(k in r["Kernel_Name"] for k in HARNESS):
                 per[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {}
     for k, d2 in per.items():
