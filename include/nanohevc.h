@@ -48,6 +48,18 @@ int nh_release_staging(void);
  * [1] launch (the launch API calls), [2] wait (launch returned -> completion
  * seen), [3] finish (outputs copied back).  Diagnostics (tools/percall.py). */
 int nh_last_call_times(int64_t* ns);
+/* The block-call server: while per-block calls keep coming,
+ * one resident workgroup per device takes them from mapped host memory instead
+ * of a kernel launch per call; it leaves after the idle time (default 200 us)
+ * without a call.  set_idle_us: that time for servers launched from now on
+ * (0 = never start one: every call is its own launch; 0 also stops the resident
+ * ones).  stop: ask every resident server to leave now and wait for it.
+ * stats (device): [0] calls served, [1] server launches, [2] calls run as their
+ * own kernel (k_small / staged), [3] the idle time in us.  Runtime control, no
+ * reference counterpart. */
+int nh_block_server_set_idle_us(int64_t us);
+int nh_block_server_stop(void);
+int nh_block_server_stats(int device, int64_t* out);
 
 /* ---------------- (i) per-block entry points (host pointers) ---------------- */
 

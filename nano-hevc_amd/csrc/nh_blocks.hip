@@ -14,6 +14,7 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstddef>
 #include <type_traits>
 #include <cstdio>
 #include <cstring>
@@ -545,6 +546,130 @@ __global__ void __launch_bounds__(256) k_staged(const uint8_t* in, F f, unsigned
     f(in, dw, out);
 }
 
+// ---------------------------------------------------------------------------
+// The block-call server: the small form without a launch per call.
+// ---------------------------------------------------------------------------
+// A per-block call spends most of its time in the launch API (~3.5 us) and in
+// the dispatch of a fresh kernel.  While calls keep coming, one workgroup of
+// k_srv stays resident instead and polls a request word in mapped pinned host
+// memory.  The host writes the inputs, the call's captures and the device
+// address of the body's thunk, then the request word (release):
+// seq << 12 | flags << 8 | input bytes / 16.  The server then takes thunk
+// address, captures and inputs into LDS in ONE round trip of parallel loads
+// (the word already told it how many), calls the body through the thunk (an
+// indirect call), waits for its wave's result stores, and after the barrier one
+// lane publishes the completion word seq << 8 | error code with a system-scope
+// release -- preceded, for reductions (flag 1), by the accumulator into the
+// first output word.  PCIe round trips per call: poll, intake, result
+// acknowledgement (+1 for reductions).  The server leaves -- writing its epoch
+// into `exited`, its last act -- when no request came for `idle` ticks of the
+// 100 MHz constant clock, after `life` ticks in total, after kSrvMaxPolls
+// polls, or on a stop request (thunk address 0).  Every exit path is reached by
+// every wave, so the grid always drains.  The host relaunches it when it finds
+// `exited` equal to the epoch it launched with and the call's completion word
+// unwritten.  Bodies with large LDS tiles (the transforms) or stack (the float64
+// pairwise sums) stay on k_small: a kernel with an indirect call allocates the
+// LDS of every address-taken callee and cannot size its stack.
+constexpr size_t kSrvCap = 128;                       // bytes of a body's captures
+constexpr unsigned kSrvMaxPolls = 50u * 1000u * 1000u;
+constexpr unsigned long long kSrvFlagAcc = 1;         // flags: write the accumulator to output word 0
+typedef void (*SrvFn)(const uint8_t*, unsigned long long*, uint8_t*, const uint8_t*);
+
+struct SrvReq {                        // mapped pinned host memory, 64-byte lines
+    unsigned long long word;           // host: seq << 12 | flags << 8 | input bytes / 16, written last
+    unsigned long long pad0[7];
+    unsigned long long exited;         // server: the epoch it left with (its last store)
+    unsigned long long pad1[7];
+    unsigned long long done;           // server: seq << 8 | error code (0 = ok), the call's last store
+    unsigned long long pad2[7];
+    unsigned long long fn;             // host: device address of srv_thunk<F>; 0 = stop
+    unsigned long long pad3[7];
+    alignas(16) uint8_t cap[kSrvCap];  // host: the body's captures
+    alignas(16) uint8_t in[kSmallIn];  // host: the inputs
+};
+constexpr unsigned kSrvFnWord = offsetof(SrvReq, fn) / 8, kSrvCapWord = offsetof(SrvReq, cap) / 8;
+static_assert(offsetof(SrvReq, in) == offsetof(SrvReq, cap) + kSrvCap, "captures and inputs are contiguous");
+
+template <class F>
+__device__ __attribute__((noinline)) void srv_thunk(const uint8_t* in, unsigned long long* st, uint8_t* o,
+                                                    const uint8_t* cap) {
+    (*reinterpret_cast<const F*>(cap))(in, st, o);
+}
+template <class F>
+__global__ void k_srv_addr(unsigned long long* out) {
+    out[0] = (unsigned long long)(SrvFn)&srv_thunk<F>;
+}
+
+__device__ __forceinline__ unsigned long long ld_sys(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void __launch_bounds__(256) k_srv(SrvReq* q, unsigned long long* hout, unsigned long long last,
+                                              unsigned long long epoch, unsigned long long idle,
+                                              unsigned long long life) {
+    __shared__ alignas(16) unsigned long long s_ci[(kSrvCap + kSmallIn) / 8];   // captures | inputs
+    __shared__ unsigned long long s_fn;
+    __shared__ unsigned long long s_w[2];
+    __shared__ unsigned long long s_word;     // the request word taken (== last: leave)
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long* qw = (const unsigned long long*)q;
+    unsigned polls = 0;
+    for (;;) {
+        if (threadIdx.x == 0) {
+            const unsigned long long t_idle = __builtin_amdgcn_s_memrealtime();
+            unsigned long long v = last;
+            for (;;) {
+                v = __hip_atomic_load(&q->word, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (v != last) break;
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (now - t_idle > idle || now - t_start > life || ++polls > kSrvMaxPolls) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_word = v;
+            s_w[0] = ULLONG_MAX;   // status: no error yet
+            s_w[1] = 0ull;         // accumulator of the reductions
+        }
+        __syncthreads();
+        const unsigned long long word = s_word;
+        if (word == last) {   // idle, lifetime or poll cap
+            if (threadIdx.x == 0) __hip_atomic_store(&q->exited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        // intake: thunk address, captures and inputs, one round of parallel loads
+        const unsigned nwords = (unsigned)(kSrvCap / 8 + 2 * (word & 0xff) < (kSrvCap + kSmallIn) / 8
+                                               ? kSrvCap / 8 + 2 * (word & 0xff) : (kSrvCap + kSmallIn) / 8);
+        static_assert((kSrvCap + kSmallIn) / 8 <= 2 * 256, "intake: two words per thread");
+        {   // every load issued before the first use
+            const unsigned i0 = threadIdx.x, i1 = threadIdx.x + 256;
+            unsigned long long a = 0, b = 0, c = 0;
+            if (i0 < nwords) a = ld_sys(qw + kSrvCapWord + i0);
+            if (i1 < nwords) b = ld_sys(qw + kSrvCapWord + i1);
+            if (threadIdx.x == 0) c = ld_sys(qw + kSrvFnWord);
+            if (i0 < nwords) s_ci[i0] = a;
+            if (i1 < nwords) s_ci[i1] = b;
+            if (threadIdx.x == 0) s_fn = c;
+        }
+        __syncthreads();
+        const unsigned long long fn = s_fn;
+        if (fn == 0) {   // stop request
+            if (threadIdx.x == 0) __hip_atomic_store(&q->exited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        const SrvFn f = (SrvFn)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(fn >> 32)) << 32) |
+                                (unsigned)__builtin_amdgcn_readfirstlane((unsigned)fn));
+        f((const uint8_t*)(s_ci + kSrvCap / 8), s_w, (uint8_t*)hout, (const uint8_t*)s_ci);
+        __builtin_amdgcn_s_waitcnt(0);        // this wave's result stores acknowledged
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned long long st = s_w[0];
+            if ((word >> 8) & kSrvFlagAcc) hout[0] = s_w[1];
+            __hip_atomic_store(&q->done, ((word >> 12) << 8) | (st == ULLONG_MAX ? 0ull : (st & 0xff)),
+                               __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // completion word, last
+        }
+        last = word;
+    }
+}
+
 struct Staging {
     std::mutex mu;
     bool ready = false;
@@ -557,6 +682,12 @@ struct Staging {
                                           //             status, accumulator, completion word, pad, outputs
     unsigned long long seq = 0;           //             completion sequence number of the last call
     uint8_t* hres_dev = nullptr;          //             the same memory, device view
+    SrvReq* req = nullptr;                // block-call server: request block (host view)
+    SrvReq* req_dev = nullptr;            //                    the same memory, device view
+    unsigned long long epoch = 0;         //                    epoch of the last server launched
+    bool srv_alive = false;               //                    launched and not known to have left
+    unsigned long long clock_khz = 100000;  //                    the constant clock k_srv times itself with
+    int64_t n_served = 0, n_launches = 0, n_kernel = 0;   // nh_block_server_stats
 };
 constexpr int kMaxDevices = 64;
 static Staging g_staging[kMaxDevices];
@@ -587,13 +718,21 @@ static void staging_free(Staging& s) {   // caller holds s.mu, current device = 
     if (s.hbuf) (void)hipHostFree(s.hbuf);
     if (s.dwork) (void)hipFree(s.dwork);
     if (s.hres) (void)hipHostFree(s.hres);
+    if (s.req) (void)hipHostFree(s.req);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s.dbuf = s.hbuf = s.hres = s.hres_dev = nullptr;
+    s.req = s.req_dev = nullptr;
+    s.srv_alive = false;
     s.dwork = nullptr;
     s.stream = nullptr;
     s.cap = 0;
     s.ready = false;
 }
+
+// Idle time after which the block-call server leaves (us; default 200, 0 = no
+// server: every small call is a k_small launch).  nh_block_server_set_idle_us().
+static std::atomic<long> g_srv_idle_us{200};
+static long server_idle_us() { return g_srv_idle_us.load(std::memory_order_relaxed); }
 
 static int staging_init(Staging& s) {    // caller holds s.mu
     if (s.ready) return NH_OK;
@@ -603,7 +742,61 @@ static int staging_init(Staging& s) {    // caller holds s.mu
     std::memset(s.hres, 0, 32);
     s.seq = 0;
     NH_HIP(hipHostGetDevicePointer((void**)&s.hres_dev, s.hres, 0));
+    NH_HIP(hipHostMalloc((void**)&s.req, sizeof(SrvReq), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset((void*)s.req, 0, sizeof(SrvReq));
+    NH_HIP(hipHostGetDevicePointer((void**)&s.req_dev, s.req, 0));
+    int dev = 0, khz = 0;
+    NH_HIP(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+    s.clock_khz = (unsigned long long)khz;
+    s.epoch = 0;
+    s.srv_alive = false;
     s.ready = true;
+    return NH_OK;
+}
+
+// Posts a stop request to a resident server (no wait: launches that follow on
+// the context's stream queue behind its exit).  Caller holds s.mu.
+static void server_post(Staging& s, unsigned long long word) {
+    __atomic_store_n(&s.req->word, word, __ATOMIC_RELEASE);
+}
+
+static void server_stop(Staging& s) {
+    if (!s.srv_alive) return;
+    s.req->fn = 0;
+    server_post(s, ++s.seq << 12);
+    s.srv_alive = false;
+}
+
+// Launches a server that takes the request word now posted (last = anything else).
+static int server_launch(Staging& s, unsigned long long word) {
+    const unsigned long long idle = (unsigned long long)server_idle_us() * s.clock_khz / 1000ull;
+    k_srv<<<1, 256, 0, s.stream>>>(s.req_dev, (unsigned long long*)(s.hres_dev + 32), ~word, ++s.epoch, idle,
+                                    s.clock_khz * 1000ull /* 1 s */);
+    NH_HIP(hipGetLastError());
+    s.srv_alive = true;
+    ++s.n_launches;
+    return NH_OK;
+}
+
+// Device address of srv_thunk<F> on the current device (asked once per device).
+template <class F>
+static int server_fn(Staging& s, int dev, unsigned long long* fn) {
+    static std::atomic<unsigned long long> addr[kMaxDevices];
+    unsigned long long a = addr[dev].load(std::memory_order_acquire);
+    if (!a) {
+        server_stop(s);
+        k_srv_addr<F><<<1, 1, 0, s.stream>>>(s.dwork);
+        NH_HIP(hipGetLastError());
+        NH_HIP(hipMemcpyAsync(&a, s.dwork, 8, hipMemcpyDeviceToHost, s.stream));
+        NH_HIP(hipStreamSynchronize(s.stream));
+        if (!a) {
+            set_error("block-call server: null thunk address");
+            return NH_EHIP;
+        }
+        addr[dev].store(a, std::memory_order_release);
+    }
+    *fn = a;
     return NH_OK;
 }
 
@@ -645,6 +838,42 @@ static int wait_completion(hipStream_t stream, const unsigned long long* word, u
     return NH_OK;
 }
 
+// The served form's wait: the completion word, or -- when the server left
+// without answering (its exit raced the request) -- a relaunch that takes the
+// pending request.  `exited` is the server's last store, after any completion
+// word, so the completion word is read again after `exited` before relaunching.
+static int server_wait(Staging& s, unsigned long long word, unsigned long long* done) {
+    const unsigned long long seq = word >> 12;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned spins = 1;; ++spins) {
+        unsigned long long d = __atomic_load_n(&s.req->done, __ATOMIC_ACQUIRE);
+        if ((d >> 8) == seq) { *done = d; return NH_OK; }
+        if (__atomic_load_n(&s.req->exited, __ATOMIC_ACQUIRE) == s.epoch) {
+            d = __atomic_load_n(&s.req->done, __ATOMIC_ACQUIRE);
+            if ((d >> 8) == seq) { *done = d; return NH_OK; }
+            NH_TRY_(server_launch(s, word));
+        }
+        if ((spins & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(s.stream);
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                s.srv_alive = false;
+                set_error(std::string("block-call server: ") + hipGetErrorString(q));
+                return NH_EHIP;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) break;
+        }
+    }
+    s.srv_alive = false;   // the lifetime bound (1 s) has ended it by now
+    NH_HIP(hipStreamSynchronize(s.stream));
+    const unsigned long long d = __atomic_load_n(&s.req->done, __ATOMIC_ACQUIRE);
+    if ((d >> 8) != seq) {
+        set_error("block-call server: no answer within 2 s");
+        return NH_EHIP;
+    }
+    *done = d;
+    return NH_OK;
+}
+
 class BlockCall {
   public:
     // Registers an input array (copied when the call runs); returns its byte
@@ -658,7 +887,8 @@ class BlockCall {
     // Runs body f on `grid` workgroups (staged form; the small form always runs
     // one workgroup) and returns its out_bytes of output into `out` -- or, with
     // from_acc, the 8-byte accumulator word the body's reductions added into.
-    template <class F>
+    // kServe: the body may run on the block-call server (no large LDS tiles).
+    template <bool kServe = true, class F>
     int run(unsigned grid, F f, void* out, size_t out_bytes, bool from_acc = false) {
         const int64_t t0 = now_ns();
         Staging* S = nullptr;
@@ -667,6 +897,40 @@ class BlockCall {
         NH_TRY_(staging_init(*S));
         const size_t res = from_acc ? 0 : out_bytes;
         unsigned long long st, acc;
+        if constexpr (kServe) {
+            static_assert(sizeof(F) <= kSrvCap && alignof(F) <= 16, "captures exceed the server's block");
+            if (server_idle_us() > 0 && end_ <= kSmallIn && res <= kSmallOut) {
+                unsigned long long fn = 0;
+                NH_TRY_(server_fn<F>(*S, (int)(S - g_staging), &fn));
+                SrvReq* q = S->req;
+                for (int i = 0; i < n_; ++i)
+                    if (ins_[i].bytes) std::memcpy(q->in + ins_[i].off, ins_[i].p, ins_[i].bytes);
+                std::memcpy(q->cap, (const void*)&f, sizeof(F));
+                q->fn = fn;
+                const unsigned long long word =
+                    (++S->seq << 12) | ((from_acc ? kSrvFlagAcc : 0ull) << 8) | (align_up(end_, 16) / 16);
+                const int64_t t1 = now_ns();
+                server_post(*S, word);
+                if (!S->srv_alive || __atomic_load_n(&q->exited, __ATOMIC_ACQUIRE) == S->epoch)
+                    NH_TRY_(server_launch(*S, word));
+                const int64_t t2 = now_ns();
+                unsigned long long done = 0;
+                NH_TRY_(server_wait(*S, word, &done));
+                const int64_t t3 = now_ns();
+                const unsigned long long* o = (const unsigned long long*)S->hres + 4;
+                const int code = (int)(done & 0xff);
+                if (!code && res) std::memcpy(out, o, res);
+                if (!code && from_acc) std::memcpy(out, o, 8);
+                ++S->n_served;
+                g_call_ns[0] = t1 - t0;
+                g_call_ns[1] = t2 - t1;
+                g_call_ns[2] = t3 - t2;
+                g_call_ns[3] = now_ns() - t3;
+                return -code;
+            }
+        }
+        server_stop(*S);   // launches below queue behind its exit on the same stream
+        ++S->n_kernel;
         if (end_ <= kSmallIn && res <= kSmallOut) {
             const unsigned long long seq = ++S->seq;
             int64_t t1 = 0;
@@ -779,6 +1043,7 @@ int nh_release_staging(void) {
             }
             continue;
         }
+        server_stop(s);
         (void)hipStreamSynchronize(s.stream);
         staging_free(s);
     }
@@ -788,6 +1053,44 @@ int nh_release_staging(void) {
         first_err = NH_EHIP;
     }
     return first_err;
+}
+
+int nh_block_server_stop(void) {
+    int cur = 0;
+    NH_HIP(hipGetDevice(&cur));
+    int first_err = NH_OK;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        Staging& s = g_staging[d];
+        std::lock_guard<std::mutex> lk(s.mu);
+        if (!s.ready || !s.srv_alive) continue;
+        if (hipSetDevice(d) != hipSuccess) continue;
+        server_stop(s);
+        const hipError_t e = hipStreamSynchronize(s.stream);
+        if (e != hipSuccess && first_err == NH_OK) {
+            set_error(std::string("nh_block_server_stop: ") + hipGetErrorString(e));
+            first_err = NH_EHIP;
+        }
+    }
+    (void)hipSetDevice(cur);
+    return first_err;
+}
+
+int nh_block_server_set_idle_us(int64_t us) {
+    if (us < 0 || us > 1000000) return NH_EARG;
+    g_srv_idle_us.store((long)us, std::memory_order_relaxed);
+    if (us == 0) return nh_block_server_stop();
+    return NH_OK;
+}
+
+int nh_block_server_stats(int device, int64_t* out) {
+    if (device < 0 || device >= kMaxDevices || !out) return NH_EARG;
+    Staging& s = g_staging[device];
+    std::lock_guard<std::mutex> lk(s.mu);
+    out[0] = s.n_served;
+    out[1] = s.n_launches;
+    out[2] = s.n_kernel;
+    out[3] = server_idle_us();
+    return NH_OK;
 }
 
 int nh_last_call_times(int64_t* ns) {
@@ -873,7 +1176,7 @@ template <int N, bool DST, bool FWD>
 static int block_transform_n(const int32_t* in, int32_t* out) {
     BlockCall c;
     const size_t oi = c.in(in, N * N * 4);
-    return c.run(1, [=] __device__(U8 i, ST, uint8_t* o) {
+    return c.run<false>(1, [=] __device__(U8 i, ST, uint8_t* o) {
         dev_transform<N, DST, FWD>((const int32_t*)(i + oi), (int32_t*)o, 1);
     }, out, N * N * 4);
 }
@@ -961,7 +1264,7 @@ int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits
     if (n < 0 || (abs_bits != 32 && abs_bits != 64)) return NH_EARG;
     BlockCall c;
     const size_t oi = c.in(level, n * 8);
-    return c.run(1, [=] __device__(U8 in, ST, uint8_t* o) {
+    return c.run<false>(1, [=] __device__(U8 in, ST, uint8_t* o) {   // 1.5 KB of stack: k_small
         dev_estimate_bits((const int64_t*)(in + oi), n, abs_bits, (double*)o);
     }, bits, 8);
 }
@@ -1015,7 +1318,7 @@ int nh_sum_sq_diff_f64(const double* a, const double* b, int64_t n, double* out)
     if (n < 0) return NH_EARG;
     BlockCall c;
     const size_t oa = c.in(a, n * 8), ob = c.in(b, n * 8);
-    return c.run(1, [=] __device__(U8 in, ST, uint8_t* o) {
+    return c.run<false>(1, [=] __device__(U8 in, ST, uint8_t* o) {   // 1.5 KB of stack: k_small
         dev_sum_sq_diff_f64((const double*)(in + oa), (const double*)(in + ob), n, (double*)o);
     }, out, 8);
 }

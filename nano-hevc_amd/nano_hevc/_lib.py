@@ -5,6 +5,7 @@ compute call raises ``NanoHevcUnavailable`` (a RuntimeError) -- loudly.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 
@@ -42,6 +43,9 @@ SIGNATURES = {
     "nh_staging_bytes": ([I32, P], I32),
     "nh_release_staging": ([], I32),
     "nh_last_call_times": ([P], I32),
+    "nh_block_server_set_idle_us": ([I64], I32),
+    "nh_block_server_stop": ([], I32),
+    "nh_block_server_stats": ([I32, P], I32),
     "nh_intra_dc": ([P, I64, P, I64, I64, I32, P], I32),
     "nh_intra_planar": ([P, I64, P, I64, I64, I64, I64, I64, P], I32),
     "nh_intra_angular": ([P, I64, P, I64, I64, I32, I64, P], I32),
@@ -134,6 +138,9 @@ def _open(path, how):
         f.argtypes = args
         f.restype = res
     _libs[path] = L
+    # a resident block-call server leaves on its own within its idle time; at
+    # interpreter exit it is asked to leave at once (while the runtime is up)
+    atexit.register(L.nh_block_server_stop)
     return L
 
 

@@ -28,6 +28,7 @@ INTRA_PRED_ANGLE = [
 INV_ANGLE = {-2: -4096, -5: -1638, -9: -910, -13: -630, -17: -482, -21: -390, -26: -315, -32: -256}
 
 
+_I16 = np.dtype(np.int16)
 _I64_SAFE = 1 << 62   # host-converted values beyond this would leave the kernels' int64 arithmetic
 
 
@@ -58,6 +59,8 @@ def _dc_sum(x, what):
     reference's own int(x.sum()) (numpy's sum in that dtype, then int(): the
     same truncation and the same ValueError / OverflowError / TypeError) and
     hands the kernel that one integer."""
+    if type(x) is np.ndarray and x.dtype is _I16:   # the reference's callers: int16 sample rows
+        return x.astype(np.int64).ravel()
     a = np.asarray(x)
     if a.dtype.kind in "iub":
         return np.ascontiguousarray(a.ravel(), dtype=np.int64)
@@ -87,29 +90,43 @@ def intra_dc_predict(top, left, size):
         raise ValueError("negative dimensions are not allowed")
     t, l = _dc_sum(top, "top"), _dc_sum(left, "left")
     out = np.empty((size, size), np.int16)
-    check(_lib.load().nh_intra_dc(ptr(t), t.size, ptr(l), l.size, size, 0, ptr(out)), "intra_dc_predict")
+    rc = _lib.load().nh_intra_dc(ptr(t), t.size, ptr(l), l.size, size, 0, ptr(out))
+    if rc:
+        check(rc, "intra_dc_predict")
     return out
+
+
+def _pair16(x, y):
+    """The operands of intra.py:65-72 as two C-contiguous int16 arrays of one
+    shape: x.astype(int16), y.astype(int16), broadcast.  Two C-contiguous int16
+    arrays of equal shape (the reference's callers) are used as they are."""
+    if (type(x) is np.ndarray and type(y) is np.ndarray and x.dtype is _I16 and y.dtype is _I16
+            and x.shape == y.shape and x.flags.c_contiguous and y.flags.c_contiguous):
+        return x, y
+    a = np.asarray(x).astype(np.int16)
+    b = np.asarray(y).astype(np.int16)
+    if a.shape != b.shape:
+        a, b = np.broadcast_arrays(a, b)
+    return np.ascontiguousarray(a), np.ascontiguousarray(b)
 
 
 def residual_block(orig, pred):
     """intra.py:65-67: orig.astype(int16) - pred.astype(int16) (int16 wrap, broadcasting)."""
-    a = np.asarray(orig).astype(np.int16)
-    b = np.asarray(pred).astype(np.int16)
-    a, b = np.broadcast_arrays(a, b)
-    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    a, b = _pair16(orig, pred)
     out = np.empty(a.shape, np.int16)
-    check(_lib.load().nh_residual(ptr(a), ptr(b), a.size, ptr(out)), "residual_block")
+    rc = _lib.load().nh_residual(ptr(a), ptr(b), a.size, ptr(out))
+    if rc:
+        check(rc, "residual_block")
     return out
 
 
 def reconstruct_block(pred, residual):
     """intra.py:70-72: pred.astype(int16) + residual.astype(int16) (int16 wrap)."""
-    a = np.asarray(pred).astype(np.int16)
-    b = np.asarray(residual).astype(np.int16)
-    a, b = np.broadcast_arrays(a, b)
-    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    a, b = _pair16(pred, residual)
     out = np.empty(a.shape, np.int16)
-    check(_lib.load().nh_reconstruct(ptr(a), ptr(b), a.size, ptr(out)), "reconstruct_block")
+    rc = _lib.load().nh_reconstruct(ptr(a), ptr(b), a.size, ptr(out))
+    if rc:
+        check(rc, "reconstruct_block")
     return out
 
 

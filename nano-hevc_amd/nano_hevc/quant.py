@@ -34,20 +34,32 @@ def _abs_bits(dt) -> int:
     return 0
 
 
+_AB_INT32 = np.dtype(np.int32)
+
+
+def _log2_size(size) -> int:
+    """int(np.log2(size)) (quant.py:72); exact bit arithmetic for the power-of-two
+    Python ints the reference's callers pass, numpy's own expression otherwise."""
+    if type(size) is int and 0 < size < (1 << 52) and not size & (size - 1):
+        return size.bit_length() - 1
+    return int(np.log2(size))
+
+
 def quantize(coeff, qp: int, size: int, is_intra: bool = True) -> np.ndarray:
     """quant.py:41-79: level = sign(c) * ((|c|*MF + offset) >> shift), int32."""
     qp_per, qp_rem = get_qp_params(qp)
     mf = QUANT_SCALE[qp_rem]                                  # noqa: F841 (same lookup/errors)
-    log2_size = int(np.log2(size))
+    log2_size = _log2_size(size)
     shift = 14 + qp_per + log2_size
     offset = (1 << shift) // 3 if is_intra else (1 << shift) // 6   # noqa: F841
-    c = np.asarray(coeff)
-    ab = _abs_bits(c.dtype)
+    c = coeff if type(coeff) is np.ndarray else np.asarray(coeff)
+    ab = 32 if c.dtype is _AB_INT32 else _abs_bits(c.dtype)
     if ab:
-        x = np.ascontiguousarray(c, dtype=np.int64)
+        x = c.astype(np.int64, order="C")
         out = np.empty(c.shape, np.int32)
-        check(_lib.load().nh_quantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), log2_size, int(bool(is_intra)),
-                                      ab, ptr(out)), "quantize")
+        rc = _lib.load().nh_quantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), log2_size, 1 if is_intra else 0, ab, ptr(out))
+        if rc:
+            check(rc, "quantize")
         return out
     # float (and uint64 / bool / other) coefficients: the reference's own host
     # expressions around the kernel -- np.sign (raises for bool, like quant.py:76),
@@ -65,9 +77,11 @@ def dequantize(level, qp: int, size: int) -> np.ndarray:
     """quant.py:82-123 (size unused, D4)."""
     qp_per, qp_rem = get_qp_params(qp)
     DEQUANT_SCALE[qp_rem]
-    x = np.ascontiguousarray(np.asarray(level).astype(np.int64))   # quant.py:113 cast
+    x = np.asarray(level).astype(np.int64, order="C")   # quant.py:113 cast
     out = np.empty(x.shape, np.int32)
-    check(_lib.load().nh_dequantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), ptr(out)), "dequantize")
+    rc = _lib.load().nh_dequantize(ptr(x), x.size, int(qp_per * 6 + qp_rem), ptr(out))
+    if rc:
+        check(rc, "dequantize")
     return out
 
 

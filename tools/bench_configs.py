@@ -68,6 +68,29 @@ def psnr_dev(a, b, peak=255):
     return float("inf") if mse == 0 else float(10 * np.log10(peak ** 2 / mse))
 
 
+def valu_roofline(key, ms_per_frame):
+    """`bound: "valu"` roofline of a VALU-bound config, with this run's time.
+
+    achieved = the config's VALU wave-instructions per frame (SQ_INSTS_VALU per
+    kernel, profiles/valu_roofline.json by tools/pmc_valu.py) / ms_per_frame
+    measured here (wall clock of the timed launches, gaps included); peak = the
+    attainable issue rate of the frame's static VALU mix at the measured
+    per-opcode rates (harmonic over the kernels, weighted by instructions)."""
+    p = os.path.join(ROOT, "profiles", "valu_roofline.json")
+    if not os.path.exists(p):
+        return None
+    v = json.load(open(p)).get("configs", {}).get(key)
+    if not v:
+        return None
+    ks = [k for k in v["kernels"].values() if k.get("valu_per_frame") and k.get("attainable_valu_winst_per_s")]
+    instr = sum(k["valu_per_frame"] for k in ks)
+    peak = instr / sum(k["valu_per_frame"] / k["attainable_valu_winst_per_s"] for k in ks) / 1e9
+    achieved = instr / (ms_per_frame * 1e-3) / 1e9
+    return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G VALU wave-instr/s",
+            "frac": achieved / peak, "valu_instr_per_frame": instr,
+            "profile_kernel_frac": v.get("valu_frac"), "profile_tag": json.load(open(p)).get("tag")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
@@ -81,8 +104,15 @@ def main():
     ap.add_argument("--enc-frames", type=int, default=64)
     ap.add_argument("--closed-frames", type=int, default=64)
     ap.add_argument("--ab", action="store_true", help="run on the A/B library (libnanohevc_ab.so: NH_* knobs read)")
+    ap.add_argument("--lib", default=None, help="A/B: run on another build of libnanohevc.so (e.g. tools/_ab/...)")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
+    if args.lib:
+        import ctypes
+        probe = ctypes.CDLL(os.path.abspath(args.lib))
+        for name in [n for n in _lib.SIGNATURES if not hasattr(probe, n)]:
+            del _lib.SIGNATURES[name]
+        _lib.LIB_PATH = os.path.abspath(args.lib)
     if args.ab:
         _lib.use_ab()
     _lib.load()
@@ -98,7 +128,7 @@ def main():
         print(json.dumps({"config": "cfg3 1080p YUV420 35-mode RDO per 8x8 (pred+res+DCT+Q+DQ+IDCT+recon+SSE)",
                           "ms_per_frame": ms, "frames_per_s": 1e3 / ms, "blocks_per_frame": nblk,
                           "blocks_per_s": nblk / ms * 1e3, "mode_evals_per_s": 35 * nblk / ms * 1e3,
-                          "bound": "valu (~3.3k int ops per block-mode)"}), flush=True)
+                          "roofline": valu_roofline("cfg3_1080p_yuv420", ms)}), flush=True)
 
     if 4 in cfgs:
         W, H = 3840, 2160
@@ -149,6 +179,7 @@ def main():
                           "samples_per_s": samples / ms * 1e3,
                           "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
                           "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H]), "knobs": knobs,
+                          "roofline": valu_roofline("cfg4_4k_yuv420", ms / nf),
                           "out_digest": [int(lv.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item()),
                                          int((lv.to(torch.int64) * torch.arange(lv.numel(), device="cuda") % 1000003)
                                              .sum().item())]}), flush=True)
@@ -178,6 +209,7 @@ def main():
                 "luma_chroma": "sequential" if args.closed4_seq else "concurrent", "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
                 "frames_per_s": nf / ms * 1e3, "samples_per_s": stream.numel() / ms * 1e3,
                 "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H]), "knobs": knobs,
+                "roofline": valu_roofline("cfg4_closed_4k_yuv420", ms / nf),
                 "out_digest": [int(lv.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item())]}
         if args.check:   # frames 0 and 1: the two planes of the first luma pair
             from oracle import oracle as O   # checker only
@@ -204,7 +236,7 @@ def main():
                           "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "blocks_per_s": nblk / ms * 1e3,
                           "samples_per_s": nf * fe / ms * 1e3, "bytes_per_sample": 8,
                           "achieved_GBps": nf * fe * 8 / ms / 1e6, "psnr_y_frame0": psnr_dev(stream5[:W * H], rc5[:W * H]),
-                          "knobs": knobs,
+                          "knobs": knobs, "roofline": valu_roofline("cfg5_8k_yuv420", ms / nf),
                           "out_digest": [int(lv5.to(torch.int64).sum().item()), int(rc5.to(torch.int64).sum().item()),
                                          int((lv5.to(torch.int64) * torch.arange(lv5.numel(), device="cuda") % 1000003)
                                              .sum().item())]}),
@@ -326,7 +358,8 @@ def main():
                           "row wavefront on the device, 1080p YUV420 frames",
                 "frames": nf, "ms_per_launch": ms, "ms_per_frame": ms / nf, "frames_per_s": nf / ms * 1e3,
                 "blocks_per_s": nblk / ms * 1e3, "sse_y_frame0": int(sse[0].item()),
-                "note": "one wave per block row; a frame's latency is ~(W/8 + 2*H/8) block steps"}
+                "note": "one wave per block row; a frame's latency is ~(W/8 + 2*H/8) block steps",
+                "roofline": valu_roofline("cfg3_closed_1080p_yuv420", ms / nf)}
         if args.check:
             from oracle import oracle as O   # checker only
             y = stream[:W * H].view(H, W).cpu().numpy()

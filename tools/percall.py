@@ -3,6 +3,7 @@
     python tools/percall.py                          # the MI355X shim (nano-hevc_amd/nano_hevc), on a GPU box
     python tools/percall.py --impl /root/reference   # the reference numpy package (build container only)
     python tools/percall.py --lib tools/_ab/libnanohevc_r01_staging.so   # the shim over another build (A/B)
+    python tools/percall.py --server-idle-us 0       # without the block-call server (a launch per call)
 
 Times every compute function the reference exports (nano_hevc/__init__.py:50-91)
 one block per call, as the reference's callers use them, at sizes 4 / 8 / 16 / 32
@@ -159,7 +160,9 @@ def main():
             for name in [n for n in _lib.SIGNATURES if not hasattr(probe, n)]:
                 del _lib.SIGNATURES[name]
             _lib.LIB_PATH = path
-        _lib.load()
+        L = _lib.load()
+        if "--server-idle-us" in sys.argv and hasattr(L, "nh_block_server_set_idle_us"):   # 0: launch per call
+            _lib.check(L.nh_block_server_set_idle_us(int(sys.argv[sys.argv.index("--server-idle-us") + 1])))
     rng = np.random.default_rng(7)
     res, ph = {}, {}
     want_phases = impl == "shim" and "--phases" in sys.argv
