@@ -1567,6 +1567,9 @@ struct Closed4Args {
     uint32_t seed;
     QuantParams q[4];       // log2 N = 2..5
     int32_t dqs, dq_per;
+    int32_t probe;          // A/B timing probes (k_tu_closed_pair; wrong outputs): 1 no wait on the row
+                            // above, 2 no chains, 4 no rounds, 8 no recon-image clear, 16 no quadtree
+                            // hashes (0 in the product)
 };
 
 // cnt TUs of size N at once: lane l codes column / row t = l % N of TU j = l / N
@@ -2162,7 +2165,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     bool ok = true;
                     if (need) {
                         const uint64_t v = ld_sys64(line[hq] + x0c / 2 + hl);
-                        ok = (int)(v >> 32) == cy;
+                        ok = (int)(v >> 32) == cy || (NH_AB && (a.probe & 1));
                         val = (uint32_t)v;
                     }
                     if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
@@ -2189,7 +2192,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 const int ux = lane % U, uy = lane / U, x = x0c + 4 * ux, y = y0c + 4 * uy;
                 int own = lane;
                 if (x < a.w && y < a.h) {
-                    const int n = tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y), nu = n / 4;
+                    const int n = (NH_AB && (a.probe & 16)) ? 4 : tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y), nu = n / 4;
                     ox = ux - ux % nu;
                     oy = uy - uy % nu;
                     own = oy * U + ox;
@@ -2200,7 +2203,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 done_of[lane] = 0;
             }
             __syncthreads();
-            for (int round = 0; round < UU && __ballot(pending); ++round) {
+            for (int round = 0; round < UU && __ballot(pending) && !(NH_AB && (a.probe & 4)); ++round) {
                 bool ready = pending;
                 if (pending) {
                     const int nu = tn / 4;
@@ -2221,7 +2224,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     }                                                                                        \
                     __syncthreads();                                                                         \
                     const int tot = cnt << two;                                                              \
-                    for (int c0 = 0; c0 < tot; c0 += 64 / NN)                                                \
+                    for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                   \
                         tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, slx, sly, rc, t16, Q);   \
                 }
                 NH_BATCH2(32, false, cq[3]);
@@ -2245,7 +2248,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             int16_t keep = 0;
             if (hl < ctb) keep = rc[hq][1 + hl][ctb];
             __syncthreads();
-            for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
+            if (!(NH_AB && (a.probe & 8)))
+                for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
             __syncthreads();
             if (hl < ctb) rc[hq][1 + hl][0] = keep;
             __syncthreads();
@@ -2495,6 +2499,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     qp_split(qp, &per, &rem);
     a.dqs = dequant_scale(rem);
     a.dq_per = per;
+    a.probe = NH_KNOB("NH_CLOSED4_PROBE", 0);
     const int64_t rows = (int64_t)a.crows * np;
     // A/B knob NH_TU_CLOSED_WAVES: 1 = compiler allocation (218 VGPRs, 2 waves/SIMD), 3 = capped (spills)
     static const int cw = NH_KNOB("NH_TU_CLOSED_WAVES", 1);

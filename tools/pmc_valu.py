@@ -21,8 +21,8 @@ Per kernel: achieved = SQ_INSTS_VALU per dispatch / average duration (chip-wide
 VALU wave-instructions per second); attainable = the kernel's static VALU mix
 priced at the measured per-opcode rates, N / sum(n_i / r_i); frac = achieved /
 attainable.  Per config: the same over one frame's worth of its kernels
-(instructions summed, attainable combined harmonically, time = the kernels'
-summed average durations per frame).  SQ ratios say where the rest goes:
+(instructions summed, attainable combined harmonically, time = the union of the
+kernels' trace intervals per frame, so concurrent launches count once).  SQ ratios say where the rest goes:
 valu_active = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, wait_any = SQ_WAIT_ANY /
 SQ_WAVE_CYCLES, clock = GRBM_GUI_ACTIVE / duration.
 """
@@ -65,6 +65,28 @@ def kernel_times(d):
             if "nh::" in r["Name"] and not any(k in r["Name"] for k in HARNESS):
                 out[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
     return out, p
+
+
+def busy_ns(d):
+    """Union of the config's kernel intervals in the trace (ns): concurrent launches
+    (config 4's closed loop runs its luma and chroma wavefronts side by side)
+    count once."""
+    p = _find(d, "*kernel_trace.csv")
+    if not p:
+        return None
+    iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(p))
+                if "nh::" in r["Kernel_Name"] and not any(k in r["Kernel_Name"] for k in HARNESS))
+    tot, cur_s, cur_e = 0, None, None
+    for a, b in iv:
+        if cur_e is None or a > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    if cur_e is not None:
+        tot += cur_e - cur_s
+    return tot
 
 
 def counters(d):
@@ -154,17 +176,19 @@ def main():
                 e["ms_per_frame"] = t["avg_ns"] * t["calls"] / f_kt / 1e6
                 t_ms += e["ms_per_frame"]
             kernels[name] = e
+        busy = busy_ns(os.path.join(a.dir, f"valu_kt_{a.tag}_{c}"))
+        busy_ms = busy / f_kt / 1e6 if busy else t_ms
         ent = {"kernels": kernels, "frames_counted": f_pmc, "frames_traced": f_kt,
-               "valu_per_frame": instr, "kernel_ms_per_frame": t_ms,
+               "valu_per_frame": instr, "kernel_ms_per_frame": t_ms, "busy_ms_per_frame": busy_ms,
                "source": {"kernel_trace": os.path.relpath(kt_path, ROOT) if kt_path else None,
                           "pmc1": os.path.relpath(p1_path, ROOT) if p1_path else None,
                           "pmc2": os.path.relpath(p2_path, ROOT) if p2_path else None, "rates": os.path.relpath(rates_path, ROOT)}}
-        if t_ms and t_att:
-            ent["achieved_valu_winst_per_s"] = instr / (t_ms * 1e-3)
+        if busy_ms and t_att:   # over the time the GPU was running the config's kernels (union of intervals)
+            ent["achieved_valu_winst_per_s"] = instr / (busy_ms * 1e-3)
             ent["attainable_valu_winst_per_s"] = instr / t_att
             ent["valu_frac"] = ent["achieved_valu_winst_per_s"] / ent["attainable_valu_winst_per_s"]
         res["configs"][key] = ent
-        print(f"{key:28s} frac {ent.get('valu_frac', float('nan')):.3f}  {t_ms:.4f} ms/frame (kernel sum)  "
+        print(f"{key:28s} frac {ent.get('valu_frac', float('nan')):.3f}  {busy_ms:.4f} ms/frame busy ({t_ms:.4f} kernel sum)  "
               f"VALU/frame {instr:.4g}", flush=True)
         for name, e in kernels.items():
             if e.get("valu_per_frame", 0) > 0.01 * instr:
