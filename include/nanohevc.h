@@ -48,7 +48,7 @@ int nh_release_staging(void);
  * [1] launch (the launch API calls), [2] wait (launch returned -> completion
  * seen), [3] finish (outputs copied back).  Diagnostics (tools/percall.py). */
 int nh_last_call_times(int64_t* ns);
-/* The block-call server (DESIGN.md §3.1): while per-block calls keep coming,
+/* The block-call server (DESIGN.md §4.6): while per-block calls keep coming,
  * one resident workgroup per device takes them from mapped host memory instead
  * of a kernel launch per call; it leaves after the idle time (default 200 us)
  * without a call.  set_idle_us: that time for servers launched from now on
@@ -237,7 +237,7 @@ int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane_set* set, 
 /* Config 5: every full 32x32 block of an int16 source plane through the
  * config-4 chain at N=32.  variant 0 = butterfly
  * (k_tu_process<32>), 1 = matrix cores: blocks whose samples and neighbours
- * are 8-bit on f16 MFMA (exact, DESIGN.md §4.4d), the others on int8 MFMA
+ * are 8-bit on f16 MFMA (exact, DESIGN.md §4.4), the others on int8 MFMA
  * (v_mfma_i32_32x32x32_i8 with exact int8 part splitting), 2 = int8 MFMA for
  * every block (A/B).  Identical outputs.  pitch % 8 == 0. */
 int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl,

@@ -21,7 +21,7 @@
 //   3. the waves claim batches of 64/N TUs of one size (lane l: column / row
 //      l mod N of TU l / N), 32x32 TUs first.
 // Two kernels per plane set: k_ctu_open codes the groups whose samples are all
-// 8-bit with the packed 16-bit chain (nh_packed.hpp, DESIGN.md §4.4c) and their
+// 8-bit with the packed 16-bit chain (nh_packed.hpp, DESIGN.md §4.4) and their
 // 32x32 TUs on exact f16 matrix cores (§4.4d); the groups it marks in the TU
 // map k_ctu_wide codes with the 32-bit chain (any int16 input).  No global
 // atomics, no per-size relaunch, the source read once.  Levels and recon rows
@@ -96,7 +96,7 @@ __device__ __forceinline__ void st_rec4(int16_t* p, uint2 v) { *(uint2*)p = v; }
 // instead of 129 VGPRs for the luma kernel.  Since the kernels are capped at 3-4
 // resident waves per SIMD (lds_cap) the registers are free, and hoisting saves
 // VALU: 37.2 vs 38.1 us per 4K YUV420 frame, config 5 0.129 vs 0.138 ms per 8K
-// frame (DESIGN.md §4.4d).
+// frame (DESIGN.md §4.4).
 __device__ __forceinline__ int opaque_lane() {
     int l = threadIdx.x & 63;
 #ifdef NH_OPAQUE_LANE
@@ -245,7 +245,7 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
 }
 
 // The same chain for a NARROW workgroup (every sample of its strips and their
-// neighbours in [0, 255]): int16 pairs end to end (DESIGN.md §4.4c).  Source
+// neighbours in [0, 255]): int16 pairs end to end (DESIGN.md §4.4).  Source
 // column, planar prediction (v_pk_mad_u16: numerators < 2^15) and residual as
 // row pairs, residual energies with v_dot2 in 32 bits (<= N^2 * 255^2), the
 // transforms of nh_packed.hpp, and an int16 coefficient tile: each pass stores
@@ -471,7 +471,7 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
     }
 }
 
-// A 32x32 TU of a NARROW group on the f16 matrix cores (DESIGN.md §4.4d): one
+// A 32x32 TU of a NARROW group on the f16 matrix cores (DESIGN.md §4.4): one
 // TU per wave, the four transform passes as v_mfma_f32_32x32x16_f16 pairs.
 // Exact: every operand is an integer of at most 11 bits (residual + 1536 for
 // pass 1, pass outputs <= 510, dequantized <= 180, inverse pass-1 outputs
@@ -1194,7 +1194,7 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     const dim3 grid_wide((unsigned)((groups + kWideGroups - 1) / kWideGroups), (unsigned)planes);
     // Narrow groups (8-bit content) are coded by k_ctu_open with the packed
     // chain, their 32x32 TUs on the f16 matrix cores (rocprof: 428.5 vs 459.9
-    // us per 16 luma planes for the packed butterflies, DESIGN.md §4.4d); the
+    // us per 16 luma planes for the packed butterflies, DESIGN.md §4.4); the
     // groups it marks (any sample outside [0, 255]) by k_ctu_wide with the
     // 32-bit chain.  A/B build: NH_CTU_T32 = 0 (narrow 32x32 TUs on packed
     // butterflies) / 1 (wide 32x32 TUs on int8 MFMA), NH_CTU_PERSIST = 1 / 2
@@ -1205,11 +1205,11 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     static const int persist = NH_KNOB("NH_CTU_PERSIST", 0);
     // The luma f16-MFMA form runs at 6 waves/SIMD: 76 VGPRs with zero-initialised
     // accumulators (90 with the rounding constant as their initial value) and
-    // 27 KB of LDS per workgroup with the 4 KB bases (DESIGN.md §4.4d).
+    // 27 KB of LDS per workgroup with the 4 KB bases (DESIGN.md §4.4).
     a.wide_only = NH_KNOB("NH_CTU_NARROW", 1) == 0;
     a.probe = NH_KNOB("NH_CTU_PROBE", 0);
     // Group size GS (strips pooled per workgroup of 64 GS threads) and the
-    // occupancy cap (resident workgroups per CU, lds_cap; DESIGN.md §4.4d).
+    // occupancy cap (resident workgroups per CU, lds_cap; DESIGN.md §4.4).
     // A/B build: NH_CTU_GS = 4 / 6 / 8, NH_CTU_CAP = workgroups per CU,
     // NH_OCC_CAP = 0 uncapped.
     static const int gs_knob = NH_KNOB("NH_CTU_GS", 4), cap_knob = NH_KNOB("NH_CTU_CAP", 0);

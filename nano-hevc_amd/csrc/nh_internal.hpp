@@ -45,7 +45,7 @@ inline bool xcd_order() {
 // Dynamic LDS that caps `kern` at `wgs` resident workgroups per CU: the
 // workgroup then reserves just over 1 / (wgs + 1) of the CU's LDS (static +
 // this pad; the pad is never touched).  These kernels run faster with fewer
-// resident workgroups (DESIGN.md §4.4d, §4.5).  Cached per kernel; 0 for wgs <= 0 or when
+// resident workgroups (DESIGN.md §4.4, §4.5).  Cached per kernel; 0 for wgs <= 0 or when
 // the device reports no per-CU LDS figure.  A/B build: NH_OCC_CAP = 0 disables it.
 template <class K>
 inline unsigned lds_cap(K kern, int wgs) {

@@ -1682,7 +1682,7 @@ __device__ __forceinline__ void tu_closed_batch(const Closed4Args& a, const int1
 
 // tu_closed_batch for a stream whose every source sample is 8-bit (the
 // reconstruction is clipped to [0, 255], so neighbours are too): the packed
-// 16-bit chain of DESIGN.md §4.4c (nh_packed.hpp; bounds: tools/packed_bounds.py)
+// 16-bit chain of DESIGN.md §4.4 (nh_packed.hpp; bounds: tools/packed_bounds.py)
 // with an int16 view of the tile (rows of TP = 34: pair reads conflict-free).
 // Same results as tu_closed_batch on such input.
 __device__ __forceinline__ int opaque_lane64() {
@@ -2368,7 +2368,7 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
     int per, rem;
     qp_split(qp, &per, &rem);
     const int dqs = dequant_scale(rem);
-    // One CTU-granular launch (k_ctu_open, DESIGN.md §4.4b) unless the layout
+    // One CTU-granular launch (k_ctu_open, DESIGN.md §4.4) unless the layout
     // rules out its vector accesses; A/B build: NH_CFG4_FORM=1 forces the
     // per-size launches below.
     static const int form = NH_KNOB("NH_CFG4_FORM", 0);

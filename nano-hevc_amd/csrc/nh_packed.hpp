@@ -1,5 +1,5 @@
 // nh_packed.hpp -- packed 16-bit 1-D transforms for narrow (8-bit) TUs
-// (DESIGN.md §4.4c).
+// (DESIGN.md §4.4).
 //
 // One N-point vector per lane, held as int16 PAIRS.  The butterfly's add / sub
 // stages are v_pk_add / v_pk_sub on two elements at once (the mirrored operand

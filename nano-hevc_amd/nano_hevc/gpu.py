@@ -243,7 +243,11 @@ def intra_rdo_closed(src, sets: Sequence[PlaneSet], qp: int = 32, lvl=None, rec=
     """Config 3 in CLOSED loop over every plane of ``sets``:
     raster block order, neighbours from the reconstruction, wavefront schedule
     on the device.  Returns (modes uint8 [sum of per-plane (h/8)*(w/8)],
-    lvl int32, recon int16 (source layout), sse int64 per plane)."""
+    lvl int32, recon int16 (source layout), sse int64 per plane).
+    Speed note: the packed 16-bit form runs only when EVERY source sample of
+    the call (all sets) is in [0, 255]; one sample outside sends the whole call
+    to the 32-bit form (same results, ~1.4x the time).  Split
+    such streams into separate calls to keep the 8-bit ones fast."""
     torch = _torch()
     _need(src, torch.int16, "intra_rdo_closed(src)")
     sets_fit(sets, src.numel(), "intra_rdo_closed")
@@ -376,7 +380,10 @@ def tu_pipeline_closed(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
     """Config 4 in CLOSED loop over every plane of one plane
     set: TUs in z-order with neighbours from the reconstruction, a device
     wavefront over CTU rows.  Returns (lvl int32, recon int16 -- source
-    layout, zeros outside every TU --, tu uint8 (planes, h/4, w/4))."""
+    layout, zeros outside every TU --, tu uint8 (planes, h/4, w/4)).
+    Speed note: the packed 16-bit plane-pair form runs only when EVERY source
+    sample of the set is in [0, 255]; one sample outside sends the whole set to
+    the 32-bit form (same results, ~1.7x the time)."""
     torch = _torch()
     strm = stream if stream is not None else torch.cuda.current_stream(src.device)
     st = _stream(strm, src.device)

@@ -1,4 +1,4 @@
-"""The block-call server (nh_blocks.hip k_srv, DESIGN.md §3.1) on the GPU.
+"""The block-call server (nh_blocks.hip k_srv, DESIGN.md §4.6) on the GPU.
 
 Per-block calls are taken by one resident workgroup from mapped host memory
 while calls keep coming; it leaves after its idle time and is relaunched by the

@@ -617,7 +617,7 @@ def test_tu_pipeline_int16_extremes(nh, torch_dev):
 
 @pytest.mark.parametrize("qp", [0, 22, 51])
 def test_tu_pipeline_narrow_extremes_and_mixed(nh, torch_dev, qp):
-    """Config 4's packed 16-bit chain (narrow workgroups, DESIGN.md §4.4c) at its
+    """Config 4's packed 16-bit chain (narrow workgroups, DESIGN.md §4.4) at its
     range limits -- samples only 0 / 255, so residuals reach +-255 -- and planes
     where a few samples leave [0, 255] (those workgroups take the 32-bit chain,
     their neighbours the packed one), against the oracle at QP 0 / 22 / 51."""

@@ -13,6 +13,8 @@
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
   closed4 config 4 in CLOSED loop over a 4K YUV420 stream (TUs in z-order, CTU-row
         wavefront; with --check, frame 0's luma against the oracle).
+  closed4mix  config 4 closed loop on an 8-bit stream vs the same stream with one
+        9-bit sample (the stream-wide packed / 32-bit form choice)
   closed  config 3 in CLOSED loop (neighbours from the reconstruction, wavefront
         schedule) over a batch of 1080p YUV420 frames; with --check, frame 0's
         luma against the oracle.
@@ -221,6 +223,31 @@ def main():
                     np.array_equal(er, rc[f * fe:f * fe + W * H].view(H, W).cpu().numpy()) and
                     np.array_equal(el, lv[f * fe:f * fe + W * H].view(H, W).cpu().numpy()))
         print(json.dumps(line), flush=True)
+
+    if "closed4mix" in cfgs:   # the stream-wide wide flag: one 9-bit sample in the last frame
+        W, H, nf = 3840, 2160, args.closed4_frames
+        planes = []
+        for f in range(nf):
+            planes += [synth_plane(H, W, 40 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 41 + 3 * f).reshape(-1),
+                       synth_plane(H // 2, W // 2, 42 + 3 * f).reshape(-1)]
+        stream = torch.cat(planes)
+        sy, suv = gpu.yuv420_plane_sets(nf, W, H)
+        fe = gpu.yuv420_frame_elems(W, H)
+        lv = torch.zeros(stream.shape, dtype=torch.int32, device="cuda")
+        rc = torch.zeros(stream.shape, dtype=torch.int16, device="cuda")
+        tuy = torch.zeros((nf, H // 4, W // 4), dtype=torch.uint8, device="cuda")
+        tuc = torch.zeros((2 * nf, H // 8, W // 8), dtype=torch.uint8, device="cuda")
+        res = {}
+        for name in ("8bit", "one_sample_300"):
+            if name != "8bit":
+                stream[(nf - 1) * fe + 1234] = 300   # one luma sample of the last frame
+            ms = timed(lambda: gpu.tu_pipeline_closed_yuv420(stream, sy, suv, 1234, args.qp, lvl=lv, rec=rc,
+                                                              tu_luma=tuy, tu_chroma=tuc), max(3, args.reps // 4))
+            res[name] = {"ms_per_frame": ms / nf}
+        print(json.dumps({"config": "cfg4 closed loop, the stream-wide form choice: an 8-bit stream vs the same "
+                                    "stream with one luma sample at 300 (whole luma set on the 32-bit form)",
+                          "frames": nf, **res, "ratio": res["one_sample_300"]["ms_per_frame"] / res["8bit"]["ms_per_frame"]}),
+              flush=True)
 
     if "5b" in cfgs:   # config 5 batched only (the product launch), for per-config profiler runs
         W, H, nf = 7680, 4320, args.cfg5_frames

@@ -1,4 +1,4 @@
-"""Range proof for the packed 16-bit config-4 chain (DESIGN.md §4.4c).
+"""Range proof for the packed 16-bit config-4 chain (DESIGN.md §4.4).
 
 Narrow workgroups: every source sample and neighbour in [0, 255], so the
 residual is in [-255, 255].  This enumerates, for every TU kind (DST4, DCT
@@ -87,7 +87,7 @@ def main():
         print("%-6s %8d %6d %8d %6d %6d %6d %6d %12d" % r)
     print("largest int16 operand %d (limit 32767), largest int32 sum %d (limit 2^31-1)" % (worst16, worst32))
     assert worst16 <= 32767 and worst32 < 2 ** 31
-    # f16 matrix-core 32x32 chain (DESIGN.md §4.4d): operands integers of <= 11 bits,
+    # f16 matrix-core 32x32 chain (DESIGN.md §4.4): operands integers of <= 11 bits,
     # every |partial sum| < 2^24 units of 2^-10 (pass 1 carries the +1536 offset)
     T = mat(32, False)
     rs, rl1, cl1 = T.sum(1), int(np.abs(T).sum(1).max()), int(np.abs(T).sum(0).max())
