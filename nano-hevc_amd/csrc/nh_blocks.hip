@@ -164,13 +164,12 @@ __device__ __forceinline__ void dev_clip(const int64_t* x, int64_t n, int64_t ma
 // accesses are coalesced and both passes read conflict-free (row pitch N+1).
 // Full 32-bit wrap arithmetic (MulWrap): exact for any int32 input.
 // ---------------------------------------------------------------------------
+// tile: LDS for min(nblocks, 256 / N) blocks of N x (N + 1) int32.
 template <int N, bool DST, bool FWD>
-__device__ __forceinline__ void dev_transform(const int32_t* __restrict__ in, int32_t* __restrict__ out,
-                                              int64_t nblocks) {
+__device__ __forceinline__ void dev_transform_on(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                 int64_t nblocks, int32_t (*tile)[N][N + 1]) {
     constexpr int BPW = 256 / N;  // blocks per workgroup
-    constexpr int P = N + 1;
     constexpr int S = Log2<N>::v + 5;  // transform.py:173 (D1: same shift both passes)
-    __shared__ int32_t tile[BPW][N][P];
     const int64_t b0 = (int64_t)blockIdx.x * BPW;
     const int nb = (int)((nblocks - b0) < BPW ? (nblocks - b0) : BPW);
     // coalesced load of nb blocks
@@ -213,6 +212,13 @@ __device__ __forceinline__ void dev_transform(const int32_t* __restrict__ in, in
         int bb = e / (N * N), r = (e / N) % N, c = e % N;
         dst[e] = tile[bb][r][c];
     }
+}
+
+template <int N, bool DST, bool FWD>
+__device__ __forceinline__ void dev_transform(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                              int64_t nblocks) {
+    __shared__ int32_t tile[256 / N][N][N + 1];
+    dev_transform_on<N, DST, FWD>(in, out, nblocks, tile);
 }
 
 template <int N, bool DST, bool FWD>
@@ -503,6 +509,25 @@ static inline int64_t now_ns() {
 // then one lane publishes status, accumulator and -- with a system-scope
 // release -- the completion word.  (NH_SMALL_OLD builds the previous form:
 // device-memory words reset under __threadfence(), a system fence per wave.)
+// A body that needs an LDS scratch tile (the per-block transforms: their
+// tiles are too large to live in the server's kernel as static LDS, DESIGN.md
+// §4.6): every form hands it kScratch bytes of LDS as a fourth argument.
+constexpr size_t kScratch = 32 * 33 * 4;   // one 32x32 transform tile (pitch 33)
+template <class F>
+struct ScratchBody {
+    F f;
+};
+template <class F>
+struct is_scratch_body : std::false_type {};
+template <class F>
+struct is_scratch_body<ScratchBody<F>> : std::true_type {};
+template <class F>
+__device__ __forceinline__ void run_body(const F& f, const uint8_t* in, unsigned long long* st, uint8_t* o,
+                                         uint8_t* scratch) {
+    if constexpr (is_scratch_body<F>::value) f.f(in, st, o, scratch);
+    else f(in, st, o);
+}
+
 template <class F, size_t SZ>
 __global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned long long* dw, unsigned long long* hres,
                                                unsigned long long seq) {
@@ -514,7 +539,12 @@ __global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned lon
         s_w[1] = 0ull;         // accumulator of the reductions
     }
     __syncthreads();
-    f(in.b, s_w, (uint8_t*)(hres + 4));
+    if constexpr (is_scratch_body<F>::value) {
+        __shared__ __attribute__((aligned(16))) uint8_t s_scr[kScratch];
+        run_body(f, in.b, s_w, (uint8_t*)(hres + 4), s_scr);
+    } else {
+        f(in.b, s_w, (uint8_t*)(hres + 4));
+    }
     __builtin_amdgcn_s_waitcnt(0);        // this wave's result stores acknowledged
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -529,7 +559,12 @@ __global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned lon
     }
     __threadfence();
     __syncthreads();
-    f(in.b, dw, (uint8_t*)(hres + 4));
+    if constexpr (is_scratch_body<F>::value) {
+        __shared__ __attribute__((aligned(16))) uint8_t s_scr[kScratch];
+        run_body(f, in.b, dw, (uint8_t*)(hres + 4), s_scr);
+    } else {
+        f(in.b, dw, (uint8_t*)(hres + 4));
+    }
     __threadfence_system();               // this thread's result stores have reached host memory
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -543,7 +578,12 @@ __global__ void __launch_bounds__(256) k_small(SmallIn<SZ> in, F f, unsigned lon
 
 template <class F>
 __global__ void __launch_bounds__(256) k_staged(const uint8_t* in, F f, unsigned long long* dw, uint8_t* out) {
-    f(in, dw, out);
+    if constexpr (is_scratch_body<F>::value) {
+        __shared__ __attribute__((aligned(16))) uint8_t s_scr[kScratch];
+        run_body(f, in, dw, out, s_scr);
+    } else {
+        f(in, dw, out);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -567,16 +607,19 @@ __global__ void __launch_bounds__(256) k_staged(const uint8_t* in, F f, unsigned
 // polls, or on a stop request (thunk address 0).  Every exit path is reached by
 // every wave, so the grid always drains.  The host relaunches it when it finds
 // `exited` equal to the epoch it launched with and the call's completion word
-// unwritten.  Bodies with large LDS tiles (the transforms) or stack (the float64
-// pairwise sums) stay on k_small: a kernel with an indirect call allocates the
-// LDS of every address-taken callee and cannot size its stack.
+// unwritten.  A kernel with an indirect call allocates the static LDS of every
+// address-taken callee and cannot size its stack, so the transforms take their
+// tile from the server's LDS scratch (ScratchBody) and the bodies with 1.5 KB of
+// stack (the float64 pairwise sums) stay on k_small.  Requests carry up to
+// kSrvIn bytes of inputs (k_small's argument block: 3 KB).
 constexpr size_t kSrvCap = 128;                       // bytes of a body's captures
+constexpr size_t kSrvIn = 8192;                       // input bytes a served call may carry
 constexpr unsigned kSrvMaxPolls = 50u * 1000u * 1000u;
 constexpr unsigned long long kSrvFlagAcc = 1;         // flags: write the accumulator to output word 0
-typedef void (*SrvFn)(const uint8_t*, unsigned long long*, uint8_t*, const uint8_t*);
+typedef void (*SrvFn)(const uint8_t*, unsigned long long*, uint8_t*, const uint8_t*, uint8_t*);
 
 struct SrvReq {                        // mapped pinned host memory, 64-byte lines
-    unsigned long long word;           // host: seq << 12 | flags << 8 | input bytes / 16, written last
+    unsigned long long word;           // host: seq << 16 | flags << 12 | input bytes / 16, written last
     unsigned long long pad0[7];
     unsigned long long exited;         // server: the epoch it left with (its last store)
     unsigned long long pad1[7];
@@ -585,15 +628,15 @@ struct SrvReq {                        // mapped pinned host memory, 64-byte lin
     unsigned long long fn;             // host: device address of srv_thunk<F>; 0 = stop
     unsigned long long pad3[7];
     alignas(16) uint8_t cap[kSrvCap];  // host: the body's captures
-    alignas(16) uint8_t in[kSmallIn];  // host: the inputs
+    alignas(16) uint8_t in[kSrvIn];    // host: the inputs
 };
 constexpr unsigned kSrvFnWord = offsetof(SrvReq, fn) / 8, kSrvCapWord = offsetof(SrvReq, cap) / 8;
 static_assert(offsetof(SrvReq, in) == offsetof(SrvReq, cap) + kSrvCap, "captures and inputs are contiguous");
 
 template <class F>
 __device__ __attribute__((noinline)) void srv_thunk(const uint8_t* in, unsigned long long* st, uint8_t* o,
-                                                    const uint8_t* cap) {
-    (*reinterpret_cast<const F*>(cap))(in, st, o);
+                                                    const uint8_t* cap, uint8_t* scratch) {
+    run_body(*reinterpret_cast<const F*>(cap), in, st, o, scratch);
 }
 template <class F>
 __global__ void k_srv_addr(unsigned long long* out) {
@@ -607,7 +650,8 @@ __device__ __forceinline__ unsigned long long ld_sys(const unsigned long long* p
 __global__ void __launch_bounds__(256) k_srv(SrvReq* q, unsigned long long* hout, unsigned long long last,
                                               unsigned long long epoch, unsigned long long idle,
                                               unsigned long long life) {
-    __shared__ alignas(16) unsigned long long s_ci[(kSrvCap + kSmallIn) / 8];   // captures | inputs
+    __shared__ alignas(16) unsigned long long s_ci[(kSrvCap + kSrvIn) / 8];   // captures | inputs
+    __shared__ alignas(16) uint8_t s_scr[kScratch];                          // ScratchBody bodies' tile
     __shared__ unsigned long long s_fn;
     __shared__ unsigned long long s_w[2];
     __shared__ unsigned long long s_word;     // the request word taken (== last: leave)
@@ -636,17 +680,22 @@ __global__ void __launch_bounds__(256) k_srv(SrvReq* q, unsigned long long* hout
             return;
         }
         // intake: thunk address, captures and inputs, one round of parallel loads
-        const unsigned nwords = (unsigned)(kSrvCap / 8 + 2 * (word & 0xff) < (kSrvCap + kSmallIn) / 8
-                                               ? kSrvCap / 8 + 2 * (word & 0xff) : (kSrvCap + kSmallIn) / 8);
-        static_assert((kSrvCap + kSmallIn) / 8 <= 2 * 256, "intake: two words per thread");
+        const unsigned nwords = (unsigned)(kSrvCap / 8 + 2 * (word & 0xfff) < (kSrvCap + kSrvIn) / 8
+                                               ? kSrvCap / 8 + 2 * (word & 0xfff) : (kSrvCap + kSrvIn) / 8);
+        constexpr unsigned kIw = (unsigned)((kSrvCap + kSrvIn) / 8 + 255) / 256;   // words per thread
         {   // every load issued before the first use
-            const unsigned i0 = threadIdx.x, i1 = threadIdx.x + 256;
-            unsigned long long a = 0, b = 0, c = 0;
-            if (i0 < nwords) a = ld_sys(qw + kSrvCapWord + i0);
-            if (i1 < nwords) b = ld_sys(qw + kSrvCapWord + i1);
+            unsigned long long v[kIw], c = 0;
+#pragma unroll
+            for (unsigned k = 0; k < kIw; ++k) {
+                const unsigned i = threadIdx.x + 256 * k;
+                v[k] = i < nwords ? ld_sys(qw + kSrvCapWord + i) : 0ull;
+            }
             if (threadIdx.x == 0) c = ld_sys(qw + kSrvFnWord);
-            if (i0 < nwords) s_ci[i0] = a;
-            if (i1 < nwords) s_ci[i1] = b;
+#pragma unroll
+            for (unsigned k = 0; k < kIw; ++k) {
+                const unsigned i = threadIdx.x + 256 * k;
+                if (i < nwords) s_ci[i] = v[k];
+            }
             if (threadIdx.x == 0) s_fn = c;
         }
         __syncthreads();
@@ -657,13 +706,13 @@ __global__ void __launch_bounds__(256) k_srv(SrvReq* q, unsigned long long* hout
         }
         const SrvFn f = (SrvFn)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(fn >> 32)) << 32) |
                                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)fn));
-        f((const uint8_t*)(s_ci + kSrvCap / 8), s_w, (uint8_t*)hout, (const uint8_t*)s_ci);
+        f((const uint8_t*)(s_ci + kSrvCap / 8), s_w, (uint8_t*)hout, (const uint8_t*)s_ci, s_scr);
         __builtin_amdgcn_s_waitcnt(0);        // this wave's result stores acknowledged
         __syncthreads();
         if (threadIdx.x == 0) {
             const unsigned long long st = s_w[0];
-            if ((word >> 8) & kSrvFlagAcc) hout[0] = s_w[1];
-            __hip_atomic_store(&q->done, ((word >> 12) << 8) | (st == ULLONG_MAX ? 0ull : (st & 0xff)),
+            if ((word >> 12) & kSrvFlagAcc) hout[0] = s_w[1];
+            __hip_atomic_store(&q->done, ((word >> 16) << 8) | (st == ULLONG_MAX ? 0ull : (st & 0xff)),
                                __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);   // completion word, last
         }
         last = word;
@@ -687,6 +736,7 @@ struct Staging {
     unsigned long long epoch = 0;         //                    epoch of the last server launched
     bool srv_alive = false;               //                    launched and not known to have left
     unsigned long long clock_khz = 100000;  //                    the constant clock k_srv times itself with
+    bool stack_ok = false;                //                    the per-thread stack limit covers the callees' stack
     int64_t n_served = 0, n_launches = 0, n_kernel = 0;   // nh_block_server_stats
 };
 constexpr int kMaxDevices = 64;
@@ -749,6 +799,10 @@ static int staging_init(Staging& s) {    // caller holds s.mu
     NH_HIP(hipGetDevice(&dev));
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
     s.clock_khz = (unsigned long long)khz;
+    // k_srv's indirect calls run on the runtime's per-thread stack (hipLimitStackSize);
+    // the served bodies need at most 32 B of it (inverse 32x32 transform)
+    size_t stack = 0;
+    s.stack_ok = hipDeviceGetLimit(&stack, hipLimitStackSize) == hipSuccess && stack >= 256;
     s.epoch = 0;
     s.srv_alive = false;
     s.ready = true;
@@ -764,7 +818,7 @@ static void server_post(Staging& s, unsigned long long word) {
 static void server_stop(Staging& s) {
     if (!s.srv_alive) return;
     s.req->fn = 0;
-    server_post(s, ++s.seq << 12);
+    server_post(s, ++s.seq << 16);
     s.srv_alive = false;
 }
 
@@ -843,7 +897,7 @@ static int wait_completion(hipStream_t stream, const unsigned long long* word, u
 // pending request.  `exited` is the server's last store, after any completion
 // word, so the completion word is read again after `exited` before relaunching.
 static int server_wait(Staging& s, unsigned long long word, unsigned long long* done) {
-    const unsigned long long seq = word >> 12;
+    const unsigned long long seq = word >> 16;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned spins = 1;; ++spins) {
         unsigned long long d = __atomic_load_n(&s.req->done, __ATOMIC_ACQUIRE);
@@ -899,7 +953,8 @@ class BlockCall {
         unsigned long long st, acc;
         if constexpr (kServe) {
             static_assert(sizeof(F) <= kSrvCap && alignof(F) <= 16, "captures exceed the server's block");
-            if (server_idle_us() > 0 && end_ <= kSmallIn && res <= kSmallOut) {
+            if (server_idle_us() > 0 && end_ <= kSrvIn && res <= kSmallOut &&
+                (S->stack_ok || !is_scratch_body<F>::value)) {
                 unsigned long long fn = 0;
                 NH_TRY_(server_fn<F>(*S, (int)(S - g_staging), &fn));
                 SrvReq* q = S->req;
@@ -908,7 +963,7 @@ class BlockCall {
                 std::memcpy(q->cap, (const void*)&f, sizeof(F));
                 q->fn = fn;
                 const unsigned long long word =
-                    (++S->seq << 12) | ((from_acc ? kSrvFlagAcc : 0ull) << 8) | (align_up(end_, 16) / 16);
+                    (++S->seq << 16) | ((from_acc ? kSrvFlagAcc : 0ull) << 12) | (align_up(end_, 16) / 16);
                 const int64_t t1 = now_ns();
                 server_post(*S, word);
                 if (!S->srv_alive || __atomic_load_n(&q->exited, __ATOMIC_ACQUIRE) == S->epoch)
@@ -1176,9 +1231,10 @@ template <int N, bool DST, bool FWD>
 static int block_transform_n(const int32_t* in, int32_t* out) {
     BlockCall c;
     const size_t oi = c.in(in, N * N * 4);
-    return c.run<false>(1, [=] __device__(U8 i, ST, uint8_t* o) {
-        dev_transform<N, DST, FWD>((const int32_t*)(i + oi), (int32_t*)o, 1);
-    }, out, N * N * 4);
+    auto body = [=] __device__(U8 i, ST, uint8_t* o, uint8_t* scr) {
+        dev_transform_on<N, DST, FWD>((const int32_t*)(i + oi), (int32_t*)o, 1, (int32_t (*)[N][N + 1])scr);
+    };
+    return c.run(1, ScratchBody<decltype(body)>{body}, out, N * N * 4);
 }
 template <bool FWD>
 static int block_transform(const int32_t* in, int64_t size, int use_dst, int32_t* out) {

@@ -1567,6 +1567,7 @@ struct Closed4Args {
     uint32_t seed;
     QuantParams q[4];       // log2 N = 2..5
     int32_t dqs, dq_per;
+    const uint8_t* plan;    // k_tu_closed_pair: per-(plane of the group, CTU) TU schedules (k_closed4_plan)
     int32_t probe;          // A/B timing probes (k_tu_closed_pair; wrong outputs): 1 no wait on the row
                             // above, 2 no chains, 4 no rounds, 8 no recon-image clear, 16 no quadtree
                             // hashes (0 in the product)
@@ -1980,16 +1981,35 @@ struct PairPlanes {
     uint8_t* tu[2];
 };
 
+// k_tu_closed_pair runs ONE wave per workgroup: its LDS accesses execute in
+// program order, so a wave-level code-motion barrier is all the chains and the
+// round loop need between an LDS write and another lane's read (no
+// s_waitcnt on the LDS queue, no barrier).  -DNH_CLOSED4_WGSYNC=1 builds the
+// previous workgroup barriers (A/B).
+#ifndef NH_CLOSED4_WGSYNC
+#define NH_CLOSED4_WGSYNC 0
+#endif
+#ifndef NH_CLOSED4_EARLYPOLL
+#define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
+#endif
+__device__ __forceinline__ void pair_sync() {
+#if NH_CLOSED4_WGSYNC
+    __syncthreads();
+#else
+    __builtin_amdgcn_wave_barrier();
+#endif
+}
+
 template <int N, bool DST>
 __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
-                                                    int cnt, int total, int c0, const int* slx, const int* sly,
+                                                    int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq) {
     constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
     constexpr int32_t BIAS = 1 << (S - 1);
     const int lane = opaque_lane64(), t = lane % N, e = c0 + lane / N;
     const bool on = e < total;
     const int p = on && e >= cnt ? 1 : 0, k = on ? e - p * cnt : 0;   // idle lanes shadow plane 0's first TU
-    const int lx = slx[k], ly = sly[k], x = x0c + lx, y = y0c + ly;
+    const int code = ent[k], lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4, x = x0c + lx, y = y0c + ly;
     int16_t (*rc)[33] = rc2[p];
     const int16_t* src = p ? pp.src[1] : pp.src[0];
     int16_t* tl = t16 + p * (32 * TP) + ly * TP + lx;   // tl[line * TP + slot]
@@ -2039,7 +2059,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
 #pragma unroll
         for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(yv[i] >> S);
     }
-    __syncthreads();
+    pair_sync();
     const int st = inv_slot<N, DST>(t);
     {
         pk16 P[H];   // forward pass 2 (transform.py:188-194): row t
@@ -2047,7 +2067,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         for (int m = 0; m < H; ++m) P[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
         fwd1d_pk<N, DST>(P, yv, BIAS);
     }
-    __syncthreads();
+    pair_sync();
     if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
         int32_t* lrow = (p ? pp.lvl[1] : pp.lvl[0]) + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
@@ -2057,7 +2077,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
             tl[kk * TP + st] = (int16_t)dequant_s(l, cq);
         }
     }
-    __syncthreads();
+    pair_sync();
     int32_t xv[N];
     {
         pk16 Y[H];   // inverse pass 1 (transform.py:221-227): column t -> line i, slot inv_slot(t)
@@ -2065,12 +2085,12 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
         inv1d_pk<N, DST>(Y, xv, BIAS);
     }
-    __syncthreads();
+    pair_sync();
     if (on) {
 #pragma unroll
         for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(xv[i] >> S);
     }
-    __syncthreads();
+    pair_sync();
     {
         pk16 Y[H];   // inverse pass 2 (transform.py:230-236): row t
 #pragma unroll
@@ -2094,7 +2114,70 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
             for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
         }
     }
+    pair_sync();
+}
+
+// The TU schedule of one CTU of one plane id (k_closed4_plan, NH_CLOSED4_PLAN):
+// the quadtree and so the dataflow rounds depend on (plane id, CTU) only, not
+// on the frame, so they are found once per launch instead of once per CTU row of
+// every plane pair.  Record (128 B): bytes 0..63 the TUs' codes
+// (ox | oy << 3 | size index << 6, in 4x4 units; size index 0 = 32 .. 3 = 4) in
+// execution order -- round by round, sizes 32, 16, 8, 4, lane order within --
+// and bytes 64..127 the count of each (round, size) pair, 4 * round + size.
+#ifndef NH_CLOSED4_PLAN
+#define NH_CLOSED4_PLAN 1
+#endif
+constexpr int kPlanBytes = 128;
+__global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* plan) {
+    __shared__ int owner_of[64], done_of[64];
+    const int lane = threadIdx.x, ctb = a.ctb, U = ctb / 4, UU = U * U;
+    const int cx = (int)blockIdx.x % a.ccols, cy = (int)blockIdx.x / a.ccols, c = (int)blockIdx.y;
+    const int pid = a.plane_id + c, x0c = cx * ctb, y0c = cy * ctb;
+    uint8_t* rec = plan + ((int64_t)c * a.crows * a.ccols + blockIdx.x) * kPlanBytes;
+    int tn = 0, ox = 0, oy = 0;
+    bool pending = false;
+    if (lane < UU) {
+        const int ux = lane % U, uy = lane / U, x = x0c + 4 * ux, y = y0c + 4 * uy;
+        int own = lane;
+        if (x < a.w && y < a.h) {
+            const int n = tu_leaf(a.w, a.h, ctb, pid, a.seed, x, y), nu = n / 4;
+            ox = ux - ux % nu;
+            oy = uy - uy % nu;
+            own = oy * U + ox;
+            pending = ox == ux && oy == uy && x + n <= a.w && y + n <= a.h;
+            tn = n;
+        }
+        owner_of[lane] = own;
+        done_of[lane] = 0;
+    }
+    rec[64 + lane] = 0;
     __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    int off = 0;
+    for (int round = 0; round < 16 && __ballot(pending); ++round) {
+        bool ready = pending;
+        if (pending) {
+            const int nu = tn / 4;
+            for (int k = 0; k < nu; ++k) {
+                if (oy > 0 && !done_of[owner_of[(oy - 1) * U + ox + k]]) ready = false;
+                if (ox > 0 && !done_of[owner_of[(oy + k) * U + ox - 1]]) ready = false;
+            }
+        }
+#pragma unroll
+        for (int si = 0; si < 4; ++si) {
+            const bool mine = ready && tn == (32 >> si);
+            const uint64_t m = __ballot(mine);
+            if (mine) rec[off + __popcll(m & lt)] = (uint8_t)(ox | (oy << 3) | (si << 6));
+            if (lane == 0) rec[64 + 4 * round + si] = (uint8_t)__popcll(m);
+            off += __popcll(m);
+        }
+        __syncthreads();
+        if (ready) {
+            done_of[lane] = 1;
+            pending = false;
+        }
+        __syncthreads();
+    }
 }
 
 // The pair form of k_tu_closed (NARROW streams only: the wide flag work[2]
@@ -2110,7 +2193,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
     __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * TP];
-    __shared__ int owner_of[64], done_of[64], slx[16], sly[16];
+    __shared__ int owner_of[64], done_of[64];
+    __shared__ __attribute__((aligned(16))) uint8_t ent_s[NH_CLOSED4_PLAN ? kPlanBytes : 16];
     __shared__ int row_s, stall_s;
     if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
     const int lane = threadIdx.x;
@@ -2128,7 +2212,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             row_s = atomicAdd(&a.work[0], 1);
             stall_s = 0;
         }
-        __syncthreads();
+        pair_sync();
         const int tk = row_s;
         if (tk >= total) break;
         const int cy = tk / npairs, q = tk - cy * npairs;
@@ -2149,11 +2233,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
         }
         const int pid = a.plane_id + c, y0c = cy * ctb;
         for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;   // recon starts as zeros (Frame.zeros)
-        __syncthreads();
+        pair_sync();
         if (hl < ctb) rc[hq][1 + hl][0] = 128;                             // x == 0: left = 128 (block.py:45-50)
+        // the first poll of a CTU's line words is issued at the end of the previous CTU,
+        // before its publish store, so the two round trips overlap (NH_CLOSED4_EARLYPOLL)
+        uint64_t early = 0;
+        const uint32_t* plan_row = (const uint32_t*)(a.plan + ((int64_t)c * a.crows + cy) * a.ccols * kPlanBytes);
         for (int cx = 0; cx < a.ccols; ++cx) {
             const int x0c = cx * ctb;
             const int nw = (min(ctb, a.w - x0c) + 1) / 2;
+            // this CTU's TU schedule (128 B), loaded under the wait on the row above
+            uint32_t planw = 0;
+            if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) planw = plan_row[cx * (kPlanBytes / 4) + lane];
             // top row of this CTU: 128 at y == 0, else the CTU above's bottom row (tagged line words)
             if (cy == 0) {
                 if (hl < ctb) rc[hq][0][1 + hl] = 128;
@@ -2164,7 +2255,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 for (;;) {
                     bool ok = true;
                     if (need) {
-                        const uint64_t v = ld_sys64(line[hq] + x0c / 2 + hl);
+                        const uint64_t v = (NH_CLOSED4_EARLYPOLL && spins == 0 && cx > 0) ? early
+                                                                                        : ld_sys64(line[hq] + x0c / 2 + hl);
                         ok = (int)(v >> 32) == cy || (NH_AB && (a.probe & 1));
                         val = (uint32_t)v;
                     }
@@ -2182,8 +2274,37 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     if (2 * hl + 1 < ctb) rc[hq][0][2 + 2 * hl] = (int16_t)(val >> 16);
                 }
             }
-            __syncthreads();
+            if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) ((uint32_t*)ent_s)[lane] = planw;
+            pair_sync();
             if (stall_s) break;
+#if NH_CLOSED4_PLAN
+            {   // the CTU's TUs in dataflow rounds, from the schedule: lane rs holds the count of
+                // (round rs / 4, size index rs % 4); batches run in the schedule's order
+                const int cntv = ent_s[64 + lane];
+                const uint64_t nz = __ballot(cntv != 0);
+                const int last = nz ? 63 - __clzll(nz) : -1;
+                int off = 0;
+                for (int rs = 0; rs <= last && !(NH_AB && (a.probe & 4)); ++rs) {
+                    const int cnt = __builtin_amdgcn_readlane(cntv, rs);
+                    if (cnt == 0) continue;
+                    const int tot = cnt << two;
+                    const uint8_t* ent = ent_s + off;
+                    switch (rs & 3) {
+#define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
+                        for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
+                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q);
+                        case 0: NH_PLAN_BATCH(32, false, cq[3]) break;
+                        case 1: NH_PLAN_BATCH(16, false, cq[2]) break;
+                        case 2: NH_PLAN_BATCH(8, false, cq[1]) break;
+                        default:
+                            if (a.is_luma) { NH_PLAN_BATCH(4, true, cq[0]) }
+                            else { NH_PLAN_BATCH(4, false, cq[0]) }
+#undef NH_PLAN_BATCH
+                    }
+                    off += cnt;
+                }
+            }
+#else
             // the CTU's TUs in dataflow rounds (as k_tu_closed), found once for both planes
             const int U = ctb / 4, UU = U * U;
             int tn = 0, ox = 0, oy = 0;
@@ -2202,7 +2323,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 owner_of[lane] = own;
                 done_of[lane] = 0;
             }
-            __syncthreads();
+            pair_sync();
             for (int round = 0; round < UU && __ballot(pending) && !(NH_AB && (a.probe & 4)); ++round) {
                 bool ready = pending;
                 if (pending) {
@@ -2217,15 +2338,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 {                                                                                            \
                     const uint64_t m = __ballot(ready && tn == NN);                                          \
                     const int cnt = __popcll(m);                                                             \
-                    if (ready && tn == NN) {                                                                 \
-                        const int k = __popcll(m & lt);                                                      \
-                        slx[k] = ox * 4;                                                                     \
-                        sly[k] = oy * 4;                                                                     \
-                    }                                                                                        \
-                    __syncthreads();                                                                         \
+                    if (ready && tn == NN) ent_s[__popcll(m & lt)] = (uint8_t)(ox | (oy << 3));            \
+                    pair_sync();                                                                             \
                     const int tot = cnt << two;                                                              \
                     for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                   \
-                        tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, slx, sly, rc, t16, Q);   \
+                        tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent_s, rc, t16, Q);      \
                 }
                 NH_BATCH2(32, false, cq[3]);
                 NH_BATCH2(16, false, cq[2]);
@@ -2236,7 +2353,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     done_of[lane] = 1;
                     pending = false;
                 }
-                __syncthreads();
+                pair_sync();
+            }
+#endif
+            if (NH_CLOSED4_EARLYPOLL && cy > 0 && cx + 1 < a.ccols) {
+                const int nwn = (min(ctb, a.w - x0c - ctb) + 1) / 2;
+                if (hl < nwn && hq <= two) early = ld_sys64(line[hq] + (x0c + ctb) / 2 + hl);
             }
             // publish both bottom rows (the next CTU row polls them), then slide: right column -> left column
             if (cy + 1 < a.crows && hl < nw && hq <= two) {
@@ -2244,17 +2366,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 const uint32_t hi = 2 * hl + 1 < ctb ? (uint16_t)rc[hq][ctb][2 + 2 * hl] : 0u;
                 st_sys64(line[hq] + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
             }
-            __syncthreads();
+            pair_sync();
             int16_t keep = 0;
             if (hl < ctb) keep = rc[hq][1 + hl][ctb];
-            __syncthreads();
+            pair_sync();
             if (!(NH_AB && (a.probe & 8)))
                 for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
-            __syncthreads();
+            pair_sync();
             if (hl < ctb) rc[hq][1 + hl][0] = keep;
-            __syncthreads();
+            pair_sync();
         }
-        __syncthreads();
+        pair_sync();
         if (stall_s) break;
     }
 }
@@ -2450,10 +2572,18 @@ static int closed4_layout(const nh_plane_set* set, int ctb, int64_t& lines0, int
     return NH_OK;
 }
 
+// Workspace: [ticket, status, wide flag, pad | 64-bit line words of every plane |
+// the TU schedules of k_closed4_plan: planes per group x CTUs x kPlanBytes].
+static int64_t closed4_plan_offset(int64_t lines0, int64_t lw, int64_t np) { return 4 * lines0 + 8 * lw * np; }
+static int64_t closed4_plan_bytes(const nh_plane_set* set, int ctb) {
+    return (int64_t)set->planes_per_group * ((set->height + ctb - 1) / ctb) * ((set->width + ctb - 1) / ctb) *
+           kPlanBytes;
+}
+
 extern "C" int64_t nh_tu_pipeline_closed_workspace_bytes(const nh_plane_set* set, int ctb) {
     int64_t lines0, lw, np;
     if (closed4_layout(set, ctb, lines0, lw, np)) return -1;
-    return 4 * lines0 + 8 * lw * np;
+    return closed4_plan_offset(lines0, lw, np) + closed4_plan_bytes(set, ctb);
 }
 
 extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
@@ -2470,7 +2600,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         return NH_EARG;
     }
     hipStream_t s = as_stream(stream);
-    NH_HIP(hipMemsetAsync(d_work, 0, 4 * lines0 + 8 * lw * np, s));
+    NH_HIP(hipMemsetAsync(d_work, 0, closed4_plan_offset(lines0, lw, np), s));   // not the schedules
     if (!np || !set->height) return NH_OK;
     Closed4Args a{};
     a.src = d_src + set->base;
@@ -2533,6 +2663,12 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
 #endif
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
         const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
+        if (NH_CLOSED4_PLAN) {   // the TU schedule of every (plane of the group, CTU), once per launch
+            uint8_t* plan = (uint8_t*)d_work + closed4_plan_offset(lines0, lw, np);
+            a.plan = plan;
+            k_closed4_plan<<<dim3((unsigned)(a.crows * a.ccols), (unsigned)a.ppg), 64, 0, s>>>(a, plan);
+            NH_HIP(hipGetLastError());
+        }
         // A/B build: resident waves per CU, for both sets or per luma / chroma set
         static const int wpc = NH_KNOB("NH_CLOSED4_WPC", 0), wpc_l = NH_KNOB("NH_CLOSED4_WPC_L", 0),
                          wpc_c = NH_KNOB("NH_CLOSED4_WPC_C", 0);

@@ -3,8 +3,8 @@
 Per-block calls are taken by one resident workgroup from mapped host memory
 while calls keep coming; it leaves after its idle time and is relaunched by the
 next call.  These tests check that (i) a long mixed sequence of served calls and
-calls that run as their own kernel (the transforms: stop request, then k_small)
-is bit-exact against the oracle, (ii) a call after the server left is served by
+calls that run as their own kernel (inputs over 8 KB: stop request, then the
+staged form) is bit-exact against the oracle, (ii) a call after the server left is served by
 a relaunched one, (iii) torch work and other threads are not held up, and (iv)
 the launch-per-call form (nh_block_server_set_idle_us(0)) gives the same answers."""
 import ctypes as C
@@ -53,7 +53,7 @@ def one_round(nh, rng, n):
     assert np.array_equal(an, O.intra_angular(top, left, int(left[0]), mode, n)), mode
     res = nh.residual_block(orig, an)
     assert np.array_equal(res, O.residual(orig, an))
-    coeff = nh.forward_transform(res)          # k_small: the server is asked to leave first
+    coeff = nh.forward_transform(res)          # served, tile in the server's LDS scratch
     assert np.array_equal(coeff, O.forward_transform(res))
     qp = int(rng.integers(0, 52))
     lvl = nh.quantize_block(coeff, qp)
@@ -76,8 +76,8 @@ def test_mixed_sequence_served_and_kernel_calls(nh):
         one_round(nh, rng, (4, 8, 16, 32)[i % 4])
     s1 = stats()
     if s1[3] > 0:   # server enabled (default)
-        assert s1[0] - s0[0] >= 120 * 5, (s0, s1)        # served calls (32x32 inputs > 3 KB are staged)
-        assert s1[2] - s0[2] >= 120 * 2, (s0, s1)        # the transforms ran as kernels
+        assert s1[0] - s0[0] >= 120 * 10, (s0, s1)       # served calls (transforms on the LDS scratch too)
+        assert s1[2] - s0[2] >= 30, (s0, s1)             # 32x32 mse (16 KB of int64 inputs) is staged
         assert s1[1] - s0[1] >= 2, (s0, s1)              # relaunched after each stop
 
 
