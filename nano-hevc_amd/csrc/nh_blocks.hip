@@ -1111,6 +1111,12 @@ int nh_release_staging(void) {
 }
 
 int nh_block_server_stop(void) {
+    bool any = false;   // no HIP call at all unless a server was started (it runs at interpreter exit)
+    for (int d = 0; d < kMaxDevices && !any; ++d) {
+        std::lock_guard<std::mutex> lk(g_staging[d].mu);
+        any = g_staging[d].ready && g_staging[d].srv_alive;
+    }
+    if (!any) return NH_OK;
     int cur = 0;
     NH_HIP(hipGetDevice(&cur));
     int first_err = NH_OK;
