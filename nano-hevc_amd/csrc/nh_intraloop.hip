@@ -1989,6 +1989,9 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_WGSYNC
 #define NH_CLOSED4_WGSYNC 0
 #endif
+#ifndef NH_CLOSED4_PRIO
+#define NH_CLOSED4_PRIO 0
+#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -2197,6 +2200,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     __shared__ __attribute__((aligned(16))) uint8_t ent_s[NH_CLOSED4_PLAN ? kPlanBytes : 16];
     __shared__ int row_s, stall_s;
     if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
+    if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // A/B: the luma wavefront's issue first
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
     ChainQ cq[4];
@@ -2374,6 +2378,284 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
             pair_sync();
             if (hl < ctb) rc[hq][1 + hl][0] = keep;
+            pair_sync();
+        }
+        pair_sync();
+        if (stall_s) break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Config 4 closed loop, 8-bit streams: P planes per wave (k_tu_closed_multi).
+// The pair form above, generalised to P planes (groups P*m .. P*m + P - 1 of
+// the set, same plane of the group) with the CTB a compile-time size, so a
+// chroma CTU (CTB 16: 16 4x4 units) fills the wave's lanes with the TUs of
+// four frames instead of two.  Per lane the batch entry e names plane
+// p = e / cnt and TU e mod cnt of the CTU's schedule; each plane keeps its own
+// LDS reconstruction and int16 tile, publishes and polls its own line words
+// (lanes [64/P * p, 64/P * (p+1)) serve plane p), and the planes never exchange
+// data: same TUs, same inputs, same chain as tu_closed_batch_pk2, so the same
+// results.  The CTU's LDS reconstruction is cleared once per CTU row, not per
+// CTU: a TU only reads samples of TUs coded before it (z-order) or the CTU's
+// top row / left column, which are rewritten for every CTU; samples past a
+// ragged plane edge belong to no TU and are never read.
+template <int N, bool DST, int P, int CTB>
+__device__ __forceinline__ void tu_closed_batch_pkm(const Closed4Args& a, int g0, int c, int x0c, int y0c, int cnt,
+                                                    int total, int c0, const uint8_t* ent,
+                                                    int16_t (*rcm)[CTB + 1][CTB + 1], int16_t* t16,
+                                                    const ChainQ& cq) {
+    constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = CTB + 2;
+    constexpr int32_t BIAS = 1 << (S - 1);
+    const int lane = opaque_lane64(), t = lane % N, e = c0 + lane / N;
+    const bool on = e < total;
+    int p = 0;   // idle lanes shadow plane 0's first TU
+    if (on) {
+#pragma unroll
+        for (int j = 1; j < P; ++j) p += e >= j * cnt ? 1 : 0;
+    }
+    const int k = on ? e - p * cnt : 0;
+    const int code = ent[k], lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4, x = x0c + lx, y = y0c + ly;
+    int16_t (*rc)[CTB + 1] = rcm[p];
+    const int64_t off = (int64_t)(g0 + p) * a.group_stride + (int64_t)c * a.plane_stride;
+    int16_t* tl = t16 + p * (CTB * TP) + ly * TP + lx;   // tl[line * TP + slot]
+    const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
+    const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
+    int32_t sum = topt + leftt;                                // DC (intra.py:46-62)
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    const int32_t dc = (sum + N) >> (L2 + 1);
+    const pk16 dc2 = pk_splat(dc);
+    pk16 o2[H];
+    pku16 pl2[H];
+    {
+        const int32_t b = (t + 1) * tr + (N - 1) * topt + bl + N, st = bl - topt;
+        pku16 bs = {(unsigned short)b, (unsigned short)(b + st)};
+        const pku16 st2 = {(unsigned short)(2 * st), (unsigned short)(2 * st)};
+        const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
+        const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
+        const int16_t* sp = a.src + off + (int64_t)y * a.pitch + x + t;
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
+            const pku16 lf = {(unsigned short)rc[ly + 1 + 2 * m][lx], (unsigned short)rc[ly + 2 + 2 * m][lx]};
+            pl2[m] = (lf * wl + bs) >> sh;
+            bs += st2;
+        }
+    }
+    int32_t ed = 0, ep = 0;
+#pragma unroll
+    for (int m = 0; m < H; ++m) {
+        const pk16 d0 = o2[m] - dc2, d1 = o2[m] - __builtin_bit_cast(pk16, pl2[m]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+    }
+#pragma unroll
+    for (int m = 1; m < N; m <<= 1) {
+        ed += __shfl_xor(ed, m, 64);
+        ep += __shfl_xor(ep, m, 64);
+    }
+    const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
+    pk16 r2[H];
+#pragma unroll
+    for (int m = 0; m < H; ++m) r2[m] = o2[m] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[m]));
+    int32_t yv[N];
+    fwd1d_pk<N, DST>(r2, yv, BIAS);   // forward pass 1 (transform.py:179-185): column t -> line i, slot t
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(yv[i] >> S);
+    }
+    pair_sync();
+    const int st = inv_slot<N, DST>(t);
+    {
+        pk16 Pv[H];   // forward pass 2 (transform.py:188-194): row t
+#pragma unroll
+        for (int m = 0; m < H; ++m) Pv[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        fwd1d_pk<N, DST>(Pv, yv, BIAS);
+    }
+    pair_sync();
+    if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
+        int32_t* lrow = a.lvl + off + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) {
+            const int32_t l = quant_s(yv[kk] >> S, cq.qs, cq.h_v, cq.hneg_v);
+            lrow[kk] = l;
+            tl[kk * TP + st] = (int16_t)dequant_s(l, cq);
+        }
+    }
+    pair_sync();
+    int32_t xv[N];
+    {
+        pk16 Y[H];   // inverse pass 1 (transform.py:221-227): column t -> line i, slot inv_slot(t)
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        inv1d_pk<N, DST>(Y, xv, BIAS);
+    }
+    pair_sync();
+    if (on) {
+#pragma unroll
+        for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(xv[i] >> S);
+    }
+    pair_sync();
+    {
+        pk16 Y[H];   // inverse pass 2 (transform.py:230-236): row t
+#pragma unroll
+        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
+        inv1d_pk<N, DST>(Y, xv, BIAS);
+    }
+    if (on) {   // reconstruct + clip (intra.py:70-78); planar in row layout
+        const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, stv = tr - leftt;
+        int16_t* rrow = a.rec + off + (int64_t)(y + t) * a.pitch + x;
+#pragma unroll
+        for (int kk = 0; kk < N; ++kk) {
+            const int32_t pr = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + kk] + b + kk * stv) >> (L2 + 1);
+            int32_t q = pr + (xv[kk] >> S);
+            q = q < 0 ? 0 : (q > 255 ? 255 : q);
+            rrow[kk] = (int16_t)q;
+            rc[ly + 1 + t][lx + 1 + kk] = (int16_t)q;   // no TU of this batch reads the TU's own samples
+        }
+        if (t < N / 4) {
+            uint8_t* tu = a.tu + (int64_t)((g0 + p) * a.ppg + c) * a.tu_plane;
+            const int w4 = a.w / 4;
+            for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
+        }
+    }
+    pair_sync();
+}
+
+#ifndef NH_CLOSED4_CLEAR_EVERY_CTU
+#define NH_CLOSED4_CLEAR_EVERY_CTU 0   // A/B: clear the LDS reconstruction before every CTU (the pair form's rule)
+#endif
+// Tickets run row-major over the P-plane sets ("multis"): ticket t = CTU row
+// t / nm of multi t % nm; multi m = (groups P * (m / ppg) .., plane m % ppg);
+// a wave only waits on the same multi's CTU row above, claimed before it.  A
+// tail multi with act < P planes leaves its slots >= act idle.
+#ifndef NH_MULTI_L   // planes per wave; -DNH_MULTI_L / _C: library builds for A/B
+#define NH_MULTI_L 0
+#endif
+#ifndef NH_MULTI_C
+#define NH_MULTI_C 0
+#endif
+constexpr int kMultiLuma = NH_MULTI_L, kMultiChroma = NH_MULTI_C;
+template <int P, int CTB, int WAVES = 1>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_multi(Closed4Args a) {
+    constexpr int TP = CTB + 2, LQ = 64 / P, NW = CTB / 2;
+    static_assert(NW <= LQ, "a CTU's line words must fit the lanes of its plane");
+    __shared__ int16_t rc[P][CTB + 1][CTB + 1];
+    __shared__ __attribute__((aligned(16))) int16_t t16[P * CTB * TP];
+    __shared__ __attribute__((aligned(16))) uint8_t ent_s[kPlanBytes];
+    __shared__ int row_s, stall_s;
+    if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
+    const int lane = threadIdx.x;
+    ChainQ cq[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
+    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
+    const int ngroups = a.nplanes / a.ppg, nm = ((ngroups + P - 1) / P) * a.ppg;
+    const int total = a.crows * nm;
+    const int hq = lane / LQ, hl = lane % LQ;   // line words and the left column: lanes of plane hq
+    for (;;) {
+        if (lane == 0) {
+            row_s = atomicAdd(&a.work[0], 1);
+            stall_s = 0;
+        }
+        pair_sync();
+        const int tk = row_s;
+        if (tk >= total) break;
+        const int cy = tk / nm, q = tk - cy * nm;
+        const int c = q % a.ppg, g0 = P * (q / a.ppg);
+        const int act = min(P, ngroups - g0);   // planes of this multi
+        const bool mine = hq < act;
+        uint64_t* line = lines + (int64_t)((g0 + (mine ? hq : 0)) * a.ppg + c) * a.lw;
+        const int y0c = cy * CTB;
+        for (int i = lane; i < P * (CTB + 1) * (CTB + 1); i += 64) (&rc[0][0][0])[i] = 0;   // Frame.zeros
+        pair_sync();
+        for (int i = hl; i < CTB; i += LQ) rc[hq][1 + i][0] = 128;   // x == 0: left = 128 (block.py:45-50)
+        const uint32_t* plan_row = (const uint32_t*)(a.plan + ((int64_t)c * a.crows + cy) * a.ccols * kPlanBytes);
+        for (int cx = 0; cx < a.ccols; ++cx) {
+            const int x0c = cx * CTB;
+            const int nw = (min(CTB, a.w - x0c) + 1) / 2;
+            // this CTU's TU schedule (128 B), loaded under the wait on the row above
+            uint32_t planw = 0;
+            if (lane < kPlanBytes / 4) planw = plan_row[cx * (kPlanBytes / 4) + lane];
+            // top row of this CTU: 128 at y == 0, else the CTU above's bottom row (tagged line words)
+            if (cy == 0) {
+                for (int i = hl; i < CTB; i += LQ) rc[hq][0][1 + i] = 128;
+            } else {
+                const bool need = hl < nw && mine;
+                uint32_t val = 0;
+                int spins = 0;
+                for (;;) {
+                    bool ok = true;
+                    if (need) {
+                        const uint64_t v = ld_sys64(line + x0c / 2 + hl);
+                        ok = (int)(v >> 32) == cy || (NH_AB && (a.probe & 1));
+                        val = (uint32_t)v;
+                    }
+                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                    ++spins;
+                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
+                        if (lane == 0) atomicMax(&a.work[1], 1);
+                        stall_s = 1;
+                        break;
+                    }
+                }
+                if (need) {
+                    rc[hq][0][1 + 2 * hl] = (int16_t)(val & 0xffffu);
+                    rc[hq][0][2 + 2 * hl] = (int16_t)(val >> 16);
+                }
+            }
+            if (lane < kPlanBytes / 4) ((uint32_t*)ent_s)[lane] = planw;
+            pair_sync();
+            if (stall_s) break;
+            {   // the CTU's TUs in dataflow rounds, from the schedule (k_closed4_plan): lane rs holds
+                // the count of (round rs / 4, size index rs % 4); batches run in the schedule's order
+                const int cntv = ent_s[64 + lane];
+                const uint64_t nz = __ballot(cntv != 0);
+                const int last = nz ? 63 - __clzll(nz) : -1;
+                int off = 0;
+                for (int rs = 0; rs <= last && !(NH_AB && (a.probe & 4)); ++rs) {
+                    const int cnt = __builtin_amdgcn_readlane(cntv, rs);
+                    if (cnt == 0) continue;
+                    const int tot = cnt * act;
+                    const uint8_t* ent = ent_s + off;
+                    switch (rs & 3) {
+#define NH_MULTI_BATCH(NN, DST, Q)                                                                            \
+                        for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
+                            tu_closed_batch_pkm<NN, DST, P, CTB>(a, g0, c, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q);
+                        case 0:
+                            if constexpr (CTB >= 32) { NH_MULTI_BATCH(32, false, cq[3]) }
+                            break;
+                        case 1:
+                            if constexpr (CTB >= 16) { NH_MULTI_BATCH(16, false, cq[2]) }
+                            break;
+                        case 2: NH_MULTI_BATCH(8, false, cq[1]) break;
+                        default:
+                            if (a.is_luma) { NH_MULTI_BATCH(4, true, cq[0]) }
+                            else { NH_MULTI_BATCH(4, false, cq[0]) }
+#undef NH_MULTI_BATCH
+                    }
+                    off += cnt;
+                }
+            }
+            // publish the bottom rows (the next CTU row polls them), then slide: right column -> left column
+            if (cy + 1 < a.crows && hl < nw && mine) {
+                const uint32_t lo = (uint16_t)rc[hq][CTB][1 + 2 * hl];
+                const uint32_t hi = (uint16_t)rc[hq][CTB][2 + 2 * hl];
+                st_sys64(line + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
+            }
+            pair_sync();
+            int16_t keep[(CTB + LQ - 1) / LQ];
+#pragma unroll
+            for (int j = 0; j < (CTB + LQ - 1) / LQ; ++j)
+                keep[j] = hl + j * LQ < CTB ? rc[hq][1 + hl + j * LQ][CTB] : (int16_t)0;
+            pair_sync();
+            if (NH_CLOSED4_CLEAR_EVERY_CTU || (NH_AB && (a.probe & 32)))
+                for (int i = lane; i < P * (CTB + 1) * (CTB + 1); i += 64) (&rc[0][0][0])[i] = 0;
+            pair_sync();
+#pragma unroll
+            for (int j = 0; j < (CTB + LQ - 1) / LQ; ++j)
+                if (hl + j * LQ < CTB) rc[hq][1 + hl + j * LQ][0] = keep[j];
             pair_sync();
         }
         pair_sync();
@@ -2655,7 +2937,36 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     // holds more than one group; A/B build: NH_TU_CLOSED_PAIR = 0 codes one plane
     // per wave, = 4 the pair form capped at 4 waves/SIMD
     static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
-    if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
+    // P planes per wave (k_tu_closed_multi) for CTB 32 (luma) / 16 (chroma);
+    // A/B build: NH_CLOSED4_MULTI_L / _C = planes per wave (0: the pair kernel)
+    static const int multi_l = NH_KNOB("NH_CLOSED4_MULTI_L", kMultiLuma),
+                     multi_c = NH_KNOB("NH_CLOSED4_MULTI_C", kMultiChroma);
+    const int multi = ctb == 32 ? multi_l : ctb == 16 ? multi_c : 0;
+    // A/B build: NH_CLOSED4_WAVES_L / _C = the register budget's waves per SIMD (product: the compiler's)
+    static const int mw_l = NH_KNOB("NH_CLOSED4_WAVES_L", 1), mw_c = NH_KNOB("NH_CLOSED4_WAVES_C", 1);
+    const int mw = ctb == 32 ? mw_l : mw_c;
+    void (*mkern)(Closed4Args) = nullptr;
+#define NH_MULTI_PICK(PP, CC)                                                              \
+    if (multi == PP && ctb == CC) {                                                        \
+        mkern = k_tu_closed_multi<PP, CC>;                                                 \
+        if (NH_AB && mw == 5) mkern = k_tu_closed_multi<PP, CC, NH_AB ? 5 : 1>;            \
+        if (NH_AB && mw == 6) mkern = k_tu_closed_multi<PP, CC, NH_AB ? 6 : 1>;            \
+    }
+    NH_MULTI_PICK(1, 32) NH_MULTI_PICK(1, 16) NH_MULTI_PICK(2, 32) NH_MULTI_PICK(2, 16)
+    NH_MULTI_PICK(4, 32) NH_MULTI_PICK(4, 16) NH_MULTI_PICK(8, 16)
+#undef NH_MULTI_PICK
+    if (narrow_ok != 0 && pair_ok != 0 && mkern && (set->num_groups > 1 || multi == 1)) {
+        int per_cu = 0;
+        NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mkern, 64, 0));
+        const int64_t nm = (int64_t)a.crows * ((set->num_groups + multi - 1) / multi) * set->planes_per_group;
+        uint8_t* plan = (uint8_t*)d_work + closed4_plan_offset(lines0, lw, np);
+        a.plan = plan;
+        k_closed4_plan<<<dim3((unsigned)(a.crows * a.ccols), (unsigned)a.ppg), 64, 0, s>>>(a, plan);
+        NH_HIP(hipGetLastError());
+        static const int wpc = NH_KNOB("NH_CLOSED4_WPC", 0);
+        const int64_t cap_n = (int64_t)(wpc > 0 ? wpc : std::max(1, per_cu)) * cus;
+        mkern<<<(unsigned)(nm < cap_n ? nm : cap_n), 64, 0, s>>>(a);
+    } else if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
         int per_cu = 0;
         auto kern = k_tu_closed_pair<kPairWaves>;
 #if NH_AB
