@@ -505,6 +505,31 @@ __device__ __forceinline__ h8_t ld_crow_h8(const uint16_t* row, int s, int hh) {
     const uint2 p = *(const uint2*)(row + 16 * s + 4 * hh), q = *(const uint2*)(row + 16 * s + 8 + 4 * hh);
     return __builtin_bit_cast(h8_t, make_uint4(p.x, p.y, q.x, q.y));
 }
+// The four operand pieces of each basis a lane reads, as accessors over the LDS
+// copy (BasisH) or over registers loaded once per wave (BasisRegs, k_tc32_h:
+// 32 VGPRs, no LDS copy and no workgroup barrier).
+__device__ __forceinline__ h8_t bq_t(const BasisH& b, int r, int hh, int s) { return ld_h8(&b.t[r][16 * s + 8 * hh]); }
+__device__ __forceinline__ h8_t bq_tc(const BasisH& b, int r, int hh, int s) { return ld_crow_h8(b.t[r], s, hh); }
+__device__ __forceinline__ h8_t bq_tt(const BasisH& b, int r, int hh, int s) { return ld_h8(&b.tt[r][16 * s + 8 * hh]); }
+__device__ __forceinline__ h8_t bq_ttc(const BasisH& b, int r, int hh, int s) { return ld_crow_h8(b.tt[r], s, hh); }
+struct BasisRegs {
+    h8_t t[2], tc[2], tt[2], ttc[2];
+};
+__device__ __forceinline__ BasisRegs load_basis_regs(const BasisH& g, int r, int hh) {
+    BasisRegs b;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        b.t[s] = bq_t(g, r, hh, s);
+        b.tc[s] = bq_tc(g, r, hh, s);
+        b.tt[s] = bq_tt(g, r, hh, s);
+        b.ttc[s] = bq_ttc(g, r, hh, s);
+    }
+    return b;
+}
+__device__ __forceinline__ h8_t bq_t(const BasisRegs& b, int, int, int s) { return b.t[s]; }
+__device__ __forceinline__ h8_t bq_tc(const BasisRegs& b, int, int, int s) { return b.tc[s]; }
+__device__ __forceinline__ h8_t bq_tt(const BasisRegs& b, int, int, int s) { return b.tt[s]; }
+__device__ __forceinline__ h8_t bq_ttc(const BasisRegs& b, int, int, int s) { return b.ttc[s]; }
 __device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
     return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
 }
@@ -537,8 +562,8 @@ __device__ __forceinline__ f16x_t splat16(float v) {
 // rows -- 8 rows of 128 B (levels), 16 rows of 64 B (recon) -- instead of 32-B
 // / 16-B pieces of 32 rows.
 constexpr int kOutP = 36, kRecP = 24;   // int32 per row: level tile, recon tile (48 halves; 16-B rows)
-template <bool TSTORE = false>
-__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, const BasisH& bs,
+template <bool TSTORE = false, class B = BasisH>
+__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, const B& bs,
                                               int gx0, int gy0,
                                               int32_t* __restrict__ lvl, int16_t* __restrict__ rec,
                                               int32_t* ot = nullptr, int64_t opitch = -1) {
@@ -592,13 +617,13 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     const float b1 = r == 0 ? 0.5f - 3072.0f : 0.5f;
     f16x_t acc = splat16(initb(b1));
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
-                                                 ld_h8(&bs.t[r][8 * hh]), acc, 0, 0, 0);
+                                                 bq_t(bs, r, hh, 0), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
-                                                 ld_h8(&bs.t[r][16 + 8 * hh]), acc, 0, 0, 0);
+                                                 bq_t(bs, r, hh, 1), acc, 0, 0, 0);
     // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
     f16x_t acc2 = splat16(initb(0.5f));
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 0, hh), acc_h8(acc, 0, b1), acc2, 0, 0, 0);
-    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.t[r], 1, hh), acc_h8(acc, 1, b1), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 0), acc_h8(acc, 0, b1), acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 1), acc_h8(acc, 1, b1), acc2, 0, 0, 0);
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
     int32_t* lrow = lvl + (int64_t)(gy0 + r) * op + gx0;
 #pragma unroll
@@ -624,14 +649,14 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     }
     // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
     f16x_t acc3 = splat16(initb(0.5f));
-    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), ld_h8(&bs.tt[r][8 * hh]), acc3,
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 8 * hh), bq_tt(bs, r, hh, 0), acc3,
                                                   0, 0, 0);
     acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * QH + 16 + 8 * hh),
-                                                  ld_h8(&bs.tt[r][16 + 8 * hh]), acc3, 0, 0, 0);
+                                                  bq_tt(bs, r, hh, 1), acc3, 0, 0, 0);
     // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
     f16x_t acc4 = splat16(initb(0.5f));
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 0, hh), acc_h8(acc3, 0, 0.5f), acc4, 0, 0, 0);
-    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_crow_h8(bs.tt[r], 1, hh), acc_h8(acc3, 1, 0.5f), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 0), acc_h8(acc3, 0, 0.5f), acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 1), acc_h8(acc3, 1, 0.5f), acc4, 0, 0, 0);
     // reconstruct + clip (intra.py:70-78), row y = r
     int16_t* rrow = rec + (int64_t)(gy0 + r) * op + gx0;
 #pragma unroll
@@ -1094,12 +1119,14 @@ constexpr int16_t kWideMark = (int16_t)0x8000;
 // chain's outputs leave in whole rows through an LDS tile (ctu_chain32_h).
 // The strip loads are issued before the bases are copied to LDS, so the copy
 // and its barrier run under the loads.
-template <int K, bool XCD = false, bool TSTORE = false>
+// BREG: every lane keeps its basis operands in registers (BasisRegs, loaded
+// from the constant copy under the strip loads): no LDS copy, no barrier.
+template <int K, bool XCD = false, bool TSTORE = false, bool BREG = false>
 __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
     using G = Strip<32>;
     __shared__ __attribute__((aligned(16))) int16_t s_img[4][G::IMG];
     __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * G::QH];
-    __shared__ BasisH s_basis;
+    __shared__ std::conditional_t<BREG, int, BasisH> s_basis;
     __shared__ __attribute__((aligned(16))) int32_t s_out[TSTORE ? 4 : 1][TSTORE ? 32 * kOutP : 4];
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint32_t bx = blockIdx.x, by = blockIdx.y;
@@ -1114,9 +1141,15 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
     // strip_issue addresses strip 4 * grp + wave: block b is grp = b / 4 with this wave's slot b % 4
     auto issue = [&](int b) { strip_issue<32>(a, b >> 2, pz, ld, b & 3); };
     if (b0 < nblk) issue(b0);   // in flight under the bases' copy and the barrier
-    copy_basis_h(s_basis);
-    __syncthreads();
-    if (b0 >= nblk) return;   // whole wave
+    std::conditional_t<BREG, BasisRegs, int> breg;
+    if constexpr (BREG) {
+        if (b0 >= nblk) return;   // whole wave
+        breg = load_basis_regs(c_basis_h, lane & 31, lane >> 5);
+    } else {
+        copy_basis_h(s_basis);
+        __syncthreads();
+        if (b0 >= nblk) return;   // whole wave
+    }
     const int64_t poff = plane_off(a, pz);
     for (int k = 0; k < K; ++k) {
         const int b = b0 + k;
@@ -1131,8 +1164,12 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
                 if (a.wide_flag) *a.wide_flag = a.epoch;   // the fix-up launch has work
             }
         } else {
-            ctu_chain32_h<TSTORE>(a, s_img[wv] + 4, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff,
-                                  TSTORE ? s_out[TSTORE ? wv : 0] : nullptr);
+            if constexpr (BREG)
+                ctu_chain32_h<TSTORE>(a, s_img[wv] + 4, s_q[wv], breg, sx0, sy0, a.lvl + poff, a.rec + poff,
+                                      TSTORE ? s_out[TSTORE ? wv : 0] : nullptr);
+            else
+                ctu_chain32_h<TSTORE>(a, s_img[wv] + 4, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff,
+                                      TSTORE ? s_out[TSTORE ? wv : 0] : nullptr);
         }
         wave_sync();   // this wave's LDS reads of block k before block k+1's image writes
     }
@@ -1288,6 +1325,10 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     return NH_OK;
 }
 
+#ifndef NH_TC32H_BREG   // -DNH_TC32H_BREG=1: the bases in registers (k_tc32_h BREG; A/B builds: 0.113 vs 0.106
+#define NH_TC32H_BREG 0   // ms per 8K frame with the LDS copy, profiles/r03/cfg5/ab_libs_5b_breg.jsonl)
+#endif
+[[maybe_unused]] constexpr bool kTc32hBreg = NH_TC32H_BREG != 0;
 // Config 5's narrow launch over one plane set (full 32x32 blocks only).
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s) {
@@ -1331,6 +1372,9 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
 #endif
     // whole-row output stores: 0.106 vs 0.125 ms per 8K YUV420 frame (forms 2 vs 0 of
     // profiles/r03/cfg5/ab_tc32h_forms.jsonl; the XCD-ordered grid is slower, 0.132)
+#if NH_AB || NH_TC32H_BREG
+    else if (NH_KNOB("NH_TC32H_BREG", kTc32hBreg ? 1 : 0)) launch(k_tc32_h<1, false, true, true>, 1);
+#endif
     else launch(k_tc32_h<1, false, true>, 1);
     (void)form;
     NH_HIP(hipGetLastError());

@@ -1989,8 +1989,8 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_WGSYNC
 #define NH_CLOSED4_WGSYNC 0
 #endif
-#ifndef NH_CLOSED4_PRIO
-#define NH_CLOSED4_PRIO 0
+#ifndef NH_CLOSED4_PRIO   // the luma wavefront's waves issue at a higher priority than chroma's (s_setprio):
+#define NH_CLOSED4_PRIO 1   // 0.1196-0.1200 vs 0.1205-0.1209 ms per 4K YUV420 frame concurrent (-DNH_CLOSED4_PRIO=0)
 #endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
@@ -2196,11 +2196,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
     __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * TP];
+#if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
+#endif
     __shared__ __attribute__((aligned(16))) uint8_t ent_s[NH_CLOSED4_PLAN ? kPlanBytes : 16];
     __shared__ int row_s, stall_s;
     if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
-    if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // A/B: the luma wavefront's issue first
+    if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // the critical (luma) wavefront issues first
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
     ChainQ cq[4];
@@ -2235,7 +2237,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             pp.tu[s] = a.tu + (int64_t)pl * a.tu_plane;
             line[s] = lines + (int64_t)pl * a.lw;
         }
-        const int pid = a.plane_id + c, y0c = cy * ctb;
+        const int y0c = cy * ctb;
+#if !NH_CLOSED4_PLAN
+        const int pid = a.plane_id + c;
+#endif
         for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;   // recon starts as zeros (Frame.zeros)
         pair_sync();
         if (hl < ctb) rc[hq][1 + hl][0] = 128;                             // x == 0: left = 128 (block.py:45-50)
@@ -2945,7 +2950,9 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     // A/B build: NH_CLOSED4_WAVES_L / _C = the register budget's waves per SIMD (product: the compiler's)
     static const int mw_l = NH_KNOB("NH_CLOSED4_WAVES_L", 1), mw_c = NH_KNOB("NH_CLOSED4_WAVES_C", 1);
     const int mw = ctb == 32 ? mw_l : mw_c;
+    (void)mw;
     void (*mkern)(Closed4Args) = nullptr;
+#if NH_AB || NH_MULTI_L || NH_MULTI_C   // the multi-plane form is not in the product build (Appendix A.4a)
 #define NH_MULTI_PICK(PP, CC)                                                              \
     if (multi == PP && ctb == CC) {                                                        \
         mkern = k_tu_closed_multi<PP, CC>;                                                 \
@@ -2955,6 +2962,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     NH_MULTI_PICK(1, 32) NH_MULTI_PICK(1, 16) NH_MULTI_PICK(2, 32) NH_MULTI_PICK(2, 16)
     NH_MULTI_PICK(4, 32) NH_MULTI_PICK(4, 16) NH_MULTI_PICK(8, 16)
 #undef NH_MULTI_PICK
+#endif
     if (narrow_ok != 0 && pair_ok != 0 && mkern && (set->num_groups > 1 || multi == 1)) {
         int per_cu = 0;
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mkern, 64, 0));
