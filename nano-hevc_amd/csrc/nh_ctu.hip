@@ -541,6 +541,24 @@ constexpr bool kBiasInit = true;
 constexpr bool kBiasInit = false;
 #endif
 __device__ __forceinline__ float addb(float x, float b) { if constexpr (kBiasInit) return x; else return x + b; }
+// (int)floor(x + 0.5) of an accumulator -- the arithmetic shift of the integer
+// chain -- in ONE instruction: v_cvt_rpi_i32_f32 rounds half up (floor(x + 0.5))
+// as it converts, and x is a multiple of 2^-10 below 2^14, so x + 0.5 is exact
+// and the result equals the add / floor / convert sequence.  With the bias in
+// the accumulators (kBiasInit) it is floor alone: v_cvt_flr_i32_f32.
+#ifndef NH_CVT_RPI
+#define NH_CVT_RPI 1
+#endif
+__device__ __forceinline__ int32_t shift_rnd(float x) {
+    if constexpr (!NH_CVT_RPI) {
+        return (int32_t)__builtin_floorf(addb(x, 0.5f));
+    } else {
+        int32_t r;
+        if constexpr (kBiasInit) asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+        else asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+        return r;
+    }
+}
 __device__ __forceinline__ float initb(float b) { if constexpr (kBiasInit) return b; else return 0.0f; }
 __device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s, float b) {   // registers 8s .. 8s+7 + b, floored, as f16
     uint4 u;
@@ -632,7 +650,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
             const int g = 4 * q + e;
-            L4[e] = quant_s((int32_t)__builtin_floorf(addb(acc2[g], 0.5f)), cq.qs, cq.h_v, cq.hneg_v);
+            L4[e] = quant_s(shift_rnd(acc2[g]), cq.qs, cq.h_v, cq.hneg_v);
             qt[crow(g, hh) * QH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
         }
         if constexpr (TSTORE) *(int4*)&ot[r * kOutP + 8 * q + 4 * hh] = make_int4(L4[0], L4[1], L4[2], L4[3]);
@@ -667,7 +685,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
             const int x = 8 * q + 4 * hh + e;
             const int32_t p = use_dc ? dc
                                      : ((31 - x) * leftr + (x + 1) * tr + (31 - r) * (int32_t)img[x] + (r + 1) * bl + 32) >> 6;
-            const int32_t v = p + (int32_t)__builtin_floorf(addb(acc4[4 * q + e], 0.5f));
+            const int32_t v = p + shift_rnd(acc4[4 * q + e]);
             R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
         }
         const uint2 pk = make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
