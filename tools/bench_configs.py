@@ -90,7 +90,13 @@ def valu_roofline(key, ms_per_frame):
     achieved = instr / (ms_per_frame * 1e-3) / 1e9
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G VALU wave-instr/s",
             "frac": achieved / peak, "valu_instr_per_frame": instr,
-            "profile_kernel_frac": v.get("valu_frac"), "profile_tag": json.load(open(p)).get("tag")}
+            "profile_kernel_frac": v.get("valu_frac"), "profile_tag": _profile_tag(json.load(open(p)), key)}
+
+
+def _profile_tag(d, key):
+    """The profiler pass a config's entry came from (one tag, or one per config)."""
+    t = d.get("tag")
+    return t.get(key) if isinstance(t, dict) else t
 
 
 def main():

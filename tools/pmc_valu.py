@@ -116,6 +116,8 @@ def main():
     ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "valu_roofline.json"))
     ap.add_argument("--configs", default=",".join(CONFIGS))
+    ap.add_argument("--merge", action="store_true",
+                    help="keep the other configs of an existing --out file (per-config tags)")
     a = ap.parse_args()
     rates_path = os.path.join(a.dir, f"valu_rate_{a.tag}.jsonl")
     rates = [json.loads(x) for x in open(rates_path) if x.startswith("{")]
@@ -194,6 +196,11 @@ def main():
             if e.get("valu_per_frame", 0) > 0.01 * instr:
                 print(f"    {e.get('valu_frac', float('nan')):6.3f} act {e.get('valu_active_of_wave_cycles', float('nan')):.3f} "
                       f"wait {e.get('wait_any_of_wave_cycles', float('nan')):.3f} {name[:90]}")
+    if a.merge and os.path.exists(a.out):   # per-config tags: configs re-profiled after a change
+        old = json.load(open(a.out))
+        tags = old.get("tag") if isinstance(old.get("tag"), dict) else {k: old.get("tag") for k in old.get("configs", {})}
+        tags.update({k: a.tag for k in res["configs"]})
+        res = {**old, "configs": {**old.get("configs", {}), **res["configs"]}, "tag": tags}
     with open(a.out, "w") as f:
         json.dump(res, f, indent=1, sort_keys=True)
         f.write("\n")
