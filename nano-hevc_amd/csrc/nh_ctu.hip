@@ -35,6 +35,13 @@
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 #include "nh_mfma.hpp"
+// The open-loop CTU kernels keep the builtin's v_dot2c seeding (pdot_first,
+// nh_packed.hpp): the VOP3P form measured 1.3 % slower here (0.0390 vs 0.0385
+// ms per 4K frame, profiles/r03/cfg4/ab_libs_4b_pd.jsonl) and 2-4 % faster in
+// the closed loop (nh_intraloop.hip).
+#ifndef NH_PDOT_FIRST
+#define NH_PDOT_FIRST 0
+#endif
 #include "nh_packed.hpp"
 #include "nh_tree.hpp"
 

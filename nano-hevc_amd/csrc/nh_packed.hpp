@@ -35,14 +35,37 @@ __device__ __forceinline__ int32_t pdot(pk16 a, int c0, int c1, int32_t acc) {
     return __builtin_amdgcn_sdot2(a, (pk16){(short)c0, (short)c1}, acc, false);
 }
 
+// The first term of a sum whose initial accumulator is the constant `init`:
+// v_dot2_i32_i16 (VOP3P) with the basis pair from an SGPR (s_mov, SALU) and the
+// accumulator an inline 0 or a VGPR -- one VALU instruction, where the
+// builtin's VOP2 form (v_dot2c with a literal basis pair) first needs a v_mov to
+// seed its accumulator.  Same arithmetic (int32, no clamp).
+#ifndef NH_PDOT_FIRST
+#define NH_PDOT_FIRST 1
+#endif
+__device__ __forceinline__ int32_t pdot_first(pk16 a, int c0, int c1, int32_t init) {
+    if constexpr (!NH_PDOT_FIRST) {
+        return pdot(a, c0, c1, init);
+    } else {
+        if (c0 == 0 && c1 == 0) return init;
+        const uint32_t w = (uint32_t)(uint16_t)c0 | ((uint32_t)(uint16_t)c1 << 16);
+        int32_t r;
+        if (__builtin_constant_p(init) && init == 0)
+            asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(r) : "s"(w), "v"(a));
+        else
+            asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(r) : "s"(w), "v"(a), "v"(init));
+        return r;
+    }
+}
+
 // Forward N-point DCT of the vector in P (P[j] = (x[2j], x[2j+1])):
 // y[k] = bias + sum_n DCT_N[k][n] x[n].  E / O pairs: E[j] = (x[2j] + x[N-1-2j],
 // x[2j+1] + x[N-2-2j]) = P[j] + swap(P[N/2-1-j]).
 template <int N>
 __device__ __forceinline__ void fwd_pk(const pk16* P, int32_t* y, int32_t bias) {
     if constexpr (N == 2) {
-        y[0] = pdot(P[0], 64, 64, bias);
-        y[1] = pdot(P[0], 64, -64, bias);
+        y[0] = pdot_first(P[0], 64, 64, bias);
+        y[1] = pdot_first(P[0], 64, -64, bias);
     } else {
         constexpr int H = N / 2, Q = N / 4;
         pk16 E[Q], O[Q];
@@ -59,9 +82,9 @@ __device__ __forceinline__ void fwd_pk(const pk16* P, int32_t* y, int32_t bias) 
         // odd rows: y[2m+1] = bias + sum_j (O[2j], O[2j+1]) . (T[2m+1][2j], T[2m+1][2j+1])
 #pragma unroll
         for (int m = 0; m < H; ++m) {
-            int32_t acc = bias;
+            int32_t acc = pdot_first(O[0], dctc<N>(2 * m + 1, 0), dctc<N>(2 * m + 1, 1), bias);
 #pragma unroll
-            for (int j = 0; j < Q; ++j) acc = pdot(O[j], dctc<N>(2 * m + 1, 2 * j), dctc<N>(2 * m + 1, 2 * j + 1), acc);
+            for (int j = 1; j < Q; ++j) acc = pdot(O[j], dctc<N>(2 * m + 1, 2 * j), dctc<N>(2 * m + 1, 2 * j + 1), acc);
             y[2 * m + 1] = acc;
         }
     }
@@ -75,17 +98,17 @@ __device__ __forceinline__ void fwd_pk(const pk16* P, int32_t* y, int32_t bias) 
 template <int N>
 __device__ __forceinline__ void inv_pk(const pk16* Y, int32_t* x, int32_t bias) {
     if constexpr (N == 2) {
-        x[0] = pdot(Y[0], 64, 64, bias);
-        x[1] = pdot(Y[0], 64, -64, bias);
+        x[0] = pdot_first(Y[0], 64, 64, bias);
+        x[1] = pdot_first(Y[0], 64, -64, bias);
     } else {
         constexpr int H = N / 2, Q = N / 4;
         int32_t E[H];
         inv_pk<H>(Y + Q, E, bias);
 #pragma unroll
         for (int n = 0; n < H; ++n) {
-            int32_t o = 0;
+            int32_t o = pdot_first(Y[0], dctc<N>(1, n), dctc<N>(3, n), 0);
 #pragma unroll
-            for (int i = 0; i < Q; ++i) o = pdot(Y[i], dctc<N>(4 * i + 1, n), dctc<N>(4 * i + 3, n), o);
+            for (int i = 1; i < Q; ++i) o = pdot(Y[i], dctc<N>(4 * i + 1, n), dctc<N>(4 * i + 3, n), o);
             x[n] = E[n] + o;
             x[N - 1 - n] = E[n] - o;
         }
@@ -107,12 +130,12 @@ __device__ __forceinline__ int inv_slot(int k) {
 __device__ __forceinline__ void fwd_dst4_pk(const pk16* P, int32_t* y, int32_t bias) {
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        y[k] = pdot(P[1], dst4c(k, 2), dst4c(k, 3), pdot(P[0], dst4c(k, 0), dst4c(k, 1), bias));
+        y[k] = pdot(P[1], dst4c(k, 2), dst4c(k, 3), pdot_first(P[0], dst4c(k, 0), dst4c(k, 1), bias));
 }
 __device__ __forceinline__ void inv_dst4_pk(const pk16* Y, int32_t* x, int32_t bias) {
 #pragma unroll
     for (int n = 0; n < 4; ++n)
-        x[n] = pdot(Y[1], dst4c(2, n), dst4c(3, n), pdot(Y[0], dst4c(0, n), dst4c(1, n), bias));
+        x[n] = pdot(Y[1], dst4c(2, n), dst4c(3, n), pdot_first(Y[0], dst4c(0, n), dst4c(1, n), bias));
 }
 
 template <int N, bool DST>
