@@ -808,6 +808,9 @@ struct ClosedSet {
     int32_t lw;                     // line-buffer words per plane
     int32_t np;                     // planes in this set
 };
+#ifndef NH_CLOSED_PRIO
+#define NH_CLOSED_PRIO 1
+#endif
 struct ClosedArgs {
     const int16_t* src;
     int32_t* lvl;
@@ -824,6 +827,7 @@ struct ClosedArgs {
     int32_t order;                  // tagged form: 0 plane-major tickets, 1 row-major across planes
     int32_t max_bh;                 // largest block-row count of any set
     int32_t probe;                  // A/B build only (NH_CLOSED_PROBE=1): skip the chain (wrong outputs); 0 otherwise
+    int32_t prio_set;               // the set with the longest wavefront (bw + 2 bh block steps): its rows issue first
 };
 // The tagged closed-loop kernel's forms: both chains per block (0), the packed
 // chain only, for streams whose every source sample is 8-bit (1), both chains
@@ -1045,6 +1049,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
         if (row >= a.total_rows) break;
         int si, pl, by;
         closed_ticket(a, row, si, pl, by);
+        if (NH_CLOSED_PRIO) {   // the critical (longest) wavefront's rows issue before the others' (s_setprio)
+            if (si == a.prio_set) __builtin_amdgcn_s_setprio(2);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         const ClosedSet& S = a.set[si];
         const int g = pl / S.ppg, c = pl - g * S.ppg;
         const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
@@ -3089,6 +3097,9 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
     a.sse = d_sse;
     a.work = (int32_t*)d_work;
     a.qp = qparams(qp, 3, true);
+    a.prio_set = 0;
+    for (int k = 1; k < a.nsets; ++k)
+        if (a.set[k].bw + 2 * a.set[k].bh > a.set[a.prio_set].bw + 2 * a.set[a.prio_set].bh) a.prio_set = k;
     a.dq_scale = dequant_scale(rem);
     a.dq_per = per;
     hipStream_t s = as_stream(stream);
