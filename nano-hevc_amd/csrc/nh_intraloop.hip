@@ -1997,6 +1997,9 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_WGSYNC
 #define NH_CLOSED4_WGSYNC 0
 #endif
+#ifndef NH_CLOSED4_PAIR_CLEAR   // 1: clear the pair kernel's LDS reconstruction before every CTU (A/B)
+#define NH_CLOSED4_PAIR_CLEAR 0
+#endif
 #ifndef NH_CLOSED4_PRIO   // the luma wavefront's waves issue at a higher priority than chroma's (s_setprio):
 #define NH_CLOSED4_PRIO 1   // 0.1196-0.1200 vs 0.1205-0.1209 ms per 4K YUV420 frame concurrent (-DNH_CLOSED4_PRIO=0)
 #endif
@@ -2387,7 +2390,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             int16_t keep = 0;
             if (hl < ctb) keep = rc[hq][1 + hl][ctb];
             pair_sync();
-            if (!(NH_AB && (a.probe & 8)))
+            // (the LDS reconstruction is cleared once per CTU row, above: a TU reads only
+            // samples coded before it or the top row / left column rewritten per CTU;
+            // samples past a ragged edge belong to no TU and are never read)
+            if (NH_CLOSED4_PAIR_CLEAR && !(NH_AB && (a.probe & 8)))
                 for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
             pair_sync();
             if (hl < ctb) rc[hq][1 + hl][0] = keep;
