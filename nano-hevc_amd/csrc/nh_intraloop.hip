@@ -446,198 +446,6 @@ __device__ __forceinline__ unsigned long long rdo8_chain_n(const RdoSlotLds& L, 
     return (unsigned long long)acc;
 }
 
-// ---------------------------------------------------------------------------
-// Lane-pair form of the chain (closed loop): one mode on TWO lanes, l and
-// l ^ 32 (half h = l >> 5), so a block step's VALU path is about half as long.
-// A half owns columns 4h..4h+3 for the column passes and rows 4h..4h+3 for the
-// row passes; the transposes between passes are register-pair swaps with the
-// partner lane (v_permlane32_swap, one VALU op per dword).  Same arithmetic,
-// element for element, as rdo8_chain (bit-exact by construction).
-//   column layout: X[u][v] = (row u, column 4h+v), u 0..7, v 0..3
-//   row layout:    X[i][c] = (row 4h+i, column c), X[4+i][c] = (row 4h+i, column 4+c), i, c 0..3
-// pair_swap on (X[i][v], X[4+i][v]) maps one layout to the other (an involution).
-// ---------------------------------------------------------------------------
-// v_permlane32_swap exchanges the upper 32 lanes of its first operand with the
-// lower 32 lanes of its second: lanes 0-31 send r1 and receive the partner's r0
-// into r1, lanes 32-63 send r0 and receive the partner's r1 into r0.
-__device__ __forceinline__ void pair_swap(uint32_t& r0, uint32_t& r1) {
-    const auto t = __builtin_amdgcn_permlane32_swap(r0, r1, false, false);
-    r0 = t[0];
-    r1 = t[1];
-}
-__device__ __forceinline__ void pair_transpose(uint32_t (&X)[8][4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) pair_swap(X[i][v], X[4 + i][v]);
-}
-__device__ __forceinline__ uint32_t pair_other(uint32_t x) {   // the partner lane's x
-    const auto t = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-    return (threadIdx.x & 32) ? t[0] : t[1];
-}
-
-// Recon + clip + SSE of this half's 4 rows (row layout X = inverse pass-1
-// output rows), prediction pairs Pp in row layout (Pp[i][m]: row 4h+i pairs
-// m = 0,1 of columns 0..3; Pp[4+i][m]: pairs of columns 4..7).
-template <bool WIDE>
-__device__ __forceinline__ unsigned long long rdo8_pair_recon_sse(uint32_t (&X)[8][4], uint32_t (&Pp)[8][2],
-                                                                  const uint32_t* opk, int h, uint32_t (&Rpk)[16]) {
-    const v2s zero = {0, 0}, maxv = {255, 255};
-    unsigned long long sse = 0;
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        uint32_t row[8], x[8];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            row[c] = X[i][c];
-            row[4 + c] = X[4 + i][c];
-        }
-        inv_dct<8, Mul24>(row, x, 128u);
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            const v2s rr = as_v2s(pack16((int32_t)x[2 * m] >> 8, (int32_t)x[2 * m + 1] >> 8));
-            const uint32_t pp = m < 2 ? Pp[i][m] : Pp[4 + i][m - 2];
-            v2s rc = as_v2s(pp) + rr;
-            rc = __builtin_elementwise_min(__builtin_elementwise_max(rc, zero), maxv);
-            Rpk[i * 4 + m] = as_u32(rc);
-            const v2s d = as_v2s(opk[(4 * h + i) * 4 + m]) - rc;
-            if constexpr (!WIDE) {
-                acc = dot2_acc(as_u32(d), acc);
-            } else {
-                const int32_t d0 = d.x, d1 = d.y;
-                sse += (unsigned long long)((uint32_t)(d0 * d0) + (uint32_t)(d1 * d1));
-            }
-        }
-    }
-    return WIDE ? sse : (unsigned long long)acc;
-}
-
-// Returns this half's SSE (rows 4h..4h+3); Rpk / Lpk receive this half's recon /
-// level rows (row-major int16 pairs, Rpk[i*4+m] = row 4h+i, columns 2m, 2m+1).
-__device__ __forceinline__ unsigned long long rdo8_chain_pair(const RdoSlotLds& L, int mode, int h, uint32_t* refp,
-                                                              const ChainQ& q, uint32_t (&Rpk)[16], uint32_t (&Lpk)[16]) {
-    const uint32_t* rp[8];          // per scan line s: pair-array row, weights, extract width
-    uint32_t wf[8], wd[8];
-    bool vert = true;
-    if (mode >= 2) {            // _build_ref_array (intra.py:159-188) as pairs, as rdo8_chain
-        const int angle = intra_angle_alu(mode);
-        vert = mode >= 18;
-        const int16_t* pri = vert ? L.topA : L.leftA;
-        const int16_t* sec = vert ? L.leftA : L.topA;
-        const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
-        int32_t r[25];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = 0;
-        r[8] = pri[0];
-#pragma unroll
-        for (int i = 1; i <= 16; ++i) r[8 + i] = pri[i < np ? i : np - 1];
-        if (angle < 0) {
-            const int inv = inv_angle_alu(angle), next = (8 * angle) >> 5;
-#pragma unroll
-            for (int i = -1; i >= -8; --i) {
-                const int proj = ((i + 1) * inv + 128) >> 8;
-                if (i >= next && proj < ns) r[8 + i] = sec[proj];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 24; ++i) refp[i] = pack16(r[i], r[i + 1]);
-        refp[24] = (uint32_t)r[24] & 0xffffu;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int proj = (s + 1) * angle, f = proj & 31;
-            rp[s] = refp + 9 + (proj >> 5);
-            wf[s] = (uint32_t)(32 - f) | ((uint32_t)f << 16);
-            wd[s] = f ? 11u : 27u;
-        }
-    } else {
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            rp[s] = mode == 0 ? L.planar + 8 * s : L.dcv;
-            wf[s] = 32u;
-            wd[s] = 27u;
-        }
-    }
-    // scan lines 4h..4h+3 (the horizontal modes' columns of P)
-    const uint32_t* rpH[4];
-    uint32_t wfH[4], wdH[4];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        rpH[v] = h ? rp[4 + v] : rp[v];
-        wfH[v] = h ? wf[4 + v] : wf[v];
-        wdH[v] = h ? wd[4 + v] : wd[v];
-    }
-    // prediction P(u, 4h+v) = Q[u][4h+v] (vertical, planar, DC) or Q[4h+v][u] (horizontal)
-    uint32_t X[8][4];
-    uint32_t Pp[8][2];
-    const uint32_t* opk = (const uint32_t*)L.orig;
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-        int32_t pv[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const uint32_t* a = vert ? rp[u] + (4 * h + v) : rpH[v] + u;
-            const uint32_t w = vert ? wf[u] : wfH[v];
-            const uint32_t d = vert ? wd[u] : wdH[v];
-            const int t = dot2_16(*a, w);
-            pv[v] = __builtin_amdgcn_sbfe(t, 5u, d);
-        }
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            const uint32_t pp = pack16(pv[2 * m], pv[2 * m + 1]);
-            Pp[u][m] = pp;
-            const uint32_t dd = as_u32(as_v2s(opk[u * 4 + 2 * h + m]) - as_v2s(pp));   // residual_block: int16 wrap
-            X[u][2 * m] = (uint32_t)(int32_t)(int16_t)(dd & 0xffffu);
-            X[u][2 * m + 1] = (uint32_t)((int32_t)dd >> 16);
-        }
-    }
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {           // forward pass 1: this half's 4 columns
-        uint32_t x[8], y[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = X[k][v];
-        fwd_dct<8, Mul24>(x, y, 128u);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) X[k][v] = (uint32_t)((int32_t)y[k] >> 8);
-    }
-    pair_transpose(X);                      // -> rows 4h..4h+3
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {           // forward pass 2 + quant + dequant on this half's rows
-        uint32_t row[8], y[8];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            row[c] = X[i][c];
-            row[4 + c] = X[4 + i][c];
-        }
-        fwd_dct<8, Mul24>(row, y, 128u);
-        int32_t l[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) l[j] = quant_s((int32_t)y[j] >> 8, q.qs, q.h_v, q.hneg_v);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            X[i][c] = (uint32_t)dequant_s(l[c], q);
-            X[4 + i][c] = (uint32_t)dequant_s(l[4 + c], q);
-        }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) Lpk[i * 4 + m] = pack16(l[2 * m], l[2 * m + 1]);
-    }
-    pair_transpose(X);                      // -> columns 4h..4h+3
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {           // inverse pass 1 (transform.py:221-227)
-        uint32_t yv[8], x[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) yv[k] = X[k][v];
-        inv_dct<8, Mul24>(yv, x, 128u);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) X[k][v] = (uint32_t)((int32_t)x[k] >> 8);
-    }
-    pair_transpose(X);                      // -> rows
-#pragma unroll
-    for (int i = 0; i < 4; ++i)             // the prediction pairs to the row layout too
-#pragma unroll
-        for (int m = 0; m < 2; ++m) pair_swap(Pp[i][m], Pp[4 + i][m]);
-    return (L.wide & 1) ? rdo8_pair_recon_sse<true>(X, Pp, opk, h, Rpk) : rdo8_pair_recon_sse<false>(X, Pp, opk, h, Rpk);
-}
 
 // CHAIN: 0 = either chain per block; 1 = the packed chain only -- a group with
 // any wide block is marked (modes = 0xFF) and left to the CHAIN 2 launch that
@@ -850,128 +658,6 @@ __device__ __forceinline__ void st_sys64(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <int WAVES>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8_closed(ClosedArgs a) {
-    __shared__ RdoSlotLds L;
-    __shared__ uint32_t refs[64][kRefStride];
-    __shared__ int16_t leftcol[8];
-    __shared__ int32_t topw[9];
-    __shared__ int row_s, stall_s;
-    const int lane = threadIdx.x;
-    const ChainQ rq = make_chainq(a.qp, a.dq_scale, a.dq_per);
-    for (;;) {
-        if (lane == 0) {
-            row_s = atomicAdd(&a.work[0], 1);
-            stall_s = 0;
-        }
-        __syncthreads();
-        const int row = row_s;
-        if (row >= a.total_rows) break;
-        int si = 0;
-        for (int k = 1; k < a.nsets; ++k)
-            if (row >= a.set[k].row0) si = k;
-        const ClosedSet& S = a.set[si];
-        const int local = row - S.row0, pl = local / S.bh, by = local - pl * S.bh;
-        const int g = pl / S.ppg, c = pl - g * S.ppg;
-        const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
-        const int16_t* src = a.src + off;
-        int16_t* rec = a.rec + off;
-        int32_t* lvl = a.lvl + off;
-        int32_t* line = a.work + a.lines0 + S.line0 + (int64_t)pl * S.lw;   // int16 pairs
-        const int y0 = by * 8;
-        int16_t tl_next = 128;   // recon(y0-1, x0-1) for the next block
-        unsigned long long row_sse = 0;   // added to the plane's word once per row, not per block
-        for (int bx = 0; bx < S.bw; ++bx) {
-            const int x0 = bx * 8;
-            // this block's source sample: independent of the wait, issued before it
-            const int16_t ov = src[(int64_t)(y0 + lane / 8) * S.pitch + x0 + (lane % 8)];
-            if (by > 0 && lane == 0) {   // wait for the top / top-right references
-                const int need = bx + 2 < S.bw ? bx + 2 : S.bw;
-                int spins = 0;
-                while (ld_sys(&a.work[2 + row - 1]) < need) {
-                    __builtin_amdgcn_s_sleep(1);
-                    ++spins;
-                    // give up on our own limit, or as soon as any wave has given up
-                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
-                        atomicMax(&a.work[1], 1);
-                        stall_s = 1;
-                        break;
-                    }
-                }
-            }
-            __syncthreads();
-            if (stall_s) break;
-            // top row x0-1 .. x0+15 of the row above: 9 line words from word x0/2 - 1
-            if (by > 0 && lane < 9) topw[lane] = (x0 == 0 && lane == 0) ? 0 : ld_sys(line + x0 / 2 - 1 + lane);
-            __syncthreads();
-            // block samples and neighbours (block.py:38-55 on the reconstruction)
-            {
-                const int k = lane;
-                L.orig[k] = ov;
-                if (k < 16) {
-                    int16_t v = 128;
-                    if (y0 > 0 && x0 + k < S.w) {
-                        const int xi = k + 1;   // sample x0 + k = halfword 2 + k of topw
-                        v = (int16_t)(topw[(xi + 1) >> 1] >> (((xi + 1) & 1) * 16));
-                    }
-                    L.topA[1 + k] = v;
-                    if (k < 8) L.topN[k] = v;
-                } else if (k < 24) {
-                    const int kk = k - 16;
-                    const int16_t v = x0 == 0 ? (int16_t)128 : leftcol[kk];
-                    L.leftA[1 + kk] = v;
-                    L.leftN[kk] = v;
-                } else if (k == 24) {
-                    const int16_t tl = (y0 == 0 || x0 == 0) ? (int16_t)128 : tl_next;
-                    L.topA[0] = tl;
-                    L.leftA[0] = tl;
-                    L.ntA = 1 + (y0 == 0 ? 16 : min(16, S.w - x0));
-                    L.nlA = 1 + 8;   // get_left_neighbors(N): the reconstructed samples only
-                    L.wide = 0;
-                }
-            }
-            __syncthreads();
-            rdo8_block_prep(L, lane);
-            __syncthreads();
-            tl_next = L.topA[8];   // recon(y0-1, x0+7): the next block's top-left
-            uint32_t P[32], Lv[32];
-            unsigned long long key = ULLONG_MAX;
-            if (lane < kModes) key = (rdo8_chain(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
-            unsigned long long best = key;
-            for (int m = 32; m > 0; m >>= 1) {
-                const unsigned long long o = __shfl_xor(best, m, 64);
-                best = o < best ? o : best;
-            }
-            if (key == best) {   // the winning mode (lowest SSE, lowest mode on ties)
-                // publish first (the next row waits on it): the bottom row -> line
-                // (coherent stores), retire them, then the progress counter; the
-                // block's outputs go out after, off the wavefront's critical path
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    st_sys(line + x0 / 2 + q, (int)P[28 + q]);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // line stores retired
-                st_sys(&a.work[2 + row], bx + 1);
-                a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)lane;
-                row_sse += best >> 6;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        lvl[(int64_t)(y0 + i) * S.pitch + x0 + j] = (int32_t)(int16_t)(Lv[i * 4 + j / 2] >> (16 * (j & 1)));
-                        rec[(int64_t)(y0 + i) * S.pitch + x0 + j] = (int16_t)(P[i * 4 + j / 2] >> (16 * (j & 1)));
-                    }
-                    leftcol[i] = (int16_t)(P[i * 4 + 3] >> 16);
-                }
-            }
-            __syncthreads();
-        }
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) row_sse += __shfl_xor(row_sse, m, 64);
-        if (lane == 0 && row_sse) atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], row_sse);
-        __syncthreads();
-        if (stall_s) break;   // the whole launch is failing: leave (status word set)
-    }
-}
 
 // Tagged-line form (default): the line buffer holds 64-bit words
 // (tag << 32 | int16 pair), written with one single-copy-atomic coherent store
@@ -1165,144 +851,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     }
 }
 
-// Lane-pair form (NH_CLOSED_FORM=2): the tagged-line wavefront of
-// k_intra_rdo8_closed_tag with every mode on a lane pair (rdo8_chain_pair):
-// a workgroup of two waves per block row, modes 0..31 on wave 0 (lanes m and
-// m + 32), modes 32..34 on wave 1; the winner is the minimum over both waves.
-template <int WAVES>
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8_closed_pair(ClosedArgs a) {
-    __shared__ RdoSlotLds L;
-    __shared__ uint32_t refs[128][kRefStride];
-    __shared__ uint32_t outP[32], outL[32];   // the winner's recon / level pairs, row-major
-    __shared__ int32_t topw[9];
-    __shared__ unsigned long long wmin[2];
-    __shared__ int row_s, stall_s, win_s;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int h = lane >> 5, mode = wave * 32 + (lane & 31);
-    const bool on = mode < kModes;
-    const ChainQ rq = make_chainq(a.qp, a.dq_scale, a.dq_per);
-    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
-    for (;;) {
-        if (tid == 0) {
-            row_s = atomicAdd(&a.work[0], 1);
-            stall_s = 0;
-        }
-        __syncthreads();
-        const int row = row_s;
-        if (row >= a.total_rows) break;
-        int si, pl, by;
-        closed_ticket(a, row, si, pl, by);
-        const ClosedSet& S = a.set[si];
-        const int g = pl / S.ppg, c = pl - g * S.ppg;
-        const int64_t off = S.base + (int64_t)g * S.group_stride + (int64_t)c * S.plane_stride;
-        const int16_t* src = a.src + off;
-        int16_t* rec = a.rec + off;
-        int32_t* lvl = a.lvl + off;
-        uint64_t* line = lines + S.line0 + (int64_t)pl * S.lw;
-        const int y0 = by * 8, full_words = S.bw * 4;
-        int16_t tl_next = 128;
-        unsigned long long row_sse = 0;
-        for (int bx = 0; bx < S.bw; ++bx) {
-            const int x0 = bx * 8;
-            int16_t ov = 0;
-            if (wave == 0) ov = src[(int64_t)(y0 + lane / 8) * S.pitch + x0 + (lane % 8)];
-            if (by > 0 && wave == 0) {
-                const int wi = x0 / 2 + lane;
-                const bool need = lane < 8 && wi < full_words;
-                uint32_t val = 0;
-                int spins = 0;
-                for (;;) {
-                    bool ok = true;
-                    if (need) {
-                        const uint64_t v = ld_sys64(line + wi);
-                        ok = (int)(v >> 32) == by;
-                        val = (uint32_t)v;
-                    }
-                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    ++spins;
-                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
-                        if (lane == 0) atomicMax(&a.work[1], 1);
-                        stall_s = 1;
-                        break;
-                    }
-                }
-                if (lane < 8) topw[1 + lane] = (int32_t)val;
-            }
-            __syncthreads();
-            if (stall_s) break;
-            if (wave == 0) {
-                const int k = lane;
-                L.orig[k] = ov;
-                if (k < 16) {
-                    int16_t v = 128;
-                    if (y0 > 0 && x0 + k < S.w) v = (int16_t)(topw[1 + (k >> 1)] >> ((k & 1) * 16));
-                    L.topA[1 + k] = v;
-                    if (k < 8) L.topN[k] = v;
-                } else if (k < 24) {
-                    const int kk = k - 16;
-                    const int16_t v = x0 == 0 ? (int16_t)128 : (int16_t)(outP[kk * 4 + 3] >> 16);
-                    L.leftA[1 + kk] = v;
-                    L.leftN[kk] = v;
-                } else if (k == 24) {
-                    const int16_t tl = (y0 == 0 || x0 == 0) ? (int16_t)128 : tl_next;
-                    L.topA[0] = tl;
-                    L.leftA[0] = tl;
-                    L.ntA = 1 + (y0 == 0 ? 16 : min(16, S.w - x0));
-                    L.nlA = 1 + 8;
-                    L.wide = 0;
-                }
-            }
-            __syncthreads();
-            if (wave == 0) rdo8_block_prep(L, lane);
-            __syncthreads();
-            tl_next = L.topA[8];
-            uint32_t Rp[16], Lp[16];
-            unsigned long long key = ULLONG_MAX;
-            if (on) {
-                const unsigned long long e = rdo8_chain_pair(L, mode, h, refs[tid], rq, Rp, Lp);
-                const uint32_t lo = pair_other((uint32_t)e), hi = pair_other((uint32_t)(e >> 32));
-                key = ((e + (((unsigned long long)hi << 32) | lo)) << 6) | (unsigned long long)mode;
-            }
-            unsigned long long best = key;
-            for (int m = 32; m > 0; m >>= 1) {
-                const unsigned long long o = __shfl_xor(best, m, 64);
-                best = o < best ? o : best;
-            }
-            if (lane == 0) wmin[wave] = best;
-            __syncthreads();
-            best = wmin[0] < wmin[1] ? wmin[0] : wmin[1];
-            if (key == best) {   // the winning mode's two lanes
-                if (h == 1) {    // publish the bottom row (row 7 = this half's row 3) first
-                    const uint64_t tag = (uint64_t)(uint32_t)(by + 1) << 32;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) st_sys64(line + x0 / 2 + q, tag | Rp[12 + q]);
-                } else {
-                    win_s = mode;
-                    row_sse += best >> 6;
-                }
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    outP[h * 16 + q] = Rp[q];
-                    outL[h * 16 + q] = Lp[q];
-                }
-            }
-            __syncthreads();
-            if (wave == 0) {   // wave 0 stores one sample per lane
-                const int i = lane >> 3, j = lane & 7;
-                const int64_t e = (int64_t)(y0 + i) * S.pitch + x0 + j;
-                rec[e] = (int16_t)(outP[i * 4 + j / 2] >> (16 * (j & 1)));
-                lvl[e] = (int32_t)(int16_t)(outL[i * 4 + j / 2] >> (16 * (j & 1)));
-                if (lane == 0) a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)win_s;
-            }
-        }
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) row_sse += __shfl_xor(row_sse, m, 64);
-        if (lane == 0 && row_sse) atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], row_sse);
-        __syncthreads();
-        if (stall_s) break;
-    }
-}
 
 // Samples outside full 8x8 blocks read as 0 (Frame.zeros) by the closed loop.
 __global__ void k_zero_partial(int16_t* rec, ClosedSet S, int nplanes) {
@@ -2404,283 +1952,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     }
 }
 
-// ---------------------------------------------------------------------------
-// Config 4 closed loop, 8-bit streams: P planes per wave (k_tu_closed_multi).
-// The pair form above, generalised to P planes (groups P*m .. P*m + P - 1 of
-// the set, same plane of the group) with the CTB a compile-time size, so a
-// chroma CTU (CTB 16: 16 4x4 units) fills the wave's lanes with the TUs of
-// four frames instead of two.  Per lane the batch entry e names plane
-// p = e / cnt and TU e mod cnt of the CTU's schedule; each plane keeps its own
-// LDS reconstruction and int16 tile, publishes and polls its own line words
-// (lanes [64/P * p, 64/P * (p+1)) serve plane p), and the planes never exchange
-// data: same TUs, same inputs, same chain as tu_closed_batch_pk2, so the same
-// results.  The CTU's LDS reconstruction is cleared once per CTU row, not per
-// CTU: a TU only reads samples of TUs coded before it (z-order) or the CTU's
-// top row / left column, which are rewritten for every CTU; samples past a
-// ragged plane edge belong to no TU and are never read.
-template <int N, bool DST, int P, int CTB>
-__device__ __forceinline__ void tu_closed_batch_pkm(const Closed4Args& a, int g0, int c, int x0c, int y0c, int cnt,
-                                                    int total, int c0, const uint8_t* ent,
-                                                    int16_t (*rcm)[CTB + 1][CTB + 1], int16_t* t16,
-                                                    const ChainQ& cq) {
-    constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = CTB + 2;
-    constexpr int32_t BIAS = 1 << (S - 1);
-    const int lane = opaque_lane64(), t = lane % N, e = c0 + lane / N;
-    const bool on = e < total;
-    int p = 0;   // idle lanes shadow plane 0's first TU
-    if (on) {
-#pragma unroll
-        for (int j = 1; j < P; ++j) p += e >= j * cnt ? 1 : 0;
-    }
-    const int k = on ? e - p * cnt : 0;
-    const int code = ent[k], lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4, x = x0c + lx, y = y0c + ly;
-    int16_t (*rc)[CTB + 1] = rcm[p];
-    const int64_t off = (int64_t)(g0 + p) * a.group_stride + (int64_t)c * a.plane_stride;
-    int16_t* tl = t16 + p * (CTB * TP) + ly * TP + lx;   // tl[line * TP + slot]
-    const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
-    const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
-    int32_t sum = topt + leftt;                                // DC (intra.py:46-62)
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
-    const int32_t dc = (sum + N) >> (L2 + 1);
-    const pk16 dc2 = pk_splat(dc);
-    pk16 o2[H];
-    pku16 pl2[H];
-    {
-        const int32_t b = (t + 1) * tr + (N - 1) * topt + bl + N, st = bl - topt;
-        pku16 bs = {(unsigned short)b, (unsigned short)(b + st)};
-        const pku16 st2 = {(unsigned short)(2 * st), (unsigned short)(2 * st)};
-        const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
-        const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
-        const int16_t* sp = a.src + off + (int64_t)y * a.pitch + x + t;
-#pragma unroll
-        for (int m = 0; m < H; ++m) {
-            o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
-            const pku16 lf = {(unsigned short)rc[ly + 1 + 2 * m][lx], (unsigned short)rc[ly + 2 + 2 * m][lx]};
-            pl2[m] = (lf * wl + bs) >> sh;
-            bs += st2;
-        }
-    }
-    int32_t ed = 0, ep = 0;
-#pragma unroll
-    for (int m = 0; m < H; ++m) {
-        const pk16 d0 = o2[m] - dc2, d1 = o2[m] - __builtin_bit_cast(pk16, pl2[m]);
-        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
-        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
-    }
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) {
-        ed += __shfl_xor(ed, m, 64);
-        ep += __shfl_xor(ep, m, 64);
-    }
-    const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
-    pk16 r2[H];
-#pragma unroll
-    for (int m = 0; m < H; ++m) r2[m] = o2[m] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[m]));
-    int32_t yv[N];
-    fwd1d_pk<N, DST>(r2, yv, BIAS);   // forward pass 1 (transform.py:179-185): column t -> line i, slot t
-    if (on) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(yv[i] >> S);
-    }
-    pair_sync();
-    const int st = inv_slot<N, DST>(t);
-    {
-        pk16 Pv[H];   // forward pass 2 (transform.py:188-194): row t
-#pragma unroll
-        for (int m = 0; m < H; ++m) Pv[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
-        fwd1d_pk<N, DST>(Pv, yv, BIAS);
-    }
-    pair_sync();
-    if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
-        int32_t* lrow = a.lvl + off + (int64_t)(y + t) * a.pitch + x;
-#pragma unroll
-        for (int kk = 0; kk < N; ++kk) {
-            const int32_t l = quant_s(yv[kk] >> S, cq.qs, cq.h_v, cq.hneg_v);
-            lrow[kk] = l;
-            tl[kk * TP + st] = (int16_t)dequant_s(l, cq);
-        }
-    }
-    pair_sync();
-    int32_t xv[N];
-    {
-        pk16 Y[H];   // inverse pass 1 (transform.py:221-227): column t -> line i, slot inv_slot(t)
-#pragma unroll
-        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
-        inv1d_pk<N, DST>(Y, xv, BIAS);
-    }
-    pair_sync();
-    if (on) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(xv[i] >> S);
-    }
-    pair_sync();
-    {
-        pk16 Y[H];   // inverse pass 2 (transform.py:230-236): row t
-#pragma unroll
-        for (int m = 0; m < H; ++m) Y[m] = pk_pair(tl[t * TP + 2 * m], tl[t * TP + 2 * m + 1]);
-        inv1d_pk<N, DST>(Y, xv, BIAS);
-    }
-    if (on) {   // reconstruct + clip (intra.py:70-78); planar in row layout
-        const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, stv = tr - leftt;
-        int16_t* rrow = a.rec + off + (int64_t)(y + t) * a.pitch + x;
-#pragma unroll
-        for (int kk = 0; kk < N; ++kk) {
-            const int32_t pr = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + kk] + b + kk * stv) >> (L2 + 1);
-            int32_t q = pr + (xv[kk] >> S);
-            q = q < 0 ? 0 : (q > 255 ? 255 : q);
-            rrow[kk] = (int16_t)q;
-            rc[ly + 1 + t][lx + 1 + kk] = (int16_t)q;   // no TU of this batch reads the TU's own samples
-        }
-        if (t < N / 4) {
-            uint8_t* tu = a.tu + (int64_t)((g0 + p) * a.ppg + c) * a.tu_plane;
-            const int w4 = a.w / 4;
-            for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
-        }
-    }
-    pair_sync();
-}
-
-#ifndef NH_CLOSED4_CLEAR_EVERY_CTU
-#define NH_CLOSED4_CLEAR_EVERY_CTU 0   // A/B: clear the LDS reconstruction before every CTU (the pair form's rule)
-#endif
-// Tickets run row-major over the P-plane sets ("multis"): ticket t = CTU row
-// t / nm of multi t % nm; multi m = (groups P * (m / ppg) .., plane m % ppg);
-// a wave only waits on the same multi's CTU row above, claimed before it.  A
-// tail multi with act < P planes leaves its slots >= act idle.
-#ifndef NH_MULTI_L   // planes per wave; -DNH_MULTI_L / _C: library builds for A/B
-#define NH_MULTI_L 0
-#endif
-#ifndef NH_MULTI_C
-#define NH_MULTI_C 0
-#endif
-constexpr int kMultiLuma = NH_MULTI_L, kMultiChroma = NH_MULTI_C;
-template <int P, int CTB, int WAVES = 1>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_multi(Closed4Args a) {
-    constexpr int TP = CTB + 2, LQ = 64 / P, NW = CTB / 2;
-    static_assert(NW <= LQ, "a CTU's line words must fit the lanes of its plane");
-    __shared__ int16_t rc[P][CTB + 1][CTB + 1];
-    __shared__ __attribute__((aligned(16))) int16_t t16[P * CTB * TP];
-    __shared__ __attribute__((aligned(16))) uint8_t ent_s[kPlanBytes];
-    __shared__ int row_s, stall_s;
-    if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
-    const int lane = threadIdx.x;
-    ChainQ cq[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
-    uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
-    const int ngroups = a.nplanes / a.ppg, nm = ((ngroups + P - 1) / P) * a.ppg;
-    const int total = a.crows * nm;
-    const int hq = lane / LQ, hl = lane % LQ;   // line words and the left column: lanes of plane hq
-    for (;;) {
-        if (lane == 0) {
-            row_s = atomicAdd(&a.work[0], 1);
-            stall_s = 0;
-        }
-        pair_sync();
-        const int tk = row_s;
-        if (tk >= total) break;
-        const int cy = tk / nm, q = tk - cy * nm;
-        const int c = q % a.ppg, g0 = P * (q / a.ppg);
-        const int act = min(P, ngroups - g0);   // planes of this multi
-        const bool mine = hq < act;
-        uint64_t* line = lines + (int64_t)((g0 + (mine ? hq : 0)) * a.ppg + c) * a.lw;
-        const int y0c = cy * CTB;
-        for (int i = lane; i < P * (CTB + 1) * (CTB + 1); i += 64) (&rc[0][0][0])[i] = 0;   // Frame.zeros
-        pair_sync();
-        for (int i = hl; i < CTB; i += LQ) rc[hq][1 + i][0] = 128;   // x == 0: left = 128 (block.py:45-50)
-        const uint32_t* plan_row = (const uint32_t*)(a.plan + ((int64_t)c * a.crows + cy) * a.ccols * kPlanBytes);
-        for (int cx = 0; cx < a.ccols; ++cx) {
-            const int x0c = cx * CTB;
-            const int nw = (min(CTB, a.w - x0c) + 1) / 2;
-            // this CTU's TU schedule (128 B), loaded under the wait on the row above
-            uint32_t planw = 0;
-            if (lane < kPlanBytes / 4) planw = plan_row[cx * (kPlanBytes / 4) + lane];
-            // top row of this CTU: 128 at y == 0, else the CTU above's bottom row (tagged line words)
-            if (cy == 0) {
-                for (int i = hl; i < CTB; i += LQ) rc[hq][0][1 + i] = 128;
-            } else {
-                const bool need = hl < nw && mine;
-                uint32_t val = 0;
-                int spins = 0;
-                for (;;) {
-                    bool ok = true;
-                    if (need) {
-                        const uint64_t v = ld_sys64(line + x0c / 2 + hl);
-                        ok = (int)(v >> 32) == cy || (NH_AB && (a.probe & 1));
-                        val = (uint32_t)v;
-                    }
-                    if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
-                    __builtin_amdgcn_s_sleep(1);
-                    ++spins;
-                    if (spins > kSpinLimit || ((spins & 1023) == 0 && ld_sys(&a.work[1]))) {
-                        if (lane == 0) atomicMax(&a.work[1], 1);
-                        stall_s = 1;
-                        break;
-                    }
-                }
-                if (need) {
-                    rc[hq][0][1 + 2 * hl] = (int16_t)(val & 0xffffu);
-                    rc[hq][0][2 + 2 * hl] = (int16_t)(val >> 16);
-                }
-            }
-            if (lane < kPlanBytes / 4) ((uint32_t*)ent_s)[lane] = planw;
-            pair_sync();
-            if (stall_s) break;
-            {   // the CTU's TUs in dataflow rounds, from the schedule (k_closed4_plan): lane rs holds
-                // the count of (round rs / 4, size index rs % 4); batches run in the schedule's order
-                const int cntv = ent_s[64 + lane];
-                const uint64_t nz = __ballot(cntv != 0);
-                const int last = nz ? 63 - __clzll(nz) : -1;
-                int off = 0;
-                for (int rs = 0; rs <= last && !(NH_AB && (a.probe & 4)); ++rs) {
-                    const int cnt = __builtin_amdgcn_readlane(cntv, rs);
-                    if (cnt == 0) continue;
-                    const int tot = cnt * act;
-                    const uint8_t* ent = ent_s + off;
-                    switch (rs & 3) {
-#define NH_MULTI_BATCH(NN, DST, Q)                                                                            \
-                        for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_pkm<NN, DST, P, CTB>(a, g0, c, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q);
-                        case 0:
-                            if constexpr (CTB >= 32) { NH_MULTI_BATCH(32, false, cq[3]) }
-                            break;
-                        case 1:
-                            if constexpr (CTB >= 16) { NH_MULTI_BATCH(16, false, cq[2]) }
-                            break;
-                        case 2: NH_MULTI_BATCH(8, false, cq[1]) break;
-                        default:
-                            if (a.is_luma) { NH_MULTI_BATCH(4, true, cq[0]) }
-                            else { NH_MULTI_BATCH(4, false, cq[0]) }
-#undef NH_MULTI_BATCH
-                    }
-                    off += cnt;
-                }
-            }
-            // publish the bottom rows (the next CTU row polls them), then slide: right column -> left column
-            if (cy + 1 < a.crows && hl < nw && mine) {
-                const uint32_t lo = (uint16_t)rc[hq][CTB][1 + 2 * hl];
-                const uint32_t hi = (uint16_t)rc[hq][CTB][2 + 2 * hl];
-                st_sys64(line + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
-            }
-            pair_sync();
-            int16_t keep[(CTB + LQ - 1) / LQ];
-#pragma unroll
-            for (int j = 0; j < (CTB + LQ - 1) / LQ; ++j)
-                keep[j] = hl + j * LQ < CTB ? rc[hq][1 + hl + j * LQ][CTB] : (int16_t)0;
-            pair_sync();
-            if (NH_CLOSED4_CLEAR_EVERY_CTU || (NH_AB && (a.probe & 32)))
-                for (int i = lane; i < P * (CTB + 1) * (CTB + 1); i += 64) (&rc[0][0][0])[i] = 0;
-            pair_sync();
-#pragma unroll
-            for (int j = 0; j < (CTB + LQ - 1) / LQ; ++j)
-                if (hl + j * LQ < CTB) rc[hq][1 + hl + j * LQ][0] = keep[j];
-            pair_sync();
-        }
-        pair_sync();
-        if (stall_s) break;
-    }
-}
 
 int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t* d_lvl, int16_t* d_recon,
                    hipStream_t s) {
@@ -2707,52 +1978,17 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
     int per, rem;
     qp_split(qp, &per, &rem);
     const uint32_t ngroups = (uint32_t)((nblk + kRdoSlots - 1) / kRdoSlots);
-    // Launch form (A/B knob NH_RDO_FORM, read once): 0 = one group per
-    // workgroup, packed-chain-only launch + fallback launch (default), 1 =
-    // persistent at the compiler's register allocation, 2 = persistent forced
-    // to 2 waves/SIMD, 3 = one group per workgroup, one launch.
-    static const int form = NH_KNOB("NH_RDO_FORM", 0);
     const hipStream_t s = as_stream(stream);
     const QuantParams q = qparams(qp, 3, true);
     unsigned long long* sse = (unsigned long long*)d_sse;
-    if (form == 0) {   // the packed-chain-only launch (3 waves/SIMD), then the fallback for groups with wide blocks
+    {   // the packed-chain-only launch (3 waves/SIMD), then the fallback for groups with wide blocks
         // A/B build: NH_CAP_RDO = resident workgroups per CU (LDS reservation, lds_cap)
-        static const int cap_rdo = NH_KNOB("NH_CAP_RDO", 0), w4 = NH_KNOB("NH_RDO_W4", 0);
-#if NH_AB   // A/B: the packed-only kernel capped at 128 VGPRs (4 waves/SIMD, 19 spilled)
-        if (w4)
-            k_intra_rdo8<4, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<4, true, 1>, cap_rdo), s>>>(
-                d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups);
-        else
-#endif
+        static const int cap_rdo = NH_KNOB("NH_CAP_RDO", 0);
         k_intra_rdo8<1, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
             d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups);
-        (void)w4;
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
                                                         d_recon, sse, ngroups);
     }
-#if NH_AB
-    else if (form == 3) {   // A/B: one launch, either chain per block
-        k_intra_rdo8<1, true><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
-                                                     d_recon, sse, ngroups);
-    } else {
-        static const int cus = [] {
-            int dev = 0, n = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-                n = 256;
-            return n;
-        }();
-        // as many workgroups as fit, every workgroup the same number of groups +-1
-        const uint32_t cap = (uint32_t)cus * (form == 2 ? 2 : 1), iters = (ngroups + cap - 1) / cap;
-        const unsigned grid = (ngroups + iters - 1) / iters;
-        if (form == 2)
-            k_intra_rdo8<2, false><<<grid, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
-                                                       d_recon, sse, ngroups);
-        else
-            k_intra_rdo8<1, false><<<grid, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
-                                                       d_recon, sse, ngroups);
-    }
-#endif
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
@@ -2932,10 +2168,8 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     a.dq_per = per;
     a.probe = NH_KNOB("NH_CLOSED4_PROBE", 0);
     const int64_t rows = (int64_t)a.crows * np;
-    // A/B knob NH_TU_CLOSED_WAVES: 1 = compiler allocation (218 VGPRs, 2 waves/SIMD), 3 = capped (spills)
-    static const int cw = NH_KNOB("NH_TU_CLOSED_WAVES", 1);
-    // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x waves/SIMD)
-    const int64_t cap = cw == 3 ? 3072 : 2048;
+    // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x 2 waves/SIMD)
+    const int64_t cap = 2048;
     const unsigned waves = (unsigned)(rows < cap ? rows : cap);
     // the stream's wide flag, then the packed-chain form (codes the stream iff no
     // sample is outside [0, 255]) and the 32-bit form (iff one is); A/B knob
@@ -2953,47 +2187,11 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     int cus = 0;
     NH_TRY(device_cus(&cus));
     // 8-bit streams: plane pairs (k_tu_closed_pair) when the set
-    // holds more than one group; A/B build: NH_TU_CLOSED_PAIR = 0 codes one plane
-    // per wave, = 4 the pair form capped at 4 waves/SIMD
+    // holds more than one group; A/B build: NH_TU_CLOSED_PAIR = 0 codes one plane per wave
     static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
-    // P planes per wave (k_tu_closed_multi) for CTB 32 (luma) / 16 (chroma);
-    // A/B build: NH_CLOSED4_MULTI_L / _C = planes per wave (0: the pair kernel)
-    static const int multi_l = NH_KNOB("NH_CLOSED4_MULTI_L", kMultiLuma),
-                     multi_c = NH_KNOB("NH_CLOSED4_MULTI_C", kMultiChroma);
-    const int multi = ctb == 32 ? multi_l : ctb == 16 ? multi_c : 0;
-    // A/B build: NH_CLOSED4_WAVES_L / _C = the register budget's waves per SIMD (product: the compiler's)
-    static const int mw_l = NH_KNOB("NH_CLOSED4_WAVES_L", 1), mw_c = NH_KNOB("NH_CLOSED4_WAVES_C", 1);
-    const int mw = ctb == 32 ? mw_l : mw_c;
-    (void)mw;
-    void (*mkern)(Closed4Args) = nullptr;
-#if NH_AB || NH_MULTI_L || NH_MULTI_C   // the multi-plane form is not in the product build (Appendix A.4a)
-#define NH_MULTI_PICK(PP, CC)                                                              \
-    if (multi == PP && ctb == CC) {                                                        \
-        mkern = k_tu_closed_multi<PP, CC>;                                                 \
-        if (NH_AB && mw == 5) mkern = k_tu_closed_multi<PP, CC, NH_AB ? 5 : 1>;            \
-        if (NH_AB && mw == 6) mkern = k_tu_closed_multi<PP, CC, NH_AB ? 6 : 1>;            \
-    }
-    NH_MULTI_PICK(1, 32) NH_MULTI_PICK(1, 16) NH_MULTI_PICK(2, 32) NH_MULTI_PICK(2, 16)
-    NH_MULTI_PICK(4, 32) NH_MULTI_PICK(4, 16) NH_MULTI_PICK(8, 16)
-#undef NH_MULTI_PICK
-#endif
-    if (narrow_ok != 0 && pair_ok != 0 && mkern && (set->num_groups > 1 || multi == 1)) {
-        int per_cu = 0;
-        NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mkern, 64, 0));
-        const int64_t nm = (int64_t)a.crows * ((set->num_groups + multi - 1) / multi) * set->planes_per_group;
-        uint8_t* plan = (uint8_t*)d_work + closed4_plan_offset(lines0, lw, np);
-        a.plan = plan;
-        k_closed4_plan<<<dim3((unsigned)(a.crows * a.ccols), (unsigned)a.ppg), 64, 0, s>>>(a, plan);
-        NH_HIP(hipGetLastError());
-        static const int wpc = NH_KNOB("NH_CLOSED4_WPC", 0);
-        const int64_t cap_n = (int64_t)(wpc > 0 ? wpc : std::max(1, per_cu)) * cus;
-        mkern<<<(unsigned)(nm < cap_n ? nm : cap_n), 64, 0, s>>>(a);
-    } else if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
+    if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
         int per_cu = 0;
         auto kern = k_tu_closed_pair<kPairWaves>;
-#if NH_AB
-        if (pair_ok == 4) kern = k_tu_closed_pair<4>;   // A/B: capped at 4 waves/SIMD
-#endif
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
         const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
         if (NH_CLOSED4_PLAN) {   // the TU schedule of every (plane of the group, CTU), once per launch
@@ -3014,11 +2212,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
         k_tu_closed<1, true><<<(unsigned)(rows < cap_n ? rows : cap_n), 64, 0, s>>>(a);
     }
-#if NH_AB
-    if (cw == 3) k_tu_closed<3><<<waves, 64, 0, s>>>(a);
-    else
-#endif
-        k_tu_closed<1><<<waves, 64, 0, s>>>(a);
+    k_tu_closed<1><<<waves, 64, 0, s>>>(a);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
@@ -3122,32 +2316,14 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
     if (a.total_rows > 0) {
         // persistent waves: enough to cover every row, capped at what can be resident (2 waves/SIMD)
         const int waves = a.total_rows < 2048 ? a.total_rows : 2048;
-        {   // A/B knobs: NH_CLOSED_WAVES=2 register allocation for 2 waves/SIMD (spills);
-            // NH_CLOSED_FORM=0 the progress-counter form (default 1: tagged line words)
-            static const int cw = NH_KNOB("NH_CLOSED_WAVES", 1);
-            static const int cf = NH_KNOB("NH_CLOSED_FORM", 1);
+        {   // A/B knobs: NH_CLOSED_ORDER=0 plane-major tickets; NH_CLOSED_PROBE timing probes
             static const int co = NH_KNOB("NH_CLOSED_ORDER", 1);
             a.order = co ? 1 : 0;
             a.probe = NH_KNOB("NH_CLOSED_PROBE", 0);
-#if NH_AB
-            if (cf == 0) {
-                if (cw == 2) k_intra_rdo8_closed<2><<<waves, 64, 0, s>>>(a);
-                else k_intra_rdo8_closed<1><<<waves, 64, 0, s>>>(a);
-            } else if (cf == 2) {
-                if (cw == 3) k_intra_rdo8_closed_pair<3><<<waves, 128, 0, s>>>(a);
-                else k_intra_rdo8_closed_pair<2><<<waves, 128, 0, s>>>(a);
-            } else if (cw == 2) {
-                k_intra_rdo8_closed_tag<2><<<waves, 64, 0, s>>>(a);
-            } else if (cf == 3) {   // A/B: one kernel, either chain per block (round 1)
-                k_intra_rdo8_closed_tag<1><<<waves, 64, 0, s>>>(a);
-            } else
-#endif
             {
-                (void)cf;
-                (void)cw;
                 // the stream's wide flag, then the packed-only form (codes the stream iff every source
                 // sample is 8-bit: every neighbour is then too, the reconstruction being clipped) and the
-                // both-chains form (codes it otherwise); A/B build: NH_CLOSED_FORM = 3, one kernel
+                // both-chains form (codes it otherwise)
                 int32_t* flag = (int32_t*)d_work + 2 + a.total_rows;
                 for (int k = 0; k < nsets; ++k) {
                     const nh_plane_set& p = sets[k];
@@ -3163,14 +2339,6 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
                 NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_intra_rdo8_closed_tag<1, kClosedNarrow>,
                                                                     64, 0));
                 const int64_t cap_n = (int64_t)std::max(1, per_cu) * cus;
-#if NH_AB   // A/B: NH_CLOSED_W3 = 1 the packed-only form capped at 168 VGPRs (3 waves/SIMD, 33 spilled)
-                static const int w3 = NH_KNOB("NH_CLOSED_W3", 0);
-                if (w3) {
-                    const int64_t cap3 = 3ll * 4 * cus;
-                    k_intra_rdo8_closed_tag<3, kClosedNarrow>
-                        <<<(unsigned)(a.total_rows < cap3 ? a.total_rows : cap3), 64, 0, s>>>(a);
-                } else
-#endif
                 k_intra_rdo8_closed_tag<1, kClosedNarrow>
                     <<<(unsigned)(a.total_rows < cap_n ? a.total_rows : cap_n), 64, 0, s>>>(a);
                 k_intra_rdo8_closed_tag<1, kClosedWide><<<waves, 64, 0, s>>>(a);

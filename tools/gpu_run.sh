@@ -20,6 +20,9 @@
 #   counters   rocprofv3 -L (the counters this box offers)
 #   valu_kt / valu_pmc1 / valu_pmc2   the VALU roofline passes over bench_configs $VALU_CFGS
 #              (kernel trace; SQ wave/instruction counters; MFMA busy + GRBM clock) -> tools/pmc_valu.py
+#   valu_pmc3 / valu_pmc4   instruction counts per unit and per VALU class over the same configs
+#              (the measured totals the dynamic mix of tools/valu_dyn.py must reproduce)
+#   pmc_cal    tools/ab/_pmc_cal under the pmc3 / pmc4 counter sets: which counter counts which instruction
 # pytest selection: PYTEST_K="expr" (passed as -k expr); bench args: BENCH_ARGS="...".
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -29,6 +32,8 @@ TAG=${TAG:-r03}
 VALU_CFGS=${VALU_CFGS:-3,4b,5b,closed,closed4}
 STEPS=${STEPS:-20}
 FRAMES=${FRAMES:-128}
+PMC3="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_INSTS_MFMA SQ_INSTS_VMEM_RD"
+PMC4="SQ_INSTS_VMEM_WR SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32"
 PT="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 
 run_step() {
@@ -95,13 +100,20 @@ run_step() {
       echo "== rocprofv3 -L"
       timeout -s KILL 90 rocprofv3 -L > gpurun_out/counters_${TAG}.txt 2>&1; rc=$?
       grep -c "" gpurun_out/counters_${TAG}.txt; return $rc ;;
-    valu_kt|valu_pmc1|valu_pmc2)
+    pmc_cal)
+      echo "== counter calibration (tools/ab/_pmc_cal)"
+      timeout -s KILL 60 rocprofv3 --pmc $PMC3 --output-format csv -d gpurun_out/pmc_cal3_${TAG} -o run -- tools/ab/_pmc_cal > gpurun_out/pmc_cal_${TAG}.log 2>&1 && \
+      timeout -s KILL 60 rocprofv3 --pmc $PMC4 --output-format csv -d gpurun_out/pmc_cal4_${TAG} -o run -- tools/ab/_pmc_cal >> gpurun_out/pmc_cal_${TAG}.log 2>&1; rc=$?
+      tail -2 gpurun_out/pmc_cal_${TAG}.log; return $rc ;;
+    valu_kt|valu_pmc1|valu_pmc2|valu_pmc3|valu_pmc4)
       # one profiler run per config (a config's kernels alone in each CSV)
       for c in ${VALU_CFGS//,/ }; do
         echo "== $1 over bench_configs --configs $c"
         case "$1" in
           valu_kt)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
           valu_pmc1) timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
+          valu_pmc3) timeout -s KILL 300 rocprofv3 --pmc $PMC3 --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
+          valu_pmc4) timeout -s KILL 300 rocprofv3 --pmc $PMC4 --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
           valu_pmc2) timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d gpurun_out/$1_${TAG}_$c -o run -- python3 tools/bench_configs.py --configs $c --reps 3 > gpurun_out/$1_${TAG}_$c.log 2>&1 || return 1 ;;
         esac
         python3 tools/trim_prof.py gpurun_out/$1_${TAG}_$c
