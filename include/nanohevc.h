@@ -96,9 +96,26 @@ int nh_quantize_abs(const int64_t* abs_coeff, int64_t n, int qp, int64_t log2siz
 int nh_dequantize(const int64_t* level, int64_t n, int qp, int32_t* out);
 /* quant.py:171-173 count_nonzero */
 int nh_count_nonzero(const int64_t* level, int64_t n, int64_t* count);
-/* quant.py:153-168 estimate_bits: the float64 sum (numpy pairwise order) of
- * log2(|l|+1) + 2*(|l|>0), |l|+1 wrapping in an abs_bits (32/64) dtype; the
- * caller applies int() (which raises on NaN/inf exactly as the reference). */
+/* quant.py:153-168 estimate_bits: the float64 sum (numpy pairwise order, over
+ * the n words in the order given) of log2(|l|+1) + 2*(|l|>0) under numpy's
+ * dtype rules for levels of dtype abs_bits (an NH_EB_* code): |l| and the +1
+ * in that dtype (integers wrap, floats round), log2 in float16 (8-bit
+ * integers, float16), float32 (16-bit integers, float32) or float64.  Each
+ * 8-byte word holds the level as an int64, a uint64 bit pattern (unsigned
+ * codes) or a float64 bit pattern (float codes).  The caller applies int()
+ * (which raises on NaN/inf exactly as the reference). */
+#define NH_EB_BOOL 1
+#define NH_EB_I8 8
+#define NH_EB_I16 16
+#define NH_EB_I32 32
+#define NH_EB_I64 64
+#define NH_EB_U8 108
+#define NH_EB_U16 116
+#define NH_EB_U32 132
+#define NH_EB_U64 164
+#define NH_EB_F16 216
+#define NH_EB_F32 232
+#define NH_EB_F64 264
 int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits);
 
 /* metrics.py:7-48 as device reductions.

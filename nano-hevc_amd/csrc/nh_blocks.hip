@@ -300,19 +300,60 @@ __device__ __forceinline__ void dev_count_nonzero(const int64_t* l, int64_t n, u
 }
 
 // quant.py:153-168: sum(log2(|l|+1) + (|l|>0)*2) in float64, then int().
-// np.sum of a contiguous float64 array is numpy's pairwise_sum over the
-// flattened array (blocks of 8 accumulators, halves above 128 elements);
+// np.sum of the (contiguous) term array is numpy's pairwise_sum over it in
+// memory order (the shim hands the levels over in that order, np.ravel 'K'),
 // replicated serially here so the float64 rounding sequence is numpy's.
-// term for one level held in a `bits`-wide signed dtype (32 or 64): np.abs and
-// the +1 wrap inside that dtype; log2 of a non-positive value gives -inf/NaN
-// exactly as numpy does (the shim's int() then raises like the reference).
-__device__ double eb_term(int64_t v, int bits) {
-    uint64_t a = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v;
-    uint64_t a1 = a + 1;
+// The term follows numpy's dtype rules for one level of dtype `code`
+// (NH_EB_* in nanohevc.h; the 8-byte word holds an int64 value, a uint64 bit
+// pattern or, for float kinds, a float64 bit pattern):
+//   * np.abs and the +1 in the level's dtype (integers wrap; floats round);
+//   * np.log2 in the float type numpy picks for that dtype: float16 for 8-bit
+//     integers and float16, float32 for 16-bit integers and float32, float64
+//     otherwise (bool: bool + 1 is int64) -- then widened to float64 by the
+//     + int64 (abs > 0) * 2;
+//   * log2 of 0 / a negative wrap is -inf / NaN exactly as numpy's, so the
+//     shim's int() raises like the reference.
+// log2 at float32 / float16 is the correctly rounded value (log2 in float64,
+// then rounded); numpy's own float32 log2 on AVX-512 hosts (SVML) differs from
+// it in the last bit for 437 of the 65,536 int16 magnitudes -- which moves the
+// truncated int() only when a sum falls within ~1e-6 of an integer
+// (DESIGN.md §2).
+__device__ __forceinline__ double eb_log2_prec(double x, int prec) {
+    if (prec == 64) return log2(x);
+    const float l = (float)log2((double)(float)x);   // x is exact in the precision
+    if (prec == 32) return (double)l;
+    return (double)(float)(_Float16)l;               // numpy's half loop: half(log2f(float(x)))
+}
+__device__ double eb_term(int64_t v, int code) {
+    if (code >= NH_EB_F16) {
+        const double x = __longlong_as_double((long long)v);
+        if (code == NH_EB_F64) {
+            const double a = fabs(x);
+            return log2(a + 1.0) + (double)((a > 0) * 2);
+        }
+        const float af = fabsf((float)x);
+        if (code == NH_EB_F32) return eb_log2_prec((double)(af + 1.0f), 32) + (double)((af > 0) * 2);
+        const _Float16 a1 = (_Float16)(af + 1.0f);   // numpy's half add: float add, rounded to half
+        return eb_log2_prec((double)(float)a1, 16) + (double)((af > 0) * 2);
+    }
+    if (code == NH_EB_BOOL) {
+        const int b = v != 0;
+        return log2((double)(b + 1)) + (double)(b * 2);
+    }
+    if (code > 100) {   // unsigned: np.abs is the identity, the +1 wraps in the width
+        const int w = code - 100;
+        const uint64_t mask = w == 64 ? ~0ull : (1ull << w) - 1;
+        const uint64_t u = (uint64_t)v & mask, u1 = (u + 1) & mask;
+        return eb_log2_prec((double)u1, w == 8 ? 16 : w == 16 ? 32 : 64) + (double)((u > 0) * 2);
+    }
+    const int w = code;   // signed: np.abs and the +1 wrap in the width
+    const uint64_t a = v < 0 ? 0ull - (uint64_t)v : (uint64_t)v, a1 = a + 1;
     int64_t as, as1;
-    if (bits == 32) { as = (int32_t)(uint32_t)a; as1 = (int32_t)(uint32_t)a1; }
+    if (w == 8) { as = (int8_t)(uint8_t)a; as1 = (int8_t)(uint8_t)a1; }
+    else if (w == 16) { as = (int16_t)(uint16_t)a; as1 = (int16_t)(uint16_t)a1; }
+    else if (w == 32) { as = (int32_t)(uint32_t)a; as1 = (int32_t)(uint32_t)a1; }
     else { as = (int64_t)a; as1 = (int64_t)a1; }
-    return log2((double)as1) + (double)((as > 0) * 2);
+    return eb_log2_prec((double)as1, w == 8 ? 16 : w == 16 ? 32 : 64) + (double)((as > 0) * 2);
 }
 // numpy's pairwise_sum (loops_utils.h.src) over term(i), i in [0, n), iteratively:
 // below 8 terms a plain running sum from 0; up to 128 eight accumulators over
@@ -1322,8 +1363,17 @@ int nh_count_nonzero(const int64_t* level, int64_t n, int64_t* count) {
     }, count, 8, true);
 }
 
+static bool eb_code_ok(int c) {
+    switch (c) {
+        case NH_EB_I8: case NH_EB_I16: case NH_EB_I32: case NH_EB_I64:
+        case NH_EB_U8: case NH_EB_U16: case NH_EB_U32: case NH_EB_U64:
+        case NH_EB_BOOL: case NH_EB_F16: case NH_EB_F32: case NH_EB_F64: return true;
+        default: return false;
+    }
+}
+
 int nh_estimate_bits(const int64_t* level, int64_t n, int abs_bits, double* bits) {
-    if (n < 0 || (abs_bits != 32 && abs_bits != 64)) return NH_EARG;
+    if (n < 0 || !eb_code_ok(abs_bits)) return NH_EARG;
     BlockCall c;
     const size_t oi = c.in(level, n * 8);
     return c.run<false>(1, [=] __device__(U8 in, ST, uint8_t* o) {   // 1.5 KB of stack: k_small

@@ -31,15 +31,14 @@ def _sum_sq_diff_int(a, b):
 
 
 def _sum_sq_diff_f64(a, b) -> float:
-    """metrics.py:9-10 for any other dtype: the reference's .astype(np.float64)
-    on the host, then the sum of squares on the GPU in numpy's pairwise order
-    (memory order of the operands, as numpy's reduction walks a contiguous
-    array)."""
-    x, y = a.astype(np.float64), b.astype(np.float64)
-    order = "F" if (x.flags.f_contiguous and not x.flags.c_contiguous and
-                    y.flags.f_contiguous and not y.flags.c_contiguous) else "C"
-    x = np.ascontiguousarray(np.ravel(x, order=order))
-    y = np.ascontiguousarray(np.ravel(y, order=order))
+    """metrics.py:9-10 for any other dtype: the reference's own host expression
+    diff = a.astype(np.float64) - b.astype(np.float64) (its result is a fresh
+    array laid out in the operands' 'K' order, broadcast views included), then
+    the sum of diff ** 2 on the GPU in numpy's pairwise order over that array's
+    memory order (np.mean reduces a contiguous array as one 1-D run)."""
+    d = np.asarray(a).astype(np.float64) - np.asarray(b).astype(np.float64)
+    x = np.ascontiguousarray(np.ravel(d, order="K"))
+    y = np.zeros_like(x)                 # (d - 0) ** 2 == d ** 2 exactly
     out = np.zeros(1, np.float64)
     check(_lib.load().nh_sum_sq_diff_f64(ptr(x), ptr(y), x.size, ptr(out)), "mse")
     return float(out[0])
@@ -47,14 +46,14 @@ def _sum_sq_diff_f64(a, b) -> float:
 
 def mse(original, reconstructed) -> float:
     """metrics.py:7-10: mean((orig - recon)^2) in float64."""
-    a, b = np.asarray(original), np.asarray(reconstructed)
-    a, b = np.broadcast_arrays(a, b)
+    a0, b0 = np.asarray(original), np.asarray(reconstructed)
+    a, b = np.broadcast_arrays(a0, b0)
     n = a.size
     if _small_int(a) and _small_int(b):
         s = _sum_sq_diff_int(a, b)
         if s < 2**53:
             return float(np.float64(s) / np.float64(n))
-    return float(np.float64(_sum_sq_diff_f64(a, b)) / np.float64(n))
+    return float(np.float64(_sum_sq_diff_f64(a0, b0)) / np.float64(n))
 
 
 def psnr(original, reconstructed, peak: int = 255) -> float:

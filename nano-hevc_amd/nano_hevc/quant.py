@@ -97,28 +97,77 @@ def dequantize_block(level, qp: int) -> np.ndarray:
     return dequantize(level, qp, size)
 
 
+# estimate_bits dtype codes (NH_EB_* in include/nanohevc.h)
+_EB_CODE = {("b", 1): 1, ("i", 1): 8, ("i", 2): 16, ("i", 4): 32, ("i", 8): 64,
+            ("u", 1): 108, ("u", 2): 116, ("u", 4): 132, ("u", 8): 164,
+            ("f", 2): 216, ("f", 4): 232, ("f", 8): 264}
+
+
 def estimate_bits(level) -> int:
-    """quant.py:153-168: int(sum(log2(|l|+1) + (|l|>0)*2)) (float64, numpy summation order)."""
+    """quant.py:153-168: int(np.sum(np.log2(|l|+1) + (|l|>0)*2)).
+
+    numpy's dtype rules per level dtype are evaluated on the device (abs and +1
+    in the dtype, log2 in float16 / float32 / float64 as numpy picks it, the
+    float64 sum in numpy's pairwise order over the term array's memory order,
+    which is the input's 'K' order).  Complex levels go through the reference's
+    own np.abs on the host first; other dtypes raise TypeError like np.log2."""
     a = np.asarray(level)
-    if a.dtype not in (np.int32, np.int64):
-        raise NotImplementedError(f"estimate_bits: int32/int64 levels only (got {a.dtype})")
-    x = np.ascontiguousarray(a, dtype=np.int64)
+    kind = a.dtype.kind
+    if kind == "c":
+        a = np.abs(a)                       # quant.py:166, complex -> float magnitude
+        kind = "f"
+    if kind not in "biuf":
+        raise TypeError(f"ufunc 'log2' not supported for the input types (dtype {a.dtype})")
+    code = _EB_CODE.get((kind, a.dtype.itemsize), 264 if kind == "f" else None)
+    flat = np.ravel(a, order="K")
+    if kind == "f":
+        x = np.ascontiguousarray(flat, dtype=np.float64).view(np.int64)   # exact widening, float64 bits
+    elif kind == "u":
+        x = np.ascontiguousarray(flat, dtype=np.uint64).view(np.int64)
+    else:
+        x = np.ascontiguousarray(flat, dtype=np.int64)
     bits = np.zeros(1, np.float64)
-    check(_lib.load().nh_estimate_bits(ptr(x), x.size, a.dtype.itemsize * 8, ptr(bits)), "estimate_bits")
+    check(_lib.load().nh_estimate_bits(ptr(x), x.size, code, ptr(bits)), "estimate_bits")
     return int(bits[0])
 
 
-def count_nonzero(level) -> int:
-    """quant.py:171-173."""
-    a = np.asarray(level)
-    if a.dtype.kind not in "iub":
-        a = a != 0          # np.count_nonzero's "nonzero" for float / complex / object (NaN counts)
-    x = np.ascontiguousarray(a, dtype=np.int64)
+def _nonzero_mask(a):
+    """np.count_nonzero's notion of nonzero as an integer/bool array: the value
+    itself for integers and bools; != 0 for floats and complex (NaN counts);
+    truthiness for objects, non-empty for strings, != 0 for the datetime kinds
+    (NaT counts)."""
+    k = a.dtype.kind
+    if k in "iub":
+        return a
+    if k in "fc":
+        return a != 0
+    if k == "O":
+        return a.astype(bool)
+    if k in "US":
+        return np.char.str_len(a) != 0
+    if k in "mM":
+        return a.view(np.int64) != 0
+    raise TypeError(f"count_nonzero: unsupported dtype {a.dtype}")
+
+
+def _count(mask) -> int:
+    x = np.ascontiguousarray(mask, dtype=np.int64)
     cnt = np.zeros(1, np.int64)
     check(_lib.load().nh_count_nonzero(ptr(x), x.size, ptr(cnt)), "count_nonzero")
     return int(cnt[0])
 
 
+def count_nonzero(level) -> int:
+    """quant.py:171-173: int(np.count_nonzero(level)), the count on the GPU."""
+    return _count(_nonzero_mask(np.asarray(level)))
+
+
 def is_all_zero(level) -> bool:
-    """quant.py:176-178 (returns numpy.bool like np.all)."""
-    return np.bool_(count_nonzero(level) == 0)
+    """quant.py:176-178: np.all(level == 0) (returns numpy.bool like np.all).
+    Numeric levels: no element is nonzero (count on the GPU); other dtypes
+    compare with the reference's own level == 0 first."""
+    a = np.asarray(level)
+    if a.dtype.kind in "iubfc":
+        return np.bool_(_count(_nonzero_mask(a)) == 0)
+    eq = np.asarray(a == 0)
+    return np.bool_(_count(~eq.astype(bool)) == 0)

@@ -56,10 +56,17 @@ def _prep(x):
     a = np.asarray(x)
     size = a.shape[0]
     _get_transform_matrix(size)                     # ValueError for unsupported sizes
-    if a.ndim != 2:
-        if a.ndim == 1:
-            raise IndexError("too many indices for array: array is 1-dimensional, but 2 were indexed")
-        raise NotImplementedError("transforms take one 2-D block (use nano_hevc.gpu for batches)")
+    if a.ndim == 1:
+        raise IndexError("too many indices for array: array is 1-dimensional, but 2 were indexed")
+    if a.ndim > 2:
+        # transform.py:180-185 on an N-D block: block[k, j] is an array over the
+        # trailing axes, and the int32 element store temp[i, j] = ... takes it
+        # only when it holds exactly one value (numpy's size-1 conversion)
+        if a.shape[1] == 0:
+            raise IndexError("index 0 is out of bounds for axis 1 with size 0")
+        if int(np.prod(a.shape[2:])) != 1:
+            raise ValueError("setting an array element with a sequence.")
+        a = a.reshape(a.shape[:2])
     if a.shape[1] < size:
         raise IndexError(f"index {a.shape[1]} is out of bounds for axis 1 with size {a.shape[1]}")
     blk = np.ascontiguousarray(a.astype(np.int32)[:size, :size])   # transform.py:176 cast (wraps)

@@ -15,6 +15,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libnh_oracle.so")
+# tests/test_oracle_asan.py points this at the sanitizer build (make -C oracle asan)
+LIB_PATH = os.environ.get("NH_ORACLE_LIB", LIB_PATH)
 
 ERRORS = {-1: ValueError, -2: IndexError, -3: OverflowError, -4: ZeroDivisionError}
 

@@ -137,4 +137,65 @@ def cases():
     add("satd_4x4", x[:4, :4], y[:4, :4])
     add("residual_energy", x - y)
     add("psnr", rng.random((8, 8)) > 0.5, rng.random((8, 8)) > 0.5, 1)
+    # ---- round 4 (VERDICT r3 missing #2-#3) -- appended, so the names above keep their indices
+    # estimate_bits on every level dtype (quant.py:166-168: np.abs, +1 and log2 in the dtype's rules)
+    lv = np.array([[3, -1], [0, 7]])
+    for dt in (np.int8, np.int16, np.int32, np.int64, np.uint8, np.uint16, np.uint32, np.uint64,
+               np.float16, np.float32, np.float64, bool):
+        add("estimate_bits", lv.astype(dt))
+        add("estimate_bits", rng.integers(-60, 60, (8, 8)).astype(dt))
+        add("estimate_bits", rng.integers(0, 120, (16, 16)).astype(dt))
+        add("estimate_bits", rng.integers(-100, 100, 300).astype(dt))          # > 128 terms: pairwise halves
+    add("estimate_bits", np.array([[0, 1, 2, 3], [4, 5, 6, 7]], np.int16))
+    add("estimate_bits", rng.integers(-32767, 32768, (8, 8)).astype(np.int16))
+    add("estimate_bits", rng.integers(-32767, 32768, (32, 32)).astype(np.int16))
+    add("estimate_bits", rng.integers(-127, 128, (8, 8)).astype(np.int8))
+    add("estimate_bits", rng.integers(0, 255, (8, 8)).astype(np.uint8))
+    add("estimate_bits", rng.integers(0, 65535, (8, 8)).astype(np.uint16))
+    add("estimate_bits", np.array([5, -32768, 3], np.int16))                  # abs wraps: log2(-32767) -> NaN
+    add("estimate_bits", np.array([5, -128, 3], np.int8))
+    add("estimate_bits", np.array([5, 255, 3], np.uint8))                     # 255 + 1 wraps to 0: -inf
+    add("estimate_bits", np.array([5, 65535], np.uint16))
+    add("estimate_bits", np.array([1, 2**32 - 1], np.uint32))
+    add("estimate_bits", np.array([2**63, 2**64 - 1, 7], np.uint64))
+    add("estimate_bits", np.array([-2**31, 5], np.int32))
+    add("estimate_bits", np.array([2**31 - 1, 5], np.int64))
+    add("estimate_bits", rng.uniform(-300, 300, (8, 8)))
+    add("estimate_bits", rng.uniform(-300, 300, (8, 8)).astype(np.float32))
+    add("estimate_bits", rng.uniform(-300, 300, (8, 8)).astype(np.float16))
+    add("estimate_bits", rng.uniform(-3e4, 3e4, 200).astype(np.float16))
+    add("estimate_bits", np.array([0.25, -0.5, 1e-3, 6e4], np.float16))
+    add("estimate_bits", np.array([1.5, nan, 2.0]))
+    add("estimate_bits", np.array([1.5, inf], np.float32))
+    add("estimate_bits", np.array([-0.0, 0.0, 1e-300]))
+    add("estimate_bits", np.asfortranarray(rng.integers(-500, 500, (8, 12)).astype(np.int32)))
+    add("estimate_bits", np.asfortranarray(rng.uniform(-9, 9, (12, 20))))
+    add("estimate_bits", rng.integers(-500, 500, (20, 30)).astype(np.int16)[::2, 1::3])
+    add("estimate_bits", rng.integers(-500, 500, 400)[::-1])
+    add("estimate_bits", (rng.uniform(-9, 9, (8, 8)) + 1j * rng.uniform(-9, 9, (8, 8))).astype(np.complex64))
+    add("estimate_bits", np.array([], np.int32))
+    add("estimate_bits", np.array(["a", "b"]))
+    # N-D blocks into the transforms (transform.py:171-194: block[k, j] over the trailing axes)
+    for fn in ("forward_transform", "inverse_transform"):
+        for shp in ((4, 4, 4), (8, 8, 2), (4, 4, 1), (8, 8, 1), (32, 32, 1), (4, 4, 0), (4, 5, 2), (4, 3, 2),
+                    (4, 3, 1), (16, 16, 1, 1), (4, 4, 1, 2), (3, 4, 4), (4, 0, 1), (8, 8, 2, 1)):
+            x = rng.integers(-255, 256, int(np.prod(shp))).reshape(shp).astype(np.int16)
+            add(fn, x)
+        add(fn, rng.integers(-255, 256, (4, 4, 1)).astype(np.int16), True)
+        add(fn, rng.integers(-255, 256, (4, 4, 3)).astype(np.int16), True)
+    # mse / psnr with mixed layouts and broadcast views (metrics.py:9-10: the diff's 'K' order)
+    u = rng.uniform(0, 255, (24, 40))
+    v = rng.uniform(0, 255, (40, 24))
+    add("mse", np.asfortranarray(u), u)
+    add("mse", u, np.asfortranarray(u + 1))
+    add("mse", np.asfortranarray(u), v.T)
+    add("mse", u[::2, ::3], v.T[::2, ::3])
+    add("mse", u, u[:, :1])
+    add("mse", u, u[:1, :].copy(order="F"))
+    add("psnr", np.asfortranarray(u.astype(np.float32)), u[::-1])
+    # count_nonzero / is_all_zero on object and string levels (np.count_nonzero's truthiness)
+    add("count_nonzero", np.array([None, "", 0, 1, "x", 0.0, [1]], dtype=object))
+    add("count_nonzero", np.array(["a", "", " "]))
+    add("is_all_zero", np.array([0, 0.0, False], dtype=object))
+    add("is_all_zero", np.array(["", ""]))
     return out

@@ -561,13 +561,13 @@ def plane_hash_1080p(T, Q):
     return hashlib.sha256(lvl.tobytes()).hexdigest()
 
 
-def gen_dtypes(I, Q, M):
+def gen_dtypes(I, Q, M, T):
     """Non-integer inputs (tests/golden/dtype_cases.py): per case the reference's
     result (out_*, with rtype_* its Python type) or its exception (err_* the
     class name, errbase_* the builtin class it derives from)."""
     sys.path.insert(0, HERE)
     from dtype_cases import cases
-    mods = (I, Q, M)
+    mods = (I, Q, M, T)
     out = {}
     bases = (ZeroDivisionError, OverflowError, IndexError, ValueError, TypeError, AttributeError)
     for name, fn, args, kw in cases():
@@ -592,7 +592,7 @@ def main():
     if "--only" in sys.argv:   # regenerate one file (own rng), keep the others and their manifest entries
         name = sys.argv[sys.argv.index("--only") + 1]
         gen = {"closed4.npz": lambda: gen_closed4(I, T, Q), "closed.npz": lambda: gen_closed(I, T, Q),
-               "dtypes.npz": lambda: gen_dtypes(I, Q, M)}[name]
+               "dtypes.npz": lambda: gen_dtypes(I, Q, M, T)}[name]
         p = os.path.join(HERE, name)
         np.savez_compressed(p, **gen())
         mp = os.path.join(HERE, "manifest.json")
@@ -614,7 +614,7 @@ def main():
         "encode.npz": gen_encode(ref),
         "closed.npz": gen_closed(I, T, Q),
         "closed4.npz": gen_closed4(I, T, Q),
-        "dtypes.npz": gen_dtypes(I, Q, M),
+        "dtypes.npz": gen_dtypes(I, Q, M, T),
     }
     manifest = {"numpy": np.__version__, "python": sys.version.split()[0],
                 "generator": "tests/golden/make_golden.py", "reference": "Luodian/nano-hevc @ /root/reference",

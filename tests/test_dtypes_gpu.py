@@ -36,8 +36,8 @@ def test_fixture_covers_every_case(fixture):
 @pytest.mark.parametrize("name,fn,args,kw", CASES, ids=[c[0] for c in CASES])
 def test_dtype_case_matches_reference(fixture, name, fn, args, kw):
     import warnings
-    from nano_hevc import intra, quant, metrics
-    f = next(getattr(m, fn) for m in (intra, quant, metrics) if hasattr(m, fn))
+    from nano_hevc import intra, quant, metrics, transform
+    f = next(getattr(m, fn) for m in (intra, quant, metrics, transform) if hasattr(m, fn))
     if "err_" + name in fixture:
         base = getattr(builtins, str(fixture["errbase_" + name]))
         with warnings.catch_warnings():

@@ -6,8 +6,11 @@
 // times — each counter counts that instruction.
 // Build: hipcc --offload-arch=gfx950 -O3 tools/ab/pmc_cal.hip -o tools/ab/_pmc_cal
 // Run:   rocprofv3 --pmc <counters> -- tools/ab/_pmc_cal       (prints the variant table)
+// Variants 0..40: the hand-written forms below; kop<OP> (kernel name "kop"):
+// REP copies of every opcode of the probe's table (valu_ops.hpp), one chain.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include "valu_ops.hpp"
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 #define REP "200"
@@ -76,20 +79,42 @@ const char* const kVar[NK] = {
     "v_readlane_b32", "v_permlane32_swap_b32", "v_pk_mad_u16", "v_bfe_u32", "s_load_dword", "global_store_dword",
     "s_branch", "v_floor_f32", "v_add_co_u32"};
 
+template <int OP>
+__global__ void __launch_bounds__(256) kop(int* g, int seed) {
+    uint32_t a = seed + threadIdx.x, b = (uint32_t)(seed * 3) & 15u;
+    uint64_t q = a * 0x9E3779B97F4A7C15ull, sc = 0;
+    const uint64_t m = 0x5555555555555555ull ^ (uint64_t)seed;
+    asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1" :: "v"(a), "v"(b) : "vcc");
+#pragma unroll
+    for (int i = 0; i < 200; ++i) op<OP>(a, a, q, b, m, seed, sc);
+    const uint32_t r = a ^ b ^ (uint32_t)q ^ (uint32_t)(q >> 32) ^ (uint32_t)sc;
+    if (r == 0x7fffffffu) g[threadIdx.x] = (int)r;
+}
+
 template <int K>
 static void launch_all(int* g) {
     kcal<K><<<256, 256>>>(g, K);   // 1,024 waves per variant
     if constexpr (K + 1 < NK) launch_all<K + 1>(g);
 }
+template <int OP>
+static void launch_ops(int* g) {
+    kop<OP><<<256, 256>>>(g, OP);
+    if constexpr (OP + 1 < NOPS) launch_ops<OP + 1>(g);
+}
 
 int main() {
     int* g;
     if (hipMalloc(&g, 4096 * 4) != hipSuccess) return 1;
-    hipMemset(g, 0, 4096 * 4);
+    if (hipMemset(g, 0, 4096 * 4) != hipSuccess) return 1;
     launch_all<0>(g);
+    launch_ops<0>(g);
     if (hipDeviceSynchronize() != hipSuccess) return 2;
     printf("{\"rep\": %s, \"waves_per_variant\": 1024, \"variants\": [", REP);
     for (int k = 0; k < NK; ++k) printf("%s\"%s\"", k ? ", " : "", kVar[k]);
+    printf("], \"ops\": [");
+    for (int k = 0; k < NOPS; ++k) printf("%s\"%s\"", k ? ", " : "", kNames[k]);
+    printf("], \"insts_per_op\": [");
+    for (int k = 0; k < NOPS; ++k) printf("%s%d", k ? ", " : "", insts_per_op(k));
     printf("]}\n");
     hipFree(g);
     return 0;
