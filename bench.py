@@ -25,12 +25,14 @@ synthesises and holds only its bands plus the one source row above each band
 (all a TU reads, block.py:38-50; shard.Cfg4Layout) and reconstructs them.
 
 N > 1, both configs: after the compute-only phase, a gather-inclusive phase
-runs the path's one exchange step -- an RCCL gather to rank 0 (config 2: a
---gather-frames sample of the int16 levels, 8 of 128 frames by default;
-config 4: all reconstructed bands as uint8, clip_to_pixel_range guarantees
-[0, 255]) -- on a side stream, the gather of step k overlapped with
-the compute of step k+1 (double-buffered outputs).  Reported as
-``gather_inclusive`` with the bytes into rank 0 and the achieved xGMI rate.
+runs the path's one exchange step -- an RCCL gather to rank 0 of every rank's
+whole output (config 2: all its int16 levels, 3.2 GB per rank at 128 frames,
+in --gather-chunk-frames pieces so rank 0's receive buffers stay bounded;
+--gather-frames keeps only a sample, as an explicit option; config 4: all
+reconstructed bands as uint8, clip_to_pixel_range guarantees [0, 255]) -- on a
+side stream, the gather of step k overlapped with the compute of step k+1
+(double-buffered outputs).  Reported as ``gather_inclusive`` with the bytes
+into rank 0 and the achieved xGMI rate.
 
 Timing: W warmup steps, then K steps between barrier + synchronize; the max
 over ranks is reported; ``value`` = units of all ranks / that time.  Rank 0
@@ -85,9 +87,12 @@ def parse_args(argv=None):
     ap.add_argument("--variant", type=int, default=4341, help="config 2 launch variant (nanohevc.h); 4341 = default")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (1-thread + all-threads legs)")
     ap.add_argument("--gather-steps", type=int, default=3, help="N>1: timed steps of the gather-inclusive phase")
-    ap.add_argument("--gather-frames", type=int, default=8,
+    ap.add_argument("--gather-frames", type=int, default=None,
                     help="config 2, N>1: frames' worth of int16 levels each rank ships to rank 0 per gathered step "
-                         "(a bounded sample of its output; the whole output would be 3.2 GB per rank at 128 frames)")
+                         "(default: all --frames, the whole output; fewer = an explicit sample)")
+    ap.add_argument("--gather-chunk-frames", type=int, default=8,
+                    help="N>1: frames' worth of output per RCCL gather call (rank 0's receive buffers hold "
+                         "one chunk per rank)")
     ap.add_argument("--check", action="store_true", help="config 4, N>1: rank 0 compares the gathered recon with "
                                                           "an unsharded run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -250,19 +255,26 @@ class OverlappedGather:
     """The exchange step on a side stream: gather(k) waits for compute(k) and
     runs under compute(k+1); the two output buffers alternate, and compute(k+2)
     waits for gather(k) before overwriting its buffer.  ``send_of(k)`` returns
-    the flat tensor to send after compute(k) (on the side stream)."""
+    the flat tensor to send after compute(k) (on the side stream); it goes to
+    rank 0 in pieces of at most ``chunk`` elements (one gather call each, in
+    order on the side stream), so rank 0 holds one piece per rank, whatever the
+    output size.  ``on_chunk(off, n)``, when set, runs on the side stream after
+    each piece has landed in ``recv`` (tests: what rank 0 received)."""
 
-    def __init__(self, dist, dev, sizes, dtype):
+    def __init__(self, dist, dev, sizes, dtype, chunk=None):
         self.dist, self.dev = dist, dev
         self.gloo = dist.get_backend() == "gloo"
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.n = max(sizes)
+        self.chunk = max(1, min(self.n, chunk or self.n))
         self.side = torch.cuda.Stream(device=dev)
         self.done = [None, None]
         self.recv = None
+        self.on_chunk = None
+        self.calls = 0
         if self.rank == 0:
             rdev = "cpu" if self.gloo else dev
-            self.recv = [torch.empty(self.n, dtype=dtype, device=rdev) for _ in range(self.world)]
+            self.recv = [torch.empty(self.chunk, dtype=dtype, device=rdev) for _ in range(self.world)]
 
     def wait_free(self, slot, main):
         if self.done[slot] is not None:
@@ -274,12 +286,18 @@ class OverlappedGather:
         with torch.cuda.stream(self.side):
             self.side.wait_event(ready)
             send = send_fn()
-            if self.gloo:   # gloo gathers host tensors: a synchronous rehearsal of the same call
-                send = send.cpu()
-            if self.rank == 0:
-                self.dist.gather(send, gather_list=self.recv, dst=0)
-            else:
-                self.dist.gather(send, dst=0)
+            for off in range(0, send.numel(), self.chunk):
+                n = min(self.chunk, send.numel() - off)
+                piece = send[off:off + n]
+                if self.gloo:   # gloo gathers host tensors: a synchronous rehearsal of the same call
+                    piece = piece.cpu()
+                if self.rank == 0:
+                    self.dist.gather(piece, gather_list=[r[:n] for r in self.recv], dst=0)
+                else:
+                    self.dist.gather(piece, dst=0)
+                self.calls += 1
+                if self.on_chunk is not None:
+                    self.on_chunk(off, n)
             done = torch.cuda.Event()
             done.record(self.side)
             self.done[slot] = done
@@ -336,20 +354,26 @@ def run_cfg2(args, dist, world, rank, dev):
     gather = None
     if dist and args.gather_steps > 0:
         outs.append(torch.zeros_like(outs[0]))
-        frac = min(1.0, args.gather_frames / args.frames)
+        gf = args.frames if args.gather_frames is None else args.gather_frames
+        frac = min(1.0, gf / args.frames)
         words = min(padded, -(-int(padded * frac) // 4) * 4) // 4   # int64 words sent per rank per step
-        og = OverlappedGather(dist, dev, [words] * world, torch.int64)
+        chunk = max(1, args.gather_chunk_frames * fe // 4)
+        og = OverlappedGather(dist, dev, [words] * world, torch.int64, chunk=chunk)
         gt = run_phase_gather(step_into, lambda s: outs[s].view(torch.int64)[:words], og, args.gather_steps, dist,
                               stream)
         (gt,), _ = reduce_max_sum(dist, dev, (gt,), ())
         into_root = 8 * words * (world - 1)
+        what = ("the whole int16 output" if frac >= 1.0 else
+                f"a {gf}-frame sample of the int16 levels (the head of the output; --gather-frames)")
         gather = {"value": blocks_all * args.gather_steps / gt, "unit": "blocks/s", "steps": args.gather_steps,
                   "ms_per_step": gt / args.gather_steps * 1e3, "bytes_into_root_per_step": into_root,
                   "into_root_GBps": into_root * args.gather_steps / gt / 1e9, "overlapped": True,
                   "backend": dist.get_backend(), "levels_fraction_gathered": frac,
-                  "note": f"compute + RCCL gather to rank 0 of a {args.gather_frames}-frame sample of every rank's "
-                          "int16 levels per step (the head of its output), on a side stream, gather(k) under "
-                          "compute(k+1); the exchange is bounded by rank 0's inbound xGMI (SURVEY.md §8e E-2)"}
+                  "bytes_per_rank_per_step": 8 * words, "gather_calls_per_step": -(-words // chunk),
+                  "chunk_bytes": 8 * chunk,
+                  "note": f"compute + RCCL gather to rank 0 of {what} of every rank per step, in "
+                          f"{args.gather_chunk_frames}-frame pieces on a side stream, gather(k) under compute(k+1); "
+                          "the exchange is bounded by rank 0's inbound xGMI (SURVEY.md §8e E-2)"}
 
     if rank != 0:
         return None

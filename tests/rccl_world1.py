@@ -6,13 +6,14 @@ bench.init_dist(1, force_group=True) takes the ``nccl`` branch
 bench.OverlappedGather / bench.run_phase_gather drive device-tensor gathers on
 the side stream exactly as the N>1 bench does:
 
-* config 2: int64 words of the int16 levels (the --gather-frames sample);
+* config 2: int64 words of the WHOLE int16 output of a 128-frame step (3.2 GB),
+  in 8-frame gather calls, as bench.py's default gather-inclusive phase ships it;
 * config 4: the reconstructed bands packed as uint8 (bench.Cfg4Rank.send_of).
 
 Every step writes different outputs into its slot (the QP changes per step and
-the first int64 word of a config-2 slot is overwritten with a per-step
-sentinel), and after each gather the side stream copies what rank 0 received
-into a history buffer.  The history must equal, step by step, what that step's
+the first int64 word of every config-2 gather piece is overwritten with a
+per-step, per-piece sentinel), and after each gather call the side stream
+copies what rank 0 received into a history buffer.  The history must equal, step by step, what that step's
 compute produced: a gather that read its slot after step k+2's compute had
 overwritten it (a missing wait_free) shows up as step k+2's sentinel or QP.
 Prints one JSON line.
@@ -50,35 +51,53 @@ def main():
     steps = 6
     qps = [22 + 5 * (k % 3) for k in range(steps)]
 
-    # ---- config 2: int64 words of the int16 levels ----
-    F, W, H = 2, 3840, 2160
+    # ---- config 2: the WHOLE int16 output of a 128-frame step (bench.py's default gather), in
+    #      8-frame RCCL gather calls; every piece of every step carries its own sentinel word ----
+    F, W, H = 128, 3840, 2160
+    steps2 = 4
+    fe = gpu.yuv420_frame_elems(W, H)
     sets = gpu.yuv420_plane_sets(F, W, H)
-    n = F * gpu.yuv420_frame_elems(W, H)
+    n = F * fe
     g = torch.Generator(device=dev)
     g.manual_seed(5)
     res = torch.randint(-255, 256, (n,), dtype=torch.int16, device=dev, generator=g)
     outs = [torch.zeros(n, dtype=torch.int16, device=dev) for _ in range(2)]
     words = n // 4
-    og = bench.OverlappedGather(dist, dev, [words], torch.int64)
-    hist = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(steps + 1)]
+    chunk = 8 * fe // 4
+    og = bench.OverlappedGather(dist, dev, [words], torch.int64, chunk=chunk)
+    hist = [torch.zeros(words, dtype=torch.int64, device=dev) for _ in range(steps2 + 1)]
     cur = {"k": -1}
+    starts = list(range(0, words, chunk))
+
+    def sentinel(k, c):
+        return 1_000_000 * (k + 1) + c
 
     def step_into(slot):
         cur["k"] += 1
         k = cur["k"]
         gpu.fwd8x8_quant(res, sets, qps[k % steps], True, out=outs[slot], stream=main_s)
-        outs[slot].view(torch.int64)[0].fill_(1000 + k)   # per-step sentinel word
+        w = outs[slot].view(torch.int64)
+        for c, off in enumerate(starts):   # per-step, per-piece sentinel words
+            w[off].fill_(sentinel(k, c))
 
-    og.gather = _wrap(og, og.gather, hist, cur)
-    bench.run_phase_gather(step_into, lambda s: outs[s].view(torch.int64)[:words], og, steps, dist, main_s)
+    og.on_chunk = lambda off, m: hist[cur["k"]][off:off + m].copy_(og.recv[0][:m])
+    bench.run_phase_gather(step_into, lambda s: outs[s].view(torch.int64)[:words], og, steps2, dist, main_s)
     torch.cuda.synchronize()
     ok2 = True
-    for k in range(steps + 1):
-        exp = gpu.fwd8x8_quant(res, sets, qps[k % steps], True).view(torch.int64)[:words].clone()
-        exp[0] = 1000 + k
+    for k in range(steps2 + 1):
+        exp = gpu.fwd8x8_quant(res, sets, qps[k % steps], True).view(torch.int64)[:words]
+        for c, off in enumerate(starts):
+            exp[off] = sentinel(k, c)
         ok2 &= bool(torch.equal(hist[k], exp))
+        del exp
     out["cfg2_int64_gathers_equal_sent"] = ok2
-    out["cfg2_steps"] = steps + 1
+    out["cfg2_steps"] = steps2 + 1
+    out["cfg2_frames"] = F
+    out["cfg2_levels_fraction_gathered"] = 1.0
+    out["cfg2_bytes_per_step"] = 8 * words
+    out["cfg2_gather_calls_per_step"] = len(starts)
+    del hist, outs, res
+    torch.cuda.empty_cache()
 
     # ---- config 4: uint8 recon bands ----
     nf = 2

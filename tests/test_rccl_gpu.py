@@ -24,5 +24,7 @@ def test_rccl_world1_overlapped_gathers_match_their_steps():
     assert lines, r.stdout[-2000:] + r.stderr[-2000:]
     d = json.loads(lines[-1])
     assert d["backend"] == "nccl" and d["world"] == 1
-    assert d["cfg2_int64_gathers_equal_sent"] is True and d["cfg2_steps"] >= 6
+    assert d["cfg2_int64_gathers_equal_sent"] is True and d["cfg2_steps"] >= 5
+    assert d["cfg2_frames"] == 128 and d["cfg2_levels_fraction_gathered"] == 1.0
+    assert d["cfg2_gather_calls_per_step"] == 16
     assert d["cfg4_uint8_gathers_equal_sent"] is True and d["cfg4_bytes_per_gather"] > 0
