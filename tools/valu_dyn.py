@@ -69,9 +69,48 @@ INT32_NO = {"v_mov_b32", "v_pk_add_u16", "v_cndmask_b32", "v_perm_b32", "v_lshlr
             "v_mad_u64_u32"}
 
 
+MEMBERSHIP = {}   # measured: {mnemonic: {counter: count per instruction}} (load_membership)
+_CLASS_COUNTERS = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT",
+                   "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32")
+
+
+def load_membership(cal3, cal4, log):
+    """Per-opcode counter membership from tools/ab/pmc_cal.hip's kop<OP> kernels
+    (REP copies of one opcode each): (counter - the smallest value of that
+    counter over all opcodes) / waves / REP; SQ_INSTS_VALU per opcode is its own
+    count per op (2 for v_permlane32_swap)."""
+    meta = json.loads(next(line for line in open(log) if line.startswith("{") and '"ops"' in line))
+    ops, rep, waves = meta["ops"], meta["rep"], meta["waves_per_variant"]
+    per = collections.defaultdict(dict)
+    for d in (cal3, cal4):
+        for p in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(p)):
+                mm = re.search(r"kop<(\d+)>", r["Kernel_Name"])
+                if mm:
+                    per[int(mm.group(1))][r["Counter_Name"]] = float(r["Counter_Value"])
+    cnts = {c for k in per for c in per[k]}
+    base = {c: min(per[k][c] for k in per if c in per[k]) for c in cnts}
+    out = {}
+    for k, op in enumerate(ops):
+        if k not in per or not re.match(r"^v_[a-z0-9_]+$", op) or op.endswith(("_vamt", "_rot", "_vcc", "_init", "_s", "_vv")):
+            continue
+        e = {c: round((per[k][c] - (0.0 if c == "SQ_INSTS_VALU" else base[c])) / waves / rep) for c in per[k]
+             if c in _CLASS_COUNTERS}
+        if "SQ_INSTS_VALU" in e:
+            e["SQ_INSTS_VALU"] = round((per[k]["SQ_INSTS_VALU"] - base["SQ_INSTS_VALU"]) / waves / rep + 1)
+        out[vm.base_mnemonic(op)] = e
+        if op == "v_permlane32_swap":   # the probe's name for v_permlane32_swap_b32
+            out["v_permlane32_swap_b32"] = e
+    MEMBERSHIP.clear()
+    MEMBERSHIP.update(out)
+    return out
+
+
 def membership(m: str, counter: str):
     """(known, unknown) contribution of one instruction to one counter."""
     b = vm.base_mnemonic(m)
+    if b in MEMBERSHIP and counter in MEMBERSHIP[b]:
+        return (MEMBERSHIP[b][counter], 0)
     if counter == "SQ_INSTS_VALU":
         return (1, 0) if m.startswith("v_") else (0, 0)
     if counter == "SQ_INSTS_MFMA":
@@ -208,7 +247,7 @@ def price(m: str, rates):
         return 1.0 / rates[b], True
     if m in rates:
         return 1.0 / rates[m], True
-    return 1.0 / rates.get(vm.rate_class(m), rates["v_add_u32"]), False
+    return 1.0 / rates.get(vm.rate_class(m), rates["v_add3_u32"]), False
 
 
 # ---- measured counters
@@ -305,9 +344,13 @@ def main():
     ap.add_argument("--pmc", nargs="+", required=True, help="rocprofv3 --pmc output dirs of ONE config")
     ap.add_argument("--kernels", default="nh::")
     ap.add_argument("--tol", type=float, default=0.005)
+    ap.add_argument("--cal", nargs=3, default=None, metavar=("CAL3", "CAL4", "LOG"),
+                    help="tools/ab/_pmc_cal outputs: the measured counter membership of every probe opcode")
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     rates = load_rates(a.rates)
+    if a.cal:
+        load_membership(*a.cal)
     meas = load_counters(a.pmc)
     srcs = sorted(glob.glob(os.path.join(vm.CSRC, "*.hip")))
     with tempfile.TemporaryDirectory() as tmp:

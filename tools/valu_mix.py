@@ -38,16 +38,22 @@ HIPCC = "/opt/rocm/bin/hipcc"
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "--cuda-device-only", "--no-gpu-bundle-output"]
 
-# VALU mnemonic (regex, first match wins) -> the measured opcode whose rate it takes.
-# Every class was measured on its own (tools/ab/valu_rate.hip); the defaults at the
-# end are the plain 32-bit and the packed 16-bit issue classes.
+# VALU mnemonic (regex, first match wins) -> the measured opcode whose rate it takes,
+# for the (few) mnemonics tools/ab/valu_rate.hip does not measure itself.  The
+# round-4 probe (interleaved rounds, SIMD cycles per instruction from s_memtime
+# spans per SIMD) splits gfx950's VALU into a 2-cycle class (32-bit add / sub /
+# logic / lshrrev / ashrrev / mov, f32 add / mul / fma, non-packed 16-bit add /
+# sub / mul / shifts, bitop3, accvgpr moves: ~0.93-1.02 T wave-instr/s) and a
+# 4-cycle class (everything else: packed 16-bit, dot2, 24-bit multiplies, cmp,
+# cndmask, perm, bfe / bfi, 3-input ops, min / max, lshlrev_b32, cvt, 64-bit
+# ops: ~0.52-0.58 T/s), plus 8-cycle transcendentals.
 RATE_CLASS = [
     (r"^v_dot2", "v_dot2c_i32_i16"),
     (r"^v_(mad|mul)_(i32_i24|u32_u24)$", "v_mad_i32_i24"),
     (r"^v_mul_(lo|hi)_(u32|i32)$|^v_mad_(u64_u32|i64_i32)$|^v_mul_hi_(i32|u32)_(i24|u24)$", "v_mul_lo_u32"),
     (r"^v_pk_(mad|mul|fma)", "v_pk_mad_u16"),
     (r"^v_pk_", "v_pk_add_u16"),
-    (r"^v_(lshlrev|lshrrev|ashrrev)_(b|i)64$|^v_lshl_add_u64$|^v_(add|sub)_(co|u64)", "v_lshlrev_b64"),
+    (r"^v_(lshlrev|lshrrev|ashrrev)_(b|i)64$|^v_lshl_add_u64$|^v_(add|sub)_(co|u64)|^v_mov_b64", "v_lshlrev_b64"),
     (r"^v_cmp|^v_cmpx", "v_cmp_gt_i32"),
     (r"^v_cndmask", "v_cndmask_b32"),
     (r"^v_perm", "v_perm_b32"),
@@ -55,9 +61,14 @@ RATE_CLASS = [
     (r"^v_(add3|lshl_add|add_lshl|lshl_or|and_or|or3|xad|xor3|mad_u32_u16|max3|min3|med3)", "v_add3_u32"),
     (r"^v_readfirstlane|^v_readlane|^v_writelane", "v_readfirstlane_b32"),
     (r"^v_permlane", "v_permlane32_swap"),
-    (r"^v_(fma|mac|mad|mul|add|sub|max|min)_f32|^v_floor|^v_cvt|^v_rndne|^v_trunc", "v_fma_f32"),
+    (r"^v_(rcp|rsq|sqrt|exp|log|sin|cos)_", "v_rcp_iflag_f32"),
+    (r"^v_(add|sub|subrev|mul|fma|mac)_f32$", "v_add_f32"),
+    (r"^v_(max|min)_f32|^v_floor|^v_cvt|^v_rndne|^v_trunc|^v_fract", "v_floor_f32"),
+    (r"^v_(add|sub|subrev|and|or|xor|not)_(u32|b32)$|^v_(lshrrev_b32|ashrrev_i32)$", "v_add_u32"),
+    (r"^v_(add|sub|mul_lo|lshlrev|lshrrev)_(u16|b16)$", "v_add_u16"),
+    (r"^v_accvgpr", "v_accvgpr_read_b32"),
     (r"^v_mov", "v_mov_b32"),
-    (r"^v_", "v_add_u32"),
+    (r"^v_", "v_add3_u32"),   # unmeasured: priced at the 4-cycle class, not the 2-cycle one
 ]
 
 UNIT_RULES = [
@@ -83,7 +94,7 @@ def rate_class(m: str) -> str:
     for pat, cls in RATE_CLASS:
         if re.search(pat, m):
             return cls
-    return "v_add_u32"
+    return "v_add3_u32"
 
 
 def unit_of(m: str) -> str:
@@ -136,7 +147,8 @@ def load_rates(path):
         line = line.strip()
         if line.startswith("{"):
             d = json.loads(line)
-            rates[d["op"]] = d
+            if d.get("waves_per_simd", 8) == 8 and d["op"] not in rates:   # the all-opcode block at 8 waves/SIMD
+                rates[d["op"]] = d
     return rates
 
 
@@ -160,7 +172,7 @@ def summarize(sym, cnt, rates):
         missing = [c for c in by_class if c not in rates]
         t = 0.0
         for c, n in by_class.items():
-            r = rates.get(c, rates.get("v_add_u32"))
+            r = rates.get(c, rates.get("v_add3_u32", rates.get("v_add_u32")))
             t += n / r["chip_winst_per_s"]
         att = nv / t
         res["attainable_valu_winst_per_s"] = att
