@@ -595,6 +595,23 @@ def run_cfg4(args, dist, world, rank, dev):
     return line
 
 
+def valu_sources_match(v) -> bool:
+    """Whether a profiles/valu_roofline.json entry was profiled from the kernel
+    sources this run executes: tools/pmc_valu.py records the sha256 of the
+    config's csrc files (in order); recomputed here."""
+    src = (v or {}).get("sources")
+    if not src:
+        return False
+    import hashlib
+    h = hashlib.sha256()
+    try:
+        for f in src["files"]:
+            h.update(open(os.path.join(ROOT, "nano-hevc_amd", "csrc", f), "rb").read())
+    except OSError:
+        return False
+    return h.hexdigest() == src.get("sha256")
+
+
 def load_valu(cfg_key: str):
     """The VALU roofline inputs of a configuration, committed in
     profiles/valu_roofline.json by tools/pmc_valu.py: per kernel of the step the
@@ -626,6 +643,10 @@ def cfg4_roofline(samples, kern_ms, frames, world):
     v = load_valu("cfg4_4k_yuv420")
     if not v:
         return dict(hbm, kernel_ms_avg=kern_ms)
+    if not valu_sources_match(v):   # the committed counts describe another build: the HBM view leads
+        return dict(hbm, kernel_ms_avg=kern_ms, valu_profile_stale=True,
+                    valu_note="profiles/valu_roofline.json was profiled from other kernel sources (sha256 mismatch); "
+                              "re-run the VALU passes (tools/gpu_run.sh valu_kt valu_pmc1..4, tools/pmc_valu.py)")
     nf = samples / (W4K * H4K * 3 // 2)        # frames' worth of samples this rank coded per step
     ks = [k for k in v["kernels"].values() if k.get("valu_per_frame") and k.get("attainable_valu_winst_per_s")]
     instr = sum(k["valu_per_frame"] * nf for k in ks)
@@ -634,10 +655,13 @@ def cfg4_roofline(samples, kern_ms, frames, world):
     achieved = instr / (kern_ms * 1e-3) / 1e9
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G VALU wave-instr/s",
             "frac": achieved / peak, "traffic": hbm["traffic"], "valu_instr_per_step": instr,
-            "valu_instr_per_sample": instr * 64 / samples,
-            "peak_note": "attainable issue rate of the step's static VALU mix at the measured per-opcode rates "
-                         "(tools/valu_mix.py x tools/ab/valu_rate.hip; profiles/valu_roofline.json)",
-            "valu_source": v.get("source"), "kernel_ms_avg": kern_ms, "hbm": hbm}
+            "valu_lane_instr_per_sample": instr * 64 / samples,   # wave-instructions x 64 lanes / samples
+            "peak_note": "attainable issue rate of the step's executed VALU mix at the measured per-opcode rates: "
+                         + v.get("peak_kind", "static mix") + " (tools/ab/valu_rate.hip; profiles/valu_roofline.json)",
+            "valu_frac_range": [achieved / peak, achieved / (instr / sum(k["valu_per_frame"] * nf / k["attainable_dynamic_lo"]
+                                                                         for k in ks) / 1e9)]
+            if all(k.get("attainable_dynamic_lo") for k in ks) else None,
+            "valu_profile_matches_build": True, "valu_source": v.get("source"), "kernel_ms_avg": kern_ms, "hbm": hbm}
 
 
 def cpu_baseline_cfg4(me, src, lvl, rec, args, fe):

@@ -822,7 +822,7 @@ static void staging_free(Staging& s) {   // caller holds s.mu, current device = 
 
 // Idle time after which the block-call server leaves (us; default 200, 0 = no
 // server: every small call is a k_small launch).  nh_block_server_set_idle_us().
-static std::atomic<long> g_srv_idle_us{200};
+static std::atomic<long> g_srv_idle_us{100};   // a device-wide sync after calls waits up to this long
 static long server_idle_us() { return g_srv_idle_us.load(std::memory_order_relaxed); }
 
 static int staging_init(Staging& s) {    // caller holds s.mu

@@ -35,6 +35,7 @@
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
 #include "nh_mfma.hpp"
+#include "nh_f16mma.hpp"
 // The open-loop CTU kernels keep the builtin's v_dot2c seeding (pdot_first,
 // nh_packed.hpp): the VOP3P form measured 1.3 % slower here (0.0390 vs 0.0385
 // ms per 4K frame, profiles/r03/cfg4/ab_libs_4b_pd.jsonl) and 2-4 % faster in
@@ -49,27 +50,7 @@ namespace nh {
 
 __constant__ Basis c_basis_ctu;
 
-// f16 DCT32 bases of the narrow 32x32 chain (ctu_chain32_h), every entry
-// T[k][n] * 2^-10 (exact in f16), as the matrix and its transpose (4 KB: one
-// copy per workgroup in LDS).  Each lane's MFMA operand is one 16-byte piece of
-// a row (the data-side passes) or two 8-byte pieces of it in the accumulator
-// row order crow (passes 2 and 4, nh_mfma.hpp).
-struct BasisH {
-    uint16_t t[32][32];          // [k][n] = T[k][n]   pass 1 B operand (lane k); pass 2 A operand (lane l = k)
-    uint16_t tt[32][32];         // [n][k] = T[k][n]   inverse pass 1 B operand (lane n); inverse pass 2 A operand
-};
 __constant__ BasisH c_basis_h;
-
-static BasisH make_basis_h() {
-    auto h = [](int v) { return __builtin_bit_cast(uint16_t, (_Float16)((float)v / 1024.0f)); };
-    BasisH b;
-    for (int k = 0; k < 32; ++k)
-        for (int n = 0; n < 32; ++n) {
-            b.t[k][n] = h(dct32(k, n));
-            b.tt[n][k] = h(dct32(k, n));
-        }
-    return b;
-}
 
 struct CtuArgs {
     const int16_t* src;
@@ -494,9 +475,6 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
 // accumulator as the B operand in accumulator row order (the bases
 // pre-permuted to match), and one LDS transpose sits after dequantization.
 // Same results as ctu_chain / ctu_chain_pk on these TUs.
-typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
-typedef float f16x_t __attribute__((ext_vector_type(16)));
-
 // The bases live in LDS (one copy per workgroup, copy_basis_h): as global loads
 // every operand load after a store would wait for the wave's outstanding stores
 // (vmcnt counts both on gfx9), draining each chain's level stores.
@@ -506,82 +484,6 @@ __device__ __forceinline__ void copy_basis_h(BasisH& dst) {
     constexpr int n = (int)(sizeof(BasisH) / 16);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d4[i] = s4[i];
 }
-__device__ __forceinline__ h8_t ld_h8(const uint16_t* p) { return __builtin_bit_cast(h8_t, *(const uint4*)p); }
-// Elements crow(8s + j, hh), j = 0..7, of a basis row: [16s + 4hh, +4) and [16s + 8 + 4hh, +4).
-__device__ __forceinline__ h8_t ld_crow_h8(const uint16_t* row, int s, int hh) {
-    const uint2 p = *(const uint2*)(row + 16 * s + 4 * hh), q = *(const uint2*)(row + 16 * s + 8 + 4 * hh);
-    return __builtin_bit_cast(h8_t, make_uint4(p.x, p.y, q.x, q.y));
-}
-// The four operand pieces of each basis a lane reads, as accessors over the LDS
-// copy (BasisH) or over registers loaded once per wave (BasisRegs, k_tc32_h:
-// 32 VGPRs, no LDS copy and no workgroup barrier).
-__device__ __forceinline__ h8_t bq_t(const BasisH& b, int r, int hh, int s) { return ld_h8(&b.t[r][16 * s + 8 * hh]); }
-__device__ __forceinline__ h8_t bq_tc(const BasisH& b, int r, int hh, int s) { return ld_crow_h8(b.t[r], s, hh); }
-__device__ __forceinline__ h8_t bq_tt(const BasisH& b, int r, int hh, int s) { return ld_h8(&b.tt[r][16 * s + 8 * hh]); }
-__device__ __forceinline__ h8_t bq_ttc(const BasisH& b, int r, int hh, int s) { return ld_crow_h8(b.tt[r], s, hh); }
-struct BasisRegs {
-    h8_t t[2], tc[2], tt[2], ttc[2];
-};
-__device__ __forceinline__ BasisRegs load_basis_regs(const BasisH& g, int r, int hh) {
-    BasisRegs b;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        b.t[s] = bq_t(g, r, hh, s);
-        b.tc[s] = bq_tc(g, r, hh, s);
-        b.tt[s] = bq_tt(g, r, hh, s);
-        b.ttc[s] = bq_ttc(g, r, hh, s);
-    }
-    return b;
-}
-__device__ __forceinline__ h8_t bq_t(const BasisRegs& b, int, int, int s) { return b.t[s]; }
-__device__ __forceinline__ h8_t bq_tc(const BasisRegs& b, int, int, int s) { return b.tc[s]; }
-__device__ __forceinline__ h8_t bq_tt(const BasisRegs& b, int, int, int s) { return b.tt[s]; }
-__device__ __forceinline__ h8_t bq_ttc(const BasisRegs& b, int, int, int s) { return b.ttc[s]; }
-__device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
-    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
-}
-// Where the rounding bias enters: kBiasInit = the accumulators start at it
-// (16 more live registers per pass, no adds), else it is added before floor().
-#ifdef NH_ACC_INIT_BIAS
-constexpr bool kBiasInit = true;
-#else
-constexpr bool kBiasInit = false;
-#endif
-__device__ __forceinline__ float addb(float x, float b) { if constexpr (kBiasInit) return x; else return x + b; }
-// (int)floor(x + 0.5) of an accumulator -- the arithmetic shift of the integer
-// chain -- in ONE instruction: v_cvt_rpi_i32_f32 rounds half up (floor(x + 0.5))
-// as it converts, and x is a multiple of 2^-10 below 2^14, so x + 0.5 is exact
-// and the result equals the add / floor / convert sequence.  With the bias in
-// the accumulators (kBiasInit) it is floor alone: v_cvt_flr_i32_f32.
-#ifndef NH_CVT_RPI
-#define NH_CVT_RPI 1
-#endif
-__device__ __forceinline__ int32_t shift_rnd(float x) {
-    if constexpr (!NH_CVT_RPI) {
-        return (int32_t)__builtin_floorf(addb(x, 0.5f));
-    } else {
-        int32_t r;
-        if constexpr (kBiasInit) asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
-        else asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
-        return r;
-    }
-}
-__device__ __forceinline__ float initb(float b) { if constexpr (kBiasInit) return b; else return 0.0f; }
-__device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s, float b) {   // registers 8s .. 8s+7 + b, floored, as f16
-    uint4 u;
-    u.x = pk_floor_h(addb(acc[8 * s + 0], b), addb(acc[8 * s + 1], b));
-    u.y = pk_floor_h(addb(acc[8 * s + 2], b), addb(acc[8 * s + 3], b));
-    u.z = pk_floor_h(addb(acc[8 * s + 4], b), addb(acc[8 * s + 5], b));
-    u.w = pk_floor_h(addb(acc[8 * s + 6], b), addb(acc[8 * s + 7], b));
-    return __builtin_bit_cast(h8_t, u);
-}
-__device__ __forceinline__ f16x_t splat16(float v) {
-    f16x_t r;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) r[g] = v;
-    return r;
-}
-
 // TSTORE: the level and recon rows leave through an LDS tile `ot` (per wave,
 // kOutP int32 per row) so that every global store instruction writes whole
 // rows -- 8 rows of 128 B (levels), 16 rows of 64 B (recon) -- instead of 32-B
@@ -649,6 +551,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     f16x_t acc2 = splat16(initb(0.5f));
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 0), acc_h8(acc, 0, b1), acc2, 0, 0, 0);
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 1), acc_h8(acc, 1, b1), acc2, 0, 0, 0);
+    mfma_result_ready(acc2);   // before shift_rnd's inline-asm reads
     // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
     int32_t* lrow = lvl + (int64_t)(gy0 + r) * op + gx0;
 #pragma unroll
@@ -682,6 +585,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
     f16x_t acc4 = splat16(initb(0.5f));
     acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 0), acc_h8(acc3, 0, 0.5f), acc4, 0, 0, 0);
     acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 1), acc_h8(acc3, 1, 0.5f), acc4, 0, 0, 0);
+    mfma_result_ready(acc4);
     // reconstruct + clip (intra.py:70-78), row y = r
     int16_t* rrow = rec + (int64_t)(gy0 + r) * op + gx0;
 #pragma unroll

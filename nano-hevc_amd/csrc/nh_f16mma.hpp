@@ -1,0 +1,124 @@
+// nh_f16mma.hpp -- the exact f16 matrix-core pieces of the narrow 32x32 chain
+// (DESIGN.md §4.4, §4.5): the DCT32 basis scaled by 2^-10 (exact in f16), its
+// operand accessors, and the accumulator helpers.  Shared by the open-loop
+// chain (ctu_chain32_h, nh_ctu.hip: configs 4 and 5) and the closed-loop one
+// (closed_chain32_h, nh_intraloop.hip: config 4 in closed loop).
+#pragma once
+#include <hip/hip_runtime.h>
+#include "nh_common.hpp"
+#include "nh_mfma.hpp"
+
+namespace nh {
+
+// f16 DCT32 bases of the narrow 32x32 chain (ctu_chain32_h), every entry
+// T[k][n] * 2^-10 (exact in f16), as the matrix and its transpose (4 KB: one
+// copy per workgroup in LDS).  Each lane's MFMA operand is one 16-byte piece of
+// a row (the data-side passes) or two 8-byte pieces of it in the accumulator
+// row order crow (passes 2 and 4, nh_mfma.hpp).
+struct BasisH {
+    uint16_t t[32][32];          // [k][n] = T[k][n]   pass 1 B operand (lane k); pass 2 A operand (lane l = k)
+    uint16_t tt[32][32];         // [n][k] = T[k][n]   inverse pass 1 B operand (lane n); inverse pass 2 A operand
+};
+inline BasisH make_basis_h() {
+    auto h = [](int v) { return __builtin_bit_cast(uint16_t, (_Float16)((float)v / 1024.0f)); };
+    BasisH b;
+    for (int k = 0; k < 32; ++k)
+        for (int n = 0; n < 32; ++n) {
+            b.t[k][n] = h(dct32(k, n));
+            b.tt[n][k] = h(dct32(k, n));
+        }
+    return b;
+}
+
+typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+typedef float f16x_t __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ h8_t ld_h8(const uint16_t* p) { return __builtin_bit_cast(h8_t, *(const uint4*)p); }
+// Elements crow(8s + j, hh), j = 0..7, of a basis row: [16s + 4hh, +4) and [16s + 8 + 4hh, +4).
+__device__ __forceinline__ h8_t ld_crow_h8(const uint16_t* row, int s, int hh) {
+    const uint2 p = *(const uint2*)(row + 16 * s + 4 * hh), q = *(const uint2*)(row + 16 * s + 8 + 4 * hh);
+    return __builtin_bit_cast(h8_t, make_uint4(p.x, p.y, q.x, q.y));
+}
+// The four operand pieces of each basis a lane reads, as accessors over the LDS
+// copy (BasisH) or over registers loaded once per wave (BasisRegs, k_tc32_h:
+// 32 VGPRs, no LDS copy and no workgroup barrier).
+__device__ __forceinline__ h8_t bq_t(const BasisH& b, int r, int hh, int s) { return ld_h8(&b.t[r][16 * s + 8 * hh]); }
+__device__ __forceinline__ h8_t bq_tc(const BasisH& b, int r, int hh, int s) { return ld_crow_h8(b.t[r], s, hh); }
+__device__ __forceinline__ h8_t bq_tt(const BasisH& b, int r, int hh, int s) { return ld_h8(&b.tt[r][16 * s + 8 * hh]); }
+__device__ __forceinline__ h8_t bq_ttc(const BasisH& b, int r, int hh, int s) { return ld_crow_h8(b.tt[r], s, hh); }
+struct BasisRegs {
+    h8_t t[2], tc[2], tt[2], ttc[2];
+};
+__device__ __forceinline__ BasisRegs load_basis_regs(const BasisH& g, int r, int hh) {
+    BasisRegs b;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        b.t[s] = bq_t(g, r, hh, s);
+        b.tc[s] = bq_tc(g, r, hh, s);
+        b.tt[s] = bq_tt(g, r, hh, s);
+        b.ttc[s] = bq_ttc(g, r, hh, s);
+    }
+    return b;
+}
+__device__ __forceinline__ h8_t bq_t(const BasisRegs& b, int, int, int s) { return b.t[s]; }
+__device__ __forceinline__ h8_t bq_tc(const BasisRegs& b, int, int, int s) { return b.tc[s]; }
+__device__ __forceinline__ h8_t bq_tt(const BasisRegs& b, int, int, int s) { return b.tt[s]; }
+__device__ __forceinline__ h8_t bq_ttc(const BasisRegs& b, int, int, int s) { return b.ttc[s]; }
+__device__ __forceinline__ uint32_t pk_floor_h(float a, float b) {   // (floor a, floor b) as an f16 pair
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(__builtin_floorf(a), __builtin_floorf(b)));
+}
+// Where the rounding bias enters: kBiasInit = the accumulators start at it
+// (16 more live registers per pass, no adds), else it is added before floor().
+#ifdef NH_ACC_INIT_BIAS
+constexpr bool kBiasInit = true;
+#else
+constexpr bool kBiasInit = false;
+#endif
+__device__ __forceinline__ float addb(float x, float b) { if constexpr (kBiasInit) return x; else return x + b; }
+// (int)floor(x + 0.5) of an accumulator -- the arithmetic shift of the integer
+// chain -- in ONE instruction: v_cvt_rpi_i32_f32 rounds half up (floor(x + 0.5))
+// as it converts, and x is a multiple of 2^-10 below 2^14, so x + 0.5 is exact
+// and the result equals the add / floor / convert sequence.  With the bias in
+// the accumulators (kBiasInit) it is floor alone: v_cvt_flr_i32_f32.
+#ifndef NH_CVT_RPI
+#define NH_CVT_RPI 1
+#endif
+__device__ __forceinline__ int32_t shift_rnd(float x) {
+    if constexpr (!NH_CVT_RPI) {
+        return (int32_t)__builtin_floorf(addb(x, 0.5f));
+    } else {
+        int32_t r;
+        if constexpr (kBiasInit) asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+        else asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+        return r;
+    }
+}
+// shift_rnd's v_cvt_rpi is inline asm, and the compiler's hazard recognizer
+// inserts no wait states for an inline-asm read of an MFMA result: a conversion
+// scheduled right behind the MFMA reads the accumulator's OLD value (seen as
+// wrong levels in column 0 of a closed-loop 32x32 TU at QP 0).  Every chain
+// therefore passes an accumulator through this block before shift_rnd reads
+// it: an s_nop run tied to the accumulator (after the MFMA that writes it,
+// before every reader), 24 wait states -- more than the 32x32 MFMA's result
+// latency -- for ~24 cycles per pass.
+__device__ __forceinline__ void mfma_result_ready(f16x_t& acc) {
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
+}
+__device__ __forceinline__ float initb(float b) { if constexpr (kBiasInit) return b; else return 0.0f; }
+__device__ __forceinline__ h8_t acc_h8(const f16x_t& acc, int s, float b) {   // registers 8s .. 8s+7 + b, floored, as f16
+    uint4 u;
+    u.x = pk_floor_h(addb(acc[8 * s + 0], b), addb(acc[8 * s + 1], b));
+    u.y = pk_floor_h(addb(acc[8 * s + 2], b), addb(acc[8 * s + 3], b));
+    u.z = pk_floor_h(addb(acc[8 * s + 4], b), addb(acc[8 * s + 5], b));
+    u.w = pk_floor_h(addb(acc[8 * s + 6], b), addb(acc[8 * s + 7], b));
+    return __builtin_bit_cast(h8_t, u);
+}
+__device__ __forceinline__ f16x_t splat16(float v) {
+    f16x_t r;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) r[g] = v;
+    return r;
+}
+
+
+}  // namespace nh

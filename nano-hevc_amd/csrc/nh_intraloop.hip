@@ -15,6 +15,7 @@
 #include "nh_internal.hpp"
 #include "nh_tree.hpp"
 #include "nh_packed.hpp"
+#include "nh_f16mma.hpp"
 
 namespace nh {
 
@@ -1126,8 +1127,11 @@ struct Closed4Args {
     const uint8_t* plan;    // k_tu_closed_pair: per-(plane of the group, CTU) TU schedules (k_closed4_plan)
     int32_t probe;          // A/B timing probes (k_tu_closed_pair; wrong outputs): 1 no wait on the row
                             // above, 2 no chains, 4 no rounds, 8 no recon-image clear, 16 no quadtree
-                            // hashes (0 in the product)
+                            // hashes, 32 no source loads in the chains (0 in the product)
+    int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_h); set
+                            // for luma when the level / recon rows allow 16-B / 8-B stores
 };
+__constant__ BasisH c_basis_h_cl;   // the f16 DCT32 bases of closed_chain32_h (copied to LDS per workgroup)
 
 // cnt TUs of size N at once: lane l codes column / row t = l % N of TU j = l / N
 // (local origin (slx[j], sly[j]) in the CTU); reductions over a TU's N lanes are
@@ -1551,6 +1555,9 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_PRIO   // the luma wavefront's waves issue at a higher priority than chroma's (s_setprio):
 #define NH_CLOSED4_PRIO 1   // 0.1196-0.1200 vs 0.1205-0.1209 ms per 4K YUV420 frame concurrent (-DNH_CLOSED4_PRIO=0)
 #endif
+#ifndef NH_CLOSED4_MFMA_FUSED   // 1: the two planes' 32x32 MFMA chains interleaved (closed_chain32_h<2>)
+#define NH_CLOSED4_MFMA_FUSED 0
+#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -1593,7 +1600,10 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
 #pragma unroll
         for (int m = 0; m < H; ++m) {
-            o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
+            if (NH_AB && (a.probe & 32))   // A/B timing probe: no source loads (wrong outputs)
+                o2[m] = pk_pair(rc[ly + 1 + 2 * m][lx + 1 + t], rc[ly + 2 + 2 * m][lx + 1 + t]);
+            else
+                o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
             const pku16 lf = {(unsigned short)rc[ly + 1 + 2 * m][lx], (unsigned short)rc[ly + 2 + 2 * m][lx]};
             pl2[m] = (lf * wl + bs) >> sh;
             bs += st2;
@@ -1679,6 +1689,176 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     pair_sync();
 }
 
+// A 32x32 luma TU of the closed loop on the f16 matrix cores: the open loop's
+// ctu_chain32_h (nh_ctu.hip; exactness argued there: every
+// operand an integer of <= 11 bits, the basis scaled by 2^-10 exact in f16,
+// every partial sum a multiple of 2^-10 below 2^14, so the fp32 accumulators
+// hold the reference's integer sums) with the closed loop's inputs: the
+// neighbours from the plane's LDS reconstruction rc (top row rc[0][1 + x],
+// left column rc[1 + y][0], tr = rc[0][32], bl = rc[32][0]) and the source
+// samples from global memory.  NP TUs -- the same CTU of the pair's NP planes
+// (the quadtree depends on the plane id, not the frame) -- each on all 64 lanes
+// (lane (r, hh) = column / row r, half hh), their passes interleaved so one
+// plane's MFMAs and conversions run under the other's latency.  A 32x32 TU is
+// the whole CTU: only its bottom row and right column go into rc (the CTU's
+// publish and slide read nothing else; the next CTU's TUs rewrite the rest).
+// Levels and recon leave as 16-B / 8-B row pieces (the launch checks the
+// alignment, Closed4Args::mfma32).  Same results as tu_closed_batch_pk2<32>.
+constexpr int kQH = 40;   // f16 transpose tile: 32 rows of 40 halves per plane (16-B rows, conflict-free)
+template <int NP>
+__device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                                 int16_t (*rc2)[33][33], uint16_t* qt2, const BasisH& bs,
+                                                 const ChainQ& cq) {
+    const int l = opaque_lane64(), r = l & 31, hh = l >> 5;
+    int32_t topr[NP], leftr[NP], tr[NP], bl[NP], dc[NP];
+    bool use_dc[NP];
+    uint32_t hx[NP][8];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        int16_t (*rc)[33] = rc2[p];
+        topr[p] = rc[0][1 + r];
+        leftr[p] = rc[1 + r][0];
+        tr[p] = rc[0][32];
+        bl[p] = rc[32][0];
+        int32_t sdc = hh ? leftr[p] : topr[p];   // DC (intra.py:46-62): lane halves hold top / left
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sdc += __shfl_xor(sdc, o, 64);
+        dc[p] = (sdc + 32) >> 6;
+        const pk16 dc2 = pk_splat(dc[p]);
+        const int16_t* sp = pp.src[p] + (int64_t)y0c * a.pitch + x0c + r;
+        // column x = r, rows y = 8hh + 16c + j (the pass-1 A operand), as row pairs q = 4c + j/2
+        pk16 o2[8];
+        pku16 pl2[8];
+        const pku16 wl = {(unsigned short)(31 - r), (unsigned short)(31 - r)}, sh = {6, 6};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
+            if (NH_AB && (a.probe & 32))   // A/B timing probe: no source loads (wrong outputs)
+                o2[q] = pk_pair(rc[1 + y][1 + r], rc[2 + y][1 + r]);
+            else
+                o2[q] = pk_pair(sp[(int64_t)y * a.pitch], sp[(int64_t)(y + 1) * a.pitch]);
+            const int32_t b = (r + 1) * tr[p] + (31 - y) * topr[p] + (y + 1) * bl[p] + 32;   // planar, intra.py:81-113
+            const pku16 bsv = {(unsigned short)b, (unsigned short)(b + bl[p] - topr[p])};
+            const pku16 lf = {(unsigned short)rc[1 + y][0], (unsigned short)rc[2 + y][0]};
+            pl2[q] = (lf * wl + bsv) >> sh;
+        }
+        int32_t ed = 0, ep = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const pk16 d0 = o2[q] - dc2, d1 = o2[q] - __builtin_bit_cast(pk16, pl2[q]);
+            ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+            ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            ed += __shfl_xor(ed, o, 64);
+            ep += __shfl_xor(ep, o, 64);
+        }
+        use_dc[p] = ed <= ep;   // DC wins ties (__main__.py:173)
+        // residual (intra.py:65-67) + 1536 as f16 bits: 0x6600 + n for |n| < 512
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const pk16 rr = o2[q] - (use_dc[p] ? dc2 : __builtin_bit_cast(pk16, pl2[q]));
+            hx[p][q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, rr) + (pku16){0x6600, 0x6600});
+        }
+    }
+    // pass 1 (transform.py:179-185): the 1536 offset leaves with the rounding bias b1 of row 0
+    const float b1 = r == 0 ? 0.5f - 3072.0f : 0.5f;
+    f16x_t acc[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        acc[p] = splat16(initb(b1));
+        acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+            __builtin_bit_cast(h8_t, make_uint4(hx[p][0], hx[p][1], hx[p][2], hx[p][3])), bq_t(bs, r, hh, 0), acc[p], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+        acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+            __builtin_bit_cast(h8_t, make_uint4(hx[p][4], hx[p][5], hx[p][6], hx[p][7])), bq_t(bs, r, hh, 1), acc[p], 0, 0, 0);
+    // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
+    f16x_t acc2[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        acc2[p] = splat16(initb(0.5f));
+        acc2[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 0), acc_h8(acc[p], 0, b1), acc2[p], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+        acc2[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 1), acc_h8(acc[p], 1, b1), acc2[p], 0, 0, 0);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) mfma_result_ready(acc2[p]);   // before shift_rnd's inline-asm reads
+    // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        uint16_t* qt = qt2 + p * (32 * kQH);
+        int32_t* lrow = pp.lvl[p] + (int64_t)(y0c + r) * a.pitch + x0c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int32_t L4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int g = 4 * q + e;
+                L4[e] = quant_s(shift_rnd(acc2[p][g]), cq.qs, cq.h_v, cq.hneg_v);
+                qt[crow(g, hh) * kQH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
+            }
+            *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+        }
+    }
+    pair_sync();
+    // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
+    f16x_t acc3[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const uint16_t* qt = qt2 + p * (32 * kQH);
+        acc3[p] = splat16(initb(0.5f));
+        acc3[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * kQH + 8 * hh), bq_tt(bs, r, hh, 0), acc3[p], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const uint16_t* qt = qt2 + p * (32 * kQH);
+        acc3[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * kQH + 16 + 8 * hh), bq_tt(bs, r, hh, 1), acc3[p],
+                                                         0, 0, 0);
+    }
+    // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
+    f16x_t acc4[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        acc4[p] = splat16(initb(0.5f));
+        acc4[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 0), acc_h8(acc3[p], 0, 0.5f), acc4[p], 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+        acc4[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 1), acc_h8(acc3[p], 1, 0.5f), acc4[p], 0, 0, 0);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) mfma_result_ready(acc4[p]);
+    // reconstruct + clip (intra.py:70-78), row y = r; the bottom row and the right column into rc
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        int16_t (*rc)[33] = rc2[p];
+        int16_t* rrow = pp.rec[p] + (int64_t)(y0c + r) * a.pitch + x0c;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int32_t R4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int x = 8 * q + 4 * hh + e;
+                const int32_t pr = use_dc[p] ? dc[p]
+                                             : ((31 - x) * leftr[p] + (x + 1) * tr[p] + (31 - r) * (int32_t)rc[0][1 + x] +
+                                                (r + 1) * bl[p] + 32) >> 6;
+                const int32_t v = pr + shift_rnd(acc4[p][4 * q + e]);
+                R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
+                if (r == 31) rc[32][1 + x] = (int16_t)R4[e];
+            }
+            if (q == 3 && hh == 1) rc[1 + r][32] = (int16_t)R4[3];
+            *(uint2*)(rrow + 8 * q + 4 * hh) =
+                make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
+        }
+        const int w4 = a.w / 4;   // the TU map: 8 x 8 units of log2 size 5
+        pp.tu[p][(int64_t)(y0c / 4 + (l >> 3)) * w4 + x0c / 4 + (l & 7)] = (uint8_t)5;
+    }
+    pair_sync();
+}
+
 // The TU schedule of one CTU of one plane id (k_closed4_plan, NH_CLOSED4_PLAN):
 // the quadtree and so the dataflow rounds depend on (plane id, CTU) only, not
 // on the frame, so they are found once per launch instead of once per CTU row of
@@ -1749,12 +1929,15 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // pair's CTU row above, claimed before it.
 // The compiler's allocation (135 VGPRs, 3 waves/SIMD): 0.150 ms per 4K YUV420
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
-constexpr int kPairWaves = 1;
+constexpr int kPairWaves = 3;
 template <int WAVES>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
-    __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * TP];
+    // the packed chains' int16 tiles (2 x 32 rows of TP) or closed_chain32_h's f16 transpose tiles (2 x 32 x kQH)
+    __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * kQH];
+    __shared__ __attribute__((aligned(16))) BasisH basis_s;
+    static_assert(32 * TP <= 32 * kQH, "tile layout");
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
 #endif
@@ -1764,6 +1947,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // the critical (luma) wavefront issues first
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
+    if (a.mfma32) {   // closed_chain32_h's bases: 4 KB, once per workgroup
+        const uint4* s4 = (const uint4*)&c_basis_h_cl;
+        for (int i = lane; i < (int)(sizeof(BasisH) / 16); i += 64) ((uint4*)&basis_s)[i] = s4[i];
+        pair_sync();
+    }
     ChainQ cq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
@@ -1861,7 +2049,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
                             tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q);
-                        case 0: NH_PLAN_BATCH(32, false, cq[3]) break;
+                        case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
+                            if (a.mfma32) {
+                                if (NH_CLOSED4_MFMA_FUSED && two) {
+                                    closed_chain32_h<2>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
+                                } else {   // one plane after the other (fewer live accumulators)
+                                    closed_chain32_h<1>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
+                                    if (two) {
+                                        PairPlanes p1;
+                                        p1.src[0] = pp.src[1];
+                                        p1.lvl[0] = pp.lvl[1];
+                                        p1.rec[0] = pp.rec[1];
+                                        p1.tu[0] = pp.tu[1];
+                                        closed_chain32_h<1>(a, p1, x0c, y0c, rc + 1, (uint16_t*)t16 + 32 * kQH, basis_s,
+                                                            cq[3]);
+                                    }
+                                }
+                            } else {
+                                NH_PLAN_BATCH(32, false, cq[3])
+                            }
+                            break;
                         case 1: NH_PLAN_BATCH(16, false, cq[2]) break;
                         case 2: NH_PLAN_BATCH(8, false, cq[1]) break;
                         default:
@@ -2167,6 +2374,20 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     a.dqs = dequant_scale(rem);
     a.dq_per = per;
     a.probe = NH_KNOB("NH_CLOSED4_PROBE", 0);
+    // 32x32 luma TUs on the f16 matrix cores (closed_chain32_h): 16-B level and 8-B recon row pieces;
+    // A/B build: NH_CLOSED4_MFMA32 = 0 keeps them on the packed butterfly chain
+    static const int mfma32 = NH_KNOB("NH_CLOSED4_MFMA32", 1);
+    a.mfma32 = mfma32 && ctb == 32 && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
+               !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 7);
+    if (a.mfma32) {
+        static PerDeviceOnce once;
+        const int rcb = once.run([] {
+            const BasisH bh = make_basis_h();
+            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_h_cl), &bh, sizeof(bh)));
+            return (int)NH_OK;
+        });
+        if (rcb) return rcb;
+    }
     const int64_t rows = (int64_t)a.crows * np;
     // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x 2 waves/SIMD)
     const int64_t cap = 2048;

@@ -114,6 +114,38 @@ def test_torch_work_not_blocked(nh):
     assert dt < 5.0, dt      # 50 rounds; each waits at most one idle time
 
 
+def test_device_sync_after_calls_waits_at_most_the_idle_time(nh):
+    """a device-wide synchronize right after per-block calls waits
+    for the resident server's idle exit -- bounded by the idle time (100 us by
+    default), and not at all after block_server_stop()."""
+    import statistics
+    import torch
+    from nano_hevc import gpu
+    idle_us = gpu.block_server_stats()["idle_us"]
+    assert 0 < idle_us <= 100
+    rng = np.random.default_rng(4)
+    o = rng.integers(0, 256, (8, 8)).astype(np.int16)
+    p = rng.integers(0, 256, (8, 8)).astype(np.int16)
+    torch.cuda.synchronize()
+    base, after, stopped = [], [], []
+    for _ in range(40):
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()                 # nothing resident: the bare cost of the call
+        base.append(time.perf_counter() - t0)
+        nh.residual_block(o, p)
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()                 # waits for the server's idle exit
+        after.append(time.perf_counter() - t0)
+        nh.residual_block(o, p)
+        gpu.block_server_stop()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        stopped.append(time.perf_counter() - t0)
+    b, a, s = (statistics.median(v) * 1e6 for v in (base, after, stopped))
+    assert a - b < idle_us + 150, (b, a, s)     # the idle time + a PCIe poll round, no more
+    assert s - b < 100, (b, a, s)
+
+
 def test_threads_share_the_server(nh):
     errs = []
 

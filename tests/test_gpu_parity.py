@@ -942,7 +942,7 @@ def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
 
 
 @pytest.mark.parametrize("conc", [False, True])
-@pytest.mark.parametrize("F,W,H,qp", [(1, 104, 72, 32), (2, 136, 104, 22), (3, 104, 72, 32), (5, 72, 40, 0),
+@pytest.mark.parametrize("F,W,H,qp", [(1, 104, 72, 32), (2, 136, 104, 22), (3, 104, 72, 32), (5, 72, 40, 0), (2, 136, 104, 4),
                                       (4, 136, 104, 51)])
 def test_tu_pipeline_closed_pairs_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
     """8-bit YUV420 streams in closed loop: the plane-pair form (one wave codes

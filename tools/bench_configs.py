@@ -84,13 +84,17 @@ def valu_roofline(key, ms_per_frame):
     v = json.load(open(p)).get("configs", {}).get(key)
     if not v:
         return None
+    sys.path.insert(0, ROOT)
+    from bench import valu_sources_match
+    stale = not valu_sources_match(v)
     ks = [k for k in v["kernels"].values() if k.get("valu_per_frame") and k.get("attainable_valu_winst_per_s")]
     instr = sum(k["valu_per_frame"] for k in ks)
     peak = instr / sum(k["valu_per_frame"] / k["attainable_valu_winst_per_s"] for k in ks) / 1e9
     achieved = instr / (ms_per_frame * 1e-3) / 1e9
     return {"bound": "valu", "achieved": achieved, "peak": peak, "unit": "G VALU wave-instr/s",
             "frac": achieved / peak, "valu_instr_per_frame": instr,
-            "profile_kernel_frac": v.get("valu_frac"), "profile_tag": _profile_tag(json.load(open(p)), key)}
+            "profile_kernel_frac": v.get("valu_frac"), "profile_tag": _profile_tag(json.load(open(p)), key),
+            "peak_kind": v.get("peak_kind"), "valu_profile_stale": stale}
 
 
 def _profile_tag(d, key):

@@ -50,6 +50,26 @@ CONFIGS = {
     "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair", 2 / 64),
     "5b": ("cfg5_8k_yuv420", "k_tc32_h<1", 2 / 8),
 }
+# the sources a config's kernels are compiled from: their digest goes into the
+# entry, and bench.py / tools/bench_configs.py recompute it to tell whether the
+# committed instruction counts still describe the build they run
+_HDRS = ["nh_common.hpp", "nh_internal.hpp", "nh_packed.hpp", "nh_tree.hpp", "nh_mfma.hpp", "nh_f16mma.hpp"]
+SOURCES = {
+    "3": ["nh_intraloop.hip"] + _HDRS,
+    "closed": ["nh_intraloop.hip"] + _HDRS,
+    "4b": ["nh_ctu.hip"] + _HDRS,
+    "closed4": ["nh_intraloop.hip"] + _HDRS,
+    "5b": ["nh_ctu.hip", "nh_tc32.hip"] + _HDRS,
+}
+
+
+def sources_digest(files):
+    """sha256 over the listed nano-hevc_amd/csrc files, in order (bench.py: same rule)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in files:
+        h.update(open(os.path.join(ROOT, "nano-hevc_amd", "csrc", f), "rb").read())
+    return h.hexdigest()
 
 
 def _find(d, pattern):
@@ -116,12 +136,22 @@ def main():
     ap.add_argument("--dir", default=os.path.join(ROOT, "gpurun_out"))
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "valu_roofline.json"))
     ap.add_argument("--configs", default=",".join(CONFIGS))
+    ap.add_argument("--cal", default=None, help="tag of the tools/ab/_pmc_cal passes (pmc_cal3_<tag>, pmc_cal4_<tag>, "
+                                                "pmc_cal_<tag>.log in --cal-dir): dynamic mix from valu_pmc3/4")
+    ap.add_argument("--cal-dir", default=None)
     ap.add_argument("--merge", action="store_true",
                     help="keep the other configs of an existing --out file (per-config tags)")
     a = ap.parse_args()
     rates_path = os.path.join(a.dir, f"valu_rate_{a.tag}.jsonl")
     rates = [json.loads(x) for x in open(rates_path) if x.startswith("{")]
     mix = static_mix(rates_path)
+    dyn = None
+    if a.cal:
+        import valu_dyn
+        cd = a.cal_dir or a.dir
+        valu_dyn.load_membership(os.path.join(cd, f"pmc_cal3_{a.cal}"), os.path.join(cd, f"pmc_cal4_{a.cal}"),
+                                 os.path.join(cd, f"pmc_cal_{a.cal}.log"))
+        dyn = valu_dyn
     res = {"tag": a.tag, "rates_chip_winst_per_s": {r["op"]: r["chip_winst_per_s"] for r in rates},
            "method": "achieved = SQ_INSTS_VALU per dispatch / kernel-trace average duration; attainable = static "
                      "VALU mix (tools/valu_mix.py) priced at the measured per-opcode rates (tools/ab/valu_rate.hip)",
@@ -136,7 +166,7 @@ def main():
             continue
         f_pmc = next(v["_dispatches"] for k, v in c1.items() if anchor in k) / anchor_pf
         f_kt = next(v["calls"] for k, v in times.items() if anchor in k) / anchor_pf
-        kernels, instr, t_att, t_ms = {}, 0.0, 0.0, 0.0
+        kernels, instr, t_att, t_ms, t_lo = {}, 0.0, 0.0, 0.0, 0.0
         for name in sorted(set(times) | set(c1)):
             t, p, q, m = times.get(name), c1.get(name, {}), c2.get(name, {}), mix.get(name)
             e = {"calls_traced": t["calls"] if t else 0, "avg_ms": t["avg_ns"] / 1e6 if t else None,
@@ -178,6 +208,27 @@ def main():
                 e["ms_per_frame"] = t["avg_ns"] * t["calls"] / f_kt / 1e6
                 t_ms += e["ms_per_frame"]
             kernels[name] = e
+        if dyn is not None:   # the dynamic mix: LP bounds per kernel from the instruction counters (valu_dyn)
+            d3, d4 = (os.path.join(a.dir, f"valu_pmc{i}_{a.tag}_{c}") for i in (3, 4))
+            dr = dyn.run_config([d3, d4], rates_path)
+            t_att = 0.0
+            for name, e in kernels.items():
+                r = dr.get(name)
+                if not r or not r.get("feasible") or not e.get("valu_per_frame"):
+                    continue
+                e["attainable_dynamic_lo"] = r["attainable_lo"]
+                e["attainable_dynamic_hi"] = r["attainable_hi"]
+                e["attainable_static"] = e.get("attainable_valu_winst_per_s")
+                e["attainable_valu_winst_per_s"] = r["attainable_hi"]   # the peak: the most the executed mix allows
+                e["valu_priced_measured_frac"] = r.get("valu_priced_measured_frac")
+                if e.get("achieved_valu_winst_per_s"):
+                    e["valu_frac"] = e["achieved_valu_winst_per_s"] / r["attainable_hi"]
+                    e["valu_frac_range"] = [e["achieved_valu_winst_per_s"] / r["attainable_hi"],
+                                            e["achieved_valu_winst_per_s"] / r["attainable_lo"]]
+            t_att = sum(e["valu_per_frame"] / e["attainable_valu_winst_per_s"] for e in kernels.values()
+                        if e.get("valu_per_frame") and e.get("attainable_valu_winst_per_s"))
+            t_lo = sum(e["valu_per_frame"] / e["attainable_dynamic_lo"] for e in kernels.values()
+                       if e.get("valu_per_frame") and e.get("attainable_dynamic_lo"))
         busy = busy_ns(os.path.join(a.dir, f"valu_kt_{a.tag}_{c}"))
         busy_ms = busy / f_kt / 1e6 if busy else t_ms
         ent = {"kernels": kernels, "frames_counted": f_pmc, "frames_traced": f_kt,
@@ -189,6 +240,13 @@ def main():
             ent["achieved_valu_winst_per_s"] = instr / (busy_ms * 1e-3)
             ent["attainable_valu_winst_per_s"] = instr / t_att
             ent["valu_frac"] = ent["achieved_valu_winst_per_s"] / ent["attainable_valu_winst_per_s"]
+            if dyn is not None and t_lo:
+                ent["attainable_dynamic_range"] = [instr / t_lo, instr / t_att]
+                ent["valu_frac_range"] = [ent["valu_frac"], ent["achieved_valu_winst_per_s"] / (instr / t_lo)]
+                ent["peak_kind"] = "dynamic mix (LP upper bound, tools/valu_dyn.py)"
+            else:
+                ent["peak_kind"] = "static mix (tools/valu_mix.py)"
+        ent["sources"] = {"files": SOURCES[c], "sha256": sources_digest(SOURCES[c])}
         res["configs"][key] = ent
         print(f"{key:28s} frac {ent.get('valu_frac', float('nan')):.3f}  {busy_ms:.4f} ms/frame busy ({t_ms:.4f} kernel sum)  "
               f"VALU/frame {instr:.4g}", flush=True)

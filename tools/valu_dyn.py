@@ -338,6 +338,41 @@ def solve(blocks, meas, rates, tol=0.005):
     return {"feasible": True, "counters": used, "tol": tol, **res}
 
 
+_TEXT = None
+
+
+def _kernel_text():
+    global _TEXT
+    if _TEXT is None:
+        srcs = sorted(glob.glob(os.path.join(vm.CSRC, "*.hip")))
+        with tempfile.TemporaryDirectory() as tmp:
+            objs = vm.compile_objects(tmp, srcs)
+            text = {}
+            for o in objs:
+                text.update(kernels_text(o))
+        dm = vm.demangle(list(text))
+        _TEXT = {dm.get(s, s): text[s] for s in text}
+    return _TEXT
+
+
+def run_config(pmc_dirs, rates_path, tol=0.005):
+    """{demangled kernel: LP result} for one config's counter directories."""
+    rates = load_rates(rates_path)
+    meas = load_counters(pmc_dirs)
+    text = _kernel_text()
+    out = {}
+    for kname, m in meas.items():
+        if kname not in text or not m.get("SQ_WAVES") or not m.get("SQ_INSTS_VALU"):
+            continue
+        r = solve(build_cfg(text[kname]), m, rates, tol)
+        if r["feasible"]:
+            r["attainable_lo"] = m["SQ_INSTS_VALU"] / r["max"]["T_s"]
+            r["attainable_hi"] = m["SQ_INSTS_VALU"] / r["min"]["T_s"]
+            r["valu_priced_measured_frac"] = r["min"]["valu_priced_measured"] / max(1.0, r["min"]["valu"])
+        out[kname] = r
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rates", required=True)
