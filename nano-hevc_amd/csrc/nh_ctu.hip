@@ -142,8 +142,7 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
     const int32_t bl = img[N * IP - 1];           // left[-1]
     // DC (intra.py:46-62): sum over the TU's N lanes
     int32_t sum = topt + leftt;
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    sum = grp_sum<N>(sum);
     const int32_t dc = (sum + N) >> (L2 + 1);
     // planar (intra.py:81-113) for column t: num(i) = (N-1-t) left[i] + (t+1) tr + (N-1-i) top[t] + (i+1) bl + N
     int32_t pl[N];
@@ -162,11 +161,8 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
         ed += sq2(sext16(o[i] - dc), sext16(o[i + 1] - dc));
         ep += sq2(sext16(o[i] - pl[i]), sext16(o[i + 1] - pl[i + 1]));
     }
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) {
-        ed += __shfl_xor(ed, m, 64);
-        ep += __shfl_xor(ep, m, 64);
-    }
+    ed = grp_sum<N>(ed);
+    ep = grp_sum<N>(ep);
     const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
     uint32_t v[N], r[N];
     // forward pass 1 (transform.py:179-185) on column t of the residual
@@ -265,8 +261,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
     const int32_t tr = img[N - 1];                // top[-1]  (__main__.py:168)
     const int32_t bl = img[N * IP - 1];           // left[-1]
     int32_t sum = topt + leftt;                   // DC (intra.py:46-62)
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    sum = grp_sum<N>(sum);
     const int32_t dc = (sum + N) >> (L2 + 1);
     const pk16 dc2 = pk_splat(dc);
     // column t: source rows (2m, 2m+1) and planar (intra.py:81-113)
@@ -294,11 +289,8 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) {
-        ed += __shfl_xor(ed, m, 64);
-        ep += __shfl_xor(ep, m, 64);
-    }
+    ed = grp_sum<N>(ed);
+    ep = grp_sum<N>(ep);
     const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
     pk16 r2[H];
 #pragma unroll
@@ -387,8 +379,7 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
     const int l = opaque_lane(), r = l & 31, hh = l >> 5;
     const int32_t my_nb = hh == 0 ? img[r] : img[(1 + r) * IP - 1];
     int32_t s = my_nb;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = grp_sum<64>(s);
     const int32_t dc = (s + 32) >> 6;
     const int32_t tr = img[31], bl = img[32 * IP - 1];
     auto planar = [&](int y, int x) -> int32_t {
@@ -403,11 +394,8 @@ __device__ __forceinline__ void ctu_chain32(const CtuArgs& a, const int16_t* img
         e_dc += sq2(sext16(o0 - dc), sext16(o1 - dc));
         e_pl += sq2(sext16(o0 - planar(k, r)), sext16(o1 - planar(k + 1, r)));
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        e_dc += __shfl_xor(e_dc, o, 64);
-        e_pl += __shfl_xor(e_pl, o, 64);
-    }
+    e_dc = grp_sum<64>(e_dc);
+    e_pl = grp_sum<64>(e_pl);
     const bool use_dc = e_dc <= e_pl;   // DC wins ties (__main__.py:173)
     int32_t X[16];
 #pragma unroll
@@ -489,19 +477,37 @@ __device__ __forceinline__ void copy_basis_h(BasisH& dst) {
 // rows -- 8 rows of 128 B (levels), 16 rows of 64 B (recon) -- instead of 32-B
 // / 16-B pieces of 32 rows.
 constexpr int kOutP = 36, kRecP = 24;   // int32 per row: level tile, recon tile (48 halves; 16-B rows)
-template <bool TSTORE = false, class B = BasisH>
-__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* img, uint16_t* qt, const B& bs,
+// The block image a chain reads: sample (y, x) for y, x in [0, 32), the row
+// above (top, y = -1) and the column to the left (left, x = -1).  ImgStrip: a
+// CTB-32 strip image (img[r * IP + c] = sample (r - 1, c), c = -1 the left
+// column); ImgDma: the LDS-DMA image of k_tc32_hd (the block body in 64-B rows,
+// the top row and left column side by side in a 64-sample edge array).
+struct ImgStrip {
+    const int16_t* p;
+    static constexpr int IP = Strip<32>::IP;
+    __device__ __forceinline__ int32_t at(int y, int x) const { return p[(1 + y) * IP + x]; }
+    __device__ __forceinline__ int32_t top(int x) const { return p[x]; }
+    __device__ __forceinline__ int32_t left(int y) const { return p[(1 + y) * IP - 1]; }
+};
+struct ImgDma {
+    const int16_t* body;   // [y][x], 32 x 32
+    const int16_t* edge;   // [0, 32): top[x]; [32, 96): left[y] at 32 + 2y (the 16-bit LDS-DMA writes a dword per lane)
+    __device__ __forceinline__ int32_t at(int y, int x) const { return body[y * 32 + x]; }
+    __device__ __forceinline__ int32_t top(int x) const { return edge[x]; }
+    __device__ __forceinline__ int32_t left(int y) const { return edge[32 + 2 * y]; }
+};
+template <bool TSTORE = false, class B = BasisH, class IMG = ImgStrip>
+__device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, uint16_t* qt, const B& bs,
                                               int gx0, int gy0,
                                               int32_t* __restrict__ lvl, int16_t* __restrict__ rec,
                                               int32_t* ot = nullptr, int64_t opitch = -1) {
     const int64_t op = opitch >= 0 ? opitch : (int64_t)a.pitch;   // row pitch of lvl / rec (an LDS image's: OST)
-    constexpr int IP = Strip<32>::IP, QH = Strip<32>::QH;   // img[r * IP + c]: sample (r - 1, c), c = -1: left
+    constexpr int QH = Strip<32>::QH;
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
     const int l = opaque_lane(), r = l & 31, hh = l >> 5;
-    const int32_t topr = img[r], leftr = img[(1 + r) * IP - 1], tr = img[31], bl = img[32 * IP - 1];
+    const int32_t topr = img.top(r), leftr = img.left(r), tr = img.top(31), bl = img.left(31);
     int32_t sdc = hh ? leftr : topr;   // DC (intra.py:46-62): lane halves hold top / left
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) sdc += __shfl_xor(sdc, o, 64);
+    sdc = grp_sum<64>(sdc);
     const int32_t dc = (sdc + 32) >> 6;
     const pk16 dc2 = pk_splat(dc);
     // column x = r, rows y = 8hh + 16c + j (the pass-1 A operand), as row pairs p = 4c + q
@@ -512,10 +518,10 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
             const int y = 8 * hh + 16 * (p >> 2) + 2 * (p & 3);
-            o2[p] = pk_pair(img[(1 + y) * IP + r], img[(2 + y) * IP + r]);
+            o2[p] = pk_pair(img.at(y, r), img.at(y + 1, r));
             const int32_t b = (r + 1) * tr + (31 - y) * topr + (y + 1) * bl + 32;   // planar, intra.py:81-113
             const pku16 bs = {(unsigned short)b, (unsigned short)(b + bl - topr)};
-            const pku16 lf = {(unsigned short)img[(1 + y) * IP - 1], (unsigned short)img[(2 + y) * IP - 1]};
+            const pku16 lf = {(unsigned short)img.left(y), (unsigned short)img.left(y + 1)};
             pl2[p] = (lf * wl + bs) >> sh;
         }
     }
@@ -526,11 +532,8 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        ed += __shfl_xor(ed, o, 64);
-        ep += __shfl_xor(ep, o, 64);
-    }
+    ed = grp_sum<64>(ed);
+    ep = grp_sum<64>(ep);
     const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
     // residual (intra.py:65-67) + 1536 as f16 bits: 0x6600 + n for |n| < 512
     uint32_t hx[8];
@@ -595,7 +598,7 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const int16_t* i
         for (int e = 0; e < 4; ++e) {
             const int x = 8 * q + 4 * hh + e;
             const int32_t p = use_dc ? dc
-                                     : ((31 - x) * leftr + (x + 1) * tr + (31 - r) * (int32_t)img[x] + (r + 1) * bl + 32) >> 6;
+                                     : ((31 - x) * leftr + (x + 1) * tr + (31 - r) * img.top(x) + (r + 1) * bl + 32) >> 6;
             const int32_t v = p + shift_rnd(acc4[4 * q + e]);
             R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
         }
@@ -914,10 +917,10 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
                 if constexpr (NARROW && MFMA32) {   // one TU per wave on the f16 matrix cores
                     const int e = sm.list[3][item], sw = e >> 6;
                     if constexpr (OST)
-                        ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.basis, 0, 0,
+                        ctu_chain32_h(a, ImgStrip{sm.img + sw * G::IMG + 4}, (uint16_t*)sm.tile + sw * G::T16, sm.basis, 0, 0,
                                       sm.olvl + sw * (CTB * G::SW), sm.orec + sw * (CTB * G::SW), nullptr, G::SW);
                     else
-                        ctu_chain32_h(a, sm.img + sw * G::IMG + 4, (uint16_t*)sm.tile + sw * G::T16, sm.basis,
+                        ctu_chain32_h(a, ImgStrip{sm.img + sw * G::IMG + 4}, (uint16_t*)sm.tile + sw * G::T16, sm.basis,
                                       sm.org[2 * sw], sm.org[2 * sw + 1], lvl, rec);
                 } else if constexpr (MFMA32) {   // one TU per wave on the int8 matrix cores (A/B form)
                     const int e = sm.list[3][item], sw = e >> 6;
@@ -1094,10 +1097,10 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
             }
         } else {
             if constexpr (BREG)
-                ctu_chain32_h<TSTORE>(a, s_img[wv] + 4, s_q[wv], breg, sx0, sy0, a.lvl + poff, a.rec + poff,
+                ctu_chain32_h<TSTORE>(a, ImgStrip{s_img[wv] + 4}, s_q[wv], breg, sx0, sy0, a.lvl + poff, a.rec + poff,
                                       TSTORE ? s_out[TSTORE ? wv : 0] : nullptr);
             else
-                ctu_chain32_h<TSTORE>(a, s_img[wv] + 4, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff,
+                ctu_chain32_h<TSTORE>(a, ImgStrip{s_img[wv] + 4}, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff,
                                       TSTORE ? s_out[TSTORE ? wv : 0] : nullptr);
         }
         wave_sync();   // this wave's LDS reads of block k before block k+1's image writes
@@ -1106,6 +1109,113 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
 
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, hipStream_t s);
+
+// LDS-DMA (global_load_lds_*): each active lane's bytes from gsrc land at the
+// LDS byte address lds + lane * 16 for dwordx4, lds + lane * 4 for ushort (one
+// zero-extended dword per lane; tools/ab/lds_dma_probe.hip); the LDS base travels in M0, which the
+// compiler reserves, so it is saved and restored in the same statement.  As
+// inline asm the load is invisible to the compiler's waitcnt bookkeeping: the
+// caller retires it with an explicit vmcnt (wait_vm) -- the compiler's own
+// counts are only made more conservative by it (in-order completion).
+typedef __attribute__((address_space(3))) void lds_void_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void_t*)(p); }
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+__device__ __forceinline__ void glds2(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+
+// Config 5, 8-bit blocks, with the next block's image loaded under this one's
+// chain: a wave codes KB consecutive blocks; block k+1's
+// body (two 1-KiB LDS-DMA pieces: 16 B per lane, rows of 64 B), its top row and
+// its left column land in the wave's other LDS slot by LDS-DMA while block k
+// runs -- no registers hold them.  Before block k+1 reads its slot the wave
+// waits with vmcnt(4 + the stores block k issued): the loads complete in issue
+// order, so that retires exactly block k+1's DMA and leaves the next block's in
+// flight; `lgkmcnt(0)` before a DMA is issued retires the wave's reads of the
+// slot it overwrites.  At the frame's top / left edge the DMA reads the block's
+// own row / column and the 128s of block.py:41-48 overwrite it after the wait.
+// Same chain (ctu_chain32_h over an ImgDma image), same marks for wide blocks.
+constexpr int kTc32hdStoresNarrow = 6;   // ctu_chain32_h<TSTORE>: 4 level-row + 2 recon-row store instructions
+template <int KB>
+__global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
+    __shared__ __attribute__((aligned(16))) int16_t s_body[4][2][32 * 32];
+    __shared__ __attribute__((aligned(16))) int16_t s_edge[4][2][96];
+    __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * Strip<32>::QH];
+    __shared__ BasisH s_basis;
+    __shared__ __attribute__((aligned(16))) int32_t s_out[4][32 * kOutP];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b0 = ((int)blockIdx.x * 4 + wv) * KB, pz = (int)blockIdx.y;
+    const int64_t poff = plane_off(a, pz);
+    const int16_t* src = a.src + poff;
+    copy_basis_h(s_basis);
+    __syncthreads();   // (before any DMA is in flight)
+    if (b0 >= nblk) return;   // whole wave
+    auto issue = [&](int b, int slot) {   // 4 DMA instructions per block
+        const int sx0 = (b % a.strips_x) * 32, sy0 = (b / a.strips_x) * 32;
+        const int16_t* blk = src + (int64_t)sy0 * a.pitch + sx0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+            glds16(blk + (int64_t)((lane >> 2) + 16 * i) * a.pitch + 8 * (lane & 3), lds_addr(&s_body[wv][slot][512 * i]));
+        if (lane < 4) glds16(blk - (sy0 > 0 ? (int64_t)a.pitch : 0) + 8 * lane, lds_addr(&s_edge[wv][slot][0]));
+        if (lane < 32) glds2(blk + (int64_t)lane * a.pitch - (sx0 > 0 ? 1 : 0), lds_addr(&s_edge[wv][slot][32]));
+    };
+    issue(b0, 0);
+    int prev = 0;   // store instructions the previous block issued (0: none, 1: a wide mark, 6: a chain)
+    for (int k = 0; k < KB; ++k) {
+        const int b = b0 + k;
+        if (b >= nblk) break;
+        const int slot = k & 1;
+        const bool next = k + 1 < KB && b + 1 < nblk;
+        if (next) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // WAR on the slot block k+1 overwrites
+            issue(b + 1, slot ^ 1);
+        }
+        // retire block b's DMA: it was issued before the previous block's stores and block b+1's DMA
+        if (next) {
+            if (prev == kTc32hdStoresNarrow) wait_vm<4 + kTc32hdStoresNarrow>();
+            else if (prev == 1) wait_vm<5>();
+            else wait_vm<4>();
+        } else {
+            if (prev == kTc32hdStoresNarrow) wait_vm<kTc32hdStoresNarrow>();
+            else if (prev == 1) wait_vm<1>();
+            else wait_vm<0>();
+        }
+        const int sx0 = (b % a.strips_x) * 32, sy0 = (b / a.strips_x) * 32;
+        const int16_t* body = s_body[wv][slot];
+        int16_t* edge = s_edge[wv][slot];
+        if (sy0 == 0 && lane < 32) edge[lane] = 128;        // above the frame (block.py:41)
+        if (sx0 == 0 && lane < 32) edge[32 + 2 * lane] = 128;   // left of the frame (block.py:48)
+        wave_sync();
+        uint32_t hi;   // any sample of the block, its top row or its left column outside [0, 255]?
+        {
+            const uint4 v0 = ((const uint4*)body)[lane], v1 = ((const uint4*)body)[64 + lane];
+            hi = v0.x | v0.y | v0.z | v0.w | v1.x | v1.y | v1.z | v1.w;
+            if (lane < 48) hi |= ((const uint32_t*)edge)[lane];
+        }
+        const bool wide = __any((hi & 0xff00ff00u) != 0);
+        if (wide) {
+            if (lane == 0) {
+                a.rec[poff + (int64_t)sy0 * a.pitch + sx0] = kWideMark;
+                if (a.wide_flag) *a.wide_flag = a.epoch;   // the fix-up launch has work
+            }
+            prev = 1;
+        } else {
+            ctu_chain32_h<true>(a, ImgDma{body, edge}, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff, s_out[wv]);
+            prev = kTc32hdStoresNarrow;
+        }
+        wave_sync();
+    }
+}
+
+
 
 // The bases in constant memory, once per device.  hipMemcpyToSymbol is
 // host-synchronous, so every kernel queued afterwards -- on any stream -- reads
@@ -1292,6 +1402,15 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     auto launch = [&](auto kern, int K) {
         kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, cap), s>>>(a, nblk);
     };
+    // two blocks per wave, the second's image by LDS-DMA under the first's chain (k_tc32_hd<2>):
+    // 0.0966-0.0976 vs 0.0982-0.0983 ms per 8K YUV420 frame, 4 / 8 blocks per wave 0.102 / 0.107
+    // (profiles/r04/cfg5/ab_tc32hd_r04h.jsonl; A/B knob NH_TC32H_DMA = blocks per wave, 0 = k_tc32_h).
+    // Its 16-B DMA pieces need 16-B aligned rows; other layouts take k_tc32_h.
+    static const int dma = NH_KNOB("NH_TC32H_DMA", 2);
+    const bool dma_ok = !((S.pitch | S.base | S.plane_stride | S.group_stride) & 7) && !((uintptr_t)src & 15);
+    if (dma_ok && dma == 2) { launch(k_tc32_hd<2>, 2); NH_HIP(hipGetLastError()); return NH_OK; }
+    if (NH_AB && dma_ok && dma == 4) { launch(k_tc32_hd<4>, 4); NH_HIP(hipGetLastError()); return NH_OK; }
+    if (NH_AB && dma_ok && dma == 8) { launch(k_tc32_hd<8>, 8); NH_HIP(hipGetLastError()); return NH_OK; }
     if (NH_AB && kk == 2) launch(k_tc32_h<2, false, true>, 2);
     else if (NH_AB && kk == 4) launch(k_tc32_h<4, false, true>, 4);
 #if NH_AB

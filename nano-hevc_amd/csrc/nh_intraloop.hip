@@ -1127,9 +1127,11 @@ struct Closed4Args {
     const uint8_t* plan;    // k_tu_closed_pair: per-(plane of the group, CTU) TU schedules (k_closed4_plan)
     int32_t probe;          // A/B timing probes (k_tu_closed_pair; wrong outputs): 1 no wait on the row
                             // above, 2 no chains, 4 no rounds, 8 no recon-image clear, 16 no quadtree
-                            // hashes, 32 no source loads in the chains (0 in the product)
+                            // hashes, 32 no source loads in the chains, 64 no level / recon / TU-map
+                            // stores in the chains (0 in the product)
     int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_h); set
                             // for luma when the level / recon rows allow 16-B / 8-B stores
+    uint64_t* stamps;       // A/B build only (NH_CLOSED4_STAMPS): per (ticket, CTU) shader-clock stamps
 };
 __constant__ BasisH c_basis_h_cl;   // the f16 DCT32 bases of closed_chain32_h (copied to LDS per workgroup)
 
@@ -1156,8 +1158,7 @@ __device__ __forceinline__ void tu_closed_batch(const Closed4Args& a, const int1
     }
     // DC (intra.py:46-62): sum over the TU's N lanes
     int32_t sum = topt + leftt;
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    sum = grp_sum<N>(sum);
     const int32_t dc = (sum + N) >> (Log2<N>::v + 1);
     const int32_t tr = on ? rc[ly][lx + N] : 0, bl = on ? rc[ly + N][lx] : 0;   // top[-1], left[-1]
     auto planar = [&](int yy, int xx) -> int32_t {
@@ -1173,11 +1174,8 @@ __device__ __forceinline__ void tu_closed_batch(const Closed4Args& a, const int1
             ep += (long long)d2 * d2;
         }
     }
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) {
-        ed += __shfl_xor(ed, m, 64);
-        ep += __shfl_xor(ep, m, 64);
-    }
+    ed = grp_sum<N>(ed);
+    ep = grp_sum<N>(ep);
     const bool use_dc = ed <= ep;                        // __main__.py:173: DC wins ties
     auto pred_at = [&](int yy, int xx) -> int32_t { return use_dc ? dc : planar(yy, xx); };
     uint32_t v[N], r[N];
@@ -1266,8 +1264,7 @@ __device__ __forceinline__ void tu_closed_batch_pk(const Closed4Args& a, const i
     const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
     const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
     int32_t sum = topt + leftt;                                // DC (intra.py:46-62)
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    sum = grp_sum<N>(sum);
     const int32_t dc = (sum + N) >> (L2 + 1);
     const pk16 dc2 = pk_splat(dc);
     pk16 o2[H];
@@ -1294,11 +1291,8 @@ __device__ __forceinline__ void tu_closed_batch_pk(const Closed4Args& a, const i
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) {
-        ed += __shfl_xor(ed, m, 64);
-        ep += __shfl_xor(ep, m, 64);
-    }
+    ed = grp_sum<N>(ed);
+    ep = grp_sum<N>(ep);
     const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
     pk16 r2[H];
 #pragma unroll
@@ -1582,11 +1576,21 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     int16_t (*rc)[33] = rc2[p];
     const int16_t* src = p ? pp.src[1] : pp.src[0];
     int16_t* tl = t16 + p * (32 * TP) + ly * TP + lx;   // tl[line * TP + slot]
+    // the TU's source column, every load issued before any use: the waits for them then
+    // overlap the neighbour reads and the DC / planar sums, not one round trip per row pair
+    int32_t sv[N];
+    {
+        const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            sv[i] = (NH_AB && (a.probe & 32)) ? rc[ly + 1 + i][lx + 1 + t]   // A/B probe: no source loads
+                                              : sp[(int64_t)i * a.pitch];
+        __builtin_amdgcn_sched_barrier(0);
+    }
     const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
     const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
     int32_t sum = topt + leftt;                                // DC (intra.py:46-62)
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) sum += __shfl_xor(sum, m, 64);
+    sum = grp_sum<N>(sum);
     const int32_t dc = (sum + N) >> (L2 + 1);
     const pk16 dc2 = pk_splat(dc);
     pk16 o2[H];
@@ -1597,13 +1601,9 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         const pku16 st2 = {(unsigned short)(2 * st), (unsigned short)(2 * st)};
         const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)};
         const pku16 sh = {(unsigned short)(L2 + 1), (unsigned short)(L2 + 1)};
-        const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
 #pragma unroll
         for (int m = 0; m < H; ++m) {
-            if (NH_AB && (a.probe & 32))   // A/B timing probe: no source loads (wrong outputs)
-                o2[m] = pk_pair(rc[ly + 1 + 2 * m][lx + 1 + t], rc[ly + 2 + 2 * m][lx + 1 + t]);
-            else
-                o2[m] = pk_pair(sp[(2 * m) * a.pitch], sp[(2 * m + 1) * a.pitch]);
+            o2[m] = pk_pair(sv[2 * m], sv[2 * m + 1]);
             const pku16 lf = {(unsigned short)rc[ly + 1 + 2 * m][lx], (unsigned short)rc[ly + 2 + 2 * m][lx]};
             pl2[m] = (lf * wl + bs) >> sh;
             bs += st2;
@@ -1616,11 +1616,8 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) {
-        ed += __shfl_xor(ed, m, 64);
-        ep += __shfl_xor(ep, m, 64);
-    }
+    ed = grp_sum<N>(ed);
+    ep = grp_sum<N>(ep);
     const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
     pk16 r2[H];
 #pragma unroll
@@ -1645,7 +1642,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
 #pragma unroll
         for (int kk = 0; kk < N; ++kk) {
             const int32_t l = quant_s(yv[kk] >> S, cq.qs, cq.h_v, cq.hneg_v);
-            lrow[kk] = l;
+            if (!(NH_AB && (a.probe & 64))) lrow[kk] = l;
             tl[kk * TP + st] = (int16_t)dequant_s(l, cq);
         }
     }
@@ -1677,10 +1674,10 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
             const int32_t pr = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + kk] + b + kk * stv) >> (L2 + 1);
             int32_t q = pr + (xv[kk] >> S);
             q = q < 0 ? 0 : (q > 255 ? 255 : q);
-            rrow[kk] = (int16_t)q;
+            if (!(NH_AB && (a.probe & 64))) rrow[kk] = (int16_t)q;
             rc[ly + 1 + t][lx + 1 + kk] = (int16_t)q;   // no TU of this batch reads the TU's own samples
         }
-        if (t < N / 4) {
+        if (t < N / 4 && !(NH_AB && (a.probe & 64))) {
             uint8_t* tu = p ? pp.tu[1] : pp.tu[0];
             const int w4 = a.w / 4;
             for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
@@ -1713,6 +1710,21 @@ __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const Pai
     int32_t topr[NP], leftr[NP], tr[NP], bl[NP], dc[NP];
     bool use_dc[NP];
     uint32_t hx[NP][8];
+    // the TUs' source columns, every load issued before any use (one wait, not one per row pair)
+    int32_t sv[NP][16];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        const int16_t* sp = pp.src[p] + (int64_t)y0c * a.pitch + x0c + r;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
+#pragma unroll
+            for (int e = 0; e < 2; ++e)
+                sv[p][2 * q + e] = (NH_AB && (a.probe & 32)) ? rc2[p][1 + y + e][1 + r]   // A/B probe: no source loads
+                                                             : sp[(int64_t)(y + e) * a.pitch];
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         int16_t (*rc)[33] = rc2[p];
@@ -1721,11 +1733,9 @@ __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const Pai
         tr[p] = rc[0][32];
         bl[p] = rc[32][0];
         int32_t sdc = hh ? leftr[p] : topr[p];   // DC (intra.py:46-62): lane halves hold top / left
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sdc += __shfl_xor(sdc, o, 64);
+        sdc = grp_sum<64>(sdc);
         dc[p] = (sdc + 32) >> 6;
         const pk16 dc2 = pk_splat(dc[p]);
-        const int16_t* sp = pp.src[p] + (int64_t)y0c * a.pitch + x0c + r;
         // column x = r, rows y = 8hh + 16c + j (the pass-1 A operand), as row pairs q = 4c + j/2
         pk16 o2[8];
         pku16 pl2[8];
@@ -1733,10 +1743,7 @@ __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const Pai
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
             const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
-            if (NH_AB && (a.probe & 32))   // A/B timing probe: no source loads (wrong outputs)
-                o2[q] = pk_pair(rc[1 + y][1 + r], rc[2 + y][1 + r]);
-            else
-                o2[q] = pk_pair(sp[(int64_t)y * a.pitch], sp[(int64_t)(y + 1) * a.pitch]);
+            o2[q] = pk_pair(sv[p][2 * q], sv[p][2 * q + 1]);
             const int32_t b = (r + 1) * tr[p] + (31 - y) * topr[p] + (y + 1) * bl[p] + 32;   // planar, intra.py:81-113
             const pku16 bsv = {(unsigned short)b, (unsigned short)(b + bl[p] - topr[p])};
             const pku16 lf = {(unsigned short)rc[1 + y][0], (unsigned short)rc[2 + y][0]};
@@ -1749,11 +1756,8 @@ __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const Pai
             ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
             ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            ed += __shfl_xor(ed, o, 64);
-            ep += __shfl_xor(ep, o, 64);
-        }
+        ed = grp_sum<64>(ed);
+        ep = grp_sum<64>(ep);
         use_dc[p] = ed <= ep;   // DC wins ties (__main__.py:173)
         // residual (intra.py:65-67) + 1536 as f16 bits: 0x6600 + n for |n| < 512
 #pragma unroll
@@ -1801,7 +1805,7 @@ __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const Pai
                 L4[e] = quant_s(shift_rnd(acc2[p][g]), cq.qs, cq.h_v, cq.hneg_v);
                 qt[crow(g, hh) * kQH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
             }
-            *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+            if (!(NH_AB && (a.probe & 64))) *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
         }
     }
     pair_sync();
@@ -1850,11 +1854,12 @@ __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const Pai
                 if (r == 31) rc[32][1 + x] = (int16_t)R4[e];
             }
             if (q == 3 && hh == 1) rc[1 + r][32] = (int16_t)R4[3];
-            *(uint2*)(rrow + 8 * q + 4 * hh) =
-                make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
+            if (!(NH_AB && (a.probe & 64)))
+                *(uint2*)(rrow + 8 * q + 4 * hh) =
+                    make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
         }
         const int w4 = a.w / 4;   // the TU map: 8 x 8 units of log2 size 5
-        pp.tu[p][(int64_t)(y0c / 4 + (l >> 3)) * w4 + x0c / 4 + (l & 7)] = (uint8_t)5;
+        if (!(NH_AB && (a.probe & 64))) pp.tu[p][(int64_t)(y0c / 4 + (l >> 3)) * w4 + x0c / 4 + (l & 7)] = (uint8_t)5;
     }
     pair_sync();
 }
@@ -1930,6 +1935,7 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // The compiler's allocation (135 VGPRs, 3 waves/SIMD): 0.150 ms per 4K YUV420
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
 constexpr int kPairWaves = 3;
+constexpr int kStampWords = 16;   // A/B stamps per (ticket, CTU)
 template <int WAVES>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
@@ -1998,6 +2004,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
         for (int cx = 0; cx < a.ccols; ++cx) {
             const int x0c = cx * ctb;
             const int nw = (min(ctb, a.w - x0c) + 1) / 2;
+            uint64_t st0 = 0, st1 = 0, st2 = 0;   // A/B stamps: CTU start, poll done, rounds done
+            if (NH_AB && a.stamps) st0 = __builtin_amdgcn_s_memtime();
             // this CTU's TU schedule (128 B), loaded under the wait on the row above
             uint32_t planw = 0;
             if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) planw = plan_row[cx * (kPlanBytes / 4) + lane];
@@ -2033,6 +2041,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) ((uint32_t*)ent_s)[lane] = planw;
             pair_sync();
             if (stall_s) break;
+            if (NH_AB && a.stamps) st1 = __builtin_amdgcn_s_memtime();
 #if NH_CLOSED4_PLAN
             {   // the CTU's TUs in dataflow rounds, from the schedule: lane rs holds the count of
                 // (round rs / 4, size index rs % 4); batches run in the schedule's order
@@ -2131,6 +2140,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 pair_sync();
             }
 #endif
+            if (NH_AB && a.stamps) st2 = __builtin_amdgcn_s_memtime();
             if (NH_CLOSED4_EARLYPOLL && cy > 0 && cx + 1 < a.ccols) {
                 const int nwn = (min(ctb, a.w - x0c - ctb) + 1) / 2;
                 if (hl < nwn && hq <= two) early = ld_sys64(line[hq] + (x0c + ctb) / 2 + hl);
@@ -2153,6 +2163,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             pair_sync();
             if (hl < ctb) rc[hq][1 + hl][0] = keep;
             pair_sync();
+            if (NH_AB && a.stamps && lane < 8) {   // (ticket, CTU): cy, pair, 4 stamps, the 64 schedule counts
+                uint64_t* o = a.stamps + ((int64_t)tk * a.ccols + cx) * kStampWords;
+                if (lane == 0) {
+                    o[0] = ((uint64_t)cy << 32) | (uint32_t)q;
+                    o[1] = st0;
+                    o[2] = st1;
+                    o[3] = st2;
+                    o[4] = __builtin_amdgcn_s_memtime();
+                    o[5] = __builtin_amdgcn_s_memrealtime();
+                }
+                o[8 + lane] = ((const uint64_t*)(ent_s + 64))[lane];
+            }
         }
         pair_sync();
         if (stall_s) break;
@@ -2324,6 +2346,20 @@ static int64_t closed4_plan_bytes(const nh_plane_set* set, int ctb) {
            kPlanBytes;
 }
 
+#if NH_AB
+static uint64_t* g_stamps = nullptr;
+static int64_t g_stamps_n = 0, g_stamps_used = 0;
+// A/B build only: the pair kernel's per-(ticket, CTU) stamps of the last closed-loop launch
+// (NH_CLOSED4_STAMPS=1), 8 words each; returns the number of words copied.
+extern "C" int64_t nh_ab_closed4_stamps(uint64_t* host, int64_t max_words) {
+    if (!g_stamps || !host) return 0;
+    const int64_t n = std::min(max_words, g_stamps_used);
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, g_stamps, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
+}
+#endif
+
 extern "C" int64_t nh_tu_pipeline_closed_workspace_bytes(const nh_plane_set* set, int ctb) {
     int64_t lines0, lw, np;
     if (closed4_layout(set, ctb, lines0, lw, np)) return -1;
@@ -2374,6 +2410,19 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     a.dqs = dequant_scale(rem);
     a.dq_per = per;
     a.probe = NH_KNOB("NH_CLOSED4_PROBE", 0);
+#if NH_AB   // A/B timing stamps of the pair kernel: nh_ab_closed4_stamps() copies the last launch's out
+    if (NH_KNOB("NH_CLOSED4_STAMPS", 0)) {
+        const int64_t need = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group * a.ccols * kStampWords;
+        if (need > g_stamps_n) {
+            if (g_stamps) (void)hipFree(g_stamps);
+            NH_HIP(hipMalloc(&g_stamps, need * 8));
+            g_stamps_n = need;
+        }
+        NH_HIP(hipMemsetAsync(g_stamps, 0, need * 8, s));
+        a.stamps = g_stamps;
+        g_stamps_used = need;
+    }
+#endif
     // 32x32 luma TUs on the f16 matrix cores (closed_chain32_h): 16-B level and 8-B recon row pieces;
     // A/B build: NH_CLOSED4_MFMA32 = 0 keeps them on the packed butterfly chain
     static const int mfma32 = NH_KNOB("NH_CLOSED4_MFMA32", 1);

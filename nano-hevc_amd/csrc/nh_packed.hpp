@@ -147,4 +147,49 @@ __device__ __forceinline__ void inv1d_pk(const pk16* Y, int32_t* x, int32_t bias
     if constexpr (DST) inv_dst4_pk(Y, x, bias); else inv_pk<N>(Y, x, bias);
 }
 
+// Sum over every aligned group of N lanes (N = 2, 4, ..., 64), each lane receiving
+// its group's total.  Inside a 16-lane row the partners come by DPP -- xor 1 and
+// xor 2 as quad permutations, the other quad by the half-row mirror, the other
+// half-row by the row mirror -- as VALU operand modifiers, not the LDS round trip
+// of __shfl_xor's ds_bpermute on the rounds' critical path; the other row of a
+// 32-lane half by ds_swizzle (xor 16), the other half by two lane reads.  Integer
+// addition mod 2^32 / 2^64 is associative and commutative: the same totals.
+template <int CTRL>
+__device__ __forceinline__ int32_t lane_perm32(int32_t v) {
+    if constexpr (CTRL < 0) return __builtin_amdgcn_ds_swizzle(v, 0x401F);
+    else return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL, class T>
+__device__ __forceinline__ T lane_perm(T v) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit lanes");
+    if constexpr (sizeof(T) == 4) {
+        return (T)lane_perm32<CTRL>((int32_t)v);
+    } else {
+        const uint64_t u = (uint64_t)v;
+        return (T)((uint64_t)(uint32_t)lane_perm32<CTRL>((int32_t)(uint32_t)u) |
+                   ((uint64_t)(uint32_t)lane_perm32<CTRL>((int32_t)(uint32_t)(u >> 32)) << 32));
+    }
+}
+template <class T>
+__device__ __forceinline__ T lane_read(T v, int l) {
+    if constexpr (sizeof(T) == 4) {
+        return (T)__builtin_amdgcn_readlane((int32_t)v, l);
+    } else {
+        const uint64_t u = (uint64_t)v;
+        return (T)((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)u, l) |
+                   ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(uint32_t)(u >> 32), l) << 32));
+    }
+}
+template <int N, class T>
+__device__ __forceinline__ T grp_sum(T v) {
+    static_assert(N >= 2 && N <= 64 && (N & (N - 1)) == 0, "group size");
+    v += lane_perm<0xB1>(v);                      // quad_perm [1, 0, 3, 2]
+    if constexpr (N >= 4) v += lane_perm<0x4E>(v);    // quad_perm [2, 3, 0, 1]
+    if constexpr (N >= 8) v += lane_perm<0x141>(v);   // row_half_mirror
+    if constexpr (N >= 16) v += lane_perm<0x140>(v);  // row_mirror
+    if constexpr (N >= 32) v += lane_perm<-1>(v);     // ds_swizzle: lane ^ 16 inside 32
+    if constexpr (N >= 64) v = lane_read(v, 0) + lane_read(v, 32);
+    return v;
+}
+
 }  // namespace nh

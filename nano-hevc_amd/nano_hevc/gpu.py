@@ -15,6 +15,12 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   tu_pipeline_closed_yuv420 -- the same over a YUV420 stream, luma and chroma wavefronts concurrent
   widen_u8 / narrow_u8 -- frame I/O casts (YUV420p bytes <-> int16 planes)
   encode_intra_yuv420 -- encode_frame_intra (DC vs planar per block) over a frame stream
+  block_server_stop / block_server_set_idle_us / block_server_stats -- the per-block
+                        call server: after drop-in per-block calls one
+                        workgroup stays resident for its idle time (100 us by default),
+                        so a DEVICE-wide synchronize (torch.cuda.synchronize()) right
+                        after such calls waits up to that long; block_server_stop()
+                        sends it away at once, set_idle_us(0) launches per call instead
 """
 from __future__ import annotations
 
@@ -572,3 +578,24 @@ def encode_intra_yuv420(frames, width: int, height: int, block_size: int, recon=
                              stream=stream)
     y, uv = st[:nf], st[nf:].view(nf, 2, ENC_STATS)
     return _torch().cat([y.view(nf, 1, ENC_STATS), uv], 1)
+
+
+# ---------------------------------------------------------------------------
+# block-call server controls (per-block drop-in calls)
+# ---------------------------------------------------------------------------
+def block_server_stop() -> None:
+    """Ask every resident block-call server to leave now and wait until it has
+    (a device-wide synchronize then no longer waits for its idle time)."""
+    check(_lib.load().nh_block_server_stop(), "block_server_stop")
+
+
+def block_server_set_idle_us(us: int) -> None:
+    """Idle time (us) a server stays resident without a request; 0 = no server
+    (every per-block call is its own kernel launch)."""
+    check(_lib.load().nh_block_server_set_idle_us(int(us)), "block_server_set_idle_us")
+
+
+def block_server_stats(device: int = 0) -> dict:
+    out = (C.c_int64 * 4)()
+    check(_lib.load().nh_block_server_stats(int(device), out), "block_server_stats")
+    return {"served": out[0], "launches": out[1], "kernel_calls": out[2], "idle_us": out[3]}

@@ -48,7 +48,7 @@ CONFIGS = {
     "closed": ("cfg3_closed_1080p_yuv420", "k_intra_rdo8_closed_tag<1, 1>", 1 / 64),
     "4b": ("cfg4_4k_yuv420", "k_ctu_open<32", 1 / 16),
     "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair", 2 / 64),
-    "5b": ("cfg5_8k_yuv420", "k_tc32_h<1", 2 / 8),
+    "5b": ("cfg5_8k_yuv420", "k_tc32_hd<2", 2 / 8),
 }
 # the sources a config's kernels are compiled from: their digest goes into the
 # entry, and bench.py / tools/bench_configs.py recompute it to tell whether the
