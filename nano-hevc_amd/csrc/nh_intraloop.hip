@@ -1566,8 +1566,20 @@ __device__ __forceinline__ void pair_sync() {
 template <int N, bool DST>
 __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
-                                                    int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq) {
+                                                    int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq,
+                                                    uint64_t* ph = nullptr) {
     constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
+    // A/B build, NH_CLOSED4_STAMPS: shader cycles of the batch's phases, summed per TU size into ph
+    // (LDS, lane 0) -- the s_memtime reads drain the LDS queue, so they sit where the chain syncs anyway
+    uint64_t ph_t = 0;
+    auto phase = [&](int k) {
+        if (NH_AB && ph) {
+            const uint64_t tnow = __builtin_amdgcn_s_memtime();
+            if (k >= 0 && __lane_id() == 0) ph[8 * (5 - L2) + k] += tnow - ph_t;
+            ph_t = tnow;
+        }
+    };
+    phase(-1);
     constexpr int32_t BIAS = 1 << (S - 1);
     const int lane = opaque_lane64(), t = lane % N, e = c0 + lane / N;
     const bool on = e < total;
@@ -1619,6 +1631,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     ed = grp_sum<N>(ed);
     ep = grp_sum<N>(ep);
     const bool use_dc = ed <= ep;   // __main__.py:173: DC wins ties
+    phase(0);
     pk16 r2[H];
 #pragma unroll
     for (int m = 0; m < H; ++m) r2[m] = o2[m] - (use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[m]));
@@ -1629,6 +1642,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         for (int i = 0; i < N; ++i) tl[i * TP + t] = (int16_t)(yv[i] >> S);
     }
     pair_sync();
+    phase(1);
     const int st = inv_slot<N, DST>(t);
     {
         pk16 P[H];   // forward pass 2 (transform.py:188-194): row t
@@ -1637,6 +1651,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         fwd1d_pk<N, DST>(P, yv, BIAS);
     }
     pair_sync();
+    phase(2);
     if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
         int32_t* lrow = (p ? pp.lvl[1] : pp.lvl[0]) + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
@@ -1647,6 +1662,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         }
     }
     pair_sync();
+    phase(3);
     int32_t xv[N];
     {
         pk16 Y[H];   // inverse pass 1 (transform.py:221-227): column t -> line i, slot inv_slot(t)
@@ -1660,6 +1676,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         for (int i = 0; i < N; ++i) tl[i * TP + st] = (int16_t)(xv[i] >> S);
     }
     pair_sync();
+    phase(4);
     {
         pk16 Y[H];   // inverse pass 2 (transform.py:230-236): row t
 #pragma unroll
@@ -1684,6 +1701,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         }
     }
     pair_sync();
+    phase(5);
 }
 
 // A 32x32 luma TU of the closed loop on the f16 matrix cores: the open loop's
@@ -1935,7 +1953,7 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // The compiler's allocation (135 VGPRs, 3 waves/SIMD): 0.150 ms per 4K YUV420
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
 constexpr int kPairWaves = 3;
-constexpr int kStampWords = 16;   // A/B stamps per (ticket, CTU)
+constexpr int kStampWords = 48;   // A/B stamps per (ticket, CTU)
 template <int WAVES>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
@@ -1949,6 +1967,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
 #endif
     __shared__ __attribute__((aligned(16))) uint8_t ent_s[NH_CLOSED4_PLAN ? kPlanBytes : 16];
     __shared__ int row_s, stall_s;
+    __shared__ uint64_t ph_s[NH_AB ? 32 : 1];   // A/B stamps: per-(TU size, phase) cycle sums of the CTU's batches
+    uint64_t* const ph = (NH_AB && a.stamps) ? ph_s : nullptr;
+    if (NH_AB && a.stamps && threadIdx.x < 32) ph_s[threadIdx.x] = 0;
     if (__builtin_nontemporal_load(&a.work[2]) != 0) return;   // wide stream: the 32-bit form codes it
     if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // the critical (luma) wavefront issues first
     const int lane = threadIdx.x;
@@ -2041,6 +2062,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) ((uint32_t*)ent_s)[lane] = planw;
             pair_sync();
             if (stall_s) break;
+            // every load before the rounds (line words, schedule) has landed: said as a real
+            // s_waitcnt so the compiler's wait insertion knows it -- otherwise its loop analysis
+            // keeps one of them pending and puts a vmcnt(0) at the top of every batch, which then
+            // also waits for the previous batch's level / recon stores
+            __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0)
             if (NH_AB && a.stamps) st1 = __builtin_amdgcn_s_memtime();
 #if NH_CLOSED4_PLAN
             {   // the CTU's TUs in dataflow rounds, from the schedule: lane rs holds the count of
@@ -2057,7 +2083,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     switch (rs & 3) {
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q);
+                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph);
                         case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
                             if (a.mfma32) {
                                 if (NH_CLOSED4_MFMA_FUSED && two) {
@@ -2174,6 +2200,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     o[5] = __builtin_amdgcn_s_memrealtime();
                 }
                 o[8 + lane] = ((const uint64_t*)(ent_s + 64))[lane];
+            }
+            if (NH_AB && a.stamps && lane < 32) {
+                a.stamps[((int64_t)tk * a.ccols + cx) * kStampWords + 16 + lane] = ph_s[lane];
+                ph_s[lane] = 0;
             }
         }
         pair_sync();

@@ -48,7 +48,7 @@ def main():
     torch.cuda.synchronize()
     buf = np.zeros(1 << 25, np.uint64)
     n = f(buf.ctypes.data, buf.size)
-    W16 = 16
+    W16 = 48
     r = buf[:n].reshape(-1, W16).astype(np.int64)
     valid = r[:, 1] != 0
     # consecutive CTUs of one ticket: shader cycles per 100-MHz realtime tick -> clock
@@ -84,6 +84,15 @@ def main():
     out["rounds_fit_r2"] = float(r2)
     out["mean_per_ctu"] = {k: float(v) for k, v in zip(names, X.mean(0))}
     out["mean_rounds_per_ctu"] = float((cnt > 0).reshape(-1, 16, 4).any(2).sum(1).mean())
+    # per TU size: the batch phases' cycles per chain call (packed chains; the 32x32 MFMA chain has none)
+    ph = r[:, 16:48].reshape(-1, 4, 8)[:, :, :6].sum(0).astype(np.float64)
+    names_ph = ["load+neighbours+mode", "fwd pass 1 + transpose", "fwd pass 2", "quant/dequant + transpose",
+                "inv pass 1 + transpose", "inv pass 2 + recon + stores"]
+    out["batch_phases_cycles_per_call"] = {}
+    for si, nn in enumerate((32, 16, 8, 4)):
+        calls = X[:, 1 + si].sum()
+        if calls and ph[si].sum():
+            out["batch_phases_cycles_per_call"][f"{nn}x{nn}"] = {k: float(v / calls) for k, v in zip(names_ph, ph[si])}
     out["note"] = "stamps in shader-clock cycles (s_memtime); medians per CTU unless mean_*"
     print(json.dumps(out))
 
