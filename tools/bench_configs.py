@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--closed4-frames", type=int, default=64, help="frames of the closed-loop cfg4 stream")
     ap.add_argument("--closed4-seq", action="store_true", help="closed4: luma then chroma (default: concurrent wavefronts)")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
-    ap.add_argument("--configs", default="3,4,4b,5,enc,io")
+    ap.add_argument("--configs", default="3,4,4b,5,closed,closed4,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
     ap.add_argument("--closed-frames", type=int, default=64)
     ap.add_argument("--ab", action="store_true", help="run on the A/B library (libnanohevc_ab.so: NH_* knobs read)")
@@ -330,7 +330,10 @@ def main():
                               "variant": v, "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
                               "blocks_per_s": nf * nblk / ms * 1e3, "samples_per_s": samples / ms * 1e3,
                               "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
-                              "frame0_equals_per_plane": same}), flush=True)
+                              "frame0_equals_per_plane": same,
+                              # the product form (variant 1) is the one profiled for the VALU roofline (§6a)
+                              **({"roofline": valu_roofline("cfg5_8k_yuv420", ms / nf)} if v == 1 else {})}),
+                  flush=True)
 
     if "enc" in cfgs or "io" in cfgs:
         W, H = 3840, 2160
