@@ -36,6 +36,7 @@
 #include "nh_internal.hpp"
 #include "nh_mfma.hpp"
 #include "nh_f16mma.hpp"
+#include "nh_ldsdma.hpp"
 // The open-loop CTU kernels keep the builtin's v_dot2c seeding (pdot_first,
 // nh_packed.hpp): the VOP3P form measured 1.3 % slower here (0.0390 vs 0.0385
 // ms per 4K frame, profiles/r03/cfg4/ab_libs_4b_pd.jsonl) and 2-4 % faster in
@@ -1109,28 +1110,6 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
 
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, hipStream_t s);
-
-// LDS-DMA (global_load_lds_*): each active lane's bytes from gsrc land at the
-// LDS byte address lds + lane * 16 for dwordx4, lds + lane * 4 for ushort (one
-// zero-extended dword per lane; tools/ab/lds_dma_probe.hip); the LDS base travels in M0, which the
-// compiler reserves, so it is saved and restored in the same statement.  As
-// inline asm the load is invisible to the compiler's waitcnt bookkeeping: the
-// caller retires it with an explicit vmcnt (wait_vm) -- the compiler's own
-// counts are only made more conservative by it (in-order completion).
-typedef __attribute__((address_space(3))) void lds_void_t;
-__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void_t*)(p); }
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
-}
-__device__ __forceinline__ void glds2(const void* gsrc, uint32_t lds) {
-    uint32_t keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
 
 // Config 5, 8-bit blocks, with the next block's image loaded under this one's
 // chain: a wave codes KB consecutive blocks; block k+1's

@@ -1,0 +1,37 @@
+// nh_ldsdma.hpp -- LDS-DMA loads (gfx950 global_load_lds_*) for the config-5
+// and closed-loop kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace nh {
+
+// LDS-DMA (global_load_lds_*): each active lane's bytes from gsrc land at the
+// LDS byte address lds + lane * 16 for dwordx4, lds + lane * 4 for ushort (one
+// zero-extended dword per lane; tools/ab/lds_dma_probe.hip); the LDS base travels in M0, which the
+// compiler reserves, so it is saved and restored in the same statement.  As
+// inline asm the load is invisible to the compiler's waitcnt bookkeeping: the
+// caller retires it with an explicit vmcnt (wait_vm) -- the compiler's own
+// counts are only made more conservative by it (in-order completion).
+typedef __attribute__((address_space(3))) void lds_void_t;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void_t*)(p); }
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+__device__ __forceinline__ void glds4(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+__device__ __forceinline__ void glds2(const void* gsrc, uint32_t lds) {
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_ushort %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds)) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory"); }
+
+
+}  // namespace nh

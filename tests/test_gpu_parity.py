@@ -985,6 +985,37 @@ def test_tu_pipeline_closed_pairs_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
             off += ph * pw
 
 
+@pytest.mark.parametrize("lead", [1, 2])
+def test_tu_pipeline_closed_pairs_offset_planes_vs_oracle(nh, torch_dev, lead):
+    """The pair form with the plane sets starting `lead` samples into the buffer:
+    lead 1 (odd base: 2-B aligned rows) takes the global-load source path and
+    the packed 32x32 chain, lead 2 (4-B aligned) the LDS-DMA staged source and
+    the packed 32x32 chain (the f16 matrix-core chain needs 16-B level rows);
+    both equal the oracle, and the leading samples stay untouched."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H, qp = 3, 104, 72, 30
+    rng = np.random.default_rng(lead)
+    fe = gpu.yuv420_frame_elems(W, H)
+    buf = np.clip(70 + rng.integers(-60, 61, lead + F * fe), 0, 255).astype(np.int16)
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(F, W, H, base=lead)
+    lvl = torch.full(d.shape, -9, dtype=torch.int32, device="cuda")
+    rec = torch.full(d.shape, -9, dtype=torch.int16, device="cuda")
+    _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, 777, qp, lvl=lvl, rec=rec)
+    lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    assert (lv[:lead] == -9).all() and (rv[:lead] == -9).all()
+    off = lead
+    for f in range(F):
+        for k, (pw, ph) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er, et = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, 777, qp, k == 0)
+            assert np.array_equal(lv[off:off + ph * pw].reshape(ph, pw), el), (f, k)
+            assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
+            assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
+            off += ph * pw
+
+
 @pytest.mark.parametrize("ctb", [4, 8, 16])
 def test_tu_pipeline_closed_small_ctb_vs_oracle(nh, torch_dev, ctb):
     """Closed-loop config 4 with CTBs below 32 (fewer units per CTU, more CTU rows)."""
