@@ -1972,14 +1972,15 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
 constexpr int kPairWaves = 3;
 constexpr int kStampWords = 48;   // A/B stamps per (ticket, CTU)
-template <int WAVES>
+// SRCL: the CTU's source staged in LDS by LDS-DMA (Closed4Args::src_lds; 4 KB more LDS per workgroup)
+template <int WAVES, bool SRCL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
     // the packed chains' int16 tiles (2 x 32 rows of TP) or closed_chain32_h's f16 transpose tiles (2 x 32 x kQH)
     __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * kQH];
     __shared__ __attribute__((aligned(16))) BasisH basis_s;
-    __shared__ __attribute__((aligned(16))) int16_t srcs[2 * 32 * 32];   // a.src_lds: the CTU's source, [plane][y][x]
+    __shared__ __attribute__((aligned(16))) int16_t srcs[SRCL ? 2 * 32 * 32 : 2];   // the CTU's source, [plane][y][x]
     static_assert(32 * TP <= 32 * kQH, "tile layout");
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
@@ -2046,7 +2047,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             const int nw = (min(ctb, a.w - x0c) + 1) / 2;
             uint64_t st0 = 0, st1 = 0, st2 = 0;   // A/B stamps: CTU start, poll done, rounds done
             if (NH_AB && a.stamps) st0 = __builtin_amdgcn_s_memtime();
-            if (a.src_lds) {   // this CTU's source (both planes) into LDS by LDS-DMA, landing under the wait
+            if (SRCL) {   // this CTU's source (both planes) into LDS by LDS-DMA, landing under the wait
                 // on the row above: ctb / 4 dword pieces per plane (4 rows of 16 dwords each), rows and columns
                 // past the plane's edge clamped inside it (their samples belong to no TU)
                 asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous CTU's reads of srcs are done
@@ -2114,15 +2115,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     switch (rs & 3) {
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, srcs, a.src_lds);
+                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, srcs, SRCL);
                         case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
                             if (a.mfma32) {
                                 if (NH_CLOSED4_MFMA_FUSED && two) {
                                     closed_chain32_h<2>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3], srcs,
-                                                        a.src_lds);
+                                                        SRCL);
                                 } else {   // one plane after the other (fewer live accumulators)
                                     closed_chain32_h<1>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3], srcs,
-                                                        a.src_lds);
+                                                        SRCL);
                                     if (two) {
                                         PairPlanes p1;
                                         p1.src[0] = pp.src[1];
@@ -2130,7 +2131,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                                         p1.rec[0] = pp.rec[1];
                                         p1.tu[0] = pp.tu[1];
                                         closed_chain32_h<1>(a, p1, x0c, y0c, rc + 1, (uint16_t*)t16 + 32 * kQH, basis_s,
-                                                            cq[3], srcs + 1024, a.src_lds);
+                                                            cq[3], srcs + 1024, SRCL);
                                     }
                                 }
                             } else {
@@ -2529,7 +2530,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
     if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
         int per_cu = 0;
-        auto kern = k_tu_closed_pair<kPairWaves>;
+        auto kern = a.src_lds ? k_tu_closed_pair<kPairWaves, true> : k_tu_closed_pair<kPairWaves, false>;
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
         const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
         if (NH_CLOSED4_PLAN) {   // the TU schedule of every (plane of the group, CTU), once per launch
