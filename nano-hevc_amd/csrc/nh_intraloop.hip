@@ -16,7 +16,6 @@
 #include "nh_tree.hpp"
 #include "nh_packed.hpp"
 #include "nh_f16mma.hpp"
-#include "nh_ldsdma.hpp"
 
 namespace nh {
 
@@ -1133,8 +1132,6 @@ struct Closed4Args {
     int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_h); set
                             // for luma when the level / recon rows allow 16-B / 8-B stores
     uint64_t* stamps;       // A/B build only (NH_CLOSED4_STAMPS): per (ticket, CTU) shader-clock stamps
-    int32_t src_lds;        // k_tu_closed_pair: the CTU's source staged in LDS by LDS-DMA before
-                            // the wait on the row above (even widths / 4-B aligned rows)
 };
 __constant__ BasisH c_basis_h_cl;   // the f16 DCT32 bases of closed_chain32_h (copied to LDS per workgroup)
 
@@ -1570,8 +1567,7 @@ template <int N, bool DST>
 __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq,
-                                                    uint64_t* ph = nullptr, const int16_t* sl = nullptr,
-                                                    bool use_sl = false) {
+                                                    uint64_t* ph = nullptr) {
     constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
     // A/B build, NH_CLOSED4_STAMPS: shader cycles of the batch's phases, summed per TU size into ph
     // (LDS, lane 0) -- the s_memtime reads drain the LDS queue, so they sit where the chain syncs anyway
@@ -1595,11 +1591,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     // the TU's source column, every load issued before any use: the waits for them then
     // overlap the neighbour reads and the DC / planar sums, not one round trip per row pair
     int32_t sv[N];
-    if (use_sl) {   // staged in LDS at the CTU's start (sl: [plane][32][32])
-        const int16_t* sq = sl + p * 1024 + ly * 32 + lx + t;
-#pragma unroll
-        for (int i = 0; i < N; ++i) sv[i] = sq[32 * i];
-    } else {
+    {
         const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
 #pragma unroll
         for (int i = 0; i < N; ++i)
@@ -1731,36 +1723,26 @@ constexpr int kQH = 40;   // f16 transpose tile: 32 rows of 40 halves per plane 
 template <int NP>
 __device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                  int16_t (*rc2)[33][33], uint16_t* qt2, const BasisH& bs,
-                                                 const ChainQ& cq, const int16_t* sl = nullptr, bool use_sl = false) {
+                                                 const ChainQ& cq) {
     const int l = opaque_lane64(), r = l & 31, hh = l >> 5;
     int32_t topr[NP], leftr[NP], tr[NP], bl[NP], dc[NP];
     bool use_dc[NP];
     uint32_t hx[NP][8];
     // the TUs' source columns, every load issued before any use (one wait, not one per row pair)
     int32_t sv[NP][16];
-    if (use_sl) {   // staged in LDS at the CTU's start (sl: [plane][32][32])
 #pragma unroll
-        for (int p = 0; p < NP; ++p)
+    for (int p = 0; p < NP; ++p) {
+        const int16_t* sp = pp.src[p] + (int64_t)y0c * a.pitch + x0c + r;
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
+        for (int q = 0; q < 8; ++q) {
+            const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
 #pragma unroll
-                for (int e = 0; e < 2; ++e)
-                    sv[p][2 * q + e] = sl[p * 1024 + (8 * hh + 16 * (q >> 2) + 2 * (q & 3) + e) * 32 + r];
-    } else {
-#pragma unroll
-        for (int p = 0; p < NP; ++p) {
-            const int16_t* sp = pp.src[p] + (int64_t)y0c * a.pitch + x0c + r;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
-#pragma unroll
-                for (int e = 0; e < 2; ++e)
-                    sv[p][2 * q + e] = (NH_AB && (a.probe & 32)) ? rc2[p][1 + y + e][1 + r]   // A/B probe: no source loads
-                                                                 : sp[(int64_t)(y + e) * a.pitch];
-            }
+            for (int e = 0; e < 2; ++e)
+                sv[p][2 * q + e] = (NH_AB && (a.probe & 32)) ? rc2[p][1 + y + e][1 + r]   // A/B probe: no source loads
+                                                             : sp[(int64_t)(y + e) * a.pitch];
         }
-        __builtin_amdgcn_sched_barrier(0);
     }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
         int16_t (*rc)[33] = rc2[p];
@@ -1972,15 +1954,13 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
 constexpr int kPairWaves = 3;
 constexpr int kStampWords = 48;   // A/B stamps per (ticket, CTU)
-// SRCL: the CTU's source staged in LDS by LDS-DMA (Closed4Args::src_lds; 4 KB more LDS per workgroup)
-template <int WAVES, bool SRCL>
+template <int WAVES>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
     // the packed chains' int16 tiles (2 x 32 rows of TP) or closed_chain32_h's f16 transpose tiles (2 x 32 x kQH)
     __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * kQH];
     __shared__ __attribute__((aligned(16))) BasisH basis_s;
-    __shared__ __attribute__((aligned(16))) int16_t srcs[SRCL ? 2 * 32 * 32 : 2];   // the CTU's source, [plane][y][x]
     static_assert(32 * TP <= 32 * kQH, "tile layout");
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
@@ -2047,18 +2027,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             const int nw = (min(ctb, a.w - x0c) + 1) / 2;
             uint64_t st0 = 0, st1 = 0, st2 = 0;   // A/B stamps: CTU start, poll done, rounds done
             if (NH_AB && a.stamps) st0 = __builtin_amdgcn_s_memtime();
-            if (SRCL) {   // this CTU's source (both planes) into LDS by LDS-DMA, landing under the wait
-                // on the row above: ctb / 4 dword pieces per plane (4 rows of 16 dwords each), rows and columns
-                // past the plane's edge clamped inside it (their samples belong to no TU)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the previous CTU's reads of srcs are done
-                const int xx = min(x0c + 2 * (lane & 15), a.w - 2), y1 = y0c + (lane >> 4);
-                for (int s2 = 0; s2 <= two; ++s2) {
-                    for (int i = 0; i < ctb / 4; ++i)   // (CTB 16: 32-sample rows too; the right half is unused)
-                        glds4(pp.src[s2] + (uint32_t)(min(y1 + 4 * i, a.h - 1) * a.pitch + xx),
-                              lds_addr(&srcs[1024 * s2 + 128 * i]));
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
             // this CTU's TU schedule (128 B), loaded under the wait on the row above
             uint32_t planw = 0;
             if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) planw = plan_row[cx * (kPlanBytes / 4) + lane];
@@ -2115,15 +2083,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     switch (rs & 3) {
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, srcs, SRCL);
+                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph);
                         case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
                             if (a.mfma32) {
                                 if (NH_CLOSED4_MFMA_FUSED && two) {
-                                    closed_chain32_h<2>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3], srcs,
-                                                        SRCL);
+                                    closed_chain32_h<2>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
                                 } else {   // one plane after the other (fewer live accumulators)
-                                    closed_chain32_h<1>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3], srcs,
-                                                        SRCL);
+                                    closed_chain32_h<1>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
                                     if (two) {
                                         PairPlanes p1;
                                         p1.src[0] = pp.src[1];
@@ -2131,7 +2097,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                                         p1.rec[0] = pp.rec[1];
                                         p1.tu[0] = pp.tu[1];
                                         closed_chain32_h<1>(a, p1, x0c, y0c, rc + 1, (uint16_t*)t16 + 32 * kQH, basis_s,
-                                                            cq[3], srcs + 1024, SRCL);
+                                                            cq[3]);
                                     }
                                 }
                             } else {
@@ -2492,11 +2458,6 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int mfma32 = NH_KNOB("NH_CLOSED4_MFMA32", 1);
     a.mfma32 = mfma32 && ctb == 32 && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
                !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 7);
-    // the CTU's source staged in LDS by LDS-DMA before the wait on the row above (4-B pieces: even
-    // widths and 4-B aligned rows); A/B knob NH_CLOSED4_SRC_DMA (0 off, 2 luma only)
-    static const int src_dma = NH_KNOB("NH_CLOSED4_SRC_DMA", 0);
-    a.src_lds = src_dma && (ctb == 32 || (ctb == 16 && src_dma != 2)) && set->width >= 2 && !(set->width & 1) && !(set->pitch & 1) &&
-                !((set->base | set->plane_stride | set->group_stride) & 1) && !((uintptr_t)d_src & 3);
     if (a.mfma32) {
         static PerDeviceOnce once;
         const int rcb = once.run([] {
@@ -2530,7 +2491,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
     if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
         int per_cu = 0;
-        auto kern = a.src_lds ? k_tu_closed_pair<kPairWaves, true> : k_tu_closed_pair<kPairWaves, false>;
+        auto kern = k_tu_closed_pair<kPairWaves>;
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
         const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
         if (NH_CLOSED4_PLAN) {   // the TU schedule of every (plane of the group, CTU), once per launch

@@ -22,6 +22,9 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+    if os.environ.get("NH_TEST_AB") == "1":   # tools: run the parity tests on the A/B library (its NH_* knobs)
+        from nano_hevc import _lib
+        _lib.use_ab(True)
 
 
 @pytest.fixture(scope="session")
