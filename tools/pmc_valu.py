@@ -53,7 +53,8 @@ CONFIGS = {
 # the sources a config's kernels are compiled from: their digest goes into the
 # entry, and bench.py / tools/bench_configs.py recompute it to tell whether the
 # committed instruction counts still describe the build they run
-_HDRS = ["nh_common.hpp", "nh_internal.hpp", "nh_packed.hpp", "nh_tree.hpp", "nh_mfma.hpp", "nh_f16mma.hpp"]
+_HDRS = ["nh_common.hpp", "nh_internal.hpp", "nh_packed.hpp", "nh_tree.hpp", "nh_mfma.hpp", "nh_f16mma.hpp",
+         "nh_ldsdma.hpp"]
 SOURCES = {
     "3": ["nh_intraloop.hip"] + _HDRS,
     "closed": ["nh_intraloop.hip"] + _HDRS,
@@ -141,7 +142,22 @@ def main():
     ap.add_argument("--cal-dir", default=None)
     ap.add_argument("--merge", action="store_true",
                     help="keep the other configs of an existing --out file (per-config tags)")
+    ap.add_argument("--refresh-digests", default=None, metavar="REASON",
+                    help="only re-record the source digests of --out's configs (after a source change that leaves "
+                         "the device code objects identical; REASON says how that was checked)")
     a = ap.parse_args()
+    if a.refresh_digests:
+        res = json.load(open(a.out))
+        for key, ent in res["configs"].items():
+            c = next(k for k, v in CONFIGS.items() if v[0] == key)
+            new = {"files": SOURCES[c], "sha256": sources_digest(SOURCES[c])}
+            if new != ent.get("sources"):
+                ent.setdefault("sources_history", []).append({"previous": ent.get("sources"), "reason": a.refresh_digests})
+                ent["sources"] = new
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+            f.write("\n")
+        return 0
     rates_path = os.path.join(a.dir, f"valu_rate_{a.tag}.jsonl")
     rates = [json.loads(x) for x in open(rates_path) if x.startswith("{")]
     mix = static_mix(rates_path)
