@@ -11,6 +11,7 @@
 #include <type_traits>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
+#include "nh_packed.hpp"
 
 namespace nh {
 
@@ -89,11 +90,7 @@ struct EncArgs {
 };
 
 template <int N, class V>
-__device__ __forceinline__ V seg_sum(V v) {
-#pragma unroll
-    for (int m = 1; m < N; m <<= 1) v += __shfl_xor(v, m, 64);
-    return v;
-}
+__device__ __forceinline__ V seg_sum(V v) { return grp_sum<N>(v); }   // DPP group sum (nh_packed.hpp)
 
 // N samples of T at p into v[] (AL: p is aligned to min(16, N*sizeof(T)) bytes).
 template <class T, int N, bool AL>
@@ -203,7 +200,7 @@ __global__ void __launch_bounds__(256) k_encode_dcpl(EncArgs a) {
     int64_t v[5] = {st_blocks, st_dc, st_edc, st_epl, st_sse};
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        for (int m = 32; m > 0; m >>= 1) v[k] += __shfl_xor(v[k], m, 64);
+        v[k] = grp_sum<64>(v[k]);
         if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();
@@ -291,7 +288,7 @@ __global__ void __launch_bounds__(256) k_encode_small(EncArgs a) {
             for (int i = 0; i < N; ++i) {
                 // previous lane = block b-1 = (bx-1, by) whenever bx > 0
                 const unsigned last = word<T>(o[u][i], (int)(sizeof(R) / 4) - 1);
-                const unsigned prev = __shfl_up(last, 1, 64);
+                const unsigned prev = lane_up1(last);
                 left[i] = sizeof(T) == 1 ? (int)(prev >> 24) : (int)(int16_t)(prev >> 16);
             }
             if (x0[u] == 0) {
@@ -361,7 +358,7 @@ __global__ void __launch_bounds__(256) k_encode_small(EncArgs a) {
     int64_t v[5] = {st_blocks, st_dc, st_edc, st_epl, st_sse};
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        for (int m = 32; m > 0; m >>= 1) v[k] += __shfl_xor(v[k], m, 64);
+        v[k] = grp_sum<64>(v[k]);
         if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();
@@ -440,7 +437,7 @@ __device__ __forceinline__ void decide_blk_u8(const EncArgs& a, const uint8_t* s
     constexpr int L2 = N == 4 ? 2 : 3, W = N / 4;
     int left[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) left[i] = (int)(__shfl_up(k.o[i][W - 1], 1, 64) >> 24);
+    for (int i = 0; i < N; ++i) left[i] = (int)(lane_up1(k.o[i][W - 1]) >> 24);
     if (k.x0 == 0) {
 #pragma unroll
         for (int i = 0; i < N; ++i) left[i] = 128;
@@ -525,7 +522,7 @@ __device__ __forceinline__ void flush_enc_stats(const EncArgs& a, int p, EncStat
     int64_t v[5] = {st.blocks, st.dc, st.edc, st.epl, st.sse};
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
-        for (int m = 32; m > 0; m >>= 1) v[k] += __shfl_xor(v[k], m, 64);
+        v[k] = grp_sum<64>(v[k]);
         if (lane == 0) part[threadIdx.x >> 6][k] = v[k];
     }
     __syncthreads();

@@ -817,11 +817,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             if (lane < kModes) {
                 key = (rdo8_chain<FORM == kClosedNarrow>(L, lane, refs[lane], rq, P, Lv) << 6) | lane;
             }
-            unsigned long long best = key;
-            for (int m = 32; m > 0; m >>= 1) {
-                const unsigned long long o = __shfl_xor(best, m, 64);
-                best = o < best ? o : best;
-            }
+            const unsigned long long best = grp_min<64>(key);   // DPP / swizzle / lane reads (nh_packed.hpp)
             if (key == best) {
                 // publish the bottom row first (the next row polls these words)
                 const uint64_t tag = (uint64_t)(uint32_t)(by + 1) << 32;
@@ -844,8 +840,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 if (lane == 0) a.modes[S.mode0 + (int64_t)pl * S.bw * S.bh + (int64_t)by * S.bw + bx] = (uint8_t)win_s;
             }
         }
-#pragma unroll
-        for (int m = 32; m > 0; m >>= 1) row_sse += __shfl_xor(row_sse, m, 64);
+        row_sse = grp_sum<64>(row_sse);
         if (lane == 0 && row_sse) atomicAdd((unsigned long long*)&a.sse[S.plane0 + pl], row_sse);
         __syncthreads();
         if (stall_s) break;

@@ -191,5 +191,23 @@ __device__ __forceinline__ T grp_sum(T v) {
     if constexpr (N >= 64) v = lane_read(v, 0) + lane_read(v, 32);
     return v;
 }
+// The same reduction with min (unsigned / signed per T): every lane gets its group's minimum.
+template <int N, class T>
+__device__ __forceinline__ T grp_min(T v) {
+    static_assert(N >= 2 && N <= 64 && (N & (N - 1)) == 0, "group size");
+    auto mn = [](T x, T y) { return y < x ? y : x; };
+    v = mn(v, lane_perm<0xB1>(v));
+    if constexpr (N >= 4) v = mn(v, lane_perm<0x4E>(v));
+    if constexpr (N >= 8) v = mn(v, lane_perm<0x141>(v));
+    if constexpr (N >= 16) v = mn(v, lane_perm<0x140>(v));
+    if constexpr (N >= 32) v = mn(v, lane_perm<-1>(v));
+    if constexpr (N >= 64) v = mn(lane_read(v, 0), lane_read(v, 32));
+    return v;
+}
+// __shfl_up(v, 1, 64) by DPP wave_shr:1: lane i gets lane i - 1's value, lane 0 keeps its own
+// (the source lane is out of range, and without bound_ctrl the old value -- v -- stays)
+__device__ __forceinline__ uint32_t lane_up1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x138, 0xF, 0xF, false);
+}
 
 }  // namespace nh
