@@ -21,6 +21,7 @@
 #include <string>
 #include "nh_common.hpp"
 #include "nh_internal.hpp"
+#include "nh_packed.hpp"
 
 namespace nh {
 
@@ -295,7 +296,7 @@ __device__ __forceinline__ void dev_count_nonzero(const int64_t* l, int64_t n, u
     unsigned long long c = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         c += l[i] != 0;
-    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    c = grp_sum<64>(c);   // DPP / swizzle / lane reads (nh_packed.hpp): every lane holds the total
     if ((threadIdx.x & 63) == 0 && c) atomicAdd(cnt, c);
 }
 
@@ -415,7 +416,7 @@ __device__ __forceinline__ void dev_estimate_bits(const int64_t* l, int64_t n, i
 template <class T, class F>
 __device__ __forceinline__ void block_reduce_add(T v, unsigned long long* out, F) {
     __shared__ unsigned long long part[4];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+    v = grp_sum<64>(v);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = (unsigned long long)v;
     __syncthreads();
     if (threadIdx.x == 0) {

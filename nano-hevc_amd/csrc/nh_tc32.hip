@@ -30,6 +30,7 @@
 #include "nh_internal.hpp"
 #include "nh_tree.hpp"
 #include "nh_mfma.hpp"
+#include "nh_packed.hpp"
 
 namespace nh {
 
@@ -94,8 +95,7 @@ __device__ __forceinline__ void tc32_block(const int16_t* __restrict__ src, int 
     // ---- DC (intra.py:46-62) and planar (intra.py:81-113) ----
     const int32_t my_nb = hh == 0 ? s_top_w[r] : s_left_w[r];
     int32_t s = my_nb;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    s = grp_sum<64>(s);
     const int32_t dc = (s + 32) >> 6;
     const int32_t tr = s_top_w[31], bl = s_left_w[31];
     auto planar = [&](int y, int x) -> int32_t {
@@ -111,11 +111,8 @@ __device__ __forceinline__ void tc32_block(const int16_t* __restrict__ src, int 
         e_dc += (long long)d1 * d1;
         e_pl += (long long)d2 * d2;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        e_dc += __shfl_xor(e_dc, o, 64);
-        e_pl += __shfl_xor(e_pl, o, 64);
-    }
+    e_dc = grp_sum<64>(e_dc);
+    e_pl = grp_sum<64>(e_pl);
     const bool use_dc = e_dc <= e_pl;                      // DC wins ties (__main__.py:173)
     int32_t X[16];
 #pragma unroll
