@@ -326,6 +326,23 @@ def run_phase_gather(step_into, send_of, og, steps, dist, main):
 # ---------------------------------------------------------------------------
 # config 2: the headline kernel
 # ---------------------------------------------------------------------------
+def device_copy_GBps(src, dst, stream, reps=10):
+    """A plain device-to-device copy of the launch's input bytes into its output
+    buffer (torch copy_, read + write counted): the achievable streaming rate the
+    kernel's HBM fraction can be read against.  Median of reps."""
+    import statistics
+    with torch.cuda.stream(stream):
+        dst.copy_(src)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in evs:
+            a.record(stream)
+            dst.copy_(src)
+            b.record(stream)
+    torch.cuda.synchronize()
+    ms = statistics.median(a.elapsed_time(b) for a, b in evs)
+    return 2 * src.numel() * src.element_size() / (ms * 1e-3) / 1e9
+
+
 def run_cfg2(args, dist, world, rank, dev):
     from nano_hevc import gpu, shard, _lib
     _lib.load()
@@ -378,6 +395,9 @@ def run_cfg2(args, dist, world, rank, dev):
     if rank != 0:
         return None
     achieved = nblk * BYTES_PER_BLOCK / (kern_ms * 1e-3) / 1e9
+    tmp = torch.empty_like(res)   # (outs[0] keeps the levels the cpu_baseline leg compares)
+    copy_gbs = device_copy_GBps(res, tmp, stream)   # context, after the timed region
+    del tmp
     cfg_key = f"fwd8x8_qp{args.qp}_4k_yuv420_f{args.frames}_v{args.variant}_n{world}"
     line = {
         "metric": METRIC, "value": value, "unit": "blocks/s", "n_gpus": world, "steps": args.steps,
@@ -391,7 +411,8 @@ def run_cfg2(args, dist, world, rank, dev):
                    "parallelism": f"ctu-band{world} (rotated)", "kernel_variant": args.variant},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": load_traffic(cfg_key),
-                     "bytes_per_block": BYTES_PER_BLOCK, "kernel_ms_avg": kern_ms},
+                     "bytes_per_block": BYTES_PER_BLOCK, "kernel_ms_avg": kern_ms,
+                     "device_copy_GBps": copy_gbs, "frac_of_device_copy": achieved / copy_gbs if copy_gbs else None},
         "cpu_baseline": None,
     }
     if gather:
