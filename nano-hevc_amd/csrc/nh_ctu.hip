@@ -1044,6 +1044,7 @@ __global__ void __launch_bounds__(256) k_ctu_wide(CtuArgs a) {
 // -32768 at its block's recon origin (recon is always in [0, 255]); the int8
 // chain (k_tc32_mfma, nh_tc32.hip) then codes exactly the marked blocks.
 constexpr int16_t kWideMark = (int16_t)0x8000;
+#if NH_AB   // the round-2/3 one-block-per-wave forms (A/B build only; the product runs k_tc32_hd)
 // K blocks per wave (consecutive in raster order), block k+1's loads issued
 // before block k's chain.  K = 1 in the product: K = 4 measured slower (0.177
 // vs 0.159 ms per 8K frame; 114 registers, 4 waves/SIMD), DESIGN.md §4.5.
@@ -1107,6 +1108,7 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
         wave_sync();   // this wave's LDS reads of block k before block k+1's image writes
     }
 }
+#endif
 
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, hipStream_t s);
@@ -1343,10 +1345,6 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     return NH_OK;
 }
 
-#ifndef NH_TC32H_BREG   // -DNH_TC32H_BREG=1: the bases in registers (k_tc32_h BREG; A/B builds: 0.113 vs 0.106
-#define NH_TC32H_BREG 0   // ms per 8K frame with the LDS copy, profiles/r03/cfg5/ab_libs_5b_breg.jsonl)
-#endif
-[[maybe_unused]] constexpr bool kTc32hBreg = NH_TC32H_BREG != 0;
 // Config 5's narrow launch over one plane set (full 32x32 blocks only).
 int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
                        int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s) {
@@ -1371,39 +1369,44 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     a.epoch = epoch;
     const int nblk = a.strips_x * a.nrows, planes = S.planes_per_group * S.num_groups;
     if (!nblk || !planes) return NH_OK;
-    // capped at 3 resident workgroups per CU: 0.137 vs 0.153 ms per 8K YUV420 frame
-    // uncapped (5 per CU; 2 per CU: 0.164), DESIGN.md §4.5.  A/B build:
-    // NH_TC32H_K = blocks per wave (2 / 4), NH_TC32H_CAP = workgroups per CU,
+    // capped at 3 resident workgroups per CU (k_tc32_h: 0.137 vs 0.153 ms per 8K YUV420 frame
+    // uncapped; k_tc32_hd's 50 KB of LDS allow 3 anyway).  A/B build:
+    // NH_TC32H_CAP = workgroups per CU, NH_TC32H_K = k_tc32_h blocks per wave (2 / 4),
     // NH_TC32H_FORM = 1 XCD-ordered grid, 3 the same with whole-row stores,
-    // 4 row-piece stores from registers (the round-2 form).
-    static const int kk = NH_KNOB("NH_TC32H_K", 1), cap = NH_KNOB("NH_TC32H_CAP", 3),
-                     form = NH_KNOB("NH_TC32H_FORM", 0);
+    // 4 row-piece stores from registers (the round-2 form), NH_TC32H_BREG = bases in registers.
+    static const int cap = NH_KNOB("NH_TC32H_CAP", 3);
     auto launch = [&](auto kern, int K) {
         kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, cap), s>>>(a, nblk);
     };
     // two blocks per wave, the second's image by LDS-DMA under the first's chain (k_tc32_hd<2>):
-    // 0.0966-0.0976 vs 0.0982-0.0983 ms per 8K YUV420 frame, 4 / 8 blocks per wave 0.102 / 0.107
+    // 0.0966-0.0976 vs 0.0982-0.0983 ms per 8K YUV420 frame for one block per wave loading its
+    // own strip (k_tc32_h, A/B build), 4 / 8 blocks per wave 0.102 / 0.107
     // (profiles/r04/cfg5/ab_tc32hd_r04h.jsonl; A/B knob NH_TC32H_DMA = blocks per wave, 0 = k_tc32_h).
-    // Its 16-B DMA pieces need 16-B aligned rows; other layouts take k_tc32_h.
+    // Its 16-B DMA pieces need 16-B aligned rows, which nh_tc32_planes guarantees.
     static const int dma = NH_KNOB("NH_TC32H_DMA", 2);
-    const bool dma_ok = !((S.pitch | S.base | S.plane_stride | S.group_stride) & 7) && !((uintptr_t)src & 15);
-    if (dma_ok && dma == 2) { launch(k_tc32_hd<2>, 2); NH_HIP(hipGetLastError()); return NH_OK; }
-    if (NH_AB && dma_ok && dma == 4) { launch(k_tc32_hd<4>, 4); NH_HIP(hipGetLastError()); return NH_OK; }
-    if (NH_AB && dma_ok && dma == 8) { launch(k_tc32_hd<8>, 8); NH_HIP(hipGetLastError()); return NH_OK; }
-    if (NH_AB && kk == 2) launch(k_tc32_h<2, false, true>, 2);
-    else if (NH_AB && kk == 4) launch(k_tc32_h<4, false, true>, 4);
+    if (((S.pitch | S.base | S.plane_stride | S.group_stride) & 7) || ((uintptr_t)src & 15)) {
+        set_error("tc32: rows must be 16-byte aligned");
+        return NH_EARG;
+    }
+    if (!NH_AB || dma == 2) {
+        launch(k_tc32_hd<2>, 2);
+        NH_HIP(hipGetLastError());
+        return NH_OK;
+    }
 #if NH_AB
+    static const int kk = NH_KNOB("NH_TC32H_K", 1), form = NH_KNOB("NH_TC32H_FORM", 0);
+    if (dma == 4) launch(k_tc32_hd<4>, 4);
+    else if (dma == 8) launch(k_tc32_hd<8>, 8);
+    else if (kk == 2) launch(k_tc32_h<2, false, true>, 2);
+    else if (kk == 4) launch(k_tc32_h<4, false, true>, 4);
     else if (form == 1) launch(k_tc32_h<1, true, false>, 1);
     else if (form == 4) launch(k_tc32_h<1, false, false>, 1);
     else if (form == 3) launch(k_tc32_h<1, true, true>, 1);
-#endif
     // whole-row output stores: 0.106 vs 0.125 ms per 8K YUV420 frame (forms 2 vs 0 of
     // profiles/r03/cfg5/ab_tc32h_forms.jsonl; the XCD-ordered grid is slower, 0.132)
-#if NH_AB || NH_TC32H_BREG
-    else if (NH_KNOB("NH_TC32H_BREG", kTc32hBreg ? 1 : 0)) launch(k_tc32_h<1, false, true, true>, 1);
-#endif
+    else if (NH_KNOB("NH_TC32H_BREG", 0)) launch(k_tc32_h<1, false, true, true>, 1);
     else launch(k_tc32_h<1, false, true>, 1);
-    (void)form;
+#endif
     NH_HIP(hipGetLastError());
     return NH_OK;
 }
