@@ -2067,12 +2067,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             {   // the CTU's TUs in dataflow rounds, from the schedule: lane rs holds the count of
                 // (round rs / 4, size index rs % 4); batches run in the schedule's order
                 const int cntv = ent_s[64 + lane];
-                const uint64_t nz = __ballot(cntv != 0);
-                const int last = nz ? 63 - __clzll(nz) : -1;
+                // (round, size) entries with TUs only: walk the set bits of the ballot
+                uint64_t nz = __ballot(cntv != 0);
+                if (NH_AB && (a.probe & 4)) nz = 0;
                 int off = 0;
-                for (int rs = 0; rs <= last && !(NH_AB && (a.probe & 4)); ++rs) {
+                for (; nz; nz &= nz - 1) {
+                    const int rs = __builtin_ctzll(nz);
                     const int cnt = __builtin_amdgcn_readlane(cntv, rs);
-                    if (cnt == 0) continue;
                     const int tot = cnt << two;
                     const uint8_t* ent = ent_s + off;
                     switch (rs & 3) {
