@@ -2084,16 +2084,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             if (a.mfma32) {
                                 if (NH_CLOSED4_MFMA_FUSED && two) {
                                     closed_chain32_h<2>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
-                                } else {   // one plane after the other (fewer live accumulators)
-                                    closed_chain32_h<1>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
-                                    if (two) {
+                                } else {   // one plane after the other (fewer live accumulators), ONE copy
+                                    // of the chain's code: a loop the compiler keeps (instruction-cache footprint)
+#pragma clang loop unroll(disable)
+                                    for (int s2 = 0; s2 <= two; ++s2) {
                                         PairPlanes p1;
-                                        p1.src[0] = pp.src[1];
-                                        p1.lvl[0] = pp.lvl[1];
-                                        p1.rec[0] = pp.rec[1];
-                                        p1.tu[0] = pp.tu[1];
-                                        closed_chain32_h<1>(a, p1, x0c, y0c, rc + 1, (uint16_t*)t16 + 32 * kQH, basis_s,
-                                                            cq[3]);
+                                        p1.src[0] = s2 ? pp.src[1] : pp.src[0];
+                                        p1.lvl[0] = s2 ? pp.lvl[1] : pp.lvl[0];
+                                        p1.rec[0] = s2 ? pp.rec[1] : pp.rec[0];
+                                        p1.tu[0] = s2 ? pp.tu[1] : pp.tu[0];
+                                        closed_chain32_h<1>(a, p1, x0c, y0c, rc + s2, (uint16_t*)t16 + s2 * 32 * kQH,
+                                                            basis_s, cq[3]);
                                     }
                                 }
                             } else {
