@@ -1650,10 +1650,17 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
         int32_t* lrow = (p ? pp.lvl[1] : pp.lvl[0]) + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
-        for (int kk = 0; kk < N; ++kk) {
-            const int32_t l = quant_s(yv[kk] >> S, cq.qs, cq.h_v, cq.hneg_v);
-            if (!(NH_AB && (a.probe & 64))) lrow[kk] = l;
-            tl[kk * TP + st] = (int16_t)dequant_s(l, cq);
+        for (int q4 = 0; q4 < N / 4; ++q4) {   // 4 levels per piece, stored together
+            int32_t l4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int kk = 4 * q4 + e;
+                l4[e] = quant_s(yv[kk] >> S, cq.qs, cq.h_v, cq.hneg_v);
+                tl[kk * TP + st] = (int16_t)dequant_s(l4[e], cq);
+            }
+            if (NH_AB && (a.probe & 64)) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) lrow[4 * q4 + e] = l4[e];   // (adjacent: one 16-B store)
         }
     }
     pair_sync();
@@ -1682,12 +1689,19 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, stv = tr - leftt;
         int16_t* rrow = (p ? pp.rec[1] : pp.rec[0]) + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
-        for (int kk = 0; kk < N; ++kk) {
-            const int32_t pr = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + kk] + b + kk * stv) >> (L2 + 1);
-            int32_t q = pr + (xv[kk] >> S);
-            q = q < 0 ? 0 : (q > 255 ? 255 : q);
-            if (!(NH_AB && (a.probe & 64))) rrow[kk] = (int16_t)q;
-            rc[ly + 1 + t][lx + 1 + kk] = (int16_t)q;   // no TU of this batch reads the TU's own samples
+        for (int q4 = 0; q4 < N / 4; ++q4) {   // 4 samples per piece, stored together
+            int32_t r4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int kk = 4 * q4 + e;
+                const int32_t pr = use_dc ? dc : ((N - 1 - t) * (int32_t)rc[ly][lx + 1 + kk] + b + kk * stv) >> (L2 + 1);
+                int32_t q = pr + (xv[kk] >> S);
+                r4[e] = q < 0 ? 0 : (q > 255 ? 255 : q);
+                rc[ly + 1 + t][lx + 1 + kk] = (int16_t)r4[e];   // no TU of this batch reads the TU's own samples
+            }
+            if (NH_AB && (a.probe & 64)) continue;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rrow[4 * q4 + e] = (int16_t)r4[e];   // (adjacent: one 8-B store)
         }
         if (t < N / 4 && !(NH_AB && (a.probe & 64))) {
             uint8_t* tu = p ? pp.tu[1] : pp.tu[0];
