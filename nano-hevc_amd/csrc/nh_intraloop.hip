@@ -1126,6 +1126,8 @@ struct Closed4Args {
                             // stores in the chains (0 in the product)
     int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_h); set
                             // for luma when the level / recon rows allow 16-B / 8-B stores
+    int32_t rec_ctu;        // k_tu_closed_pair: a whole CTU's packed-chain recon leaves from the LDS
+                            // reconstruction at the CTU's end, as 64-B row pieces (the rows 8-B aligned)
     uint64_t* stamps;       // A/B build only (NH_CLOSED4_STAMPS): per (ticket, CTU) shader-clock stamps
 };
 __constant__ BasisH c_basis_h_cl;   // the f16 DCT32 bases of closed_chain32_h (copied to LDS per workgroup)
@@ -1562,7 +1564,7 @@ template <int N, bool DST>
 __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq,
-                                                    uint64_t* ph = nullptr) {
+                                                    uint64_t* ph = nullptr, bool rec_later = false) {
     constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
     // A/B build, NH_CLOSED4_STAMPS: shader cycles of the batch's phases, summed per TU size into ph
     // (LDS, lane 0) -- the s_memtime reads drain the LDS queue, so they sit where the chain syncs anyway
@@ -1699,7 +1701,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
                 r4[e] = q < 0 ? 0 : (q > 255 ? 255 : q);
                 rc[ly + 1 + t][lx + 1 + kk] = (int16_t)r4[e];   // no TU of this batch reads the TU's own samples
             }
-            if (NH_AB && (a.probe & 64)) continue;
+            if ((NH_AB && (a.probe & 64)) || rec_later) continue;   // (rec_later: the CTU's rows leave from rc)
 #pragma unroll
             for (int e = 0; e < 4; ++e) rrow[4 * q4 + e] = (int16_t)r4[e];   // (adjacent: one 8-B store)
         }
@@ -1963,7 +1965,9 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
 constexpr int kPairWaves = 3;
 constexpr int kStampWords = 48;   // A/B stamps per (ticket, CTU)
-template <int WAVES>
+// REC: whole CTUs' packed-chain recon leaves from rc at the CTU's end (Closed4Args::rec_ctu); a
+// separate instantiation, so the per-TU form's code is the same as without the flush
+template <int WAVES, bool REC>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
@@ -2077,6 +2081,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             // also waits for the previous batch's level / recon stores
             __builtin_amdgcn_s_waitcnt(0xF70);   // vmcnt(0)
             if (NH_AB && a.stamps) st1 = __builtin_amdgcn_s_memtime();
+            bool rec_flush = false;
 #if NH_CLOSED4_PLAN
             {   // the CTU's TUs in dataflow rounds, from the schedule: lane rs holds the count of
                 // (round rs / 4, size index rs % 4); batches run in the schedule's order
@@ -2084,6 +2089,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 // (round, size) entries with TUs only: walk the set bits of the ballot
                 uint64_t nz = __ballot(cntv != 0);
                 if (NH_AB && (a.probe & 4)) nz = 0;
+                // the CTU is whole and none of its TUs is a matrix-core 32x32 (which stores its own
+                // rows): the packed chains leave their recon in rc only, flushed as whole rows below
+                rec_flush = REC && x0c + ctb <= a.w && y0c + ctb <= a.h && !(a.mfma32 && (nz & 1));
                 int off = 0;
                 for (; nz; nz &= nz - 1) {
                     const int rs = __builtin_ctzll(nz);
@@ -2093,7 +2101,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     switch (rs & 3) {
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph);
+                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, rec_flush);
                         case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
                             if (a.mfma32) {
                                 if (NH_CLOSED4_MFMA_FUSED && two) {
@@ -2187,6 +2195,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 const uint32_t lo = (uint16_t)rc[hq][ctb][1 + 2 * hl];
                 const uint32_t hi = 2 * hl + 1 < ctb ? (uint16_t)rc[hq][ctb][2 + 2 * hl] : 0u;
                 st_sys64(line[hq] + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
+            }
+            if (rec_flush) {   // the CTU's recon rows, 8-B pieces: ctb / 4 lanes per row, 64 / (ctb / 4) rows a pass
+                const int pr = ctb / 4, rpp = 64 / pr, pc = lane % pr, r0 = lane / pr;
+                for (int s2 = 0; s2 <= two; ++s2) {
+                    int16_t* rb = (s2 ? pp.rec[1] : pp.rec[0]) + (int64_t)y0c * a.pitch + x0c + 4 * pc;
+                    for (int r = r0; r < ctb; r += rpp) {
+                        const int16_t* q4 = &rc[s2][1 + r][1 + 4 * pc];
+                        const uint32_t lo = (uint16_t)q4[0] | ((uint32_t)(uint16_t)q4[1] << 16);
+                        const uint32_t hi = (uint16_t)q4[2] | ((uint32_t)(uint16_t)q4[3] << 16);
+                        *(uint2*)(rb + (int64_t)r * a.pitch) = make_uint2(lo, hi);
+                    }
+                }
             }
             pair_sync();
             int16_t keep = 0;
@@ -2469,6 +2489,11 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int mfma32 = NH_KNOB("NH_CLOSED4_MFMA32", 1);
     a.mfma32 = mfma32 && ctb == 32 && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
                !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 7);
+    // packed-chain recon of whole CTUs as 64-B rows from the LDS reconstruction (8-B aligned row pieces);
+    // A/B knob NH_CLOSED4_REC_CTU = 0: every TU stores its own 8-B row pieces
+    static const int rec_ctu = NH_KNOB("NH_CLOSED4_REC_CTU", 1);
+    a.rec_ctu = rec_ctu && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
+                !((uintptr_t)d_recon & 7);
     if (a.mfma32) {
         static PerDeviceOnce once;
         const int rcb = once.run([] {
@@ -2479,6 +2504,9 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         if (rcb) return rcb;
     }
     const int64_t rows = (int64_t)a.crows * np;
+    // the CTU-end flush pays when many waves share each SIMD (64 frames concurrent: 0.0964 vs 0.1027
+    // ms per 4K frame); with fewer its stores' latency shows (16 frames: luma 0.240 vs 0.233 ms)
+    if (rows < 4096) a.rec_ctu = 0;
     // persistent waves: every row covered, capped at what can be resident (1,024 SIMDs x 2 waves/SIMD)
     const int64_t cap = 2048;
     const unsigned waves = (unsigned)(rows < cap ? rows : cap);
@@ -2502,7 +2530,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
     if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
         int per_cu = 0;
-        auto kern = k_tu_closed_pair<kPairWaves>;
+        auto kern = a.rec_ctu ? k_tu_closed_pair<kPairWaves, true> : k_tu_closed_pair<kPairWaves, false>;
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
         const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
         if (NH_CLOSED4_PLAN) {   // the TU schedule of every (plane of the group, CTU), once per launch

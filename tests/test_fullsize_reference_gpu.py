@@ -166,3 +166,35 @@ def test_cfg4_4k_closed_loop_equals_reference(ref, torch_dev, conc):
         assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
         assert sha(tuy[0] if k == 0 else tuc[k - 1]) == e["tu"], k
         off += ph * pw
+
+
+def test_cfg4_4k_closed_loop_64_frames_equals_reference(ref, torch_dev):
+    """64 copies of the 4K YUV420 frame in one closed-loop launch pair: enough
+    CTU rows (>= 4096 per launch) that the pair kernel leaves each whole CTU's
+    packed-chain recon from its LDS reconstruction as row pieces at the CTU's
+    end (Closed4Args::rec_ctu).  Frame 0 equals the reference's hashes and every
+    other frame equals frame 0 (the quadtree depends on the plane, not the frame)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F = 64
+    planes = FI.cfg4_frame()
+    h, w = planes[0].shape
+    one = np.concatenate([p.reshape(-1) for p in planes])
+    fe = one.size
+    d = torch.from_numpy(one).cuda().repeat(F)
+    sy, suv = gpu.yuv420_plane_sets(F, w, h)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, FI.CFG4_SEED, FI.CFG4_QP, lvl=lvl, rec=rec)
+    lvl, rec = lvl.view(F, fe), rec.view(F, fe)
+    assert bool((lvl == lvl[:1]).all()) and bool((rec == rec[:1]).all())
+    assert bool((tuy == tuy[:1]).all()) and bool((tuc.view(F, 2, -1) == tuc.view(F, 2, -1)[:1]).all())
+    l0, r0, tuy, tuc = lvl[0].cpu().numpy(), rec[0].cpu().numpy(), tuy[0].cpu().numpy(), tuc[:2].cpu().numpy()
+    off = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        e = ref[f"closed4_p{k}"]
+        assert sha(l0[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], k
+        assert sha(r0[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
+        assert sha(tuy if k == 0 else tuc[k - 1]) == e["tu"], k
+        off += ph * pw

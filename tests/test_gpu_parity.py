@@ -985,6 +985,35 @@ def test_tu_pipeline_closed_pairs_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
             off += ph * pw
 
 
+def test_tu_pipeline_closed_pairs_many_frames_vs_oracle(nh, torch_dev):
+    """2048 small 8-bit YUV420 frames (72x40: whole and ragged CTUs) in one
+    concurrent launch pair: >= 4096 CTU rows per launch, so whole CTUs leave
+    their packed-chain recon from the LDS reconstruction at the CTU's end
+    (Closed4Args::rec_ctu) and ragged ones per TU; sampled frames equal the
+    sequential oracle and untouched-by-TU samples stay zero."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H, qp = 2048, 72, 40, 27
+    rng = np.random.default_rng(2048)
+    fe = gpu.yuv420_frame_elems(W, H)
+    buf = np.clip(90 + rng.integers(-80, 81, F * fe), 0, 255).astype(np.int16)
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(F, W, H)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, 99, qp, lvl=lvl, rec=rec)
+    lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    for f in (0, 1, 1023, 2047):
+        off = f * fe
+        for k, (pw, ph) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er, et = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, 99, qp, k == 0)
+            assert np.array_equal(lv[off:off + ph * pw].reshape(ph, pw), el), (f, k)
+            assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
+            assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
+            off += ph * pw
+
+
 @pytest.mark.parametrize("lead", [1, 2])
 def test_tu_pipeline_closed_pairs_offset_planes_vs_oracle(nh, torch_dev, lead):
     """The pair form with the plane sets starting `lead` samples into the buffer:
