@@ -4,7 +4,7 @@ pin, and the internal consistency of the committed profiles/valu_roofline.json
 (achieved = VALU per frame / busy time, frac = achieved / attainable, the
 dynamic bracket ordered).  Recomputing the committed file from its committed
 inputs (`tools/pmc_valu.py --tag r04zg --dir profiles/r04/valu --cal r04zg`,
-then `--tag r04zk --cal r04zk --configs 3,closed,closed4 --merge`) takes
+then `--tag r04zq --rates-tag r04zk --cal r04zk --configs 3,closed,closed4 --merge`) takes
 minutes of hipcc disassembly and is not repeated here."""
 import json
 import os

@@ -140,6 +140,8 @@ def main():
     ap.add_argument("--cal", default=None, help="tag of the tools/ab/_pmc_cal passes (pmc_cal3_<tag>, pmc_cal4_<tag>, "
                                                 "pmc_cal_<tag>.log in --cal-dir): dynamic mix from valu_pmc3/4")
     ap.add_argument("--cal-dir", default=None)
+    ap.add_argument("--rates-tag", default=None, help="tag of the valu_rate_<tag>.jsonl issue-rate probe in --dir "
+                    "(default: --tag; the rates are the chip's, not the build's)")
     ap.add_argument("--merge", action="store_true",
                     help="keep the other configs of an existing --out file (per-config tags)")
     ap.add_argument("--refresh-digests", default=None, metavar="REASON",
@@ -158,7 +160,7 @@ def main():
             json.dump(res, f, indent=1, sort_keys=True)
             f.write("\n")
         return 0
-    rates_path = os.path.join(a.dir, f"valu_rate_{a.tag}.jsonl")
+    rates_path = os.path.join(a.dir, f"valu_rate_{a.rates_tag or a.tag}.jsonl")
     rates = [json.loads(x) for x in open(rates_path) if x.startswith("{")]
     mix = static_mix(rates_path)
     dyn = None
