@@ -31,6 +31,7 @@ extern "C" {
 #define NH_EOVERFLOW (-3) /* OverflowError: int16 store out of range (numpy 2) intra.py:62,111,173 */
 #define NH_EZERODIV (-4)  /* ZeroDivisionError: intra_dc_predict size 0, intra.py:61 */
 #define NH_EARG (-5)      /* bad argument (null pointer, misaligned plane, negative count) */
+#define NH_ETYPE (-6)     /* TypeError: planar's float h + v (float corner, or int64 + uint64 corners) >> int, intra.py:111 */
 #define NH_ENODEV (-10)   /* no HIP device visible */
 #define NH_EHIP (-11)     /* HIP runtime error (message: nh_last_error()) */
 
@@ -67,10 +68,20 @@ int nh_block_server_stats(int device, int64_t* out);
  * intra.py:46-62 intra_dc_predict: dc over the WHOLE top/left arrays (D7). out: size*size */
 int nh_intra_dc(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft,
                 int64_t size, int variant4x4, int16_t* out);
-/* intra.py:81-113 intra_planar_predict; log2size = int(np.log2(size)) */
+/* intra.py:81-113 intra_planar_predict; log2size = int(np.log2(size)).
+ * tr_kind / bl_kind: the corner argument's scalar kind, which decides numpy 2's
+ * (NEP 50) arithmetic at intra.py:109-111: NH_NP_PYINT = a Python int (exact
+ * math); NH_NP_FLOAT = a float (value ignored: h and v become floats and the >>
+ * raises, NH_ETYPE); 8/16/32/64 = numpy uintN (value passed as its bits), -8..-64 = numpy
+ * intN (np.bool_ = -64).  Python-int operands are converted to the corner's
+ * dtype (NH_EOVERFLOW out of range), results wrap in it, int64 with uint64
+ * promotes to float64 (NH_ETYPE at the >>); the first error in the reference's
+ * loop order is returned. */
+#define NH_NP_PYINT 0
+#define NH_NP_FLOAT 1
 int nh_intra_planar(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft,
-                    int64_t top_right, int64_t bottom_left, int64_t size, int64_t log2size,
-                    int16_t* out);
+                    int64_t top_right, int tr_kind, int64_t bottom_left, int bl_kind,
+                    int64_t size, int64_t log2size, int16_t* out);
 /* intra.py:116-207 intra_angular_predict (+ _build_ref_array, _project_sample_at);
  * mode uses Python list indexing into INTRA_PRED_ANGLE (D10) */
 int nh_intra_angular(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft,
@@ -306,8 +317,13 @@ int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* strea
  * (metrics.py:46-48, int16 residual wrap), DC wins ties (__main__.py:171),
  * recon = clip_to_pixel_range(best pred) (intra.py:75-78); samples outside
  * full blocks get recon 0 (Frame.zeros, frame.py:81-88).
- * d_src: uint8 (src_is_u8 = 1) or int16 samples.  block_sizes[s] in
- * {4, 8, 16, 32, 64}.  d_recon (int16) and d_recon_u8 (the recon's
+ * d_src: uint8 (src_is_u8 = 1) or int16 samples.  block_sizes[s] >= 1 (any
+ * size, like the reference's driver: 4/8/16/32/64 have their own kernels, other
+ * sizes a generic wave-per-block kernel).  d_status (int32, zero it first) is
+ * set to 1 when a planar prediction leaves int16 -- the
+ * reference raises OverflowError at intra.py:111; possible only for int16
+ * samples at a block size that is not a power of two, where d_status is
+ * required (NULL otherwise allowed).  d_recon (int16) and d_recon_u8 (the recon's
  * .astype(np.uint8), i.e. to_yuv420p bytes) are optional and use the source
  * layout.  d_stats (NH_ENC_STATS int64 per plane, planes numbered set by set
  * in plane order g * planes_per_group + c) is ACCUMULATED into (zero it first):
@@ -316,7 +332,7 @@ int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* strea
 #define NH_ENC_STATS 6
 int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set* sets, int nsets,
                            const int32_t* block_sizes, int16_t* d_recon, uint8_t* d_recon_u8,
-                           int64_t* d_stats, void* stream);
+                           int64_t* d_stats, int32_t* d_status, void* stream);
 
 #ifdef __cplusplus
 }

@@ -72,19 +72,90 @@ __device__ __forceinline__ void dev_intra_dc(const int64_t* top, int64_t nt, con
     for (int64_t i = threadIdx.x; i < n; i += 256) out[i] = v;
 }
 
-// intra.py:81-113: Python-int arithmetic, int16 store (D9), IndexError on short refs.
+// Scalar kinds of planar's corner arithmetic (intra.py:109-111 under numpy 2 /
+// NEP 50): NH_NP_PYINT (0) = a Python int (exact), NH_NP_FLOAT (1) = a float
+// (h and v become floats, the >> raises TypeError), +8/16/32/64 = numpy uintN,
+// -8/-16/-32/-64 = numpy intN (np.bool_ corners arrive as int64: Python int
+// times np.bool_ is int64).  Values are carried exactly in 128 bits; a numpy
+// kind's value always lies in its range.
+typedef __int128 i128;
+constexpr int kNpFloat = 1;   // int64 + uint64 (or intN + uint64) promotes to float64
+__device__ __forceinline__ bool np_fits(int k, i128 v) {
+    if (k == 0) return true;
+    const int w = k < 0 ? -k : k;
+    if (k < 0) return v >= -((i128)1 << (w - 1)) && v < ((i128)1 << (w - 1));
+    return v >= 0 && v < ((i128)1 << w);
+}
+__device__ __forceinline__ i128 np_wrap(int k, i128 v) {   // numpy's modular scalar result
+    if (k == 0) return v;
+    const int w = k < 0 ? -k : k;
+    const unsigned __int128 m = ((unsigned __int128)1 << w) - 1, u = (unsigned __int128)v & m;
+    if (k < 0 && (u >> (w - 1))) return (i128)u - ((i128)1 << w);
+    return (i128)u;
+}
+__device__ __forceinline__ int np_promote(int a, int b) {   // numpy's result kind of a (+) b
+    if ((a < 0) == (b < 0)) return a < 0 ? (a < b ? a : b) : (a > b ? a : b);
+    const int s = a < 0 ? -a : -b, u = a < 0 ? b : a;   // signed width, unsigned width
+    if (u < s) return -s;
+    return u < 64 ? -2 * u : kNpFloat;
+}
+__device__ __forceinline__ i128 np_value(int k, int64_t bits) {   // the corner argument's value
+    return k == 64 ? (i128)(uint64_t)bits : (i128)bits;
+}
+
+// intra.py:81-113 in the reference's own loop order, per sample (y, x):
+//   h = (size-1-x)*int(left[y]) + (x+1)*top_right
+//   v = (size-1-y)*int(top[x])  + (y+1)*bottom_left
+//   pred[y, x] = (h + v + size) >> (log2_size + 1)        (int16 store, D9)
+// With Python-int corners this is exact integer math.  A numpy-integer corner
+// makes (x+1)*corner and the sums numpy scalars: the Python-int operand is
+// converted to the corner's dtype (OverflowError when out of range), the result
+// wraps in that dtype, two numpy operands promote, int64 with uint64 becomes
+// float64 and the >> raises TypeError.  Every step that can raise has its own
+// stage, so the status word keeps the first error in the reference's order.
 __device__ __forceinline__ void dev_intra_planar(const int64_t* top, int64_t nt, const int64_t* left, int64_t nl,
-                               int64_t tr, int64_t bl, int64_t size, int64_t log2size, int16_t* out,
-                               unsigned long long* st) {
+                               int64_t trb, int ktr, int64_t blb, int kbl, int64_t size, int64_t log2size,
+                               int16_t* out, unsigned long long* st) {
     const int64_t n = size * size;
+    const i128 tr = np_value(ktr, trb), bl = np_value(kbl, blb);
+    const int sh = (int)(log2size + 1 < 127 ? log2size + 1 : 127);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        int64_t y = i / size, x = i - y * size;
-        if (y >= nl || x >= nt) { report(st, i, NH_EINDEX); continue; }
-        int64_t h = (size - 1 - x) * left[y] + (x + 1) * tr;
-        int64_t v = (size - 1 - y) * top[x] + (y + 1) * bl;
-        int64_t p = (h + v + size) >> (log2size + 1);
-        if (p < -32768 || p > 32767) { report(st, i, NH_EOVERFLOW); continue; }
-        out[i] = (int16_t)p;
+        const int64_t y = i / size, x = i - y * size;
+        const int64_t at = i * 16;   // status key: position, then stage
+        // h (stages 0-2) and v (stages 3-5): Python part first, then the corner term, then their sum
+        auto term = [&](int64_t ri, int64_t nr, const int64_t* ref, int64_t w, int64_t c, i128 corner, int k,
+                        int s0, i128& out_v) -> bool {
+            if (ri >= nr) { report(st, at + s0, NH_EINDEX); return false; }
+            const i128 py = (i128)w * ref[ri];
+            if (k == 0) { out_v = py + (i128)c * corner; return true; }
+            if (k == kNpFloat) { out_v = 0; return true; }   // a float corner: h / v are floats
+            if (!np_fits(k, c)) { report(st, at + s0 + 1, NH_EOVERFLOW); return false; }
+            const i128 m = np_wrap(k, (i128)c * corner);
+            if (!np_fits(k, py)) { report(st, at + s0 + 2, NH_EOVERFLOW); return false; }
+            out_v = np_wrap(k, py + m);
+            return true;
+        };
+        i128 h, v;
+        if (!term(y, nl, left, size - 1 - x, x + 1, tr, ktr, 0, h)) continue;
+        if (!term(x, nt, top, size - 1 - y, y + 1, bl, kbl, 3, v)) continue;
+        int k;   // kind of h + v (stage 6)
+        i128 s;
+        if (ktr == kNpFloat || kbl == kNpFloat) {
+            k = kNpFloat;
+            s = 0;
+        } else if (ktr == 0 || kbl == 0) {
+            k = ktr | kbl;
+            if (!np_fits(k, ktr == 0 ? h : v)) { report(st, at + 6, NH_EOVERFLOW); continue; }
+            s = np_wrap(k, h + v);
+        } else {
+            k = np_promote(ktr, kbl);
+            s = k == kNpFloat ? 0 : np_wrap(k, h + v);
+        }
+        if (k == kNpFloat) { report(st, at + 8, NH_ETYPE); continue; }   // float64 >> int (stage 8)
+        if (!np_fits(k, size)) { report(st, at + 7, NH_EOVERFLOW); continue; }
+        s = np_wrap(k, s + size) >> sh;                                   // floor shift (numpy's too)
+        if (s < -32768 || s > 32767) { report(st, at + 9, NH_EOVERFLOW); continue; }
+        out[i] = (int16_t)s;
     }
 }
 
@@ -1217,15 +1288,18 @@ int nh_intra_dc(const int64_t* top, int64_t ntop, const int64_t* left, int64_t n
 }
 
 int nh_intra_planar(const int64_t* top, int64_t ntop, const int64_t* left, int64_t nleft, int64_t top_right,
-                    int64_t bottom_left, int64_t size, int64_t log2size, int16_t* out) {
-    if (ntop < 0 || nleft < 0 || size < 0) return NH_EARG;
+                    int tr_kind, int64_t bottom_left, int bl_kind, int64_t size, int64_t log2size, int16_t* out) {
+    const auto kind_ok = [](int k) { return k == 0 || k == 1 || k == 8 || k == 16 || k == 32 || k == 64 || k == -8 ||
+                                            k == -16 || k == -32 || k == -64; };
+    if (ntop < 0 || nleft < 0 || size < 0 || !kind_ok(tr_kind) || !kind_ok(bl_kind)) return NH_EARG;
+    if (size > (1ll << 24)) { set_error("intra_planar: size > 2^24 unsupported"); return NH_EARG; }
     const int64_t nout = size * size;
     if (nout == 0) return NH_OK;
     BlockCall c;
     const size_t ot = c.in(top, ntop * 8), ol = c.in(left, nleft * 8);
     return c.run(grid_for(nout), [=] __device__(U8 in, ST st, uint8_t* o) {
-        dev_intra_planar((const int64_t*)(in + ot), ntop, (const int64_t*)(in + ol), nleft, top_right, bottom_left,
-                         size, log2size, (int16_t*)o, st);
+        dev_intra_planar((const int64_t*)(in + ot), ntop, (const int64_t*)(in + ol), nleft, top_right, tr_kind,
+                         bottom_left, bl_kind, size, log2size, (int16_t*)o, st);
     }, out, nout * 2);
 }
 

@@ -4,6 +4,7 @@
 //   k_widen / k_narrow      frame.py:44-54, :87-115, :176-183 (astype casts)
 //   k_encode_dcpl<T, N>     __main__.py:142-189 encode_frame_intra (and the
 //                           demo's per-block decision, __main__.py:75-100)
+//   k_encode_any<T>         the same for block sizes other than 4/8/16/32/64
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdio>
@@ -583,6 +584,100 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     flush_enc_stats(a, p, st);
 }
 
+// Any block size N >= 1 (encode_frame_intra takes any block_size,
+// __main__.py:156-158; the demo passes it unclamped, __main__.py:75-91): one
+// wave per block, lanes stride over its N*N samples.  DC is the floor division
+// of intra.py:61 (2N need not be a power of two), planar's shift is
+// int(log2 N) + 1 (intra.py:105), so for N not a power of two its weights do not
+// normalise and a wide-range int16 plane can leave int16 -- the reference's
+// store raises OverflowError there (intra.py:111), reported through *err.  Two
+// passes over the block (energies, then the winner's clipped samples); the
+// neighbour and source re-reads of the second pass hit the caches.
+template <class T>
+__global__ void __launch_bounds__(256) k_encode_any(EncArgs a, int n, int log2n, int* err) {
+    const int p = blockIdx.y;
+    const int g = p / a.ppg, c = p - g * a.ppg;
+    const int64_t off = a.base + (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
+    const T* src = static_cast<const T*>(a.src) + off;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t nn = (int64_t)n * n;
+    int64_t st_blocks = 0, st_dc = 0, st_edc = 0, st_epl = 0, st_sse = 0;
+    for (uint32_t b = blockIdx.x * 4 + wv; b < a.nblk; b += gridDim.x * 4) {
+        const uint32_t by = b / a.nbx.d, bx = b - by * a.nbx.d;   // wave-uniform
+        const int64_t x0 = (int64_t)bx * n, y0 = (int64_t)by * n;
+        if (x0 + n > a.w || y0 + n > a.h) {        // partial block: recon stays 0 (Frame.zeros)
+            const int64_t pw = std::min<int64_t>(n, a.w - x0), ph = std::min<int64_t>(n, a.h - y0);
+            for (int64_t i = lane; i < pw * ph; i += 64) {
+                const int64_t y = y0 + i / pw, x = x0 + i % pw, k = y * a.pitch + x;
+                if (a.rec) a.rec[off + k] = 0;
+                if (a.rec8) a.rec8[off + k] = 0;
+                const int d = (uint8_t)src[k];
+                st_sse += d * d;
+            }
+            continue;
+        }
+        const T* row_above = src + (y0 - 1) * a.pitch + x0;
+        const T* col_left = src + y0 * a.pitch + x0 - 1;
+        auto top = [&](int64_t i) -> int64_t { return y0 > 0 ? (int64_t)row_above[i] : 128; };
+        auto left = [&](int64_t i) -> int64_t { return x0 > 0 ? (int64_t)col_left[i * a.pitch] : 128; };
+        int64_t s = 0;
+        for (int64_t i = lane; i < n; i += 64) s += top(i) + left(i);
+        s = grp_sum<64>(s) + n;
+        const int64_t d2 = 2 * (int64_t)n, q = s / d2;
+        const int64_t dc = q - ((s % d2) != 0 && s < 0);                     // Python floor division
+        const int64_t tr = top(n - 1), bl = left(n - 1);
+        auto planar = [&](int64_t y, int64_t x) -> int64_t {
+            return ((n - 1 - x) * left(y) + (x + 1) * tr + (n - 1 - y) * top(x) + (y + 1) * bl + n) >> (log2n + 1);
+        };
+        int64_t edc = 0, epl = 0;
+        bool ovf = false;
+        for (int64_t i = lane; i < nn; i += 64) {
+            const int64_t y = i / n, x = i - y * n;
+            const int o = src[(y0 + y) * a.pitch + x0 + x];
+            const int64_t pl = planar(y, x);
+            ovf |= pl < -32768 || pl > 32767;
+            const int64_t rd = (int16_t)(o - (int)dc), rp = (int16_t)(o - (int)(int16_t)pl);
+            edc += rd * rd;
+            epl += rp * rp;
+        }
+        if (ovf && err) atomicOr(err, 1);
+        edc = grp_sum<64>(edc);
+        epl = grp_sum<64>(epl);
+        const bool use_dc = edc <= epl;
+        for (int64_t i = lane; i < nn; i += 64) {
+            const int64_t y = i / n, x = i - y * n, k = (y0 + y) * a.pitch + x0 + x;
+            const int64_t v = use_dc ? dc : (int16_t)planar(y, x);
+            const int r = v < 0 ? 0 : v > 255 ? 255 : (int)v;
+            if (a.rec) a.rec[off + k] = (int16_t)r;
+            if (a.rec8) a.rec8[off + k] = (uint8_t)r;
+            const int d = (int)(uint8_t)src[k] - r;
+            st_sse += d * d;
+        }
+        if (lane == 0) {
+            st_blocks += 1;
+            st_dc += use_dc;
+            st_edc += edc;
+            st_epl += epl;
+        }
+    }
+    __shared__ int64_t part[4][5];
+    int64_t v[5] = {st_blocks, st_dc, st_edc, st_epl, st_sse};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        v[k] = grp_sum<64>(v[k]);
+        if (lane == 0) part[wv][k] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t[5];
+        for (int k = 0; k < 5; ++k) t[k] = part[0][k] + part[1][k] + part[2][k] + part[3][k];
+        int64_t* st = a.stats + (int64_t)p * NH_ENC_STATS;
+        const int64_t add[NH_ENC_STATS] = {t[0], t[1], t[0] - t[1], t[2], t[3], t[4]};
+        for (int k = 0; k < NH_ENC_STATS; ++k)
+            if (add[k]) atomicAdd((unsigned long long*)(st + k), (unsigned long long)add[k]);
+    }
+}
+
 // Launch shape of the N = 4 / 8 kernels: blocks per lane per pass (u4, u8),
 // prefetching form (pipe) and its total workgroup cap.  Tuning knob for
 // measurement: NH_ENC_TUNE="u4,u8,pipe,cap[,xcd]", read once.
@@ -690,7 +785,7 @@ int nh_narrow_i16_u8(const int16_t* d_in, uint8_t* d_out, int64_t n, void* strea
 
 int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set* sets, int nsets,
                            const int32_t* block_sizes, int16_t* d_recon, uint8_t* d_recon_u8,
-                           int64_t* d_stats, void* stream) {
+                           int64_t* d_stats, int32_t* d_status, void* stream) {
     if (!d_src || !sets || !block_sizes || !d_stats || nsets < 0 || nsets > NH_MAX_PLANE_SETS) {
         set_error("nh_encode_intra_planes: bad arguments");
         return NH_EARG;
@@ -702,8 +797,13 @@ int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set*
         const int n = block_sizes[k];
         const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
         if (S.width < 0 || S.height < 0 || S.pitch < S.width || S.planes_per_group < 1 || S.num_groups < 0 ||
-            planes > 65535 || !(n == 4 || n == 8 || n == 16 || n == 32 || n == 64)) {
-            set_error("nh_encode_intra_planes: bad plane set or block size (4, 8, 16, 32 or 64)");
+            planes > 65535 || n < 1 || n > 65536) {
+            set_error("nh_encode_intra_planes: bad plane set or block size (1..65536)");
+            return NH_EARG;
+        }
+        const bool fast = n == 4 || n == 8 || n == 16 || n == 32 || n == 64;
+        if (!fast && !src_is_u8 && !d_status) {   // only the generic form on int16 samples can overflow
+            set_error("nh_encode_intra_planes: block size not a power of two in 4..64 on int16 samples needs d_status");
             return NH_EARG;
         }
         if (planes == 0 || S.width == 0 || S.height == 0) continue;
@@ -732,6 +832,17 @@ int nh_encode_intra_planes(const void* d_src, int src_is_u8, const nh_plane_set*
         const auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
         const bool al = al16(d_src) && (!d_recon || al16(d_recon)) && (!d_recon_u8 || al16(d_recon_u8)) &&
                         S.base % 16 == 0 && S.plane_stride % 16 == 0 && S.group_stride % 16 == 0 && S.pitch % 16 == 0;
+        if (!fast) {   // k_encode_any: one wave per block, <= 512 workgroups (atomics) per plane
+            int log2n = 0;
+            while ((2 << log2n) <= n) ++log2n;                                      // int(np.log2(n))
+            const dim3 grid((unsigned)std::min<int64_t>((nblk + 3) / 4, 512), (unsigned)planes);
+            int* err = (int*)d_status;   // NULL for uint8 samples: planar stays below 511 there
+            if (src_is_u8) k_encode_any<uint8_t><<<grid, 256, 0, s>>>(a, n, log2n, err);
+            else k_encode_any<int16_t><<<grid, 256, 0, s>>>(a, n, log2n, err);
+            NH_HIP(hipGetLastError());
+            plane0 += planes;
+            continue;
+        }
         int u4, u8;
         small_unroll(u4, u8);
         const int64_t per_wg = n == 4 ? 256 * u4 : n == 8 ? 256 * u8 : 256 / n;   // blocks per workgroup pass

@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(HERE, "libnanohevc.so")
 # (use_ab(), or a fwd8x8 launch variant that only exists there).
 LIB_AB_PATH = os.path.join(HERE, "libnanohevc_ab.so")
 
-NH_OK, NH_EVALUE, NH_EINDEX, NH_EOVERFLOW, NH_EZERODIV, NH_EARG = 0, -1, -2, -3, -4, -5
+NH_OK, NH_EVALUE, NH_EINDEX, NH_EOVERFLOW, NH_EZERODIV, NH_EARG, NH_ETYPE = 0, -1, -2, -3, -4, -5, -6
 NH_ENODEV, NH_EHIP = -10, -11
 
 
@@ -47,7 +47,7 @@ SIGNATURES = {
     "nh_block_server_stop": ([], I32),
     "nh_block_server_stats": ([I32, P], I32),
     "nh_intra_dc": ([P, I64, P, I64, I64, I32, P], I32),
-    "nh_intra_planar": ([P, I64, P, I64, I64, I64, I64, I64, P], I32),
+    "nh_intra_planar": ([P, I64, P, I64, I64, I32, I64, I32, I64, I64, P], I32),
     "nh_intra_angular": ([P, I64, P, I64, I64, I32, I64, P], I32),
     "nh_residual": ([P, P, I64, P], I32),
     "nh_reconstruct": ([P, P, I64, P], I32),
@@ -88,7 +88,7 @@ SIGNATURES = {
     "nh_intra_rdo_closed_status": ([P, P, VP], I32),
     "nh_widen_u8_i16": ([P, P, I64, VP], I32),
     "nh_narrow_i16_u8": ([P, P, I64, VP], I32),
-    "nh_encode_intra_planes": ([P, I32, C.POINTER(PlaneSet), I32, P, P, P, P, VP], I32),
+    "nh_encode_intra_planes": ([P, I32, C.POINTER(PlaneSet), I32, P, P, P, P, P, VP], I32),
 }
 
 _libs = {}
@@ -164,6 +164,8 @@ def check(rc: int, what: str = "", lib=None):
         raise OverflowError(msg + "Python integer out of bounds for int16")
     if rc == NH_EZERODIV:
         raise ZeroDivisionError(msg + "integer division or modulo by zero")
+    if rc == NH_ETYPE:
+        raise TypeError(msg + "ufunc 'right_shift' not supported for the input types")
     if rc == NH_ENODEV:
         raise NanoHevcUnavailable(msg + "no HIP device visible: nano_hevc (MI355X) has no CPU fallback")
     err = (lib or load()).nh_last_error().decode(errors="replace")

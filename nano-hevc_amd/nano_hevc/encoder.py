@@ -3,8 +3,8 @@
 Drop-in for the functions the reference keeps in ``nano_hevc/__main__.py``:
 
   encode_frame_intra(frame, block_size, output_path=None) -> (recon, stats)
-      __main__.py:142-189.  Per block (luma ``block_size``, chroma
-      max(4, block_size // 2)): DC vs planar from the source plane's
+      __main__.py:142-189.  Per block (luma max(4, block_size), chroma
+      max(4, block_size // 2); any size): DC vs planar from the source plane's
       neighbours, smaller residual energy wins (DC on ties), recon =
       clip_to_pixel_range(best prediction); partial blocks stay 0.
   create_test_frame(height, width) -> Frame
@@ -52,7 +52,7 @@ def encode_frame_intra(frame: Frame, block_size: int, output_path: str | None = 
     dev, sets, offs = _device_planes(planes)
     import torch
     rec = torch.empty(dev.numel(), dtype=torch.int16, device=dev.device)
-    bs = [block_size, gpu.chroma_block_size(block_size), gpu.chroma_block_size(block_size)]
+    bs = [gpu.luma_block_size(block_size), gpu.chroma_block_size(block_size), gpu.chroma_block_size(block_size)]
     st = gpu.encode_intra_planes(dev, sets, bs, recon=rec).sum(0).cpu().numpy()
     rec_h = rec.cpu().numpy()
     recon = Frame.zeros(frame.height, frame.width, dtype=np.int16)

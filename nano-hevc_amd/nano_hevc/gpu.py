@@ -517,21 +517,29 @@ def narrow_u8(src, out=None, stream=None):
     return out
 
 
+def luma_block_size(block_size: int) -> int:
+    """encode_frame_intra's luma block: block_size, at least 4 (__main__.py:156-158)."""
+    return max(4, block_size)
+
+
 def chroma_block_size(block_size: int) -> int:
-    """encode_frame_intra's chroma block: block_size // 2, at least 4 (__main__.py:155-157)."""
+    """encode_frame_intra's chroma block: block_size // 2, at least 4 (__main__.py:156-158)."""
     return max(4, block_size // 2)
 
 
 def _check_block_size(bs: int):
-    if bs not in (4, 8, 16, 32, 64):
-        raise NotImplementedError(f"block size {bs}: the device driver handles 4, 8, 16, 32 and 64")
+    if not 1 <= bs <= 65536:
+        raise ValueError(f"block size {bs}: the device driver takes 1..65536")
 
 
 def encode_intra_planes(src, sets: Sequence[PlaneSet], block_sizes: Sequence[int], recon=None, recon_u8=None,
                         stats=None, stream=None):
     """The per-block decision of encode_frame_intra over every plane of ``sets``
-    inside ``src`` (uint8 or int16).  Returns the (accumulated) int64 stats
-    tensor, one ENC_STATS row per plane, planes numbered set by set."""
+    inside ``src`` (uint8 or int16), any block size >= 1.  Returns the
+    (accumulated) int64 stats tensor, one ENC_STATS row per plane, planes
+    numbered set by set.  Raises OverflowError where the reference's planar
+    store does (int16 samples at a block size that is not a power of two: the
+    call then waits for the launch to read the status word)."""
     torch = _torch()
     if not isinstance(src, torch.Tensor) or not src.is_cuda or src.dtype not in (torch.uint8, torch.int16):
         raise TypeError("encode_intra_planes(src): expected a uint8 or int16 device tensor")
@@ -555,10 +563,17 @@ def encode_intra_planes(src, sets: Sequence[PlaneSet], block_sizes: Sequence[int
                 raise ValueError(f"encode_intra_planes: {nm} smaller than src")
     arr = (PlaneSet * len(sets))(*sets)
     bsz = (C.c_int32 * len(sets))(*[int(b) for b in block_sizes])
+    wide = src.dtype == torch.int16 and any(int(b) & (int(b) - 1) or int(b) < 4 or int(b) > 64 for b in block_sizes)
+    status = torch.zeros(1, dtype=torch.int32, device=src.device) if wide else None
     check(_lib.load().nh_encode_intra_planes(
         src.data_ptr(), int(src.dtype == torch.uint8), arr, len(sets), bsz,
         recon.data_ptr() if recon is not None else None, recon_u8.data_ptr() if recon_u8 is not None else None,
-        stats.data_ptr(), C.c_void_p(_stream(stream, src.device))))
+        stats.data_ptr(), status.data_ptr() if status is not None else None,
+        C.c_void_p(_stream(stream, src.device))))
+    if status is not None:
+        torch.cuda.synchronize(src.device)          # the launch may be on another stream than torch's current one
+    if status is not None and int(status.item()):
+        raise OverflowError("encode_intra_planes: planar prediction out of bounds for int16 (intra.py:111)")
     return stats
 
 
@@ -574,8 +589,8 @@ def encode_intra_yuv420(frames, width: int, height: int, block_size: int, recon=
         raise ValueError("encode_intra_yuv420: size is not a whole number of frames")
     nf = frames.numel() // fe
     sets = yuv420_plane_sets(nf, width, height)
-    st = encode_intra_planes(frames, sets, [block_size, chroma_block_size(block_size)], recon, recon_u8,
-                             stream=stream)
+    st = encode_intra_planes(frames, sets, [luma_block_size(block_size), chroma_block_size(block_size)], recon,
+                             recon_u8, stream=stream)
     y, uv = st[:nf], st[nf:].view(nf, 2, ENC_STATS)
     return _torch().cat([y.view(nf, 1, ENC_STATS), uv], 1)
 

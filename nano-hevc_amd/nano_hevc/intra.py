@@ -160,23 +160,32 @@ def clip_to_pixel_range(block, bit_depth: int = 8):
     return out
 
 
-def _narrow_corner_ok(v, n, arrays):
-    """Planar with a narrow numpy-scalar corner computes in that dtype (NEP 50);
-    it equals Python-int math iff nothing can overflow it.  Check the bound."""
-    if not isinstance(v, np.integer) or v.dtype.itemsize >= 8:
-        return
-    info = np.iinfo(v.dtype)
-    m = max([abs(int(v))] + [int(np.abs(a).max()) if a.size else 0 for a in arrays])
-    if 2 * n * m + n > min(info.max, -info.min - 1):
-        raise NotImplementedError(
-            f"intra_planar_predict: {v.dtype} corner arithmetic may wrap for these samples; pass Python ints")
+def _corner_kind(v, what):
+    """(value bits, NH kind) of a planar corner (nanohevc.h nh_intra_planar): a
+    numpy integer scalar (or 0-d array) keeps its dtype -- intra.py:109-111 then
+    computes in that dtype under NEP 50, which the kernel reproduces (wrap,
+    OverflowError on converting Python ints, float64 promotion); np.bool_ acts
+    as int64 there; anything else is a Python int (exact math)."""
+    if isinstance(v, (float, np.floating)):
+        return 0, 1                                   # NH_NP_FLOAT: TypeError at the >> (intra.py:111)
+    dt = v.dtype if isinstance(v, (np.generic, np.ndarray)) and np.ndim(v) == 0 else None
+    if dt is not None and dt.kind == "b":
+        return int(v), -64
+    if dt is not None and dt.kind in "iu":
+        bits = dt.itemsize * 8
+        val = int(v)
+        if dt.kind == "u":
+            return (val - (1 << 64) if val >= 1 << 63 else val), bits
+        return val, -bits
+    return _corner(v, what), 0
 
 
 def _planar_float_refs(top, left, size, corners):
     """intra.py:107-111 for non-integer top/left: the loop reads int(left[y]) and
     int(top[x]), in the order left[0], top[0..size-1], left[1], left[2], ... (a
     repeated read raises nothing new); any float corner makes the first (h + v +
-    size) >> k raise TypeError right after left[0] and top[0] were read.  The
+    size) >> k raise TypeError right after left[0] and top[0] were read (the
+    kernel raises it there, after any error of the other corner's arithmetic).  The
     elements are converted here exactly as int() does (truncation; ValueError for
     NaN, OverflowError for inf) up to the first IndexError, which the kernel
     raises in the same place; the kernel then runs on those integers."""
@@ -199,7 +208,7 @@ def _planar_float_refs(top, left, size, corners):
         if not conv(ta, fl_t, tv, x):
             return tv, lv
         if x == 0 and any(isinstance(c, (float, np.floating)) for c in corners):
-            raise TypeError("unsupported operand type(s) for >>: 'float' and 'int'")
+            return tv, lv                                      # the kernel raises TypeError at (0, 0)
     for y in range(1, size):
         if not conv(la, fl_l, lv, y):
             break
@@ -216,20 +225,12 @@ def intra_planar_predict(top, left, top_right, bottom_left, size):
         t, l = _ints1d(top, "top"), _ints1d(left, "left")
     else:
         t, l = _planar_float_refs(top, left, size, (top_right, bottom_left))
-    if any(isinstance(c, (float, np.floating)) for c in (top_right, bottom_left)):
-        # float corners make h and v floats: the first (h + v + size) >> k raises
-        # TypeError (intra.py:111) right after left[0] / top[0] were read; an
-        # IndexError on those reads comes first, and the kernel raises it
-        if size > 0 and t.size and l.size:
-            raise TypeError("unsupported operand type(s) for >>: 'float' and 'int'")
-        tr = bl = 0
-    else:
-        n = min(size, t.size, l.size)
-        _narrow_corner_ok(top_right, size, [t[:n], l[:n]])
-        _narrow_corner_ok(bottom_left, size, [t[:n], l[:n]])
-        tr, bl = _corner(top_right, "top_right"), _corner(bottom_left, "bottom_left")
+    # a float corner makes the first (h + v + size) >> k raise TypeError (intra.py:111)
+    # right after left[0] / top[0] were read; the kernel raises it in that place
+    tr, ktr = _corner_kind(top_right, "top_right")
+    bl, kbl = _corner_kind(bottom_left, "bottom_left")
     out = np.empty((size, size), np.int16)
-    check(_lib.load().nh_intra_planar(ptr(t), t.size, ptr(l), l.size, tr, bl, size, log2_size, ptr(out)),
+    check(_lib.load().nh_intra_planar(ptr(t), t.size, ptr(l), l.size, tr, ktr, bl, kbl, size, log2_size, ptr(out)),
           "intra_planar_predict")
     return out
 

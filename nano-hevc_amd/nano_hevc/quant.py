@@ -118,7 +118,9 @@ def estimate_bits(level) -> int:
         kind = "f"
     if kind not in "biuf":
         raise TypeError(f"ufunc 'log2' not supported for the input types (dtype {a.dtype})")
-    code = _EB_CODE.get((kind, a.dtype.itemsize), 264 if kind == "f" else None)
+    code = _EB_CODE.get((kind, a.dtype.itemsize))
+    if code is None:   # longdouble (and complex256's magnitude): numpy computes in 80-bit extended
+        raise NotImplementedError(f"estimate_bits: {a.dtype} levels (extended precision) are not supported")
     flat = np.ravel(a, order="K")
     if kind == "f":
         x = np.ascontiguousarray(flat, dtype=np.float64).view(np.int64)   # exact widening, float64 bits

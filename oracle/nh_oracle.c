@@ -619,9 +619,12 @@ void oh_encode_intra_plane(const int16_t* src, int w, int h, int pitch, int N, i
     while ((2 << l2) <= N) ++l2;                       /* int(np.log2(size)) */
     for (int y = 0; y < h; ++y)
         for (int x = 0; x < w; ++x) recon[(int64_t)y * pitch + x] = 0;
-    for (int by = 0; by + N <= h; by += N)
+    /* any block size N >= 1 (__main__.py:156-158 takes any block_size) */
+    int64_t* top = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+    int64_t* left = (int64_t*)malloc(sizeof(int64_t) * (size_t)(N > 0 ? N : 1));
+    for (int by = 0; N > 0 && by + N <= h; by += N)
         for (int bx = 0; bx + N <= w; bx += N) {
-            int64_t top[64], left[64], nt, nl, sum = 0;
+            int64_t nt, nl, sum = 0;
             get_top(src, w, pitch, bx, by, N, top, &nt);
             get_left(src, h, pitch, bx, by, N, left, &nl);
             for (int i = 0; i < N; ++i) sum += top[i] + left[i];
@@ -652,6 +655,8 @@ void oh_encode_intra_plane(const int16_t* src, int w, int h, int pitch, int N, i
             stats[3] += edc;
             stats[4] += epl;
         }
+    free(top);
+    free(left);
     for (int y = 0; y < h; ++y)
         for (int x = 0; x < w; ++x) {
             const int64_t d = (int64_t)(uint8_t)src[(int64_t)y * pitch + x] -

@@ -263,10 +263,10 @@ def encode_intra_plane(src, block_size):
 
 
 def encode_frame_intra(y, u, v, block_size):
-    """encode_frame_intra (__main__.py:142-189): chroma block = max(4, bs // 2)."""
+    """encode_frame_intra (__main__.py:142-189): luma block = max(4, bs), chroma block = max(4, bs // 2)."""
     out, tot = [], np.zeros(6, np.int64)
     for k, p in enumerate((y, u, v)):
-        bs = block_size if k == 0 else max(4, block_size // 2)
+        bs = max(4, block_size) if k == 0 else max(4, block_size // 2)
         r, st = encode_intra_plane(p, bs)
         out.append(r)
         tot += st

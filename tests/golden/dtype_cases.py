@@ -198,4 +198,39 @@ def cases():
     add("count_nonzero", np.array(["a", "", " "]))
     add("is_all_zero", np.array([0, 0.0, False], dtype=object))
     add("is_all_zero", np.array(["", ""]))
+    # ---- round 5 (VERDICT r4 missing #2): planar with numpy-integer corners, e.g.
+    # top[-1] / left[-1] of the reference rows themselves (intra.py:109-111 computes
+    # (x+1)*corner and the sums in the corner's dtype under NEP 50)
+    for n in (4, 8, 16, 32):
+        for lo, hi in ((0, 256), (0, 1024)):                  # 8-bit and 10-bit samples
+            for dt in (np.int16, np.uint8, np.int8, np.uint16, np.int32, np.int64, np.uint64):
+                info = np.iinfo(dt)
+                t = rng.integers(max(lo, info.min), min(hi, info.max + 1), n + 1).astype(dt)
+                l = rng.integers(max(lo, info.min), min(hi, info.max + 1), n + 1).astype(dt)
+                add("intra_planar_predict", t, l, t[-1], l[-1], n)
+        t = np.full(n + 1, 1000, np.int16)
+        add("intra_planar_predict", t, t.copy(), t[-1], t[-1], n)              # N = 32: -24 (wraps)
+        add("intra_planar_predict", t, t.copy(), int(t[-1]), t[-1], n)         # one Python-int corner
+        add("intra_planar_predict", t, t.copy(), t[-1], int(t[-1]), n)
+    t16 = np.full(33, 1000, np.int16)
+    add("intra_planar_predict", t16, t16, np.int32(30000), np.int32(30000), 32)    # int32: store OverflowError
+    add("intra_planar_predict", t16, t16, np.int64(1000), np.uint64(1000), 8)      # float64 >> int: TypeError
+    add("intra_planar_predict", t16, t16, np.uint64(1000), np.int8(10), 8)         # uint64 + int8: float64
+    add("intra_planar_predict", t16, t16, np.uint64(2**64 - 5), np.uint64(7), 4)   # uint64 wrap
+    add("intra_planar_predict", t16, t16, np.int16(1000), np.uint8(200), 16)       # int16 + uint8 -> int16
+    add("intra_planar_predict", t16, t16, np.uint16(60000), np.int16(-5), 8)       # uint16 + int16 -> int32
+    add("intra_planar_predict", t16, t16, np.uint32(7), np.int16(-5), 4)           # uint32 + int16 -> int64
+    add("intra_planar_predict", t16, t16, np.uint8(3), np.int8(-3), 4)             # Python int > 255: Overflow
+    add("intra_planar_predict", np.full(9, -3, np.int16), np.full(9, 2, np.int16), np.uint8(3), 4, 8)  # negative
+    add("intra_planar_predict", np.full(5, 20, np.int8), np.full(5, 10, np.int8), np.int8(20), np.int8(10), 4)
+    add("intra_planar_predict", np.full(5, 120, np.uint8), np.full(5, 2, np.uint8), np.uint8(120), np.uint8(2), 4)
+    add("intra_planar_predict", t16, t16, np.True_, np.False_, 8)                  # bool_ -> int64
+    add("intra_planar_predict", t16, t16, np.int8(100), 3.5, 8)                    # Overflow before TypeError
+    add("intra_planar_predict", t16, t16, 3.5, np.int8(100), 8)
+    add("intra_planar_predict", t16, t16, np.array(1000, np.int16), np.array(1000, np.int16), 32)   # 0-d arrays
+    add("intra_planar_predict", t16[:3], t16, np.int16(1000), np.int16(1000), 8)   # IndexError vs wrap order
+    add("intra_planar_predict", t16, t16[:2], np.int8(1), np.int8(1), 4)
+    add("intra_planar_predict", np.full(200, 1, np.int16), np.full(200, 1, np.int16), np.int8(1), np.int8(1), 128)
+    add("intra_planar_predict", np.full(300, 1, np.int16), np.full(300, 1, np.int16), np.uint8(1), np.uint8(1), 200)
+    add("intra_planar_predict", rng.uniform(0, 255, 9), rng.uniform(0, 255, 9), np.int16(900), np.int16(800), 8)
     return out

@@ -435,6 +435,39 @@ def gen_encode(ref_path):
             num(r"Total blocks:\s+(\d+)"), num(r"DC wins:\s+(\d+)"), num(r"Planar wins:\s+(\d+)"),
             num(r"DC total residual energy:\s+([\d,]+)"), num(r"Planar total residual energy:\s+([\d,]+)")], np.int64)
         out[f"d_{dh}x{dw}_bs{bs}_psnr_text"] = np.array(re.search(r"PSNR \(best mode\): (\S+) dB", txt).group(1))
+    # round 5 (VERDICT r4 missing #3): block sizes other than 4/8/16/32/64 -- the
+    # reference's driver takes any block_size (luma max(4, bs), chroma
+    # max(4, bs // 2)); (d) a 10-bit-range int16 frame, where planar's
+    # non-normalised weights at odd sizes can overflow int16 (OverflowError)
+    fd = Frame(Plane(rng.integers(0, 1024, size=(40, 56)).astype(np.int16)),
+               Plane(rng.integers(0, 1024, size=(20, 28)).astype(np.int16)),
+               Plane(rng.integers(0, 1024, size=(20, 28)).astype(np.int16)))
+    out["e_d_y"], out["e_d_u"], out["e_d_v"] = fd.y.data, fd.u.data, fd.v.data
+    more = [("a", bs, Frame.from_yuv420p(raw, h, w)) for bs in (12, 24, 3, 9, 6, 20, 40, 0, -8, 128)]
+    more += [("b", bs, fb) for bs in (12, 24, 5)]
+    more += [("c", bs, fc) for bs in (12, 10)]
+    more += [("d", bs, fd) for bs in (12, 7, 24)]
+    for tag, bs, fr in more:
+        k = f"e_{tag}_bs{bs}"
+        try:
+            recon, stats = R.encode_frame_intra(fr, bs)
+        except Exception as e:   # the reference's exception class (planar's int16 store)
+            out[k + "_err"] = np.array(type(e).__name__)
+            continue
+        out[k + "_ry"], out[k + "_ru"], out[k + "_rv"] = recon.y.data, recon.u.data, recon.v.data
+        out[k + "_stats"] = np.array([stats["blocks"], stats["dc"], stats["planar"]], np.int64)
+        out[k + "_psnr_y"] = np.float64(R.psnr(fr.y.data.astype(np.uint8), recon.y.data.astype(np.uint8)))
+    for (dh, dw, bs) in ((64, 64, 12), (48, 80, 6), (72, 40, 24)):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            R.demo_predictions(dh, dw, bs)
+        txt = buf.getvalue()
+        out[f"d_{dh}x{dw}_bs{bs}_y"] = R.create_test_frame(dh, dw).y.data
+        num = lambda pat: int(re.search(pat, txt).group(1).replace(",", ""))
+        out[f"d_{dh}x{dw}_bs{bs}"] = np.array([
+            num(r"Total blocks:\s+(\d+)"), num(r"DC wins:\s+(\d+)"), num(r"Planar wins:\s+(\d+)"),
+            num(r"DC total residual energy:\s+([\d,]+)"), num(r"Planar total residual energy:\s+([\d,]+)")], np.int64)
+        out[f"d_{dh}x{dw}_bs{bs}_psnr_text"] = np.array(re.search(r"PSNR \(best mode\): (\S+) dB", txt).group(1))
     return out
 
 
@@ -592,7 +625,7 @@ def main():
     if "--only" in sys.argv:   # regenerate one file (own rng), keep the others and their manifest entries
         name = sys.argv[sys.argv.index("--only") + 1]
         gen = {"closed4.npz": lambda: gen_closed4(I, T, Q), "closed.npz": lambda: gen_closed(I, T, Q),
-               "dtypes.npz": lambda: gen_dtypes(I, Q, M, T)}[name]
+               "dtypes.npz": lambda: gen_dtypes(I, Q, M, T), "encode.npz": lambda: gen_encode(ref)}[name]
         p = os.path.join(HERE, name)
         np.savez_compressed(p, **gen())
         mp = os.path.join(HERE, "manifest.json")

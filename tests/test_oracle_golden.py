@@ -207,6 +207,11 @@ def test_oracle_threaded_plane_equals_single(threads):
         assert np.array_equal(O.fwd8x8_quant_plane_mt(r, 27, False, threads), O.fwd8x8_quant_plane(r, 27, False))
 
 
+# block sizes other than 4/8/16/32/64 recorded by make_golden.gen_encode (round 5);
+# ("c", 12 / 10) are the reference's OverflowError cases (tests/test_frame_gpu.py)
+ENC_ODD = {"a": (12, 24, 3, 9, 6, 20, 40, 0, -8, 128), "b": (12, 24, 5), "d": (12, 7, 24)}
+
+
 def test_oracle_encode_frame_intra_golden(golden):
     """oh_encode_intra_plane against the reference's encode_frame_intra outputs
     (recon planes, stats, Y-PSNR) and the demo's printed totals."""
@@ -215,9 +220,10 @@ def test_oracle_encode_frame_intra_golden(golden):
     w, h = 72, 40
     ys, cs = w * h, (w // 2) * (h // 2)
     frames = {"a": (raw[:ys].reshape(h, w), raw[ys:ys + cs].reshape(h // 2, w // 2), raw[ys + cs:].reshape(h // 2, w // 2))}
-    for t in "bc":
+    for t in "bcd":
         frames[t] = (g[f"e_{t}_y"], g[f"e_{t}_u"], g[f"e_{t}_v"])
-    for tag, bss in (("a", (4, 8, 16, 32)), ("b", (4, 8, 16)), ("c", (8,))):
+    for tag, bss in (("a", (4, 8, 16, 32) + ENC_ODD["a"]), ("b", (4, 8, 16) + ENC_ODD["b"]), ("c", (8,)),
+                     ("d", ENC_ODD["d"])):
         y, u, v = frames[tag]
         for bs in bss:
             k = f"e_{tag}_bs{bs}"
@@ -225,9 +231,9 @@ def test_oracle_encode_frame_intra_golden(golden):
             for a, s in ((ry, "_ry"), (ru, "_ru"), (rv, "_rv")):
                 assert np.array_equal(a, g[k + s]), (k, s)
             assert list(st[:3]) == list(g[k + "_stats"])
-            _, sy = O.encode_intra_plane(y, bs)
+            _, sy = O.encode_intra_plane(y, max(4, bs))
             assert 10 * np.log10(255 ** 2 / (np.float64(sy[5]) / np.float64(y.size))) == g[k + "_psnr_y"]
-    for key in ("d_64x64_bs8", "d_48x80_bs4", "d_72x40_bs16"):
+    for key in ("d_64x64_bs8", "d_48x80_bs4", "d_72x40_bs16", "d_64x64_bs12", "d_48x80_bs6", "d_72x40_bs24"):
         _, st = O.encode_intra_plane(g[key + "_y"], int(key.split("bs")[1]))
         assert list(st[:5]) == list(g[key])
         assert f"{10 * np.log10(255 ** 2 / (np.float64(st[5]) / g[key + '_y'].size)):.2f}" == str(g[key + "_psnr_text"])

@@ -124,3 +124,17 @@ def test_plane_sets_disjoint():
     assert not gpu.sets_disjoint(a, b)
     c = gpu.plane_set(8 * W, W, 4, 2 * W)
     assert gpu.sets_disjoint(a, c)
+
+
+def test_estimate_bits_extended_precision_is_refused():
+    """numpy computes estimate_bits of longdouble levels (and of complex256's
+    magnitude) in 80-bit extended precision (quant.py:166-168); the device has no
+    such type, so the drop-in refuses them instead of narrowing to float64
+    (ADVICE r4).  Host-side check: no device call is made."""
+    from nano_hevc.quant import estimate_bits
+    if np.dtype(np.longdouble).itemsize == 8:
+        pytest.skip("longdouble is float64 on this platform")
+    with pytest.raises(NotImplementedError):
+        estimate_bits(np.array([1.5, -3.0], np.longdouble))
+    with pytest.raises(NotImplementedError):
+        estimate_bits(np.array([1 + 2j], np.clongdouble))
