@@ -1124,7 +1124,17 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
 // slot it overwrites.  At the frame's top / left edge the DMA reads the block's
 // own row / column and the 128s of block.py:41-48 overwrite it after the wait.
 // Same chain (ctu_chain32_h over an ImgDma image), same marks for wide blocks.
-constexpr int kTc32hdStoresNarrow = 6;   // ctu_chain32_h<TSTORE>: 4 level-row + 2 recon-row store instructions
+// The two counts below are what the compiler emits; tools/isa_check.py runs the
+// built kernel's control flow as a model of the in-order vmcnt queue and fails
+// (tests/test_isa_checks.py) unless every wait retires exactly block k's DMA.
+#ifndef NH_TC32HD_STORES_NARROW   // (overridable only so that tests/test_isa_checks.py can miscount on purpose)
+#define NH_TC32HD_STORES_NARROW 6
+#endif
+#ifndef NH_TC32HD_STORES_WIDE
+#define NH_TC32HD_STORES_WIDE 2
+#endif
+constexpr int kTc32hdStoresNarrow = NH_TC32HD_STORES_NARROW;   // ctu_chain32_h<TSTORE>: 4 level-row + 2 recon-row stores
+constexpr int kTc32hdStoresWide = NH_TC32HD_STORES_WIDE;       // the wide mark and the wide flag (never null here)
 template <int KB>
 __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
     __shared__ __attribute__((aligned(16))) int16_t s_body[4][2][32 * 32];
@@ -1132,7 +1142,9 @@ __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
     __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * Strip<32>::QH];
     __shared__ BasisH s_basis;
     __shared__ __attribute__((aligned(16))) int32_t s_out[4][32 * kOutP];
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the wave index in an SGPR: block index, `next` and the loop are scalar
+    // branches, so one wave never runs both sides of a block's wait selection
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int b0 = ((int)blockIdx.x * 4 + wv) * KB, pz = (int)blockIdx.y;
     const int64_t poff = plane_off(a, pz);
     const int16_t* src = a.src + poff;
@@ -1149,7 +1161,7 @@ __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
         if (lane < 32) glds2(blk + (int64_t)lane * a.pitch - (sx0 > 0 ? 1 : 0), lds_addr(&s_edge[wv][slot][32]));
     };
     issue(b0, 0);
-    int prev = 0;   // store instructions the previous block issued (0: none, 1: a wide mark, 6: a chain)
+    int prev = 0;   // store instructions the previous block issued (0: none, kTc32hdStoresWide, kTc32hdStoresNarrow)
     for (int k = 0; k < KB; ++k) {
         const int b = b0 + k;
         if (b >= nblk) break;
@@ -1162,11 +1174,11 @@ __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
         // retire block b's DMA: it was issued before the previous block's stores and block b+1's DMA
         if (next) {
             if (prev == kTc32hdStoresNarrow) wait_vm<4 + kTc32hdStoresNarrow>();
-            else if (prev == 1) wait_vm<5>();
+            else if (prev == kTc32hdStoresWide) wait_vm<4 + kTc32hdStoresWide>();
             else wait_vm<4>();
         } else {
             if (prev == kTc32hdStoresNarrow) wait_vm<kTc32hdStoresNarrow>();
-            else if (prev == 1) wait_vm<1>();
+            else if (prev == kTc32hdStoresWide) wait_vm<kTc32hdStoresWide>();
             else wait_vm<0>();
         }
         const int sx0 = (b % a.strips_x) * 32, sy0 = (b / a.strips_x) * 32;
@@ -1185,9 +1197,9 @@ __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
         if (wide) {
             if (lane == 0) {
                 a.rec[poff + (int64_t)sy0 * a.pitch + sx0] = kWideMark;
-                if (a.wide_flag) *a.wide_flag = a.epoch;   // the fix-up launch has work
+                *a.wide_flag = a.epoch;   // the fix-up launch has work
             }
-            prev = 1;
+            prev = kTc32hdStoresWide;
         } else {
             ctu_chain32_h<true>(a, ImgDma{body, edge}, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff, s_out[wv]);
             prev = kTc32hdStoresNarrow;
@@ -1369,6 +1381,10 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
     a.epoch = epoch;
     const int nblk = a.strips_x * a.nrows, planes = S.planes_per_group * S.num_groups;
     if (!nblk || !planes) return NH_OK;
+    if (!wide_flag) {   // k_tc32_hd's wait counts assume the wide path's two stores
+        set_error("tc32: the narrow launch needs a wide flag word");
+        return NH_EARG;
+    }
     // capped at 3 resident workgroups per CU (k_tc32_h: 0.137 vs 0.153 ms per 8K YUV420 frame
     // uncapped; k_tc32_hd's 50 KB of LDS allow 3 anyway).  A/B build:
     // NH_TC32H_CAP = workgroups per CU, NH_TC32H_K = k_tc32_h blocks per wave (2 / 4),

@@ -1,0 +1,76 @@
+"""Hand-counted hardware assumptions of the product kernels, checked on the CPU
+against the SHIPPED code object (tools/isa_check.py):
+
+* k_tc32_hd<2> (config 5) retires block k's LDS-DMA image with a hand-counted
+  vmcnt (nh_ctu.hip kTc32hdStoresNarrow / kTc32hdStoresWide): an explicit-state
+  model of the in-order vmcnt queue over the kernel's control flow proves every
+  block wait retires exactly that block's DMA -- and a build with a miscounted
+  constant is caught;
+* every inline-asm v_cvt_rpi / v_cvt_flr that reads an MFMA result directly has
+  the 24 wait states of mfma_result_ready (nh_f16mma.hpp) after the MFMA;
+* the hot kernels use no scratch.
+"""
+import os
+import sys
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import isa_check as ic  # noqa: E402
+
+HOT = ("k_fwd8x8_quant", "k_tc32_hd", "k_tc32_mfma", "k_ctu_open", "k_ctu_wide", "k_tu_closed_pair",
+       "k_intra_rdo8", "k_encode_u8", "k_encode_dcpl", "k_widen", "k_narrow")
+
+
+@pytest.fixture(scope="module")
+def product():
+    if not os.path.exists(ic.LIB):
+        pytest.skip("libnanohevc.so not built (python -c 'import __graft_entry__ as g; g.build()')")
+    return ic.load(ic.LIB)
+
+
+def test_tc32hd_dma_waits_match_the_code(product):
+    funcs, _ = product
+    s = ic.check_dma_waits(funcs[ic.TC32HD])
+    # both block kinds reached a wait, with exactly the counted stores behind them
+    assert s["stores_per_segment"] == [2, 6], s
+    assert {0, 4}.issubset(s["wait_imms"]) and s["block_waits"] >= 3, s
+
+
+@pytest.mark.parametrize("define", ["NH_TC32HD_STORES_NARROW=7", "NH_TC32HD_STORES_NARROW=5",
+                                    "NH_TC32HD_STORES_WIDE=1"])
+def test_tc32hd_miscounted_constant_is_caught(define):
+    """The same kernel built with a wrong store count (UNSAFE for an over-count:
+    the wait leaves the block's DMA in flight; LOOSE for an under-count)."""
+    src = os.path.join(ROOT, "nano-hevc_amd", "csrc", "nh_ctu.hip")
+    with tempfile.TemporaryDirectory() as d:
+        elf = ic.compile_device(src, os.path.join(d, "ctu.o"), [define])
+        funcs = ic.disassemble(elf)
+    with pytest.raises(ic.DmaModelError):
+        ic.check_dma_waits(funcs[ic.TC32HD])
+
+
+def test_mfma_results_read_by_inline_asm_wait(product):
+    funcs, _ = product
+    assert ic.check_mfma_hazard(funcs) > 0   # config 4 / 5 / closed-loop 32x32 chains
+
+
+def test_mfma_hazard_checker_catches_a_short_wait():
+    mk = ic.Insn
+    body = [mk(0, "v_mfma_f32_32x32x16_f16", "v[0:15], v[16:19], v[20:23], 0", None),
+            mk(8, "s_nop", "7", None), mk(12, "s_nop", "7", None),
+            mk(16, "v_cvt_rpi_i32_f32_e32", "v30, v3", None)]
+    with pytest.raises(AssertionError):
+        ic.check_mfma_hazard({"k": body})
+    body.insert(3, mk(14, "s_nop", "7", None))
+    assert ic.check_mfma_hazard({"k": body}) == 1
+
+
+def test_hot_kernels_use_no_scratch(product):
+    _, meta = product
+    sizes = ic.private_segment_sizes(meta)
+    hot = {k: v for k, v in sizes.items() if any(h in k for h in HOT) and "ILi8ELi1ELb1ELi4E" not in k}
+    assert len(hot) >= 20, sorted(hot)
+    assert not {k: v for k, v in hot.items() if v}, "scratch in a hot kernel"
