@@ -188,13 +188,43 @@ extern "C" __attribute__((weak)) int nh_probe_copy8x8_planes(const int16_t* d_in
     return NH_EVALUE;
 }
 
+// The achievable streaming rate the hot kernel is read against (bench.py's
+// roofline context): a linear copy, 16 B per lane, so every
+// wave instruction moves one contiguous KiB, one chunk per thread.
+template <int POLICY>
+__global__ void __launch_bounds__(256) k_copy_stream(const int16_t* __restrict__ in, int16_t* __restrict__ out,
+                                                     int64_t nchunks, int xcd) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    const uint32_t wid = xcd ? xcd_eighths(blockIdx.x, gridDim.x) : blockIdx.x;
+    for (int64_t i = (int64_t)wid * 256 + threadIdx.x; i < nchunks; i += stride)
+        st16<POLICY>(out + i * 8, ld16<POLICY>(in + i * 8));
+}
+
+// Product form: M = 1 with every cache policy and the XCD order; the A/B
+// library's strong definition adds the M > 1 probe shapes.
 extern "C" __attribute__((weak)) int nh_probe_copy_linear(const int16_t* d_in, int16_t* d_out, int64_t nelems, int policy, int grid,
                                     void* stream) {
-    // policy = cache policy (0..3) + 4 * log2(M): M > 1 = k_probe_linear_m (grid ignored)
-    //          + 16: XCD-aware workgroup order (xcd_eighths; M = 1 only)
-    (void)d_in; (void)d_out; (void)nelems; (void)policy; (void)grid; (void)stream;
-    set_error("nh_probe_copy_linear: memory probes are in the A/B library only (make ab)");
-    return NH_EVALUE;
+    // policy = cache policy (0..3, 1 = nontemporal loads + stores) + 4 * log2(M) (M > 1: A/B library only)
+    //          + 16: XCD-aware workgroup order (xcd_eighths)
+    const int xcd = (policy >> 4) & 1, lm = (policy >> 2) & 3;
+    if (policy >> 5 || !d_in || !d_out || nelems < 0 || (nelems & 7)) return NH_EARG;
+    if (lm) {
+        set_error("nh_probe_copy_linear: M > 1 probe shapes are in the A/B library only (make ab)");
+        return NH_EVALUE;
+    }
+    const int64_t chunks = nelems / 8;
+    if (!chunks) return NH_OK;
+    int64_t g = grid > 0 ? grid : (chunks + 255) / 256;
+    if (g > (1 << 30)) g = 1 << 30;
+    hipStream_t s = as_stream(stream);
+    switch (policy & 3) {
+        case 0: k_copy_stream<0><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+        case 1: k_copy_stream<1><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+        case 2: k_copy_stream<2><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+        default: k_copy_stream<3><<<(unsigned)g, 256, 0, s>>>(d_in, d_out, chunks, xcd); break;
+    }
+    NH_HIP(hipGetLastError());
+    return NH_OK;
 }
 
 extern "C" int nh_fwd8x8_quant_planes_ex(const int16_t* d_res, int16_t* d_lvl, const nh_plane_set* sets, int nsets,

@@ -1017,10 +1017,9 @@ def test_tu_pipeline_closed_pairs_many_frames_vs_oracle(nh, torch_dev):
 @pytest.mark.parametrize("lead", [1, 2])
 def test_tu_pipeline_closed_pairs_offset_planes_vs_oracle(nh, torch_dev, lead):
     """The pair form with the plane sets starting `lead` samples into the buffer:
-    lead 1 (odd base: 2-B aligned rows) takes the global-load source path and
-    the packed 32x32 chain, lead 2 (4-B aligned) the LDS-DMA staged source and
-    the packed 32x32 chain (the f16 matrix-core chain needs 16-B level rows);
-    both equal the oracle, and the leading samples stay untouched."""
+    lead 1 (odd base: 2-B aligned rows) and lead 2 (4-B aligned) both take the
+    packed 32x32 chain (the f16 matrix-core chain needs 16-B level rows); both
+    equal the oracle, and the leading samples stay untouched."""
     torch = torch_dev
     from nano_hevc import gpu
     F, W, H, qp = 3, 104, 72, 30
