@@ -1291,8 +1291,7 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         if (ngrp * planes > INT32_MAX) return NH_EARG;
         const int items = (int)(ngrp * planes);
         const dim3 grid((unsigned)ngrp, (unsigned)planes);
-        const int cap_wgs = cap_knob > 0 ? cap_knob
-                          : ctb == 32 ? (GSZ == 4 ? 3 : 2) : (GSZ == 4 ? 4 : GSZ == 6 ? 3 : 2);
+        const int cap_wgs = cap_knob > 0 ? cap_knob : GSZ == 4 ? 3 : 2;   // (CTB <= 16: the LDS allows 3 anyway)
         if (NH_AB != 0 && persist) {
             int cus = 0, per_cu = 0;
             NH_TRY(device_cus(&cus));
@@ -1319,22 +1318,23 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
                          : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>, G4{})
                          : gs_knob == 6 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 6>, std::integral_constant<int, 6>{})
                          : gs_knob == 8 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 8>, std::integral_constant<int, 8>{})
-                         : ost_on       ? launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4, true>, G4{})
-                                        : launch_open(k_ctu_open<C, L, M32, 0, C == 32 ? 3 : 4, 4>, G4{});
+                         : ost_on       ? launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true>, G4{})
+                                        : launch_open(k_ctu_open<C, L, M32, 0, 3, 4>, G4{});
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>, G4{})
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>, G4{})
                        : gs_knob == 6 ? launch_open(k_ctu_open<C, L, false, 0, 5, 6>, std::integral_constant<int, 6>{})
                        : gs_knob == 8 ? launch_open(k_ctu_open<C, L, false, 0, 5, 8>, std::integral_constant<int, 8>{})
-                                      : launch_open(k_ctu_open<C, L, false, 0, C == 32 ? 3 : 4, 4>, G4{});
+                                      : launch_open(k_ctu_open<C, L, false, 0, 3, 4>, G4{});
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else {
-            // register budget = the occupancy the cap allows (3 / 4 waves per SIMD); chroma
-            // (CTB 16) writes its outputs through LDS images in whole rows: 36.8-37.5 vs
-            // 37.7-38.3 us per 4K YUV420 frame, luma does not gain (40.0-40.5,
-            // profiles/r03/cfg4/ab_ctu_ost.jsonl)
+            // register budget = the occupancy the LDS allows: 3 waves per SIMD (luma: the
+            // cap; chroma (CTB 16): its ~45 KB of LDS -- the strip images plus the output
+            // images through which it writes whole rows: 36.8-37.5 vs 37.7-38.3 us per 4K
+            // YUV420 frame, luma does not gain (40.0-40.5, profiles/r03/cfg4/ab_ctu_ost.jsonl)
+            // -- fit 3 workgroups per CU)
             if constexpr (C == 32) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4>, G4{});
-            else rc3 = launch_open(k_ctu_open<C, L, M32, 0, 4, 4, true>, G4{});
+            else rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true>, G4{});
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         }
         return rc3;
