@@ -52,6 +52,7 @@ namespace nh {
 __constant__ Basis c_basis_ctu;
 
 __constant__ BasisH c_basis_h;
+__constant__ BasisHC c_basis_hc;   // chain32_tf's crow-permuted bases (config 5)
 
 struct CtuArgs {
     const int16_t* src;
@@ -473,6 +474,12 @@ __device__ __forceinline__ void copy_basis_h(BasisH& dst) {
     constexpr int n = (int)(sizeof(BasisH) / 16);
     for (int i = threadIdx.x; i < n; i += blockDim.x) d4[i] = s4[i];
 }
+__device__ __forceinline__ void copy_basis_hc(BasisHC& dst) {
+    const uint4* s4 = (const uint4*)&c_basis_hc;
+    uint4* d4 = (uint4*)&dst;
+    constexpr int n = (int)(sizeof(BasisHC) / 16);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) d4[i] = s4[i];
+}
 // TSTORE: the level and recon rows leave through an LDS tile `ot` (per wave,
 // kOutP int32 per row) so that every global store instruction writes whole
 // rows -- 8 rows of 128 B (levels), 16 rows of 64 B (recon) -- instead of 32-B
@@ -496,6 +503,11 @@ struct ImgDma {
     __device__ __forceinline__ int32_t at(int y, int x) const { return body[y * 32 + x]; }
     __device__ __forceinline__ int32_t top(int x) const { return edge[x]; }
     __device__ __forceinline__ int32_t left(int y) const { return edge[32 + 2 * y]; }
+    // column x from row y0 on (element stride RS) and the left column from row y0 on (stride LS):
+    // constant row offsets then sit in the LDS instructions' immediate offsets
+    static constexpr int RS = 32, LS = 2;
+    __device__ __forceinline__ const int16_t* colp(int x, int y0) const { return body + y0 * 32 + x; }
+    __device__ __forceinline__ const int16_t* leftp(int y0) const { return edge + 32 + 2 * y0; }
 };
 template <bool TSTORE = false, class B = BasisH, class IMG = ImgStrip>
 __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, uint16_t* qt, const B& bs,
@@ -614,6 +626,212 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, 
             const int rr = (l >> 2) + 16 * i, c = 4 * (l & 3);
             *(uint4*)(rec + (int64_t)(gy0 + rr) * op + gx0 + 2 * c) = *(const uint4*)&ot[rr * kRecP + c];
         }
+    }
+}
+
+// A 32x32 block of an 8-bit stream on the f16 matrix cores WITHOUT a transpose
+// (round 5, config 5): every one of the four passes takes the previous pass's
+// output as its A operand straight from the accumulator registers -- each MFMA
+// output has its column index in the lanes and its row index in the registers,
+// the row index is the next pass's contraction index, and the bases are stored
+// crow-permuted (BasisHC) to match.  The data then walks
+//   X[n][x] (lane x) -> tmp[k][x] (lane k) -> C[k][l] (lane l) -> tmp'[y][l]
+//   (lane y) -> R[y][x] (lane x),
+// ending in the input's own layout, so the reconstruction adds the prediction
+// pairs kept from the residual stage.
+//
+// Between passes floor(acc + 0.5) (the arithmetic shift of transform.py:185)
+// becomes an f16 operand in ONE v_cvt_pkrtz_f16_f32 per pair: the accumulators
+// start at 0.5 (an inline constant), the value is moved into the binade [1024,
+// 2048) -- where f16 holds every integer and nothing between -- by adding 1536,
+// and there, all values being positive, rounding toward zero IS the floor.
+// Every operand is then 1536 + v, and the offsets are exact integers the next
+// pass turns into known constants:
+//  * the residual enters as the f16 of n + 768 (bits 0x6200 + 2n, |n| <= 255);
+//    DCT row 0 sums it to tmp[0][x] + 1536 (every other row sums to 0), so row
+//    k = 0's lanes add 0 instead of 1536 (kTfAdd1);
+//  * pass 2 of 1536 + tmp1 leaves +3072 on column l = 0 (row sums again): the
+//    quantizer of lanes l = 0 compares and rounds against it (QuantTf);
+//  * the dequantized coefficients enter as 1536 + d (the fma's bias), and the
+//    inverse passes leave 1.5 * S on their outputs, S[y] = sum_k T[k][y] (a
+//    column sum, even): lane y adds 1536 - 1.5 S[y] before converting, lane x
+//    subtracts 1.5 S[x] from its prediction pairs at the reconstruction.
+// Every pass's operands are integers <= 2046 against the basis * 2^-10, so each
+// product is exact in fp32 and every partial sum a multiple of 2^-10 below 2^13:
+// the accumulators hold the reference's integer sums exactly.
+constexpr int kRecH = 2 * kRecP;   // recon tile row pitch in int16
+// A per-lane 32-bit byte offset the compiler keeps as one VGPR: base (SGPRs) +
+// zext(offset) selects the global_store v_off, s[base] form.
+__device__ __forceinline__ uint64_t vofs(uint32_t o) {
+    asm("" : "+v"(o));
+    return (uint64_t)o;
+}
+typedef float f2_t __attribute__((ext_vector_type(2)));
+// (floor a, floor b) as an f16 pair, for a, b > 0 (truncation)
+__device__ __forceinline__ uint32_t pk_trunc_h(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+// floor(acc[8s .. 8s+7] + add) as f16; every value is positive
+__device__ __forceinline__ h8_t cvt_h8(const f16x_t& acc, int s, float add) {
+    uint32_t u[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+        const f2_t x = (f2_t){acc[8 * s + e], acc[8 * s + e + 1]} + (f2_t){add, add};
+        u[e / 2] = pk_trunc_h(x.x, x.y);
+    }
+    return __builtin_bit_cast(h8_t, make_uint4(u[0], u[1], u[2], u[3]));
+}
+__device__ __forceinline__ int32_t floor_i32(float x) {   // v_cvt_flr_i32_f32 (after mfma_result_ready)
+    int32_t r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// The per-lane constants of chain32_tf (lane r = lane & 31), made once per wave.
+struct TfLane {
+    float add1;        // pass 1 -> 2: 1536, 0 on row k = 0 (already 1536 from the residual's 768)
+    float add3;        // inverse 1 -> 2: 1536 - 1.5 S[y]
+    float add4;        // inverse 2 -> reconstruction: 1536 - 1.5 S[x]
+    int32_t fix;       // quantizer: the +3072 of column l = 0
+    uint32_t h_v, hneg_v;   // quant_s's rounding words minus fix * m'
+};
+__device__ __forceinline__ TfLane make_tf_lane(const ChainQ& cq, const BasisHC& bs, int r) {
+    const int32_t s = bs.csum[r];   // S[r] = sum_k T[k][r] (even)
+    TfLane t;
+    t.add1 = r == 0 ? 0.0f : 1536.0f;
+    t.add3 = 1536.0f - 1.5f * (float)s;
+    t.add4 = t.add3;
+    t.fix = r == 0 ? 3072 : 0;
+    t.h_v = cq.h_v - (uint32_t)(t.fix * cq.qs.mh);
+    t.hneg_v = cq.hneg_v - (uint32_t)(t.fix * cq.qs.mh);
+    return t;
+}
+// quant_s against the lane's offset: c = c_off - fix; the sign test compares with
+// fix and the rounding words absorb -fix * m' (|c_off * m'| < 2^31: exact)
+__device__ __forceinline__ int32_t quant_tf(int32_t c_off, const QuantS& q, const TfLane& t) {
+    int32_t r;
+    asm("v_cmp_gt_i32_e32 vcc, %6, %1\n\t"
+        "v_cndmask_b32_e32 %0, %2, %3, vcc\n\t"
+        "v_mad_i32_i24 %0, %1, %4, %0\n\t"
+        "v_ashrrev_i32_e32 %0, %5, %0"
+        : "=&v"(r)
+        : "v"(c_off), "v"(t.h_v), "v"(t.hneg_v), "s"(q.mh), "s"(q.sh), "v"(t.fix)
+        : "vcc");
+    return r;
+}
+template <class IMG>
+__device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, const BasisHC& bs, int gx0, int gy0,
+                                           int32_t* __restrict__ lvl, int16_t* __restrict__ rec, int32_t* ot,
+                                           const ChainQ& cq, const TfLane& tl) {
+    const int64_t op = a.pitch;
+    const int l = opaque_lane(), r = l & 31, hh = l >> 5;
+    const int32_t topr = img.top(r), tr = img.top(31), bl = img.left(31);
+    int32_t sdc = hh ? img.left(r) : topr;   // DC (intra.py:46-62): lane halves hold top / left
+    sdc = grp_sum<64>(sdc);
+    const int32_t dc = (sdc + 32) >> 6;
+    const pk16 dc2 = pk_splat(dc);
+    // column x = r, row pairs (y_p, y_p + 1), y_p = crow(2p, hh) = c_p + 4 hh: the pass-1 A operand in
+    // register order.  Planar (intra.py:81-113) at (y, r): (31 - r) left[y] + b(y) >> 6 with
+    // b(y) = (r + 1) tr + (31 - y) top[r] + (y + 1) bl + 32 = b(4 hh) + (y - 4 hh) (bl - top[r]).
+    pk16 o2[8];
+    pku16 pl2[8];
+    {
+        const int16_t* col = img.colp(r, 4 * hh);
+        const int16_t* lft = img.leftp(4 * hh);
+        constexpr int RS = IMG::RS, LS = IMG::LS;
+        const pku16 wl = {(unsigned short)(31 - r), (unsigned short)(31 - r)}, sh = {6, 6};
+        const int32_t d = bl - topr, b0 = (r + 1) * tr + (31 - 4 * hh) * topr + (4 * hh + 1) * bl + 32;
+        const pku16 d2 = {(unsigned short)d, (unsigned short)d}, bb0 = {(unsigned short)b0, (unsigned short)(b0 + d)};
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int c = 2 * (p & 1) + 8 * (p >> 1);   // y_p - 4 hh
+            o2[p] = (pk16){col[c * RS], col[(c + 1) * RS]};
+            const pku16 lf = {(unsigned short)lft[c * LS], (unsigned short)lft[(c + 1) * LS]};
+            pl2[p] = (lf * wl + (bb0 + (pku16){(unsigned short)c, (unsigned short)c} * d2)) >> sh;
+        }
+    }
+    int32_t ed = 0, ep = 0;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const pk16 d0 = o2[p] - dc2, d1 = o2[p] - __builtin_bit_cast(pk16, pl2[p]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+    }
+    ed = grp_sum<64>(ed);
+    ep = grp_sum<64>(ep);
+    const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+    pk16 pr2[8];                    // the chosen prediction - 0x6600 (the f16 bits of 1536)
+    uint32_t hx[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[p]);
+        const pku16 rr = __builtin_bit_cast(pku16, o2[p] - pr);   // residual, intra.py:65-67
+        hx[p] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of n + 768
+        pr2[p] = pr - pk_splat(0x6600);
+    }
+    const h8_t tc0 = ld_h8(&bs.tc[r][8 * hh]), tc1 = ld_h8(&bs.tc[r][16 + 8 * hh]);
+    // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x] (+ 1536 on k = 0) + 0.5, lane k, registers x
+    f16x_t acc = splat16(0.5f);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
+                                                 tc0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
+                                                 tc1, acc, 0, 0, 0);
+    // pass 2 (transform.py:188-194): D2[k][l] = C[k][l] (+ 3072 on l = 0) + 0.5, lane l, registers k
+    f16x_t acc2 = splat16(0.5f);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc, 0, tl.add1), tc0, acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc, 1, tl.add1), tc1, acc2, 0, 0, 0);
+    mfma_result_ready(acc2);   // before floor_i32's inline-asm reads
+    // quantize_block (levels into the tile: row k, column l) and dequantize_block
+    // in fp32 (l * dqs * 2^-dqsh (+ 0.5 when it rounds) + 1536 is exact; its f16, the floor)
+    const float dqf = (float)cq.dqs * __builtin_bit_cast(float, (127 - cq.dqsh) << 23);
+    const float dqb = (cq.dqsh ? 0.5f : 0.0f) + 1536.0f;
+    uint32_t dq[8];
+#pragma unroll
+    for (int g = 0; g < 16; g += 2) {
+        const int32_t L0 = quant_tf(floor_i32(acc2[g]), cq.qs, tl), L1 = quant_tf(floor_i32(acc2[g + 1]), cq.qs, tl);
+        ot[crow(g, hh) * kOutP + r] = L0;
+        ot[crow(g + 1, hh) * kOutP + r] = L1;
+        dq[g / 2] = pk_trunc_h(__builtin_fmaf((float)L0, dqf, dqb), __builtin_fmaf((float)L1, dqf, dqb));
+    }
+    wave_sync();
+    // the block's rows from a uniform base (SGPRs) at 32-bit per-lane byte offsets
+    char* lb = (char*)(lvl + (int64_t)gy0 * op + gx0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // 4 instructions of 8 whole 128-B level rows
+        const int rr = (l >> 3) + 8 * i, c = 4 * (l & 7);
+        *(int4*)(lb + vofs((rr * (int32_t)op + c) * 4)) = *(const int4*)&ot[rr * kOutP + c];
+    }
+    wave_sync();   // the tile's reads before the recon tile reuses it
+    const h8_t tt0 = ld_h8(&bs.ttc[r][8 * hh]), tt1 = ld_h8(&bs.ttc[r][16 + 8 * hh]);
+    // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp'[y][l] + 1.5 S[y] + 0.5, lane y, registers l
+    f16x_t acc3 = splat16(0.5f);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(dq[0], dq[1], dq[2], dq[3])),
+                                                  tt0, acc3, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(dq[4], dq[5], dq[6], dq[7])),
+                                                  tt1, acc3, 0, 0, 0);
+    // inverse pass 2 (transform.py:230-236): D4[y][x] = R[y][x] + 1.5 S[x] + 0.5, lane x, registers y
+    f16x_t acc4 = splat16(0.5f);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc3, 0, tl.add3), tt0, acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc3, 1, tl.add3), tt1, acc4, 0, 0, 0);
+    // reconstruct + clip (intra.py:70-78): rows (y_p, y_p + 1) of column x = r.  The f16 bits of
+    // floor(1536 + R + 0.5) are 0x6600 + R for |R| < 512; beyond that (|R| <= 920 for 8-bit blocks:
+    // 327 * sum |T[l][x]| / 1024, so the value stays positive) they stay monotone and on the right
+    // side of 0x6600 +- 512, so the clip to [0, 255] still gives clip(pred + R).
+    int16_t* rt = (int16_t*)ot;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const int y = 2 * (p & 1) + 8 * (p >> 1) + 4 * hh;
+        const f2_t x = (f2_t){acc4[2 * p], acc4[2 * p + 1]} + (f2_t){tl.add4, tl.add4};
+        pk16 v = __builtin_bit_cast(pk16, pk_trunc_h(x.x, x.y)) + pr2[p];
+        v = __builtin_elementwise_min(__builtin_elementwise_max(v, pk_splat(0)), pk_splat(255));
+        rt[y * kRecH + r] = v.x;
+        rt[(y + 1) * kRecH + r] = v.y;
+    }
+    wave_sync();
+    char* rb = (char*)(rec + (int64_t)gy0 * op + gx0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {   // 2 instructions of 16 whole 64-B recon rows
+        const int rr = (l >> 2) + 16 * i, c = 4 * (l & 3);
+        *(uint4*)(rb + vofs((rr * (int32_t)op + 2 * c) * 2)) = *(const uint4*)&ot[rr * kRecP + c];
     }
 }
 
@@ -1136,11 +1354,10 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
 constexpr int kTc32hdStoresNarrow = NH_TC32HD_STORES_NARROW;   // ctu_chain32_h<TSTORE>: 4 level-row + 2 recon-row stores
 constexpr int kTc32hdStoresWide = NH_TC32HD_STORES_WIDE;       // the wide mark and the wide flag (never null here)
 template <int KB>
-__global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_tc32_hd(CtuArgs a, int nblk) {
     __shared__ __attribute__((aligned(16))) int16_t s_body[4][2][32 * 32];
     __shared__ __attribute__((aligned(16))) int16_t s_edge[4][2][96];
-    __shared__ __attribute__((aligned(16))) uint16_t s_q[4][32 * Strip<32>::QH];
-    __shared__ BasisH s_basis;
+    __shared__ BasisHC s_basis;
     __shared__ __attribute__((aligned(16))) int32_t s_out[4][32 * kOutP];
     // the wave index in an SGPR: block index, `next` and the loop are scalar
     // branches, so one wave never runs both sides of a block's wait selection
@@ -1148,17 +1365,21 @@ __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
     const int b0 = ((int)blockIdx.x * 4 + wv) * KB, pz = (int)blockIdx.y;
     const int64_t poff = plane_off(a, pz);
     const int16_t* src = a.src + poff;
-    copy_basis_h(s_basis);
+    const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
+    copy_basis_hc(s_basis);
     __syncthreads();   // (before any DMA is in flight)
+    const TfLane tl = make_tf_lane(cq, s_basis, lane & 31);   // chain32_tf's per-lane offsets
     if (b0 >= nblk) return;   // whole wave
+    // per-lane byte offsets of the DMA pieces from the block's (uniform) origin
+    const uint32_t o_body = (uint32_t)(((lane >> 2) * a.pitch + 8 * (lane & 3)) * 2), o_body2 = 16u * a.pitch * 2;
+    const uint32_t o_top = 16u * lane, o_left = (uint32_t)(lane * a.pitch * 2);
     auto issue = [&](int b, int slot) {   // 4 DMA instructions per block
         const int sx0 = (b % a.strips_x) * 32, sy0 = (b / a.strips_x) * 32;
         const int16_t* blk = src + (int64_t)sy0 * a.pitch + sx0;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-            glds16(blk + (int64_t)((lane >> 2) + 16 * i) * a.pitch + 8 * (lane & 3), lds_addr(&s_body[wv][slot][512 * i]));
-        if (lane < 4) glds16(blk - (sy0 > 0 ? (int64_t)a.pitch : 0) + 8 * lane, lds_addr(&s_edge[wv][slot][0]));
-        if (lane < 32) glds2(blk + (int64_t)lane * a.pitch - (sx0 > 0 ? 1 : 0), lds_addr(&s_edge[wv][slot][32]));
+        glds16s(blk, o_body, lds_addr(&s_body[wv][slot][0]));
+        glds16s(blk, o_body + o_body2, lds_addr(&s_body[wv][slot][512]));
+        if (lane < 4) glds16s(blk - (sy0 > 0 ? (int64_t)a.pitch : 0), o_top, lds_addr(&s_edge[wv][slot][0]));
+        if (lane < 32) glds2s(blk - (sx0 > 0 ? 1 : 0), o_left, lds_addr(&s_edge[wv][slot][32]));
     };
     issue(b0, 0);
     int prev = 0;   // store instructions the previous block issued (0: none, kTc32hdStoresWide, kTc32hdStoresNarrow)
@@ -1201,7 +1422,7 @@ __global__ void __launch_bounds__(256) k_tc32_hd(CtuArgs a, int nblk) {
             }
             prev = kTc32hdStoresWide;
         } else {
-            ctu_chain32_h<true>(a, ImgDma{body, edge}, s_q[wv], s_basis, sx0, sy0, a.lvl + poff, a.rec + poff, s_out[wv]);
+            chain32_tf(a, ImgDma{body, edge}, s_basis, sx0, sy0, a.lvl + poff, a.rec + poff, s_out[wv], cq, tl);
             prev = kTc32hdStoresNarrow;
         }
         wave_sync();
@@ -1220,6 +1441,8 @@ static int ensure_basis_ctu() {
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_ctu), &b, sizeof(b)));
         const BasisH bh = make_basis_h();
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_h), &bh, sizeof(bh)));
+        const BasisHC bhc = make_basis_hc();
+        NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_hc), &bhc, sizeof(bhc)));
         return (int)NH_OK;
     });
 }

@@ -30,6 +30,34 @@ inline BasisH make_basis_h() {
     return b;
 }
 
+// The crow-permuted bases of the transposition-free chain (chain32_tf, round 5):
+// for basis row r, MFMA slice s (k range 16s..16s+15) and lane half h, the 8
+// halves [16s + 8h, +8) are the basis elements at crow(8s + e, h), e = 0..7 --
+// the accumulator row order -- so every pass takes the previous pass's output as
+// its A operand in registers, with one 16-B LDS read per basis operand.
+struct BasisHC {
+    uint16_t tc[32][32];         // [r][16s + 8h + e] = T[r][crow(8s + e, h)]   passes 1 and 2 (lane k / lane l)
+    uint16_t ttc[32][32];        // [r][16s + 8h + e] = T[crow(8s + e, h)][r]   inverse passes (lane y / lane x)
+    int32_t csum[32];            // S[r] = sum_k T[k][r], the column sums (even)
+};
+inline BasisHC make_basis_hc() {
+    auto h = [](int v) { return __builtin_bit_cast(uint16_t, (_Float16)((float)v / 1024.0f)); };
+    BasisHC b;
+    for (int r = 0; r < 32; ++r)
+        for (int s = 0; s < 2; ++s)
+            for (int hh = 0; hh < 2; ++hh)
+                for (int e = 0; e < 8; ++e) {
+                    const int c = (e & 3) + 16 * s + 8 * (e >> 2) + 4 * hh;   // crow(8s + e, hh)
+                    b.tc[r][16 * s + 8 * hh + e] = h(dct32(r, c));
+                    b.ttc[r][16 * s + 8 * hh + e] = h(dct32(c, r));
+                }
+    for (int r = 0; r < 32; ++r) {
+        b.csum[r] = 0;
+        for (int k = 0; k < 32; ++k) b.csum[r] += dct32(k, r);
+    }
+    return b;
+}
+
 typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
 typedef float f16x_t __attribute__((ext_vector_type(16)));
 
