@@ -508,6 +508,12 @@ struct ImgDma {
     static constexpr int RS = 32, LS = 2;
     __device__ __forceinline__ const int16_t* colp(int x, int y0) const { return body + y0 * 32 + x; }
     __device__ __forceinline__ const int16_t* leftp(int y0) const { return edge + 32 + 2 * y0; }
+    // ds_read_b64_tr_b16 (T10): lane L receives rows 8t + 4hh .. +3 of column L & 31 (hh = L >> 5)
+    // as two (row, row + 1) pairs; lane 4q + p of each 16-lane group addresses row q, columns 4p..4p+3
+    // of its group's 16 columns.  EXEC must be all ones.
+    __device__ __forceinline__ const int16_t* trp(int L) const {
+        return body + (4 * (L >> 5) + ((L >> 2) & 3)) * 32 + 16 * ((L >> 4) & 1) + 4 * (L & 3);
+    }
 };
 template <bool TSTORE = false, class B = BasisH, class IMG = ImgStrip>
 __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, uint16_t* qt, const B& bs,
@@ -735,17 +741,25 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
     pk16 o2[8];
     pku16 pl2[8];
     {
-        const int16_t* col = img.colp(r, 4 * hh);
-        const int16_t* lft = img.leftp(4 * hh);
-        constexpr int RS = IMG::RS, LS = IMG::LS;
+        typedef short v4s __attribute__((ext_vector_type(4)));
+        typedef __attribute__((address_space(3))) v4s lds_v4s;
+        lds_v4s* tp = (lds_v4s*)(lds_void_t*)img.trp(l);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {   // rows 8t + 4hh .. +3 of column r: o2[2t], o2[2t + 1]
+            const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(tp + 64 * t);
+            o2[2 * t] = (pk16){v[0], v[1]};
+            o2[2 * t + 1] = (pk16){v[2], v[3]};
+        }
+        // left[y], left[y + 1]: one dword each (the 16-bit LDS-DMA's layout), read as one pair
+        const uint2* lft = (const uint2*)img.leftp(4 * hh);
         const pku16 wl = {(unsigned short)(31 - r), (unsigned short)(31 - r)}, sh = {6, 6};
         const int32_t d = bl - topr, b0 = (r + 1) * tr + (31 - 4 * hh) * topr + (4 * hh + 1) * bl + 32;
         const pku16 d2 = {(unsigned short)d, (unsigned short)d}, bb0 = {(unsigned short)b0, (unsigned short)(b0 + d)};
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
             const int c = 2 * (p & 1) + 8 * (p >> 1);   // y_p - 4 hh
-            o2[p] = (pk16){col[c * RS], col[(c + 1) * RS]};
-            const pku16 lf = {(unsigned short)lft[c * LS], (unsigned short)lft[(c + 1) * LS]};
+            const uint2 lw = lft[c / 2];   // (c is even: left[y_p] is dword 4 hh + c)
+            const pku16 lf = __builtin_bit_cast(pku16, __builtin_amdgcn_perm(lw.y, lw.x, 0x05040100u));
             pl2[p] = (lf * wl + (bb0 + (pku16){(unsigned short)c, (unsigned short)c} * d2)) >> sh;
         }
     }
@@ -759,14 +773,14 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
     ed = grp_sum<64>(ed);
     ep = grp_sum<64>(ep);
     const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
-    pk16 pr2[8];                    // the chosen prediction - 0x6600 (the f16 bits of 1536)
+    pku16 pr2[8];                   // 0x6600 (the f16 bits of 1536) - the chosen prediction
     uint32_t hx[8];
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
         const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[p]);
         const pku16 rr = __builtin_bit_cast(pku16, o2[p] - pr);   // residual, intra.py:65-67
         hx[p] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of n + 768
-        pr2[p] = pr - pk_splat(0x6600);
+        pr2[p] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
     }
     const h8_t tc0 = ld_h8(&bs.tc[r][8 * hh]), tc1 = ld_h8(&bs.tc[r][16 + 8 * hh]);
     // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x] (+ 1536 on k = 0) + 0.5, lane k, registers x
@@ -781,16 +795,17 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
     acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc, 1, tl.add1), tc1, acc2, 0, 0, 0);
     mfma_result_ready(acc2);   // before floor_i32's inline-asm reads
     // quantize_block (levels into the tile: row k, column l) and dequantize_block
-    // in fp32 (l * dqs * 2^-dqsh (+ 0.5 when it rounds) + 1536 is exact; its f16, the floor)
-    const float dqf = (float)cq.dqs * __builtin_bit_cast(float, (127 - cq.dqsh) << 23);
-    const float dqb = (cq.dqsh ? 0.5f : 0.0f) + 1536.0f;
+    // on level pairs in 16 bits ((l * dqs + dqr) >> dqsh: |l * dqs| < 2^15 for 8-bit
+    // blocks), entering inverse pass 1 as the f16 bits of 1536 + d (0x6600 + d, |d| < 512)
+    const pk16 dqs2 = pk_splat(cq.dqs), dqr2 = pk_splat((int32_t)cq.dqr_v), dqsh2 = pk_splat(cq.dqsh);
     uint32_t dq[8];
 #pragma unroll
     for (int g = 0; g < 16; g += 2) {
         const int32_t L0 = quant_tf(floor_i32(acc2[g]), cq.qs, tl), L1 = quant_tf(floor_i32(acc2[g + 1]), cq.qs, tl);
         ot[crow(g, hh) * kOutP + r] = L0;
         ot[crow(g + 1, hh) * kOutP + r] = L1;
-        dq[g / 2] = pk_trunc_h(__builtin_fmaf((float)L0, dqf, dqb), __builtin_fmaf((float)L1, dqf, dqb));
+        const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
+        dq[g / 2] = __builtin_bit_cast(uint32_t, ((l2 * dqs2 + dqr2) >> dqsh2) + pk_splat(0x6600));
     }
     wave_sync();
     // the block's rows from a uniform base (SGPRs) at 32-bit per-lane byte offsets
@@ -821,8 +836,10 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
     for (int p = 0; p < 8; ++p) {
         const int y = 2 * (p & 1) + 8 * (p >> 1) + 4 * hh;
         const f2_t x = (f2_t){acc4[2 * p], acc4[2 * p + 1]} + (f2_t){tl.add4, tl.add4};
-        pk16 v = __builtin_bit_cast(pk16, pk_trunc_h(x.x, x.y)) + pr2[p];
-        v = __builtin_elementwise_min(__builtin_elementwise_max(v, pk_splat(0)), pk_splat(255));
+        // bits - (0x6600 - pred), saturating at 0 (unsigned), then min 255: the clip of pred + R
+        const pku16 v = __builtin_elementwise_min(
+            __builtin_elementwise_sub_sat(__builtin_bit_cast(pku16, pk_trunc_h(x.x, x.y)), pr2[p]),
+            (pku16){255, 255});
         rt[y * kRecH + r] = v.x;
         rt[(y + 1) * kRecH + r] = v.y;
     }
