@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include "nh_common.hpp"
 #include "nh_mfma.hpp"
+#include "nh_packed.hpp"
 
 namespace nh {
 
@@ -146,6 +147,120 @@ __device__ __forceinline__ f16x_t splat16(float v) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) r[g] = v;
     return r;
+}
+
+typedef float f2_t __attribute__((ext_vector_type(2)));
+// (floor a, floor b) as an f16 pair, for a, b > 0 (truncation)
+__device__ __forceinline__ uint32_t pk_trunc_h(float a, float b) {
+    return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+}
+// floor(acc[8s .. 8s+7] + add) as f16; every value is positive
+__device__ __forceinline__ h8_t cvt_h8(const f16x_t& acc, int s, float add) {
+    uint32_t u[4];
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+        const f2_t x = (f2_t){acc[8 * s + e], acc[8 * s + e + 1]} + (f2_t){add, add};
+        u[e / 2] = pk_trunc_h(x.x, x.y);
+    }
+    return __builtin_bit_cast(h8_t, make_uint4(u[0], u[1], u[2], u[3]));
+}
+__device__ __forceinline__ int32_t floor_i32(float x) {   // v_cvt_flr_i32_f32 (after mfma_result_ready)
+    int32_t r;
+    asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+// The per-lane constants of chain32_tf (lane r = lane & 31), made once per wave.
+struct TfLane {
+    float add1;        // pass 1 -> 2: 1536, 0 on row k = 0 (already 1536 from the residual's 768)
+    float add3;        // inverse 1 -> 2: 1536 - 1.5 S[y]
+    float add4;        // inverse 2 -> reconstruction: 1536 - 1.5 S[x]
+    int32_t fix;       // quantizer: the +3072 of column l = 0
+    uint32_t h_v, hneg_v;   // quant_s's rounding words minus fix * m'
+};
+__device__ __forceinline__ TfLane make_tf_lane(const ChainQ& cq, const BasisHC& bs, int r) {
+    const int32_t s = bs.csum[r];   // S[r] = sum_k T[k][r] (even)
+    TfLane t;
+    t.add1 = r == 0 ? 0.0f : 1536.0f;
+    t.add3 = 1536.0f - 1.5f * (float)s;
+    t.add4 = t.add3;
+    t.fix = r == 0 ? 3072 : 0;
+    t.h_v = cq.h_v - (uint32_t)(t.fix * cq.qs.mh);
+    t.hneg_v = cq.hneg_v - (uint32_t)(t.fix * cq.qs.mh);
+    return t;
+}
+// quant_s against the lane's offset: c = c_off - fix; the sign test compares with
+// fix and the rounding words absorb -fix * m' (|c_off * m'| < 2^31: exact)
+__device__ __forceinline__ int32_t quant_tf(int32_t c_off, const QuantS& q, const TfLane& t) {
+    int32_t r;
+    asm("v_cmp_gt_i32_e32 vcc, %6, %1\n\t"
+        "v_cndmask_b32_e32 %0, %2, %3, vcc\n\t"
+        "v_mad_i32_i24 %0, %1, %4, %0\n\t"
+        "v_ashrrev_i32_e32 %0, %5, %0"
+        : "=&v"(r)
+        : "v"(c_off), "v"(t.h_v), "v"(t.hneg_v), "s"(q.mh), "s"(q.sh), "v"(t.fix)
+        : "vcc");
+    return r;
+}
+
+// The four passes of the transposition-free chain, shared by the
+// config-5 block kernel (chain32_tf, nh_ctu.hip) and the config-4 closed loop's
+// 32x32 TUs (closed_chain32_tf, nh_intraloop.hip).  In: the residual + 768 as f16
+// pairs hx (lane (r, hh) = column r, rows crow(2p, hh), +1), the chosen prediction
+// as 0x6600 - pred pairs in the same layout.  put_level(g, L): the level of row
+// k = crow(g, hh), column l = r.  mid(): between the quantizer and the inverse
+// passes (e.g. the level rows out of a tile).  Out: the clipped reconstruction
+// pairs, same layout as hx.
+template <class PutLevel, class Mid>
+__device__ __forceinline__ void tf_passes(const uint32_t (&hx)[8], const pku16 (&pr2)[8], const BasisHC& bs,
+                                          const ChainQ& cq, const TfLane& tl, int r, int hh, PutLevel&& put_level,
+                                          Mid&& mid, pku16 (&rec2)[8]) {
+    const h8_t tc0 = ld_h8(&bs.tc[r][8 * hh]), tc1 = ld_h8(&bs.tc[r][16 + 8 * hh]);
+    // pass 1 (transform.py:179-185): D1[x][k] = tmp[k][x] (+ 1536 on k = 0) + 0.5, lane k, registers x
+    f16x_t acc = splat16(0.5f);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[0], hx[1], hx[2], hx[3])),
+                                                 tc0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(hx[4], hx[5], hx[6], hx[7])),
+                                                 tc1, acc, 0, 0, 0);
+    // pass 2 (transform.py:188-194): D2[k][l] = C[k][l] (+ 3072 on l = 0) + 0.5, lane l, registers k
+    f16x_t acc2 = splat16(0.5f);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc, 0, tl.add1), tc0, acc2, 0, 0, 0);
+    acc2 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc, 1, tl.add1), tc1, acc2, 0, 0, 0);
+    mfma_result_ready(acc2);   // before floor_i32's inline-asm reads
+    // quantize_block, and dequantize_block on level pairs in 16 bits ((l * dqs + dqr) >> dqsh:
+    // |l * dqs| < 2^15 for 8-bit blocks), entering inverse pass 1 as the f16 bits of 1536 + d
+    const pk16 dqs2 = pk_splat(cq.dqs), dqr2 = pk_splat((int32_t)cq.dqr_v), dqsh2 = pk_splat(cq.dqsh);
+    uint32_t dq[8];
+#pragma unroll
+    for (int g = 0; g < 16; g += 2) {
+        const int32_t L0 = quant_tf(floor_i32(acc2[g]), cq.qs, tl), L1 = quant_tf(floor_i32(acc2[g + 1]), cq.qs, tl);
+        put_level(g, L0);
+        put_level(g + 1, L1);
+        const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
+        dq[g / 2] = __builtin_bit_cast(uint32_t, ((l2 * dqs2 + dqr2) >> dqsh2) + pk_splat(0x6600));
+    }
+    mid();
+    const h8_t tt0 = ld_h8(&bs.ttc[r][8 * hh]), tt1 = ld_h8(&bs.ttc[r][16 + 8 * hh]);
+    // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp'[y][l] + 1.5 S[y] + 0.5, lane y, registers l
+    f16x_t acc3 = splat16(0.5f);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(dq[0], dq[1], dq[2], dq[3])),
+                                                  tt0, acc3, 0, 0, 0);
+    acc3 = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(h8_t, make_uint4(dq[4], dq[5], dq[6], dq[7])),
+                                                  tt1, acc3, 0, 0, 0);
+    // inverse pass 2 (transform.py:230-236): D4[y][x] = R[y][x] + 1.5 S[x] + 0.5, lane x, registers y
+    f16x_t acc4 = splat16(0.5f);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc3, 0, tl.add3), tt0, acc4, 0, 0, 0);
+    acc4 = __builtin_amdgcn_mfma_f32_32x32x16_f16(cvt_h8(acc3, 1, tl.add3), tt1, acc4, 0, 0, 0);
+    // reconstruct + clip (intra.py:70-78): the f16 bits of floor(1536 + R + 0.5) are 0x6600 + R for
+    // |R| < 512; beyond that (|R| <= 920 for 8-bit blocks: 327 * sum |T[l][x]| / 1024, so the value
+    // stays positive) they stay monotone and on the right side of 0x6600 +- 512, so
+    // bits - (0x6600 - pred), saturating at 0, then min 255 is the clip of pred + R
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+        const f2_t x = (f2_t){acc4[2 * p], acc4[2 * p + 1]} + (f2_t){tl.add4, tl.add4};
+        rec2[p] = __builtin_elementwise_min(
+            __builtin_elementwise_sub_sat(__builtin_bit_cast(pku16, pk_trunc_h(x.x, x.y)), pr2[p]),
+            (pku16){255, 255});
+    }
 }
 
 

@@ -1124,13 +1124,13 @@ struct Closed4Args {
                             // above, 2 no chains, 4 no rounds, 8 no recon-image clear, 16 no quadtree
                             // hashes, 32 no source loads in the chains, 64 no level / recon / TU-map
                             // stores in the chains (0 in the product)
-    int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_h); set
-                            // for luma when the level / recon rows allow 16-B / 8-B stores
+    int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_tf); set
+                            // for luma (CTB 32)
     int32_t rec_ctu;        // k_tu_closed_pair: a whole CTU's packed-chain recon leaves from the LDS
                             // reconstruction at the CTU's end, as 64-B row pieces (the rows 8-B aligned)
     uint64_t* stamps;       // A/B build only (NH_CLOSED4_STAMPS): per (ticket, CTU) shader-clock stamps
 };
-__constant__ BasisH c_basis_h_cl;   // the f16 DCT32 bases of closed_chain32_h (copied to LDS per workgroup)
+__constant__ BasisHC c_basis_hc_cl;   // the f16 DCT32 bases of closed_chain32_tf (copied to LDS per workgroup)
 
 // cnt TUs of size N at once: lane l codes column / row t = l % N of TU j = l / N
 // (local origin (slx[j], sly[j]) in the CTU); reductions over a TU's N lanes are
@@ -1546,9 +1546,6 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_PRIO   // the luma wavefront's waves issue at a higher priority than chroma's (s_setprio):
 #define NH_CLOSED4_PRIO 1   // 0.1196-0.1200 vs 0.1205-0.1209 ms per 4K YUV420 frame concurrent (-DNH_CLOSED4_PRIO=0)
 #endif
-#ifndef NH_CLOSED4_MFMA_FUSED   // 1: the two planes' 32x32 MFMA chains interleaved (closed_chain32_h<2>)
-#define NH_CLOSED4_MFMA_FUSED 0
-#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -1715,181 +1712,95 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     phase(5);
 }
 
-// A 32x32 luma TU of the closed loop on the f16 matrix cores: the open loop's
-// ctu_chain32_h (nh_ctu.hip; exactness argued there: every
-// operand an integer of <= 11 bits, the basis scaled by 2^-10 exact in f16,
-// every partial sum a multiple of 2^-10 below 2^14, so the fp32 accumulators
-// hold the reference's integer sums) with the closed loop's inputs: the
-// neighbours from the plane's LDS reconstruction rc (top row rc[0][1 + x],
-// left column rc[1 + y][0], tr = rc[0][32], bl = rc[32][0]) and the source
-// samples from global memory.  NP TUs -- the same CTU of the pair's NP planes
-// (the quadtree depends on the plane id, not the frame) -- each on all 64 lanes
-// (lane (r, hh) = column / row r, half hh), their passes interleaved so one
-// plane's MFMAs and conversions run under the other's latency.  A 32x32 TU is
-// the whole CTU: only its bottom row and right column go into rc (the CTU's
-// publish and slide read nothing else; the next CTU's TUs rewrite the rest).
-// Levels and recon leave as 16-B / 8-B row pieces (the launch checks the
-// alignment, Closed4Args::mfma32).  Same results as tu_closed_batch_pk2<32>.
-constexpr int kQH = 40;   // f16 transpose tile: 32 rows of 40 halves per plane (16-B rows, conflict-free)
-template <int NP>
-__device__ __forceinline__ void closed_chain32_h(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
-                                                 int16_t (*rc2)[33][33], uint16_t* qt2, const BasisH& bs,
-                                                 const ChainQ& cq) {
+// A 32x32 luma TU of the closed loop on the f16 matrix cores: the config-5
+// block chain's transposition-free passes (tf_passes, nh_f16mma.hpp; DESIGN.md
+// §4.5: exact integer sums in the fp32 accumulators) with the closed loop's
+// inputs -- the neighbours from the plane's LDS reconstruction rc (top row
+// rc[0][1 + x], left column rc[1 + y][0], tr = rc[0][32], bl = rc[32][0]) and the
+// source samples from global memory.  Lane (r, hh) = column r, rows crow(2p, hh)
+// and +1.  Levels leave as one dword per (row, column) straight from the
+// registers (each store: two whole 128-B rows), the reconstruction as 16-bit
+// samples (each store: two whole 64-B rows); a 32x32 TU is the whole CTU, so only
+// its bottom row and right column go into rc (the CTU's publish and slide read
+// nothing else; the next CTU's TUs rewrite the rest).  Same results as
+// tu_closed_batch_pk2<32>.
+__device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
+                                                  uint8_t* tu, int x0c, int y0c, int16_t (*rc)[33], const BasisHC& bs,
+                                                  const ChainQ& cq, const TfLane& tl) {
     const int l = opaque_lane64(), r = l & 31, hh = l >> 5;
-    int32_t topr[NP], leftr[NP], tr[NP], bl[NP], dc[NP];
-    bool use_dc[NP];
-    uint32_t hx[NP][8];
-    // the TUs' source columns, every load issued before any use (one wait, not one per row pair)
-    int32_t sv[NP][16];
+    // the TU's source column, every load issued before any use (one wait, not one per row pair)
+    int32_t sv[16];
+    {
+        const int16_t* sp = src + (int64_t)(y0c + 4 * hh) * a.pitch + x0c + r;
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const int16_t* sp = pp.src[p] + (int64_t)y0c * a.pitch + x0c + r;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
+        for (int p = 0; p < 8; ++p) {
+            const int c = 2 * (p & 1) + 8 * (p >> 1);   // y_p - 4 hh
 #pragma unroll
             for (int e = 0; e < 2; ++e)
-                sv[p][2 * q + e] = (NH_AB && (a.probe & 32)) ? rc2[p][1 + y + e][1 + r]   // A/B probe: no source loads
-                                                             : sp[(int64_t)(y + e) * a.pitch];
+                sv[2 * p + e] = (NH_AB && (a.probe & 32)) ? rc[1 + 4 * hh + c + e][1 + r]   // A/B probe: no source loads
+                                                          : sp[(int64_t)(c + e) * a.pitch];
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        int16_t (*rc)[33] = rc2[p];
-        topr[p] = rc[0][1 + r];
-        leftr[p] = rc[1 + r][0];
-        tr[p] = rc[0][32];
-        bl[p] = rc[32][0];
-        int32_t sdc = hh ? leftr[p] : topr[p];   // DC (intra.py:46-62): lane halves hold top / left
-        sdc = grp_sum<64>(sdc);
-        dc[p] = (sdc + 32) >> 6;
-        const pk16 dc2 = pk_splat(dc[p]);
-        // column x = r, rows y = 8hh + 16c + j (the pass-1 A operand), as row pairs q = 4c + j/2
-        pk16 o2[8];
-        pku16 pl2[8];
+    const int32_t topr = rc[0][1 + r], tr = rc[0][32], bl = rc[32][0];
+    int32_t sdc = hh ? (int32_t)rc[1 + r][0] : topr;   // DC (intra.py:46-62): lane halves hold top / left
+    sdc = grp_sum<64>(sdc);
+    const int32_t dc = (sdc + 32) >> 6;
+    const pk16 dc2 = pk_splat(dc);
+    pk16 o2[8];
+    pku16 pl2[8];
+    {   // planar (intra.py:81-113) at (y, r): (31 - r) left[y] + b(y) >> 6, b(y) = b(4 hh) + (y - 4 hh)(bl - top[r])
         const pku16 wl = {(unsigned short)(31 - r), (unsigned short)(31 - r)}, sh = {6, 6};
+        const int32_t d = bl - topr, b0 = (r + 1) * tr + (31 - 4 * hh) * topr + (4 * hh + 1) * bl + 32;
+        const pku16 d2 = {(unsigned short)d, (unsigned short)d}, bb0 = {(unsigned short)b0, (unsigned short)(b0 + d)};
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int y = 8 * hh + 16 * (q >> 2) + 2 * (q & 3);
-            o2[q] = pk_pair(sv[p][2 * q], sv[p][2 * q + 1]);
-            const int32_t b = (r + 1) * tr[p] + (31 - y) * topr[p] + (y + 1) * bl[p] + 32;   // planar, intra.py:81-113
-            const pku16 bsv = {(unsigned short)b, (unsigned short)(b + bl[p] - topr[p])};
+        for (int p = 0; p < 8; ++p) {
+            const int c = 2 * (p & 1) + 8 * (p >> 1), y = 4 * hh + c;
+            o2[p] = pk_pair(sv[2 * p], sv[2 * p + 1]);
             const pku16 lf = {(unsigned short)rc[1 + y][0], (unsigned short)rc[2 + y][0]};
-            pl2[q] = (lf * wl + bsv) >> sh;
-        }
-        int32_t ed = 0, ep = 0;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const pk16 d0 = o2[q] - dc2, d1 = o2[q] - __builtin_bit_cast(pk16, pl2[q]);
-            ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
-            ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
-        }
-        ed = grp_sum<64>(ed);
-        ep = grp_sum<64>(ep);
-        use_dc[p] = ed <= ep;   // DC wins ties (__main__.py:173)
-        // residual (intra.py:65-67) + 1536 as f16 bits: 0x6600 + n for |n| < 512
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const pk16 rr = o2[q] - (use_dc[p] ? dc2 : __builtin_bit_cast(pk16, pl2[q]));
-            hx[p][q] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(pku16, rr) + (pku16){0x6600, 0x6600});
+            pl2[p] = (lf * wl + (bb0 + (pku16){(unsigned short)c, (unsigned short)c} * d2)) >> sh;
         }
     }
-    // pass 1 (transform.py:179-185): the 1536 offset leaves with the rounding bias b1 of row 0
-    const float b1 = r == 0 ? 0.5f - 3072.0f : 0.5f;
-    f16x_t acc[NP];
+    int32_t ed = 0, ep = 0;
 #pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        acc[p] = splat16(initb(b1));
-        acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
-            __builtin_bit_cast(h8_t, make_uint4(hx[p][0], hx[p][1], hx[p][2], hx[p][3])), bq_t(bs, r, hh, 0), acc[p], 0, 0, 0);
+    for (int p = 0; p < 8; ++p) {
+        const pk16 d0 = o2[p] - dc2, d1 = o2[p] - __builtin_bit_cast(pk16, pl2[p]);
+        ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+        ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
+    ed = grp_sum<64>(ed);
+    ep = grp_sum<64>(ep);
+    const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+    uint32_t hx[8];
+    pku16 pr2[8];
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-        acc[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
-            __builtin_bit_cast(h8_t, make_uint4(hx[p][4], hx[p][5], hx[p][6], hx[p][7])), bq_t(bs, r, hh, 1), acc[p], 0, 0, 0);
-    // pass 2 (transform.py:188-194): D2[l][k] = C[k][l], lane k, registers l = crow(g, hh)
-    f16x_t acc2[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        acc2[p] = splat16(initb(0.5f));
-        acc2[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 0), acc_h8(acc[p], 0, b1), acc2[p], 0, 0, 0);
+    for (int p = 0; p < 8; ++p) {
+        const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[p]);
+        const pku16 rr = __builtin_bit_cast(pku16, o2[p] - pr);   // residual, intra.py:65-67
+        hx[p] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of n + 768
+        pr2[p] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
     }
+    const bool st = !(NH_AB && (a.probe & 64));
+    int32_t* lcol = lvl + (int64_t)y0c * a.pitch + x0c + r;
+    pku16 rec2[8];
+    tf_passes(hx, pr2, bs, cq, tl, r, hh,
+              [&](int g, int32_t L) { if (st) lcol[(int64_t)crow(g, hh) * a.pitch] = L; }, [] {}, rec2);
+    int16_t* rcol = rec + (int64_t)y0c * a.pitch + x0c + r;
 #pragma unroll
-    for (int p = 0; p < NP; ++p)
-        acc2[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_tc(bs, r, hh, 1), acc_h8(acc[p], 1, b1), acc2[p], 0, 0, 0);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) mfma_result_ready(acc2[p]);   // before shift_rnd's inline-asm reads
-    // quantize_block -> levels (row k = r), dequantize_block -> f16 into the transpose tile qt[l][k]
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        uint16_t* qt = qt2 + p * (32 * kQH);
-        int32_t* lrow = pp.lvl[p] + (int64_t)(y0c + r) * a.pitch + x0c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int32_t L4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int g = 4 * q + e;
-                L4[e] = quant_s(shift_rnd(acc2[p][g]), cq.qs, cq.h_v, cq.hneg_v);
-                qt[crow(g, hh) * kQH + r] = __builtin_bit_cast(uint16_t, (_Float16)(int16_t)dequant_s(L4[e], cq));
-            }
-            if (!(NH_AB && (a.probe & 64))) *(int4*)(lrow + 8 * q + 4 * hh) = make_int4(L4[0], L4[1], L4[2], L4[3]);
+    for (int p = 0; p < 8; ++p) {
+        const int y = 2 * (p & 1) + 8 * (p >> 1) + 4 * hh;
+        if (st) {
+            rcol[(int64_t)y * a.pitch] = (int16_t)rec2[p].x;
+            rcol[(int64_t)(y + 1) * a.pitch] = (int16_t)rec2[p].y;
+        }
+        if (r == 31) {   // the right column (the next CTU's left neighbours)
+            rc[1 + y][32] = (int16_t)rec2[p].x;
+            rc[2 + y][32] = (int16_t)rec2[p].y;
         }
     }
-    pair_sync();
-    // inverse pass 1 (transform.py:221-227): D3[l][y] = tmp[y][l], data lane l
-    f16x_t acc3[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const uint16_t* qt = qt2 + p * (32 * kQH);
-        acc3[p] = splat16(initb(0.5f));
-        acc3[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * kQH + 8 * hh), bq_tt(bs, r, hh, 0), acc3[p], 0, 0, 0);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        const uint16_t* qt = qt2 + p * (32 * kQH);
-        acc3[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ld_h8(qt + r * kQH + 16 + 8 * hh), bq_tt(bs, r, hh, 1), acc3[p],
-                                                         0, 0, 0);
-    }
-    // inverse pass 2 (transform.py:230-236): D4[x][y] = R[y][x], lane y, registers x = crow(g, hh)
-    f16x_t acc4[NP];
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        acc4[p] = splat16(initb(0.5f));
-        acc4[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 0), acc_h8(acc3[p], 0, 0.5f), acc4[p], 0, 0, 0);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-        acc4[p] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bq_ttc(bs, r, hh, 1), acc_h8(acc3[p], 1, 0.5f), acc4[p], 0, 0, 0);
-#pragma unroll
-    for (int p = 0; p < NP; ++p) mfma_result_ready(acc4[p]);
-    // reconstruct + clip (intra.py:70-78), row y = r; the bottom row and the right column into rc
-#pragma unroll
-    for (int p = 0; p < NP; ++p) {
-        int16_t (*rc)[33] = rc2[p];
-        int16_t* rrow = pp.rec[p] + (int64_t)(y0c + r) * a.pitch + x0c;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int32_t R4[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const int x = 8 * q + 4 * hh + e;
-                const int32_t pr = use_dc[p] ? dc[p]
-                                             : ((31 - x) * leftr[p] + (x + 1) * tr[p] + (31 - r) * (int32_t)rc[0][1 + x] +
-                                                (r + 1) * bl[p] + 32) >> 6;
-                const int32_t v = pr + shift_rnd(acc4[p][4 * q + e]);
-                R4[e] = v < 0 ? 0 : (v > 255 ? 255 : v);
-                if (r == 31) rc[32][1 + x] = (int16_t)R4[e];
-            }
-            if (q == 3 && hh == 1) rc[1 + r][32] = (int16_t)R4[3];
-            if (!(NH_AB && (a.probe & 64)))
-                *(uint2*)(rrow + 8 * q + 4 * hh) =
-                    make_uint2((uint32_t)R4[0] | ((uint32_t)R4[1] << 16), (uint32_t)R4[2] | ((uint32_t)R4[3] << 16));
-        }
-        const int w4 = a.w / 4;   // the TU map: 8 x 8 units of log2 size 5
-        if (!(NH_AB && (a.probe & 64))) pp.tu[p][(int64_t)(y0c / 4 + (l >> 3)) * w4 + x0c / 4 + (l & 7)] = (uint8_t)5;
-    }
+    if (hh == 1) rc[32][1 + r] = (int16_t)rec2[7].y;   // row 31 (= y_7 + 1 of the upper half): the bottom row
+    const int w4 = a.w / 4;   // the TU map: 8 x 8 units of log2 size 5
+    if (st) tu[(int64_t)(y0c / 4 + (l >> 3)) * w4 + x0c / 4 + (l & 7)] = (uint8_t)5;
     pair_sync();
 }
 
@@ -1971,10 +1882,9 @@ template <int WAVES, bool REC>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
-    // the packed chains' int16 tiles (2 x 32 rows of TP) or closed_chain32_h's f16 transpose tiles (2 x 32 x kQH)
-    __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * kQH];
-    __shared__ __attribute__((aligned(16))) BasisH basis_s;
-    static_assert(32 * TP <= 32 * kQH, "tile layout");
+    // the packed chains' int16 tiles (2 x 32 rows of TP)
+    __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * TP];
+    __shared__ __attribute__((aligned(16))) BasisHC basis_s;
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
 #endif
@@ -1987,14 +1897,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // the critical (luma) wavefront issues first
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
-    if (a.mfma32) {   // closed_chain32_h's bases: 4 KB, once per workgroup
-        const uint4* s4 = (const uint4*)&c_basis_h_cl;
-        for (int i = lane; i < (int)(sizeof(BasisH) / 16); i += 64) ((uint4*)&basis_s)[i] = s4[i];
+    if (a.mfma32) {   // closed_chain32_tf's bases: 4 KB, once per workgroup
+        const uint4* s4 = (const uint4*)&c_basis_hc_cl;
+        for (int i = lane; i < (int)(sizeof(BasisHC) / 16); i += 64) ((uint4*)&basis_s)[i] = s4[i];
         pair_sync();
     }
     ChainQ cq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
+    const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);   // (read only when a.mfma32)
     uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
     const int ngroups = a.nplanes / a.ppg, npairs = ((ngroups + 1) / 2) * a.ppg;
     const int total = a.crows * npairs;
@@ -2103,22 +2014,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
                             tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, rec_flush);
                         case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
-                            if (a.mfma32) {
-                                if (NH_CLOSED4_MFMA_FUSED && two) {
-                                    closed_chain32_h<2>(a, pp, x0c, y0c, rc, (uint16_t*)t16, basis_s, cq[3]);
-                                } else {   // one plane after the other (fewer live accumulators), ONE copy
-                                    // of the chain's code: a loop the compiler keeps (instruction-cache footprint)
+                            if (a.mfma32) {   // one plane after the other, ONE copy of the chain's code:
+                                // a loop the compiler keeps (instruction-cache footprint)
 #pragma clang loop unroll(disable)
-                                    for (int s2 = 0; s2 <= two; ++s2) {
-                                        PairPlanes p1;
-                                        p1.src[0] = s2 ? pp.src[1] : pp.src[0];
-                                        p1.lvl[0] = s2 ? pp.lvl[1] : pp.lvl[0];
-                                        p1.rec[0] = s2 ? pp.rec[1] : pp.rec[0];
-                                        p1.tu[0] = s2 ? pp.tu[1] : pp.tu[0];
-                                        closed_chain32_h<1>(a, p1, x0c, y0c, rc + s2, (uint16_t*)t16 + s2 * 32 * kQH,
-                                                            basis_s, cq[3]);
-                                    }
-                                }
+                                for (int s2 = 0; s2 <= two; ++s2)
+                                    closed_chain32_tf(a, s2 ? pp.src[1] : pp.src[0], s2 ? pp.lvl[1] : pp.lvl[0],
+                                                      s2 ? pp.rec[1] : pp.rec[0], s2 ? pp.tu[1] : pp.tu[0], x0c, y0c,
+                                                      rc[s2], basis_s, cq[3], tl);
                             } else {
                                 NH_PLAN_BATCH(32, false, cq[3])
                             }
@@ -2484,11 +2386,10 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         g_stamps_used = need;
     }
 #endif
-    // 32x32 luma TUs on the f16 matrix cores (closed_chain32_h): 16-B level and 8-B recon row pieces;
+    // 32x32 luma TUs on the f16 matrix cores (closed_chain32_tf; element stores, no alignment needed);
     // A/B build: NH_CLOSED4_MFMA32 = 0 keeps them on the packed butterfly chain
     static const int mfma32 = NH_KNOB("NH_CLOSED4_MFMA32", 1);
-    a.mfma32 = mfma32 && ctb == 32 && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
-               !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 7);
+    a.mfma32 = mfma32 && ctb == 32;
     // packed-chain recon of whole CTUs as 64-B rows from the LDS reconstruction (8-B aligned row pieces);
     // A/B knob NH_CLOSED4_REC_CTU = 0: every TU stores its own 8-B row pieces
     static const int rec_ctu = NH_KNOB("NH_CLOSED4_REC_CTU", 1);
@@ -2497,8 +2398,8 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     if (a.mfma32) {
         static PerDeviceOnce once;
         const int rcb = once.run([] {
-            const BasisH bh = make_basis_h();
-            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_h_cl), &bh, sizeof(bh)));
+            const BasisHC bh = make_basis_hc();
+            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_hc_cl), &bh, sizeof(bh)));
             return (int)NH_OK;
         });
         if (rcb) return rcb;
