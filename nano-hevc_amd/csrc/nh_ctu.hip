@@ -666,12 +666,6 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, 
 // product is exact in fp32 and every partial sum a multiple of 2^-10 below 2^13:
 // the accumulators hold the reference's integer sums exactly.
 constexpr int kRecH = 2 * kRecP;   // recon tile row pitch in int16
-// A per-lane 32-bit byte offset the compiler keeps as one VGPR: base (SGPRs) +
-// zext(offset) selects the global_store v_off, s[base] form.
-__device__ __forceinline__ uint64_t vofs(uint32_t o) {
-    asm("" : "+v"(o));
-    return (uint64_t)o;
-}
 template <class IMG>
 __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, const BasisHC& bs, int gx0, int gy0,
                                            int32_t* __restrict__ lvl, int16_t* __restrict__ rec, int32_t* ot,

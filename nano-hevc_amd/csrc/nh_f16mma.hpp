@@ -16,6 +16,13 @@ namespace nh {
 // copy per workgroup in LDS).  Each lane's MFMA operand is one 16-byte piece of
 // a row (the data-side passes) or two 8-byte pieces of it in the accumulator
 // row order crow (passes 2 and 4, nh_mfma.hpp).
+// A per-lane 32-bit byte offset the compiler keeps as one VGPR: base (SGPRs) +
+// zext(offset) selects the global_store v_off, s[base] form.
+__device__ __forceinline__ uint64_t vofs(uint32_t o) {
+    asm("" : "+v"(o));
+    return (uint64_t)o;
+}
+
 struct BasisH {
     uint16_t t[32][32];          // [k][n] = T[k][n]   pass 1 B operand (lane k); pass 2 A operand (lane l = k)
     uint16_t tt[32][32];         // [n][k] = T[k][n]   inverse pass 1 B operand (lane n); inverse pass 2 A operand

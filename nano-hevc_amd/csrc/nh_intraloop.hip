@@ -1125,7 +1125,7 @@ struct Closed4Args {
                             // hashes, 32 no source loads in the chains, 64 no level / recon / TU-map
                             // stores in the chains (0 in the product)
     int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_tf); set
-                            // for luma (CTB 32)
+                            // for luma when the level / recon rows allow 16-B stores
     int32_t rec_ctu;        // k_tu_closed_pair: a whole CTU's packed-chain recon leaves from the LDS
                             // reconstruction at the CTU's end, as 64-B row pieces (the rows 8-B aligned)
     uint64_t* stamps;       // A/B build only (NH_CLOSED4_STAMPS): per (ticket, CTU) shader-clock stamps
@@ -1546,6 +1546,9 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_PRIO   // the luma wavefront's waves issue at a higher priority than chroma's (s_setprio):
 #define NH_CLOSED4_PRIO 1   // 0.1196-0.1200 vs 0.1205-0.1209 ms per 4K YUV420 frame concurrent (-DNH_CLOSED4_PRIO=0)
 #endif
+#ifndef NH_CLOSED4_TL_INNER   // 1: closed_chain32_tf's per-lane constants made per TU, not held
+#define NH_CLOSED4_TL_INNER 0
+#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -1718,15 +1721,17 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
 // inputs -- the neighbours from the plane's LDS reconstruction rc (top row
 // rc[0][1 + x], left column rc[1 + y][0], tr = rc[0][32], bl = rc[32][0]) and the
 // source samples from global memory.  Lane (r, hh) = column r, rows crow(2p, hh)
-// and +1.  Levels leave as one dword per (row, column) straight from the
-// registers (each store: two whole 128-B rows), the reconstruction as 16-bit
-// samples (each store: two whole 64-B rows); a 32x32 TU is the whole CTU, so only
-// its bottom row and right column go into rc (the CTU's publish and slide read
-// nothing else; the next CTU's TUs rewrite the rest).  Same results as
-// tu_closed_batch_pk2<32>.
+// and +1.  Levels and reconstruction leave through the tile ot (the packed
+// chains' transpose tile; no other TU of the CTU runs) in whole rows, as in
+// config 5: 4 + 2 store instructions of 16 B per lane instead of 32 + 16 of one
+// sample per lane (the launch checks the rows' 16-B alignment,
+// Closed4Args::mfma32).  A 32x32 TU is the whole CTU, so only its bottom row and
+// right column go into rc (the CTU's publish and slide read nothing else; the
+// next CTU's TUs rewrite the rest).  Same results as tu_closed_batch_pk2<32>.
+constexpr int kClOutP = 36, kClRecP = 24;   // int32 per tile row: levels, recon (48 halves; 16-B rows)
 __device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
-                                                  uint8_t* tu, int x0c, int y0c, int16_t (*rc)[33], const BasisHC& bs,
-                                                  const ChainQ& cq, const TfLane& tl) {
+                                                  uint8_t* tu, int x0c, int y0c, int16_t (*rc)[33], int32_t* ot,
+                                                  const BasisHC& bs, const ChainQ& cq, const TfLane& tl) {
     const int l = opaque_lane64(), r = l & 31, hh = l >> 5;
     // the TU's source column, every load issued before any use (one wait, not one per row pair)
     int32_t sv[16];
@@ -1781,27 +1786,44 @@ __device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const in
         pr2[p] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
     }
     const bool st = !(NH_AB && (a.probe & 64));
-    int32_t* lcol = lvl + (int64_t)y0c * a.pitch + x0c + r;
+    const int32_t op = a.pitch;
+    char* lb = (char*)(lvl + (int64_t)y0c * a.pitch + x0c);
     pku16 rec2[8];
-    tf_passes(hx, pr2, bs, cq, tl, r, hh,
-              [&](int g, int32_t L) { if (st) lcol[(int64_t)crow(g, hh) * a.pitch] = L; }, [] {}, rec2);
-    int16_t* rcol = rec + (int64_t)y0c * a.pitch + x0c + r;
+    tf_passes(hx, pr2, bs, cq, tl, r, hh, [&](int g, int32_t L) { ot[crow(g, hh) * kClOutP + r] = L; },
+              [&] {
+                  pair_sync();
+#pragma unroll
+                  for (int i = 0; i < 4; ++i) {   // 4 instructions of 8 whole 128-B level rows
+                      const int rr = (l >> 3) + 8 * i, c = 4 * (l & 7);
+                      const int4 v = *(const int4*)&ot[rr * kClOutP + c];
+                      if (st) *(int4*)(lb + vofs((rr * op + c) * 4)) = v;
+                  }
+                  pair_sync();   // the tile's reads before the recon reuses it
+              },
+              rec2);
+    int16_t* rt = (int16_t*)ot;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
         const int y = 2 * (p & 1) + 8 * (p >> 1) + 4 * hh;
-        if (st) {
-            rcol[(int64_t)y * a.pitch] = (int16_t)rec2[p].x;
-            rcol[(int64_t)(y + 1) * a.pitch] = (int16_t)rec2[p].y;
-        }
+        rt[y * 2 * kClRecP + r] = (int16_t)rec2[p].x;
+        rt[(y + 1) * 2 * kClRecP + r] = (int16_t)rec2[p].y;
         if (r == 31) {   // the right column (the next CTU's left neighbours)
             rc[1 + y][32] = (int16_t)rec2[p].x;
             rc[2 + y][32] = (int16_t)rec2[p].y;
         }
     }
     if (hh == 1) rc[32][1 + r] = (int16_t)rec2[7].y;   // row 31 (= y_7 + 1 of the upper half): the bottom row
+    pair_sync();
+    char* rb = (char*)(rec + (int64_t)y0c * a.pitch + x0c);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {   // 2 instructions of 16 whole 64-B recon rows
+        const int rr = (l >> 2) + 16 * i, c = 4 * (l & 3);
+        const uint4 v = *(const uint4*)&ot[rr * kClRecP + c];
+        if (st) *(uint4*)(rb + vofs((rr * op + 2 * c) * 2)) = v;
+    }
     const int w4 = a.w / 4;   // the TU map: 8 x 8 units of log2 size 5
     if (st) tu[(int64_t)(y0c / 4 + (l >> 3)) * w4 + x0c / 4 + (l & 7)] = (uint8_t)5;
-    pair_sync();
+    pair_sync();   // the tile's reads before the next TU's writes
 }
 
 // The TU schedule of one CTU of one plane id (k_closed4_plan, NH_CLOSED4_PLAN):
@@ -1882,8 +1904,9 @@ template <int WAVES, bool REC>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
     constexpr int TP = 34;
     __shared__ int16_t rc[2][33][33];
-    // the packed chains' int16 tiles (2 x 32 rows of TP)
-    __shared__ __attribute__((aligned(16))) int16_t t16[2 * 32 * TP];
+    // the packed chains' int16 tiles (2 x 32 rows of TP), or closed_chain32_tf's level / recon tile
+    __shared__ __attribute__((aligned(16))) int32_t t32[32 * kClOutP > 32 * TP ? 32 * kClOutP : 32 * TP];
+    int16_t* const t16 = (int16_t*)t32;
     __shared__ __attribute__((aligned(16))) BasisHC basis_s;
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
@@ -1905,7 +1928,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     ChainQ cq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
+#if !NH_CLOSED4_TL_INNER
     const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);   // (read only when a.mfma32)
+#endif
     uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
     const int ngroups = a.nplanes / a.ppg, npairs = ((ngroups + 1) / 2) * a.ppg;
     const int total = a.crows * npairs;
@@ -2017,10 +2042,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             if (a.mfma32) {   // one plane after the other, ONE copy of the chain's code:
                                 // a loop the compiler keeps (instruction-cache footprint)
 #pragma clang loop unroll(disable)
-                                for (int s2 = 0; s2 <= two; ++s2)
+                                for (int s2 = 0; s2 <= two; ++s2) {
+#if NH_CLOSED4_TL_INNER
+                                    const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);
+#endif
                                     closed_chain32_tf(a, s2 ? pp.src[1] : pp.src[0], s2 ? pp.lvl[1] : pp.lvl[0],
                                                       s2 ? pp.rec[1] : pp.rec[0], s2 ? pp.tu[1] : pp.tu[0], x0c, y0c,
-                                                      rc[s2], basis_s, cq[3], tl);
+                                                      rc[s2], t32, basis_s, cq[3], tl);
+                                }
                             } else {
                                 NH_PLAN_BATCH(32, false, cq[3])
                             }
@@ -2386,10 +2415,11 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         g_stamps_used = need;
     }
 #endif
-    // 32x32 luma TUs on the f16 matrix cores (closed_chain32_tf; element stores, no alignment needed);
+    // 32x32 luma TUs on the f16 matrix cores (closed_chain32_tf): 16-B level and recon row pieces;
     // A/B build: NH_CLOSED4_MFMA32 = 0 keeps them on the packed butterfly chain
     static const int mfma32 = NH_KNOB("NH_CLOSED4_MFMA32", 1);
-    a.mfma32 = mfma32 && ctb == 32;
+    a.mfma32 = mfma32 && ctb == 32 && !(set->pitch & 7) && !((set->base | set->plane_stride | set->group_stride) & 7) &&
+               !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 15);
     // packed-chain recon of whole CTUs as 64-B rows from the LDS reconstruction (8-B aligned row pieces);
     // A/B knob NH_CLOSED4_REC_CTU = 0: every TU stores its own 8-B row pieces
     static const int rec_ctu = NH_KNOB("NH_CLOSED4_REC_CTU", 1);
@@ -2444,6 +2474,9 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         static const int wpc = NH_KNOB("NH_CLOSED4_WPC", 0), wpc_l = NH_KNOB("NH_CLOSED4_WPC_L", 0),
                          wpc_c = NH_KNOB("NH_CLOSED4_WPC_C", 0);
         const int wsel = is_luma ? (wpc_l > 0 ? wpc_l : wpc) : (wpc_c > 0 ? wpc_c : wpc);
+#ifdef NH_CLOSED4_PERCU_CAP   // variant builds: resident waves per CU capped at compile time
+        per_cu = std::min(per_cu, NH_CLOSED4_PERCU_CAP);
+#endif
         const int64_t cap_n = (int64_t)(wsel > 0 ? wsel : std::max(1, per_cu)) * cus;
         kern<<<(unsigned)(prow < cap_n ? prow : cap_n), 64, 0, s>>>(a);
     } else if (narrow_ok) {
