@@ -1549,6 +1549,9 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_TL_INNER   // 1: closed_chain32_tf's per-lane constants made per TU, not held
 #define NH_CLOSED4_TL_INNER 0
 #endif
+#ifndef NH_CLOSED4_MOSAIC   // 1: 16x16, 8x8 and luma 4x4 TUs on the f16 matrix cores (tu_closed_batch_mma)
+#define NH_CLOSED4_MOSAIC 1
+#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -1712,6 +1715,276 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
         }
     }
     pair_sync();
+    phase(5);
+}
+
+// ---------------------------------------------------------------------------
+// Small closed-loop TUs on the f16 matrix cores: MOSAICS (round 5).  A batch of
+// 64 / N TUs of size N (4x4 DST, 8x8 and 16x16 DCT) is NM = N / 4 mosaics of
+// 16 x 16 samples -- 16 / N x 16 / N TUs each -- and every 1-D pass of every TU
+// of a mosaic is ONE v_mfma_f32_16x16x16_f16 against a block-diagonal basis:
+// lane l = (g = l / 16, c = l % 16) holds mosaic column c, rows 4g .. 4g + 3 (the
+// A operand of X^T), and each pass's accumulator IS the next pass's A operand
+// (it is the transposed product: D1 = temp^T, D2 = coeff, D3 = tmp^T, D4 = rres),
+// so the four passes need no transpose -- where the packed chain
+// (tu_closed_batch_pk2) moves every TU through the LDS tile three times.  The
+// basis enters scaled by 2^-S (exact in f16: |T| <= 90, S <= 9), so each
+// accumulator is the reference's sum / 2^S exactly (integer operands below 2048,
+// products exact in fp32, sums below 2^24 * 2^-S: tools/packed_bounds.py's
+// bounds), and the shift's rounding is the accumulator's
+// initial 0.5 then a floor:
+//  * the residual enters as the f16 of 768 + n (bits 0x6200 + 2n); the pass-1
+//    accumulator starts at 0.5 + 1536 - 768 rs / 2^S (rs = the lane's basis-row
+//    sum), so it holds temp + 1536 + frac in [1024, 2048): the truncating
+//    conversion to f16 is the floor;
+//  * pass 2 starts at 0.5 - 1536 rs / 2^S and floors to the coefficient;
+//  * the dequantized coefficients (<= 1024) enter as exact f16 integers, the
+//    inverse pass 1 floors to tmp (<= 1936, exact in f16);
+//  * the inverse pass 2 starts at 1536.5: clamped to [1280, 1792] its f16 bits
+//    are 0x6600 + R' (R' = R clamped to [-256, 256]), and bits - (0x6600 - pred)
+//    saturating at 0, then min 255, is the clip of pred + R.
+// DCT4 (chroma 4x4) stays on the packed chain: its inverse pass 1 reaches 2223,
+// beyond f16's integers.  Same results as tu_closed_batch_pk2 on 8-bit streams.
+typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+typedef float f4_t __attribute__((ext_vector_type(4)));
+struct MosaicLane {            // per (kind, lane): 32 B
+    uint32_t bf[2], bi[2];     // the B operands: Tb^T (passes 1, 2) and Tb (inverse passes), f16 * 2^-S
+    float c1, c2;              // the initial accumulators of passes 1 and 2
+    uint32_t pad[2];
+};
+__constant__ MosaicLane c_mosaic[3][64];   // kinds: 0 DST4, 1 DCT8, 2 DCT16
+inline uint16_t f16_bits_exact(int num, int sh) {   // num * 2^-sh as f16 bits (|num| < 2048, a normal result)
+    if (num == 0) return 0;
+    uint16_t s = num < 0 ? 0x8000 : 0;
+    unsigned m = (unsigned)(num < 0 ? -num : num);
+    int e = -sh;
+    while (m < 1024) { m <<= 1; --e; }   // m in [1024, 2048): value = m * 2^(e)
+    return (uint16_t)(s | (uint16_t)((e + 10 + 15) << 10) | (uint16_t)(m & 1023));
+}
+inline void make_mosaic(MosaicLane (*out)[64]) {
+    for (int kind = 0; kind < 3; ++kind) {
+        const int N = kind == 0 ? 4 : kind == 1 ? 8 : 16, S = (kind == 0 ? 2 : kind == 1 ? 3 : 4) + 5;
+        auto T = [&](int k, int n) {
+            return kind == 0 ? dst4c(k, n) : kind == 1 ? dctc<8>(k, n) : dctc<16>(k, n);
+        };
+        for (int l = 0; l < 64; ++l) {
+            const int c = l & 15, g = l >> 4;
+            uint16_t bf[4], bi[4];
+            for (int r = 0; r < 4; ++r) {
+                const int k = 4 * g + r, same = k / N == c / N;
+                bf[r] = same ? f16_bits_exact(T(c % N, k % N), S) : 0;   // B1[k][j] = T[j][k]
+                bi[r] = same ? f16_bits_exact(T(k % N, c % N), S) : 0;   // B3[k][j] = T[k][j]
+            }
+            int rs = 0;
+            for (int n = 0; n < N; ++n) rs += T(c % N, n);
+            MosaicLane& m = out[kind][l];
+            m.bf[0] = bf[0] | ((uint32_t)bf[1] << 16);
+            m.bf[1] = bf[2] | ((uint32_t)bf[3] << 16);
+            m.bi[0] = bi[0] | ((uint32_t)bi[1] << 16);
+            m.bi[1] = bi[2] | ((uint32_t)bi[3] << 16);
+            m.c1 = 0.5f + 1536.0f - 768.0f * (float)rs / (float)(1 << S);
+            m.c2 = 0.5f - 1536.0f * (float)rs / (float)(1 << S);
+            m.pad[0] = m.pad[1] = 0;
+        }
+    }
+}
+__device__ __forceinline__ void mfma_result_ready4(f4_t& acc) {   // see mfma_result_ready (nh_f16mma.hpp)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
+}
+// sum over the lanes of one TU of the mosaic (N = 4: 4 lanes; 8: 8 lanes + the 8 lanes 16 apart; 16: all 64)
+template <int N>
+__device__ __forceinline__ int32_t tu_sum(int32_t v) {
+    if constexpr (N == 4) return grp_sum<4>(v);
+    else if constexpr (N == 8) {
+        v = grp_sum<8>(v);
+        return v + lane_perm<-1>(v);
+    } else return grp_sum<64>(v);
+}
+template <int N, bool DST>
+__device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                                    int cnt, int total, int c0, const uint8_t* ent,
+                                                    int16_t (*rc2)[33][33], int32_t* tile, const ChainQ& cq,
+                                                    uint64_t* ph = nullptr, bool rec_later = false) {
+    static_assert(N == 4 ? DST : (N == 8 || N == 16) && !DST, "mosaic kinds: DST4, DCT8, DCT16");
+    constexpr int L2 = Log2<N>::v, NM = N / 4, TS = 16 / N, TPM = TS * TS, KIND = N == 4 ? 0 : N == 8 ? 1 : 2;
+    uint64_t ph_t = 0;
+    auto phase = [&](int k) {   // A/B build, NH_CLOSED4_STAMPS (as tu_closed_batch_pk2)
+        if (NH_AB && ph) {
+            const uint64_t tnow = __builtin_amdgcn_s_memtime();
+            if (k >= 0 && __lane_id() == 0) ph[8 * (5 - L2) + k] += tnow - ph_t;
+            ph_t = tnow;
+        }
+    };
+    phase(-1);
+    const int lane = opaque_lane64(), c = lane & 15, g = lane >> 4;
+    const int t = c % N, yr0 = (4 * g) % N, bc = c / N, br = (4 * g) / N;
+    const uint4 mw0 = *(const uint4*)&c_mosaic[KIND][lane], mw1 = *((const uint4*)&c_mosaic[KIND][lane] + 1);
+    int pm[NM], lxm[NM], lym[NM];
+    bool onm[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        const int e = c0 + m * TPM + br * TS + bc;
+        onm[m] = e < total;
+        pm[m] = onm[m] && e >= cnt ? 1 : 0;
+        const int code = ent[onm[m] ? e - pm[m] * cnt : 0];   // idle lanes shadow plane 0's first TU
+        lxm[m] = (code & 7) * 4;
+        lym[m] = ((code >> 3) & 7) * 4;
+    }
+    // the TUs' source samples, every load issued before any use
+    int32_t sv[NM][4];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        const int16_t* sp = (pm[m] ? pp.src[1] : pp.src[0]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            sv[m][r] = (NH_AB && (a.probe & 32)) ? rc2[pm[m]][lym[m] + 1 + yr0 + r][lxm[m] + 1 + t]
+                                                 : sp[(int64_t)r * a.pitch];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t hx[NM][2];
+    pku16 pr2[NM][2];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        int16_t (*rc)[33] = rc2[pm[m]];
+        const int lx = lxm[m], ly = lym[m];
+        const int32_t topt = rc[ly][lx + 1 + t], tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // __main__.py:168
+        // DC (intra.py:46-62): the TU's lanes of row group 0 add top[t], of row group 1 left[t] (N = 4: both)
+        int32_t sdc = N == 4 ? topt + rc[ly + 1 + t][lx] : yr0 == 0 ? topt : yr0 == 4 ? (int32_t)rc[ly + 1 + t][lx] : 0;
+        sdc = tu_sum<N>(sdc);
+        const int32_t dc = (sdc + N) >> (L2 + 1);
+        const pk16 dc2 = pk_splat(dc);
+        pk16 o2[2];
+        pku16 pl2[2];
+        {   // planar (intra.py:81-113) at (y, t): (N-1-t) left[y] + (t+1) tr + (N-1-y) top[t] + (y+1) bl + N >> L2+1
+            const int32_t b = (t + 1) * tr + (N - 1 - yr0) * topt + (yr0 + 1) * bl + N, st = bl - topt;
+            const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)}, sh = {L2 + 1, L2 + 1};
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int y = yr0 + 2 * q;
+                o2[q] = pk_pair(sv[m][2 * q], sv[m][2 * q + 1]);
+                const pku16 lf = {(unsigned short)rc[ly + 1 + y][lx], (unsigned short)rc[ly + 2 + y][lx]};
+                const pku16 bs = {(unsigned short)(b + 2 * q * st), (unsigned short)(b + (2 * q + 1) * st)};
+                pl2[q] = (lf * wl + bs) >> sh;
+            }
+        }
+        int32_t ed = 0, ep = 0;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const pk16 d0 = o2[q] - dc2, d1 = o2[q] - __builtin_bit_cast(pk16, pl2[q]);
+            ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+            ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+        }
+        ed = tu_sum<N>(ed);
+        ep = tu_sum<N>(ep);
+        const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[q]);
+            const pku16 rr = __builtin_bit_cast(pku16, o2[q] - pr);   // residual, intra.py:65-67
+            hx[m][q] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of 768 + n
+            pr2[m][q] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
+        }
+    }
+    phase(0);
+    const h4_t bf = __builtin_bit_cast(h4_t, make_uint2(mw0.x, mw0.y)), bi = __builtin_bit_cast(h4_t, make_uint2(mw0.z, mw0.w));
+    const float c1 = __builtin_bit_cast(float, mw1.x), c2 = __builtin_bit_cast(float, mw1.y);
+    // forward passes (transform.py:179-194)
+    f4_t acc[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(hx[m][0], hx[m][1])), bf,
+                                                       (f4_t){c1, c1, c1, c1}, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+            __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(acc[m][0], acc[m][1]), pk_trunc_h(acc[m][2], acc[m][3]))), bf,
+            (f4_t){c2, c2, c2, c2}, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < NM; ++m) mfma_result_ready4(acc[m]);   // before floor_i32's inline-asm reads
+    phase(1);
+    // quantize_block (levels into the tile: TU e - c0, row, column) and dequantize_block in 16 bits
+    const pk16 dqs2 = pk_splat(cq.dqs), dqr2 = pk_splat((int32_t)cq.dqr_v), dqsh2 = pk_splat(cq.dqsh);
+    uint32_t dq[NM][2];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        int32_t* tl = tile + ((m * TPM + br * TS + bc) * N + yr0) * N + t;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int32_t L0 = quant_s(floor_i32(acc[m][2 * q]), cq.qs, cq.h_v, cq.hneg_v);
+            const int32_t L1 = quant_s(floor_i32(acc[m][2 * q + 1]), cq.qs, cq.h_v, cq.hneg_v);
+            tl[(2 * q) * N] = L0;
+            tl[(2 * q + 1) * N] = L1;
+            const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
+            const pk16 d2 = (l2 * dqs2 + dqr2) >> dqsh2;
+            const _Float16 h0 = (_Float16)d2.x, h1 = (_Float16)d2.y;
+            dq[m][q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+        }
+    }
+    phase(2);
+    // inverse passes (transform.py:221-236)
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(dq[m][0], dq[m][1])), bi,
+                                                       (f4_t){0.5f, 0.5f, 0.5f, 0.5f}, 0, 0, 0);
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+            __builtin_bit_cast(h4_t, make_uint2(pk_floor_h(acc[m][0], acc[m][1]), pk_floor_h(acc[m][2], acc[m][3]))), bi,
+            (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
+    phase(3);
+    // reconstruct + clip (intra.py:70-78) into rc (no TU of this batch reads another's samples)
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        int16_t (*rc)[33] = rc2[pm[m]];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const float x0 = __builtin_amdgcn_fmed3f(acc[m][2 * q], 1280.0f, 1792.0f);
+            const float x1 = __builtin_amdgcn_fmed3f(acc[m][2 * q + 1], 1280.0f, 1792.0f);
+            const pku16 rv = __builtin_elementwise_min(
+                __builtin_elementwise_sub_sat(__builtin_bit_cast(pku16, pk_trunc_h(x0, x1)), pr2[m][q]), (pku16){255, 255});
+            if (onm[m]) {
+                rc[lym[m] + 1 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.x;
+                rc[lym[m] + 2 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.y;
+            }
+        }
+    }
+    pair_sync();
+    phase(4);
+    // the levels (16-B row pieces from the tile), the recon (8-B row pieces from rc) and the TU map:
+    // piece i = 4 samples of one TU row, N / 4 pieces per lane
+    const bool st = !(NH_AB && (a.probe & 64));
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+        const int pc = lane + 64 * i, el = pc / (N * N / 4), row = (pc / (N / 4)) % N, c4 = pc % (N / 4);
+        const int e = c0 + el;
+        if (e < total && st) {
+            const int p = e >= cnt ? 1 : 0, code = ent[e - p * cnt];
+            const int lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4;
+            const int64_t o = (int64_t)(y0c + ly + row) * a.pitch + x0c + lx + 4 * c4;
+            const int4 lv = *(const int4*)&tile[(el * N + row) * N + 4 * c4];
+            int32_t* lp = (p ? pp.lvl[1] : pp.lvl[0]) + o;
+            lp[0] = lv.x;
+            lp[1] = lv.y;
+            lp[2] = lv.z;
+            lp[3] = lv.w;
+            if (!rec_later) {
+                const int16_t* q4 = &rc2[p][ly + 1 + row][lx + 1 + 4 * c4];
+                int16_t* rp = (p ? pp.rec[1] : pp.rec[0]) + o;
+                rp[0] = q4[0];
+                rp[1] = q4[1];
+                rp[2] = q4[2];
+                rp[3] = q4[3];
+            }
+            if (c4 == 0 && (row & 3) == 0) {
+                uint8_t* tu = p ? pp.tu[1] : pp.tu[0];
+                const int w4 = a.w / 4;
+#pragma unroll
+                for (int jj = 0; jj < N / 4; ++jj)
+                    tu[(int64_t)((y0c + ly + row) / 4) * w4 + (x0c + lx) / 4 + jj] = (uint8_t)L2;
+            }
+        }
+    }
+    pair_sync();   // the tile's and rc's reads before the next batch writes them
     phase(5);
 }
 
@@ -2054,12 +2327,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                                 NH_PLAN_BATCH(32, false, cq[3])
                             }
                             break;
-                        case 1: NH_PLAN_BATCH(16, false, cq[2]) break;
-                        case 2: NH_PLAN_BATCH(8, false, cq[1]) break;
+#define NH_MOSAIC_BATCH(NN, DST, Q)                                                                           \
+                        for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
+                            tu_closed_batch_mma<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, Q, ph, rec_flush);
+                        case 1:
+                            if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(16, false, cq[2]) }
+                            else { NH_PLAN_BATCH(16, false, cq[2]) }
+                            break;
+                        case 2:
+                            if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(8, false, cq[1]) }
+                            else { NH_PLAN_BATCH(8, false, cq[1]) }
+                            break;
                         default:
-                            if (a.is_luma) { NH_PLAN_BATCH(4, true, cq[0]) }
-                            else { NH_PLAN_BATCH(4, false, cq[0]) }
+                            if (a.is_luma) {
+                                if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(4, true, cq[0]) }
+                                else { NH_PLAN_BATCH(4, true, cq[0]) }
+                            } else {
+                                NH_PLAN_BATCH(4, false, cq[0])
+                            }
 #undef NH_PLAN_BATCH
+#undef NH_MOSAIC_BATCH
                     }
                     off += cnt;
                 }
@@ -2425,6 +2712,16 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int rec_ctu = NH_KNOB("NH_CLOSED4_REC_CTU", 1);
     a.rec_ctu = rec_ctu && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
                 !((uintptr_t)d_recon & 7);
+    {   // tu_closed_batch_mma's per-lane bases and initial accumulators
+        static PerDeviceOnce once_m;
+        const int rcm = once_m.run([] {
+            static MosaicLane mt[3][64];
+            make_mosaic(mt);
+            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic), mt, sizeof(mt)));
+            return (int)NH_OK;
+        });
+        if (rcm) return rcm;
+    }
     if (a.mfma32) {
         static PerDeviceOnce once;
         const int rcb = once.run([] {
@@ -2624,9 +2921,12 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
 
 extern "C" int nh_intra_rdo_closed_status(const void* d_work, int* status, void* stream) {
     if (!d_work || !status) return NH_EARG;
-    int32_t v = 0;
-    NH_HIP(hipMemcpyAsync(&v, (const int32_t*)d_work + 1, 4, hipMemcpyDeviceToHost, as_stream(stream)));
+    // the word lands in a per-thread pinned slot: a direct DMA, not the staged copy of a pageable
+    // destination (the call sits inside every timed closed-loop launch set)
+    static thread_local int32_t* pinned = nullptr;
+    if (!pinned) NH_HIP(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
+    NH_HIP(hipMemcpyAsync(pinned, (const int32_t*)d_work + 1, 4, hipMemcpyDeviceToHost, as_stream(stream)));
     NH_HIP(hipStreamSynchronize(as_stream(stream)));
-    *status = v;
+    *status = *(volatile int32_t*)pinned;
     return NH_OK;
 }

@@ -105,6 +105,46 @@ def main():
     print("f16 32x32 chain: operands", ops, "(exact in f16 below 2048), |sums|", sums, "(limit 2^24)")
     assert max(ops.values()) < 2048 and max(sums.values()) < 2 ** 24
     assert all(int(r) == 0 for r in rs[1:]) and int(rs[0]) == 2048
+    mosaic_bounds()
+
+
+def mosaic_bounds():
+    """The closed loop's small-TU mosaics (tu_closed_batch_mma): 16x16
+    f16 MFMA passes against the basis * 2^-S.  Each accumulator in units of 2^-S must
+    stay below 2^24 (exact fp32), every f16 operand an exact integer: the residual as
+    768 + n (|n| <= 255, binade [512, 1024)), the pass-1 output as 1536 + t in
+    [1024, 2048) (|t| <= 511: truncation = floor), the dequantized coefficients and
+    the inverse-pass-1 output below 2048.  DCT4 (chroma 4x4) is printed to show why
+    it stays on the packed chain."""
+    print("mosaic    pass1-out  pass2 op  coeff   dq  inv1-out  |sum| max (units 2^-S)  ok")
+    for n, dst in ((4, True), (8, False), (16, False), (4, False)):
+        T = mat(n, dst)
+        l2 = int(np.log2(n))
+        s = l2 + 5
+        rl1, cl1 = int(np.abs(T).sum(1).max()), int(np.abs(T).sum(0).max())
+        rsum = [int(v) for v in T.sum(1)]
+        x0 = 255
+        f1 = shift_bound(x0 * rl1, s)
+        c = shift_bound(f1 * rl1, s)
+        dq = max(dequant(quant(c, qp, l2, intra), qp) for qp in range(52) for intra in (True, False))
+        i1 = shift_bound(dq * cl1, s)
+        i2 = shift_bound(i1 * cl1, s)
+        c1 = max(abs(0.5 + 1536 - 768 * r / 2 ** s) for r in rsum)
+        c2 = max(abs(0.5 - 1536 * r / 2 ** s) for r in rsum)
+        sums = [int(np.abs(T).sum(1).max()) * (768 + x0) + int(c1 * 2 ** s),
+                rl1 * (1536 + f1) + int(c2 * 2 ** s),
+                dq * cl1 + 2 ** (s - 1),
+                i1 * cl1 + int(1536.5 * 2 ** s)]
+        ok = f1 <= 511 and 1536 + f1 < 2048 and dq < 2048 and i1 <= 2048 and max(sums) < 2 ** 24
+        print("%-8s %9d %9d %6d %4d %9d %23d  %s" % (("DST" if dst else "DCT") + str(n), f1, 1536 + f1, c, dq, i1,
+                                                      max(sums), ok))
+        # dequantize in 16-bit lanes: (l * dqs + dqr) >> dqsh with dqs = DQ << max(per - 4, 0)
+        ldq = max(quant(c, qp, l2, intra) * (DQ[qp % 6] << max(qp // 6 - 4, 0)) + (1 << 3)
+                  for qp in range(52) for intra in (True, False))
+        ok = ok and ldq < 2 ** 15
+        if (n, dst) != (4, False):
+            assert ok, (n, dst, ldq)
+        assert i2 < 1 << 15
 
 
 if __name__ == "__main__":
