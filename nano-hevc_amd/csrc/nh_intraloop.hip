@@ -1525,12 +1525,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
 // Every TU runs the same packed chain as tu_closed_batch_pk on its own plane's
 // LDS reconstruction and tile: same results.  The planes of a pair never
 // exchange data; each publishes and polls its own line words.
+// Round 5: a wave may code NPL planes (2 for luma, 4 for chroma): the planes of
+// a group are consecutive groups of the set, so plane s of the wave lies s group
+// strides past plane 0 (and its TU map s * ppg TU planes past), no pointer table.
 struct PairPlanes {
-    const int16_t* src[2];
-    int32_t* lvl[2];
-    int16_t* rec[2];
-    uint8_t* tu[2];
+    const int16_t* src0;
+    int32_t* lvl0;
+    int16_t* rec0;
+    uint8_t* tu0;
+    int64_t gs, ts;   // elements / TU-map bytes from one plane of the wave to the next
+    __device__ const int16_t* src(int p) const { return src0 + p * gs; }
+    __device__ int32_t* lvl(int p) const { return lvl0 + p * gs; }
+    __device__ int16_t* rec(int p) const { return rec0 + p * gs; }
+    __device__ uint8_t* tu(int p) const { return tu0 + p * ts; }
 };
+// plane of batch entry e (< total = cnt * planes): e / cnt for up to 4 planes, without a division
+__device__ __forceinline__ int entry_plane(int e, int cnt) {
+    return (e >= cnt ? 1 : 0) + (e >= 2 * cnt ? 1 : 0) + (e >= 3 * cnt ? 1 : 0);
+}
 
 // k_tu_closed_pair runs ONE wave per workgroup: its LDS accesses execute in
 // program order, so a wave-level code-motion barrier is all the chains and the
@@ -1549,8 +1561,8 @@ struct PairPlanes {
 #ifndef NH_CLOSED4_TL_INNER   // 1: closed_chain32_tf's per-lane constants made per TU, not held
 #define NH_CLOSED4_TL_INNER 0
 #endif
-#ifndef NH_CLOSED4_MOSAIC   // 1: 16x16, 8x8 and luma 4x4 TUs on the f16 matrix cores (tu_closed_batch_mma)
-#define NH_CLOSED4_MOSAIC 1
+#ifndef NH_CLOSED4_MOSAIC   // 1: 16x16, 8x8 and luma 4x4 TUs on the f16 matrix cores (tu_closed_batch_mma); 2: + chroma 4x4
+#define NH_CLOSED4_MOSAIC 2
 #endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
@@ -1563,10 +1575,10 @@ __device__ __forceinline__ void pair_sync() {
 #endif
 }
 
-template <int N, bool DST>
+template <int N, bool DST, int RP = 33>
 __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
-                                                    int16_t (*rc2)[33][33], int16_t* t16, const ChainQ& cq,
+                                                    int16_t (*rc2)[RP][RP], int16_t* t16, const ChainQ& cq,
                                                     uint64_t* ph = nullptr, bool rec_later = false) {
     constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
     // A/B build, NH_CLOSED4_STAMPS: shader cycles of the batch's phases, summed per TU size into ph
@@ -1583,11 +1595,11 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     constexpr int32_t BIAS = 1 << (S - 1);
     const int lane = opaque_lane64(), t = lane % N, e = c0 + lane / N;
     const bool on = e < total;
-    const int p = on && e >= cnt ? 1 : 0, k = on ? e - p * cnt : 0;   // idle lanes shadow plane 0's first TU
+    const int p = on ? entry_plane(e, cnt) : 0, k = on ? e - p * cnt : 0;   // idle lanes shadow plane 0's first TU
     const int code = ent[k], lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4, x = x0c + lx, y = y0c + ly;
-    int16_t (*rc)[33] = rc2[p];
-    const int16_t* src = p ? pp.src[1] : pp.src[0];
-    int16_t* tl = t16 + p * (32 * TP) + ly * TP + lx;   // tl[line * TP + slot]
+    int16_t (*rc)[RP] = rc2[p];
+    const int16_t* src = pp.src(p);
+    int16_t* tl = t16 + p * ((RP - 1) * TP) + ly * TP + lx;   // tl[line * TP + slot]
     // the TU's source column, every load issued before any use: the waits for them then
     // overlap the neighbour reads and the DC / planar sums, not one round trip per row pair
     int32_t sv[N];
@@ -1653,7 +1665,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     pair_sync();
     phase(2);
     if (on) {   // quantize_block -> levels; dequantize_block -> line k, slot inv_slot(t)
-        int32_t* lrow = (p ? pp.lvl[1] : pp.lvl[0]) + (int64_t)(y + t) * a.pitch + x;
+        int32_t* lrow = pp.lvl(p) + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
         for (int q4 = 0; q4 < N / 4; ++q4) {   // 4 levels per piece, stored together
             int32_t l4[4];
@@ -1692,7 +1704,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     }
     if (on) {   // reconstruct + clip (intra.py:70-78); planar in row layout
         const int32_t b = (N - 1) * leftt + tr + (t + 1) * bl + N, stv = tr - leftt;
-        int16_t* rrow = (p ? pp.rec[1] : pp.rec[0]) + (int64_t)(y + t) * a.pitch + x;
+        int16_t* rrow = pp.rec(p) + (int64_t)(y + t) * a.pitch + x;
 #pragma unroll
         for (int q4 = 0; q4 < N / 4; ++q4) {   // 4 samples per piece, stored together
             int32_t r4[4];
@@ -1709,7 +1721,7 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
             for (int e = 0; e < 4; ++e) rrow[4 * q4 + e] = (int16_t)r4[e];   // (adjacent: one 8-B store)
         }
         if (t < N / 4 && !(NH_AB && (a.probe & 64))) {
-            uint8_t* tu = p ? pp.tu[1] : pp.tu[0];
+            uint8_t* tu = pp.tu(p);
             const int w4 = a.w / 4;
             for (int jj = 0; jj < N / 4; ++jj) tu[(int64_t)(y / 4 + t) * w4 + x / 4 + jj] = (uint8_t)L2;
         }
@@ -1743,16 +1755,19 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
 //  * the inverse pass 2 starts at 1536.5: clamped to [1280, 1792] its f16 bits
 //    are 0x6600 + R' (R' = R clamped to [-256, 256]), and bits - (0x6600 - pred)
 //    saturating at 0, then min 255, is the clip of pred + R.
-// DCT4 (chroma 4x4) stays on the packed chain: its inverse pass 1 reaches 2223,
-// beyond f16's integers.  Same results as tu_closed_batch_pk2 on 8-bit streams.
+// DCT4 (chroma 4x4): its inverse pass 1 reaches 2223, beyond f16's integers, so
+// its inverse pass 2 is two MFMAs into one accumulator: tmp = 2h + b with h =
+// floor(tmp / 2) (<= 1112) against the basis * 2^-(S-1), b in {0, 1} against the
+// basis * 2^-S.  Same results as tu_closed_batch_pk2 on 8-bit streams.
 typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 typedef float f4_t __attribute__((ext_vector_type(4)));
 struct MosaicLane {            // per (kind, lane): 32 B
     uint32_t bf[2], bi[2];     // the B operands: Tb^T (passes 1, 2) and Tb (inverse passes), f16 * 2^-S
     float c1, c2;              // the initial accumulators of passes 1 and 2
-    uint32_t pad[2];
+    uint32_t bi2[2];           // DCT4: Tb * 2^-(S-1) (the inverse pass 2's h half)
 };
-__constant__ MosaicLane c_mosaic[3][64];   // kinds: 0 DST4, 1 DCT8, 2 DCT16
+__constant__ MosaicLane c_mosaic[4][64];   // kinds: 0 DST4, 1 DCT8, 2 DCT16, 3 DCT4
+constexpr int Log2Rt(int n) { return n == 4 ? 2 : n == 8 ? 3 : n == 16 ? 4 : 5; }
 inline uint16_t f16_bits_exact(int num, int sh) {   // num * 2^-sh as f16 bits (|num| < 2048, a normal result)
     if (num == 0) return 0;
     uint16_t s = num < 0 ? 0x8000 : 0;
@@ -1762,18 +1777,19 @@ inline uint16_t f16_bits_exact(int num, int sh) {   // num * 2^-sh as f16 bits (
     return (uint16_t)(s | (uint16_t)((e + 10 + 15) << 10) | (uint16_t)(m & 1023));
 }
 inline void make_mosaic(MosaicLane (*out)[64]) {
-    for (int kind = 0; kind < 3; ++kind) {
-        const int N = kind == 0 ? 4 : kind == 1 ? 8 : 16, S = (kind == 0 ? 2 : kind == 1 ? 3 : 4) + 5;
+    for (int kind = 0; kind < 4; ++kind) {
+        const int N = kind == 1 ? 8 : kind == 2 ? 16 : 4, S = Log2Rt(N) + 5;
         auto T = [&](int k, int n) {
-            return kind == 0 ? dst4c(k, n) : kind == 1 ? dctc<8>(k, n) : dctc<16>(k, n);
+            return kind == 0 ? dst4c(k, n) : kind == 1 ? dctc<8>(k, n) : kind == 2 ? dctc<16>(k, n) : dctc<4>(k, n);
         };
         for (int l = 0; l < 64; ++l) {
             const int c = l & 15, g = l >> 4;
-            uint16_t bf[4], bi[4];
+            uint16_t bf[4], bi[4], bi2[4];
             for (int r = 0; r < 4; ++r) {
                 const int k = 4 * g + r, same = k / N == c / N;
                 bf[r] = same ? f16_bits_exact(T(c % N, k % N), S) : 0;   // B1[k][j] = T[j][k]
                 bi[r] = same ? f16_bits_exact(T(k % N, c % N), S) : 0;   // B3[k][j] = T[k][j]
+                bi2[r] = same ? f16_bits_exact(T(k % N, c % N), S - 1) : 0;
             }
             int rs = 0;
             for (int n = 0; n < N; ++n) rs += T(c % N, n);
@@ -1784,7 +1800,8 @@ inline void make_mosaic(MosaicLane (*out)[64]) {
             m.bi[1] = bi[2] | ((uint32_t)bi[3] << 16);
             m.c1 = 0.5f + 1536.0f - 768.0f * (float)rs / (float)(1 << S);
             m.c2 = 0.5f - 1536.0f * (float)rs / (float)(1 << S);
-            m.pad[0] = m.pad[1] = 0;
+            m.bi2[0] = bi2[0] | ((uint32_t)bi2[1] << 16);
+            m.bi2[1] = bi2[2] | ((uint32_t)bi2[3] << 16);
         }
     }
 }
@@ -1800,13 +1817,15 @@ __device__ __forceinline__ int32_t tu_sum(int32_t v) {
         return v + lane_perm<-1>(v);
     } else return grp_sum<64>(v);
 }
-template <int N, bool DST>
+template <int N, bool DST, int RP = 33>
 __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
-                                                    int16_t (*rc2)[33][33], int32_t* tile, const ChainQ& cq,
+                                                    int16_t (*rc2)[RP][RP], int32_t* tile, const ChainQ& cq,
                                                     uint64_t* ph = nullptr, bool rec_later = false) {
-    static_assert(N == 4 ? DST : (N == 8 || N == 16) && !DST, "mosaic kinds: DST4, DCT8, DCT16");
-    constexpr int L2 = Log2<N>::v, NM = N / 4, TS = 16 / N, TPM = TS * TS, KIND = N == 4 ? 0 : N == 8 ? 1 : 2;
+    static_assert(N == 4 || ((N == 8 || N == 16) && !DST), "mosaic kinds: DST4, DCT4, DCT8, DCT16");
+    constexpr int L2 = Log2<N>::v, NM = N / 4, TS = 16 / N, TPM = TS * TS;
+    constexpr int KIND = N == 4 ? (DST ? 0 : 3) : N == 8 ? 1 : 2;
+    constexpr bool SPLIT = N == 4 && !DST;   // DCT4: the inverse pass 2 in two halves
     uint64_t ph_t = 0;
     auto phase = [&](int k) {   // A/B build, NH_CLOSED4_STAMPS (as tu_closed_batch_pk2)
         if (NH_AB && ph) {
@@ -1825,7 +1844,7 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     for (int m = 0; m < NM; ++m) {
         const int e = c0 + m * TPM + br * TS + bc;
         onm[m] = e < total;
-        pm[m] = onm[m] && e >= cnt ? 1 : 0;
+        pm[m] = onm[m] ? entry_plane(e, cnt) : 0;
         const int code = ent[onm[m] ? e - pm[m] * cnt : 0];   // idle lanes shadow plane 0's first TU
         lxm[m] = (code & 7) * 4;
         lym[m] = ((code >> 3) & 7) * 4;
@@ -1834,7 +1853,7 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     int32_t sv[NM][4];
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-        const int16_t* sp = (pm[m] ? pp.src[1] : pp.src[0]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
+        const int16_t* sp = pp.src(pm[m]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
             sv[m][r] = (NH_AB && (a.probe & 32)) ? rc2[pm[m]][lym[m] + 1 + yr0 + r][lxm[m] + 1 + t]
@@ -1845,7 +1864,7 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     pku16 pr2[NM][2];
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-        int16_t (*rc)[33] = rc2[pm[m]];
+        int16_t (*rc)[RP] = rc2[pm[m]];
         const int lx = lxm[m], ly = lym[m];
         const int32_t topt = rc[ly][lx + 1 + t], tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // __main__.py:168
         // DC (intra.py:46-62): the TU's lanes of row group 0 add top[t], of row group 1 left[t] (N = 4: both)
@@ -1926,16 +1945,36 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     for (int m = 0; m < NM; ++m)
         acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(dq[m][0], dq[m][1])), bi,
                                                        (f4_t){0.5f, 0.5f, 0.5f, 0.5f}, 0, 0, 0);
+    if constexpr (SPLIT) {
+        const h4_t bi2 = __builtin_bit_cast(h4_t, make_uint2(mw1.z, mw1.w));
 #pragma unroll
-    for (int m = 0; m < NM; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-            __builtin_bit_cast(h4_t, make_uint2(pk_floor_h(acc[m][0], acc[m][1]), pk_floor_h(acc[m][2], acc[m][3]))), bi,
-            (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
+        for (int m = 0; m < NM; ++m) {
+            float hf[4], bf1[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float f = __builtin_floorf(acc[m][r]);
+                hf[r] = __builtin_floorf(acc[m][r] * 0.5f);   // floor(floor(x) / 2) = floor(x / 2)
+                bf1[r] = __builtin_fmaf(-2.0f, hf[r], f);
+            }
+            const f4_t a4 = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(hf[0], hf[1]), pk_trunc_h(hf[2], hf[3]))), bi2,
+                (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(bf1[0], bf1[1]), pk_trunc_h(bf1[2], bf1[3]))), bi, a4,
+                0, 0, 0);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                __builtin_bit_cast(h4_t, make_uint2(pk_floor_h(acc[m][0], acc[m][1]), pk_floor_h(acc[m][2], acc[m][3]))),
+                bi, (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
+    }
     phase(3);
     // reconstruct + clip (intra.py:70-78) into rc (no TU of this batch reads another's samples)
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-        int16_t (*rc)[33] = rc2[pm[m]];
+        int16_t (*rc)[RP] = rc2[pm[m]];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const float x0 = __builtin_amdgcn_fmed3f(acc[m][2 * q], 1280.0f, 1792.0f);
@@ -1958,25 +1997,25 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
         const int pc = lane + 64 * i, el = pc / (N * N / 4), row = (pc / (N / 4)) % N, c4 = pc % (N / 4);
         const int e = c0 + el;
         if (e < total && st) {
-            const int p = e >= cnt ? 1 : 0, code = ent[e - p * cnt];
+            const int p = entry_plane(e, cnt), code = ent[e - p * cnt];
             const int lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4;
             const int64_t o = (int64_t)(y0c + ly + row) * a.pitch + x0c + lx + 4 * c4;
             const int4 lv = *(const int4*)&tile[(el * N + row) * N + 4 * c4];
-            int32_t* lp = (p ? pp.lvl[1] : pp.lvl[0]) + o;
+            int32_t* lp = pp.lvl(p) + o;
             lp[0] = lv.x;
             lp[1] = lv.y;
             lp[2] = lv.z;
             lp[3] = lv.w;
             if (!rec_later) {
                 const int16_t* q4 = &rc2[p][ly + 1 + row][lx + 1 + 4 * c4];
-                int16_t* rp = (p ? pp.rec[1] : pp.rec[0]) + o;
+                int16_t* rp = pp.rec(p) + o;
                 rp[0] = q4[0];
                 rp[1] = q4[1];
                 rp[2] = q4[2];
                 rp[3] = q4[3];
             }
             if (c4 == 0 && (row & 3) == 0) {
-                uint8_t* tu = p ? pp.tu[1] : pp.tu[0];
+                uint8_t* tu = pp.tu(p);
                 const int w4 = a.w / 4;
 #pragma unroll
                 for (int jj = 0; jj < N / 4; ++jj)
@@ -2169,18 +2208,33 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 // pair's CTU row above, claimed before it.
 // The compiler's allocation (135 VGPRs, 3 waves/SIMD): 0.150 ms per 4K YUV420
 // frame vs 0.164 capped at 4 waves (128 VGPRs, 1 spilled), DESIGN.md §4.4a.
-constexpr int kPairWaves = 3;
+#ifndef NH_CLOSED4_WAVES32   // waves-per-EU target of the CTB 32 (luma) instance
+#define NH_CLOSED4_WAVES32 3
+#endif
+constexpr int kPairWaves = NH_CLOSED4_WAVES32;
+#ifndef NH_CLOSED4_NPL16   // planes per wave of the CTB <= 16 (chroma) instance: 2 or 4
+#define NH_CLOSED4_NPL16 2
+#endif
+#ifndef NH_CLOSED4_WAVES16   // its waves-per-EU target
+#define NH_CLOSED4_WAVES16 3
+#endif
+constexpr int kPairWaves16 = NH_CLOSED4_WAVES16;
 constexpr int kStampWords = 48;   // A/B stamps per (ticket, CTU)
 // REC: whole CTUs' packed-chain recon leaves from rc at the CTU's end (Closed4Args::rec_ctu); a
 // separate instantiation, so the per-TU form's code is the same as without the flush
-template <int WAVES, bool REC>
+// CTBM: the largest CTB the instance codes (32: luma, 16: chroma; rc rows of CTBM + 1), NPL: planes
+// per wave (2 or 4; lanes [64 / NPL q, 64 / NPL (q + 1)) serve plane q's line words and left column)
+template <int WAVES, bool REC, int CTBM = 32, int NPL = 2>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed_pair(Closed4Args a) {
-    constexpr int TP = 34;
-    __shared__ int16_t rc[2][33][33];
-    // the packed chains' int16 tiles (2 x 32 rows of TP), or closed_chain32_tf's level / recon tile
-    __shared__ __attribute__((aligned(16))) int32_t t32[32 * kClOutP > 32 * TP ? 32 * kClOutP : 32 * TP];
+    constexpr int TP = 34, RP = CTBM + 1, LPP = 64 / NPL;
+    static_assert((NPL == 2 || NPL == 4) && CTBM <= LPP && (CTBM == 32 || CTBM == 16), "plane group shape");
+    __shared__ int16_t rc[NPL][RP][RP];
+    // the packed chains' int16 tiles (NPL x CTBM rows of TP), the mosaics' level tile (1,024 ints) or
+    // closed_chain32_tf's level / recon tile (CTBM 32)
+    constexpr int kT32 = std::max({NPL * CTBM * TP / 2, 1024, CTBM == 32 ? 32 * kClOutP : 0});
+    __shared__ __attribute__((aligned(16))) int32_t t32[kT32];
     int16_t* const t16 = (int16_t*)t32;
-    __shared__ __attribute__((aligned(16))) BasisHC basis_s;
+    __shared__ __attribute__((aligned(16))) std::conditional_t<CTBM == 32, BasisHC, int> basis_s;
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
 #endif
@@ -2193,22 +2247,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // the critical (luma) wavefront issues first
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
-    if (a.mfma32) {   // closed_chain32_tf's bases: 4 KB, once per workgroup
-        const uint4* s4 = (const uint4*)&c_basis_hc_cl;
-        for (int i = lane; i < (int)(sizeof(BasisHC) / 16); i += 64) ((uint4*)&basis_s)[i] = s4[i];
-        pair_sync();
+    if constexpr (CTBM == 32) {
+        if (a.mfma32) {   // closed_chain32_tf's bases: 4 KB, once per workgroup
+            const uint4* s4 = (const uint4*)&c_basis_hc_cl;
+            for (int i = lane; i < (int)(sizeof(BasisHC) / 16); i += 64) ((uint4*)&basis_s)[i] = s4[i];
+            pair_sync();
+        }
     }
     ChainQ cq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
 #if !NH_CLOSED4_TL_INNER
-    const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);   // (read only when a.mfma32)
+    TfLane tl{};
+    if constexpr (CTBM == 32) tl = make_tf_lane(cq[3], basis_s, lane & 31);   // (read only when a.mfma32)
 #endif
     uint64_t* lines = reinterpret_cast<uint64_t*>(a.work + a.lines0);
-    const int ngroups = a.nplanes / a.ppg, npairs = ((ngroups + 1) / 2) * a.ppg;
+    const int ngroups = a.nplanes / a.ppg, npairs = ((ngroups + NPL - 1) / NPL) * a.ppg;
     const int total = a.crows * npairs;
-    // lanes [32 q, 32 q + 32) serve plane q of the pair for the line words and the left column (ctb <= 32)
-    const int hq = lane >> 5, hl = lane & 31;
+    const int hq = lane / LPP, hl = lane % LPP;
     for (;;) {
         if (lane == 0) {
             row_s = atomicAdd(&a.work[0], 1);
@@ -2218,26 +2274,26 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
         const int tk = row_s;
         if (tk >= total) break;
         const int cy = tk / npairs, q = tk - cy * npairs;
-        const int c = q % a.ppg, g0 = 2 * (q / a.ppg);
-        const int two = g0 + 1 < ngroups ? 1 : 0;
+        const int c = q % a.ppg, g0 = NPL * (q / a.ppg);
+        const int npl = min(NPL, ngroups - g0);   // planes this wave codes (the set's last group may have fewer)
         PairPlanes pp;
-        uint64_t* line[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int g = g0 + (s & two);   // a lone plane: both slots name it (slot 1 never codes)
-            const int64_t off = (int64_t)g * a.group_stride + (int64_t)c * a.plane_stride;
-            const int pl = g * a.ppg + c;
-            pp.src[s] = a.src + off;
-            pp.lvl[s] = a.lvl + off;
-            pp.rec[s] = a.rec + off;
-            pp.tu[s] = a.tu + (int64_t)pl * a.tu_plane;
-            line[s] = lines + (int64_t)pl * a.lw;
+        {
+            const int64_t off = (int64_t)g0 * a.group_stride + (int64_t)c * a.plane_stride;
+            const int pl = g0 * a.ppg + c;
+            pp.src0 = a.src + off;
+            pp.lvl0 = a.lvl + off;
+            pp.rec0 = a.rec + off;
+            pp.tu0 = a.tu + (int64_t)pl * a.tu_plane;
+            pp.gs = a.group_stride;
+            pp.ts = (int64_t)a.ppg * a.tu_plane;
         }
+        // plane hq's line words (lanes of planes past npl never touch them)
+        uint64_t* const lineq = lines + (int64_t)((g0 + hq) * a.ppg + c) * a.lw;
         const int y0c = cy * ctb;
 #if !NH_CLOSED4_PLAN
         const int pid = a.plane_id + c;
 #endif
-        for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;   // recon starts as zeros (Frame.zeros)
+        for (int i = lane; i < NPL * RP * RP; i += 64) (&rc[0][0][0])[i] = 0;   // recon starts as zeros (Frame.zeros)
         pair_sync();
         if (hl < ctb) rc[hq][1 + hl][0] = 128;                             // x == 0: left = 128 (block.py:45-50)
         // the first poll of a CTU's line words is issued at the end of the previous CTU,
@@ -2256,14 +2312,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             if (cy == 0) {
                 if (hl < ctb) rc[hq][0][1 + hl] = 128;
             } else {
-                const bool need = hl < nw && hq <= two;
+                const bool need = hl < nw && hq < npl;
                 uint32_t val = 0;
                 int spins = 0;
                 for (;;) {
                     bool ok = true;
                     if (need) {
                         const uint64_t v = (NH_CLOSED4_EARLYPOLL && spins == 0 && cx > 0) ? early
-                                                                                        : ld_sys64(line[hq] + x0c / 2 + hl);
+                                                                                        : ld_sys64(lineq + x0c / 2 + hl);
                         ok = (int)(v >> 32) == cy || (NH_AB && (a.probe & 1));
                         val = (uint32_t)v;
                     }
@@ -2305,26 +2361,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 for (; nz; nz &= nz - 1) {
                     const int rs = __builtin_ctzll(nz);
                     const int cnt = __builtin_amdgcn_readlane(cntv, rs);
-                    const int tot = cnt << two;
+                    const int tot = cnt * npl;
                     const uint8_t* ent = ent_s + off;
                     switch (rs & 3) {
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
                             tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, rec_flush);
-                        case 0:   // (CTB 32: the one 32x32 TU of the CTU, in both planes)
-                            if (a.mfma32) {   // one plane after the other, ONE copy of the chain's code:
-                                // a loop the compiler keeps (instruction-cache footprint)
+                        case 0:   // (CTB 32: the one 32x32 TU of the CTU, in every plane)
+                            if constexpr (CTBM == 32) {
+                                if (a.mfma32) {   // one plane after the other, ONE copy of the chain's code:
+                                    // a loop the compiler keeps (instruction-cache footprint)
 #pragma clang loop unroll(disable)
-                                for (int s2 = 0; s2 <= two; ++s2) {
+                                    for (int s2 = 0; s2 < npl; ++s2) {
 #if NH_CLOSED4_TL_INNER
-                                    const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);
+                                        const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);
 #endif
-                                    closed_chain32_tf(a, s2 ? pp.src[1] : pp.src[0], s2 ? pp.lvl[1] : pp.lvl[0],
-                                                      s2 ? pp.rec[1] : pp.rec[0], s2 ? pp.tu[1] : pp.tu[0], x0c, y0c,
-                                                      rc[s2], t32, basis_s, cq[3], tl);
+                                        closed_chain32_tf(a, pp.src(s2), pp.lvl(s2), pp.rec(s2), pp.tu(s2), x0c, y0c,
+                                                          rc[s2], t32, basis_s, cq[3], tl);
+                                    }
+                                } else {
+                                    NH_PLAN_BATCH(32, false, cq[3])
                                 }
-                            } else {
-                                NH_PLAN_BATCH(32, false, cq[3])
                             }
                             break;
 #define NH_MOSAIC_BATCH(NN, DST, Q)                                                                           \
@@ -2343,7 +2400,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                                 if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(4, true, cq[0]) }
                                 else { NH_PLAN_BATCH(4, true, cq[0]) }
                             } else {
-                                NH_PLAN_BATCH(4, false, cq[0])
+                                if (NH_CLOSED4_MOSAIC >= 2) { NH_MOSAIC_BATCH(4, false, cq[0]) }
+                                else { NH_PLAN_BATCH(4, false, cq[0]) }
                             }
 #undef NH_PLAN_BATCH
 #undef NH_MOSAIC_BATCH
@@ -2387,7 +2445,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     const int cnt = __popcll(m);                                                             \
                     if (ready && tn == NN) ent_s[__popcll(m & lt)] = (uint8_t)(ox | (oy << 3));            \
                     pair_sync();                                                                             \
-                    const int tot = cnt << two;                                                              \
+                    const int tot = cnt * npl;                                                               \
                     for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                   \
                         tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent_s, rc, t16, Q);      \
                 }
@@ -2406,18 +2464,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             if (NH_AB && a.stamps) st2 = __builtin_amdgcn_s_memtime();
             if (NH_CLOSED4_EARLYPOLL && cy > 0 && cx + 1 < a.ccols) {
                 const int nwn = (min(ctb, a.w - x0c - ctb) + 1) / 2;
-                if (hl < nwn && hq <= two) early = ld_sys64(line[hq] + (x0c + ctb) / 2 + hl);
+                if (hl < nwn && hq < npl) early = ld_sys64(lineq + (x0c + ctb) / 2 + hl);
             }
             // publish both bottom rows (the next CTU row polls them), then slide: right column -> left column
-            if (cy + 1 < a.crows && hl < nw && hq <= two) {
+            if (cy + 1 < a.crows && hl < nw && hq < npl) {
                 const uint32_t lo = (uint16_t)rc[hq][ctb][1 + 2 * hl];
                 const uint32_t hi = 2 * hl + 1 < ctb ? (uint16_t)rc[hq][ctb][2 + 2 * hl] : 0u;
-                st_sys64(line[hq] + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
+                st_sys64(lineq + x0c / 2 + hl, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
             }
             if (rec_flush) {   // the CTU's recon rows, 8-B pieces: ctb / 4 lanes per row, 64 / (ctb / 4) rows a pass
                 const int pr = ctb / 4, rpp = 64 / pr, pc = lane % pr, r0 = lane / pr;
-                for (int s2 = 0; s2 <= two; ++s2) {
-                    int16_t* rb = (s2 ? pp.rec[1] : pp.rec[0]) + (int64_t)y0c * a.pitch + x0c + 4 * pc;
+                for (int s2 = 0; s2 < npl; ++s2) {
+                    int16_t* rb = pp.rec(s2) + (int64_t)y0c * a.pitch + x0c + 4 * pc;
                     for (int r = r0; r < ctb; r += rpp) {
                         const int16_t* q4 = &rc[s2][1 + r][1 + 4 * pc];
                         const uint32_t lo = (uint16_t)q4[0] | ((uint32_t)(uint16_t)q4[1] << 16);
@@ -2434,7 +2492,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             // samples coded before it or the top row / left column rewritten per CTU;
             // samples past a ragged edge belong to no TU and are never read)
             if (NH_CLOSED4_PAIR_CLEAR && !(NH_AB && (a.probe & 8)))
-                for (int i = lane; i < 2 * 33 * 33; i += 64) (&rc[0][0][0])[i] = 0;
+                for (int i = lane; i < NPL * RP * RP; i += 64) (&rc[0][0][0])[i] = 0;
             pair_sync();
             if (hl < ctb) rc[hq][1 + hl][0] = keep;
             pair_sync();
@@ -2715,7 +2773,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     {   // tu_closed_batch_mma's per-lane bases and initial accumulators
         static PerDeviceOnce once_m;
         const int rcm = once_m.run([] {
-            static MosaicLane mt[3][64];
+            static MosaicLane mt[4][64];
             make_mosaic(mt);
             NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic), mt, sizeof(mt)));
             return (int)NH_OK;
@@ -2758,9 +2816,15 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
     if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
         int per_cu = 0;
-        auto kern = a.rec_ctu ? k_tu_closed_pair<kPairWaves, true> : k_tu_closed_pair<kPairWaves, false>;
+        // CTB 32 (luma): plane pairs; CTB <= 16 (chroma): NH_CLOSED4_NPL16 planes per wave (4: the
+        // chroma wavefront needs half the waves, so with luma's it fits the resident slots)
+        void (*kern)(Closed4Args) =
+            ctb == 32 ? (a.rec_ctu ? k_tu_closed_pair<kPairWaves, true, 32, 2> : k_tu_closed_pair<kPairWaves, false, 32, 2>)
+                      : (a.rec_ctu ? k_tu_closed_pair<kPairWaves16, true, 16, NH_CLOSED4_NPL16>
+                                   : k_tu_closed_pair<kPairWaves16, false, 16, NH_CLOSED4_NPL16>);
+        const int npl = ctb == 32 ? 2 : NH_CLOSED4_NPL16;
         NH_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, 0));
-        const int64_t prow = (int64_t)a.crows * ((set->num_groups + 1) / 2) * set->planes_per_group;
+        const int64_t prow = (int64_t)a.crows * ((set->num_groups + npl - 1) / npl) * set->planes_per_group;
         if (NH_CLOSED4_PLAN) {   // the TU schedule of every (plane of the group, CTU), once per launch
             uint8_t* plan = (uint8_t*)d_work + closed4_plan_offset(lines0, lw, np);
             a.plan = plan;
