@@ -1359,8 +1359,12 @@ __device__ __forceinline__ void tu_closed_batch_pk(const Closed4Args& a, const i
 }
 
 // NARROW: the packed chain; the launch pairs it with the 32-bit form and the
-// stream's wide flag (work[2], set by k_closed_any_wide) makes exactly one of
-// the two code the stream -- the other returns before taking a ticket.
+// stream's wide flag (work[2], set by k_closed_any_wide -- or, after the pair
+// kernel, by the pair kernel itself when a TU's source sample left [0, 255])
+// makes exactly one of the two code the stream -- the other returns before
+// taking a ticket.  The 32-bit form takes its tickets from work[3] and tags its
+// line words kWideTag higher: it may run after the pair kernel has used both.
+constexpr int kWideTag = 1 << 20;
 template <int WAVES, bool NARROW = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))) k_tu_closed(Closed4Args a) {
     __shared__ int16_t rc[33][33];
@@ -1368,6 +1372,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     __shared__ int owner_of[64], done_of[64], slx[16], sly[16];
     __shared__ int row_s, stall_s;
     if ((__builtin_nontemporal_load(&a.work[2]) != 0) == NARROW) return;   // the other form codes this stream
+    constexpr int TK = NARROW ? 0 : 3, TG = NARROW ? 0 : kWideTag;   // ticket word, line-word tag offset
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
     ChainQ cq[4];
@@ -1377,7 +1382,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     const int total = a.crows * a.nplanes;
     for (;;) {
         if (lane == 0) {
-            row_s = atomicAdd(&a.work[0], 1);
+            row_s = atomicAdd(&a.work[TK], 1);
             stall_s = 0;
         }
         __syncthreads();
@@ -1409,7 +1414,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     bool ok = true;
                     if (need) {
                         const uint64_t v = ld_sys64(line + x0c / 2 + lane);
-                        ok = (int)(v >> 32) == cy;
+                        ok = (int)(v >> 32) == cy + TG;
                         val = (uint32_t)v;
                     }
                     if (__builtin_amdgcn_read_exec() == __ballot(ok)) break;
@@ -1497,7 +1502,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 if (lane < nw) {
                     const uint32_t lo = (uint16_t)rc[ctb][1 + 2 * lane];
                     const uint32_t hi = 2 * lane + 1 < ctb ? (uint16_t)rc[ctb][2 + 2 * lane] : 0u;
-                    st_sys64(line + x0c / 2 + lane, ((uint64_t)(uint32_t)(cy + 1) << 32) | lo | (hi << 16));
+                    st_sys64(line + x0c / 2 + lane, ((uint64_t)(uint32_t)(cy + 1 + TG) << 32) | lo | (hi << 16));
                 }
             }
             __syncthreads();
@@ -1579,7 +1584,7 @@ template <int N, bool DST, int RP = 33>
 __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[RP][RP], int16_t* t16, const ChainQ& cq,
-                                                    uint64_t* ph = nullptr, bool rec_later = false) {
+                                                    uint32_t& wb, uint64_t* ph = nullptr, bool rec_later = false) {
     constexpr int L2 = Log2<N>::v, S = L2 + 5, H = N / 2, TP = 34;
     // A/B build, NH_CLOSED4_STAMPS: shader cycles of the batch's phases, summed per TU size into ph
     // (LDS, lane 0) -- the s_memtime reads drain the LDS queue, so they sit where the chain syncs anyway
@@ -1610,6 +1615,8 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
             sv[i] = (NH_AB && (a.probe & 32)) ? rc[ly + 1 + i][lx + 1 + t]   // A/B probe: no source loads
                                               : sp[(int64_t)i * a.pitch];
         __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < N; ++i) wb |= (uint32_t)sv[i];   // the stream's wide check (k_tu_closed_pair)
     }
     const int32_t topt = rc[ly][lx + 1 + t], leftt = rc[ly + 1 + t][lx];
     const int32_t tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // top[-1], left[-1] (__main__.py:168)
@@ -1821,7 +1828,7 @@ template <int N, bool DST, int RP = 33>
 __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[RP][RP], int32_t* tile, const ChainQ& cq,
-                                                    uint64_t* ph = nullptr, bool rec_later = false) {
+                                                    uint32_t& wb, uint64_t* ph = nullptr, bool rec_later = false) {
     static_assert(N == 4 || ((N == 8 || N == 16) && !DST), "mosaic kinds: DST4, DCT4, DCT8, DCT16");
     constexpr int L2 = Log2<N>::v, NM = N / 4, TS = 16 / N, TPM = TS * TS;
     constexpr int KIND = N == 4 ? (DST ? 0 : 3) : N == 8 ? 1 : 2;
@@ -1860,6 +1867,10 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
                                                  : sp[(int64_t)r * a.pitch];
     }
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < NM; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wb |= (uint32_t)sv[m][r];   // the stream's wide check
     uint32_t hx[NM][2];
     pku16 pr2[NM][2];
 #pragma unroll
@@ -2043,7 +2054,7 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
 constexpr int kClOutP = 36, kClRecP = 24;   // int32 per tile row: levels, recon (48 halves; 16-B rows)
 __device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
                                                   uint8_t* tu, int x0c, int y0c, int16_t (*rc)[33], int32_t* ot,
-                                                  const BasisHC& bs, const ChainQ& cq, const TfLane& tl) {
+                                                  const BasisHC& bs, const ChainQ& cq, const TfLane& tl, uint32_t& wb) {
     const int l = opaque_lane64(), r = l & 31, hh = l >> 5;
     // the TU's source column, every load issued before any use (one wait, not one per row pair)
     int32_t sv[16];
@@ -2059,6 +2070,8 @@ __device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const in
         }
     }
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wb |= (uint32_t)sv[k];   // the stream's wide check
     const int32_t topr = rc[0][1 + r], tr = rc[0][32], bl = rc[32][0];
     int32_t sdc = hh ? (int32_t)rc[1 + r][0] : topr;   // DC (intra.py:46-62): lane halves hold top / left
     sdc = grp_sum<64>(sdc);
@@ -2213,7 +2226,7 @@ __global__ void __launch_bounds__(64) k_closed4_plan(Closed4Args a, uint8_t* pla
 #endif
 constexpr int kPairWaves = NH_CLOSED4_WAVES32;
 #ifndef NH_CLOSED4_NPL16   // planes per wave of the CTB <= 16 (chroma) instance: 2 or 4
-#define NH_CLOSED4_NPL16 2
+#define NH_CLOSED4_NPL16 4
 #endif
 #ifndef NH_CLOSED4_WAVES16   // its waves-per-EU target
 #define NH_CLOSED4_WAVES16 3
@@ -2247,6 +2260,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     if (NH_CLOSED4_PRIO && a.is_luma) __builtin_amdgcn_s_setprio(2);   // the critical (luma) wavefront issues first
     const int lane = threadIdx.x;
     const int ctb = a.ctb;
+    // the stream's wide check, fused: the OR of every source sample the chains load; one outside
+    // [0, 255] sets work[2] at the row's end, and the 32-bit form launched behind this kernel then
+    // recodes the whole set (the packed chains are exact only on 8-bit TUs; samples no TU reads
+    // never matter) -- instead of a scan of the whole set before the launch
+    uint32_t wb = 0;
     if constexpr (CTBM == 32) {
         if (a.mfma32) {   // closed_chain32_tf's bases: 4 KB, once per workgroup
             const uint4* s4 = (const uint4*)&c_basis_hc_cl;
@@ -2366,7 +2384,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     switch (rs & 3) {
 #define NH_PLAN_BATCH(NN, DST, Q)                                                                             \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, ph, rec_flush);
+                            tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t16, Q, wb, ph, rec_flush);
                         case 0:   // (CTB 32: the one 32x32 TU of the CTU, in every plane)
                             if constexpr (CTBM == 32) {
                                 if (a.mfma32) {   // one plane after the other, ONE copy of the chain's code:
@@ -2377,7 +2395,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                                         const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);
 #endif
                                         closed_chain32_tf(a, pp.src(s2), pp.lvl(s2), pp.rec(s2), pp.tu(s2), x0c, y0c,
-                                                          rc[s2], t32, basis_s, cq[3], tl);
+                                                          rc[s2], t32, basis_s, cq[3], tl, wb);
                                     }
                                 } else {
                                     NH_PLAN_BATCH(32, false, cq[3])
@@ -2386,7 +2404,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             break;
 #define NH_MOSAIC_BATCH(NN, DST, Q)                                                                           \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_mma<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, Q, ph, rec_flush);
+                            tu_closed_batch_mma<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, Q, wb, ph, rec_flush);
                         case 1:
                             if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(16, false, cq[2]) }
                             else { NH_PLAN_BATCH(16, false, cq[2]) }
@@ -2447,7 +2465,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                     pair_sync();                                                                             \
                     const int tot = cnt * npl;                                                               \
                     for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                   \
-                        tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent_s, rc, t16, Q);      \
+                        tu_closed_batch_pk2<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent_s, rc, t16, Q, wb);  \
                 }
                 NH_BATCH2(32, false, cq[3]);
                 NH_BATCH2(16, false, cq[2]);
@@ -2513,6 +2531,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                 ph_s[lane] = 0;
             }
         }
+        if (__ballot((wb & ~0xffu) != 0) && lane == 0) atomicOr(&a.work[2], 1);
         pair_sync();
         if (stall_s) break;
     }
@@ -2648,17 +2667,18 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
 }
 
 // Sets work[2] when any source sample of the plane set is outside [0, 255]
-// (the closed-loop stream then takes the 32-bit chain).
+// (the closed-loop stream then takes the 32-bit chain; the single-group path --
+// the pair kernel checks its own loads).  Rows grid-strided over blockIdx.x, a
+// row's samples over the threads: no per-sample division.
 __global__ void __launch_bounds__(256) k_closed_any_wide(const int16_t* __restrict__ src, int64_t group_stride,
                                                          int64_t plane_stride, int ppg, int w, int h, int pitch,
                                                          int32_t* flag) {
     const int pz = blockIdx.y, gz = pz / ppg, cz = pz - gz * ppg;
     const int16_t* p = src + (int64_t)gz * group_stride + (int64_t)cz * plane_stride;
-    const int64_t n = (int64_t)w * h;
     uint32_t bits = 0;
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-        const int yy = (int)(i / w), xx = (int)(i - (int64_t)yy * w);
-        bits |= (uint16_t)p[(int64_t)yy * pitch + xx];
+    for (int y = blockIdx.x; y < h; y += gridDim.x) {
+        const int16_t* row = p + (int64_t)y * pitch;
+        for (int x = threadIdx.x; x < w; x += 256) bits |= (uint16_t)row[x];
     }
     if (__ballot((bits & 0xff00u) != 0) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
@@ -2800,9 +2820,12 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     // sample is outside [0, 255]) and the 32-bit form (iff one is); A/B knob
     // NH_TU_CLOSED_NARROW = 0: the 32-bit form for every stream
     static const int narrow_ok = NH_KNOB("NH_TU_CLOSED_NARROW", 1);
-    if (narrow_ok) {
-        const int64_t n = (int64_t)set->width * set->height;
-        const unsigned gx = (unsigned)std::min<int64_t>(256, (n + 255 * 8) / (256 * 8));
+    static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
+    const bool pair = narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1;
+    if (pair) {
+        // the pair kernel checks the samples it loads itself (k_tu_closed_pair: work[2] starts at 0)
+    } else if (narrow_ok) {
+        const unsigned gx = (unsigned)std::max(1, std::min(256, set->height));
         k_closed_any_wide<<<dim3(gx, (unsigned)np), 256, 0, s>>>(d_src + set->base, set->group_stride, set->plane_stride,
                                                               set->planes_per_group, set->width, set->height,
                                                               set->pitch, (int32_t*)d_work + 2);
@@ -2813,8 +2836,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     NH_TRY(device_cus(&cus));
     // 8-bit streams: plane pairs (k_tu_closed_pair) when the set
     // holds more than one group; A/B build: NH_TU_CLOSED_PAIR = 0 codes one plane per wave
-    static const int pair_ok = NH_KNOB("NH_TU_CLOSED_PAIR", 1);
-    if (narrow_ok != 0 && pair_ok != 0 && set->num_groups > 1) {
+    if (pair) {
         int per_cu = 0;
         // CTB 32 (luma): plane pairs; CTB <= 16 (chroma): NH_CLOSED4_NPL16 planes per wave (4: the
         // chroma wavefront needs half the waves, so with luma's it fits the resident slots)

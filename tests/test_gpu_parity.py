@@ -985,6 +985,40 @@ def test_tu_pipeline_closed_pairs_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
             off += ph * pw
 
 
+@pytest.mark.parametrize("where", ["last", "first"])
+def test_tu_pipeline_closed_pairs_late_wide_sample(nh, torch_dev, where):
+    """The pair kernel checks the source samples its chains load (round 5; no scan
+    before the launch): ONE 9-bit sample in the last CTU of the last frame's luma --
+    found after every other row is coded -- or in the first CTU of the first frame
+    sends the whole set to the 32-bit form behind it (its own tickets and line-word
+    tags); every plane equals the sequential oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H, qp = 4, 104, 72, 27
+    rng = np.random.default_rng(404)
+    fe = gpu.yuv420_frame_elems(W, H)
+    buf = np.clip(100 + rng.integers(-90, 91, F * fe), 0, 255).astype(np.int16)
+    if where == "last":
+        buf[(F - 1) * fe + (H - 3) * W + W - 5] = 300   # inside the bottom-right whole CTU's TUs
+    else:
+        buf[7 * W + 3] = -4
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(F, W, H)
+    lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    _, _, tuy, tuc = gpu.tu_pipeline_closed_yuv420(d, sy, suv, 31, qp, lvl=lvl, rec=rec)
+    lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    for f in range(F):
+        off = f * fe
+        for k, (pw, ph) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er, et = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, 31, qp, k == 0)
+            assert np.array_equal(lv[off:off + ph * pw].reshape(ph, pw), el), (f, k)
+            assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
+            assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
+            off += ph * pw
+
+
 def test_tu_pipeline_closed_pairs_many_frames_vs_oracle(nh, torch_dev):
     """2048 small 8-bit YUV420 frames (72x40: whole and ragged CTUs) in one
     concurrent launch pair: >= 4096 CTU rows per launch, so whole CTUs leave

@@ -11,6 +11,8 @@
 #   libs:CFG       tools/ab/ab_libs.sh for bench_configs config CFG (3, closed, 4b, closed4, 5b): $LIB vs product
 #   stamps:F       per-CTU stamps of the closed loop (A/B build, tools/ab/closed4_stamps.py) at F frames
 #   cusplit        luma / chroma wavefronts on disjoint CU sets (ab_closed4_split.py --cu-split 0..3)
+#   ktrace[:LIB]   kernel trace of the concurrent YUV420 call (tools/ab/closed4_trace.py): when each
+#                  wavefront starts / ends inside the launch set (the product, or LIB copied over it)
 # Outputs: gpurun_out/*_${TAG}*.  REPS (default 2), SPLIT_REPS (reps per run, default 10 at >= 16 frames, else 5).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
@@ -40,6 +42,13 @@ step() {
     stamps)
       NH_CLOSED4_STAMPS=1 timeout -k 10 200 python tools/ab/closed4_stamps.py --frames ${arg:-2} \
         > gpurun_out/stamps_${TAG}.json || return 1 ;;
+    ktrace)
+      local d=gpurun_out/kt_closed4_${TAG}${arg:+_$(basename $arg .so)}
+      if [ -n "$arg" ]; then cp nano-hevc_amd/nano_hevc/libnanohevc.so /tmp/nh_product.so && cp "$arg" nano-hevc_amd/nano_hevc/libnanohevc.so; fi
+      timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $d -o run -- python3 tools/ab/closed4_trace.py > $d.log 2>&1; local rc=$?
+      if [ -n "$arg" ]; then cp /tmp/nh_product.so nano-hevc_amd/nano_hevc/libnanohevc.so; fi
+      [ $rc -eq 0 ] || return 1
+      python3 tools/ab/closed4_trace.py --summary $d ;;
     cusplit)
       local out=gpurun_out/ab_closed4_cusplit_${TAG}.jsonl
       for rep in $(seq $REPS); do
