@@ -16,6 +16,7 @@
 #include "nh_tree.hpp"
 #include "nh_packed.hpp"
 #include "nh_f16mma.hpp"
+#include "nh_ldsdma.hpp"
 
 namespace nh {
 
@@ -1126,6 +1127,8 @@ struct Closed4Args {
                             // stores in the chains (0 in the product)
     int32_t mfma32;         // k_tu_closed_pair: 32x32 TUs on the f16 matrix cores (closed_chain32_tf); set
                             // for luma when the level / recon rows allow 16-B stores
+    int32_t srctile;        // k_tu_closed_pair: each CTU's source samples land in an LDS tile by LDS-DMA
+                            // under the wait on the row above; the chains read them there
     int32_t rec_ctu;        // k_tu_closed_pair: a whole CTU's packed-chain recon leaves from the LDS
                             // reconstruction at the CTU's end, as 64-B row pieces (the rows 8-B aligned)
     uint64_t* stamps;       // A/B build only (NH_CLOSED4_STAMPS): per (ticket, CTU) shader-clock stamps
@@ -1539,7 +1542,13 @@ struct PairPlanes {
     int16_t* rec0;
     uint8_t* tu0;
     int64_t gs, ts;   // elements / TU-map bytes from one plane of the wave to the next
+    const int16_t* stile;   // the CTU's source samples in LDS ([plane][row][stp]), or null: read src
+    int32_t stp;            // the tile's row pitch (CTB)
     __device__ const int16_t* src(int p) const { return src0 + p * gs; }
+    // source sample (y, x) of plane p: y / x relative to the CTU (cy0 / cx0 its origin) -- from the tile
+    __device__ int32_t sample(const Closed4Args& a, int p, int y, int x, int y0c, int x0c) const {
+        return stile ? (int32_t)stile[(p * stp + y) * stp + x] : (int32_t)src(p)[(int64_t)(y0c + y) * a.pitch + x0c + x];
+    }
     __device__ int32_t* lvl(int p) const { return lvl0 + p * gs; }
     __device__ int16_t* rec(int p) const { return rec0 + p * gs; }
     __device__ uint8_t* tu(int p) const { return tu0 + p * ts; }
@@ -1610,10 +1619,15 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
     int32_t sv[N];
     {
         const int16_t* sp = src + (int64_t)y * a.pitch + x + t;
+        if (pp.stile) {
 #pragma unroll
-        for (int i = 0; i < N; ++i)
-            sv[i] = (NH_AB && (a.probe & 32)) ? rc[ly + 1 + i][lx + 1 + t]   // A/B probe: no source loads
-                                              : sp[(int64_t)i * a.pitch];
+            for (int i = 0; i < N; ++i) sv[i] = pp.stile[(p * pp.stp + ly + i) * pp.stp + lx + t];
+        } else {
+#pragma unroll
+            for (int i = 0; i < N; ++i)
+                sv[i] = (NH_AB && (a.probe & 32)) ? rc[ly + 1 + i][lx + 1 + t]   // A/B probe: no source loads
+                                                  : sp[(int64_t)i * a.pitch];
+        }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int i = 0; i < N; ++i) wb |= (uint32_t)sv[i];   // the stream's wide check (k_tu_closed_pair)
@@ -1858,13 +1872,22 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     }
     // the TUs' source samples, every load issued before any use
     int32_t sv[NM][4];
+    if (pp.stile) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) {
-        const int16_t* sp = pp.src(pm[m]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
+        for (int m = 0; m < NM; ++m) {
+            const int16_t* tp = pp.stile + (pm[m] * pp.stp + lym[m] + yr0) * pp.stp + lxm[m] + t;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-            sv[m][r] = (NH_AB && (a.probe & 32)) ? rc2[pm[m]][lym[m] + 1 + yr0 + r][lxm[m] + 1 + t]
-                                                 : sp[(int64_t)r * a.pitch];
+            for (int r = 0; r < 4; ++r) sv[m][r] = tp[r * pp.stp];
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const int16_t* sp = pp.src(pm[m]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                sv[m][r] = (NH_AB && (a.probe & 32)) ? rc2[pm[m]][lym[m] + 1 + yr0 + r][lxm[m] + 1 + t]
+                                                     : sp[(int64_t)r * a.pitch];
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -2052,13 +2075,21 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
 // right column go into rc (the CTU's publish and slide read nothing else; the
 // next CTU's TUs rewrite the rest).  Same results as tu_closed_batch_pk2<32>.
 constexpr int kClOutP = 36, kClRecP = 24;   // int32 per tile row: levels, recon (48 halves; 16-B rows)
-__device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src, int32_t* lvl, int16_t* rec,
+__device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src, const int16_t* stl,
+                                                  int32_t* lvl, int16_t* rec,
                                                   uint8_t* tu, int x0c, int y0c, int16_t (*rc)[33], int32_t* ot,
                                                   const BasisHC& bs, const ChainQ& cq, const TfLane& tl, uint32_t& wb) {
     const int l = opaque_lane64(), r = l & 31, hh = l >> 5;
     // the TU's source column, every load issued before any use (one wait, not one per row pair)
     int32_t sv[16];
-    {
+    if (stl) {   // the CTU's source tile (rows of 32)
+#pragma unroll
+        for (int p = 0; p < 8; ++p) {
+            const int c = 2 * (p & 1) + 8 * (p >> 1);   // y_p - 4 hh
+#pragma unroll
+            for (int e = 0; e < 2; ++e) sv[2 * p + e] = stl[(4 * hh + c + e) * 32 + r];
+        }
+    } else {
         const int16_t* sp = src + (int64_t)(y0c + 4 * hh) * a.pitch + x0c + r;
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
@@ -2247,7 +2278,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     constexpr int kT32 = std::max({NPL * CTBM * TP / 2, 1024, CTBM == 32 ? 32 * kClOutP : 0});
     __shared__ __attribute__((aligned(16))) int32_t t32[kT32];
     int16_t* const t16 = (int16_t*)t32;
-    __shared__ __attribute__((aligned(16))) std::conditional_t<CTBM == 32, BasisHC, int> basis_s;
+    // the CTU's source samples, [plane][row][CTBM] (LDS-DMA under the poll; Closed4Args::srctile)
+    __shared__ __attribute__((aligned(16))) int16_t stile[NPL * CTBM * CTBM];
+    // closed_chain32_tf reads its bases from the constant table (L1 / L2 hits), not an LDS copy:
+    // the 4 KB went to the source tile at the same occupancy
+    const BasisHC& basis_s = c_basis_hc_cl;
 #if !NH_CLOSED4_PLAN
     __shared__ int owner_of[64], done_of[64];
 #endif
@@ -2265,13 +2300,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
     // recodes the whole set (the packed chains are exact only on 8-bit TUs; samples no TU reads
     // never matter) -- instead of a scan of the whole set before the launch
     uint32_t wb = 0;
-    if constexpr (CTBM == 32) {
-        if (a.mfma32) {   // closed_chain32_tf's bases: 4 KB, once per workgroup
-            const uint4* s4 = (const uint4*)&c_basis_hc_cl;
-            for (int i = lane; i < (int)(sizeof(BasisHC) / 16); i += 64) ((uint4*)&basis_s)[i] = s4[i];
-            pair_sync();
-        }
-    }
     ChainQ cq[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) cq[k] = make_chainq(a.q[k], a.dqs, a.dq_per);
@@ -2304,6 +2332,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             pp.tu0 = a.tu + (int64_t)pl * a.tu_plane;
             pp.gs = a.group_stride;
             pp.ts = (int64_t)a.ppg * a.tu_plane;
+            pp.stile = a.srctile ? stile : nullptr;
+            pp.stp = CTBM;
         }
         // plane hq's line words (lanes of planes past npl never touch them)
         uint64_t* const lineq = lines + (int64_t)((g0 + hq) * a.ppg + c) * a.lw;
@@ -2326,6 +2356,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             // this CTU's TU schedule (128 B), loaded under the wait on the row above
             uint32_t planw = 0;
             if (NH_CLOSED4_PLAN && lane < kPlanBytes / 4) planw = plan_row[cx * (kPlanBytes / 4) + lane];
+            if (a.srctile) {   // the CTU's source samples into the tile, 16 B a lane, under the poll below
+                // (the vmcnt(0) before the rounds retires them; lgkmcnt(0): the previous CTU's tile
+                // reads have returned before the DMA overwrites it)
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                constexpr int PR = CTBM / 8, PP = CTBM * PR;   // 16-B pieces per row, per plane
+#pragma unroll
+                for (int i = 0; i < NPL * PP / 64; ++i) {
+                    const int q = 64 * i + lane, pq = q / PP, yy = (q / PR) % CTBM, k = q % PR;
+                    if (pq < npl && y0c + yy < a.h && x0c + 8 * k < a.w)
+                        glds16s(pp.src(0), (uint32_t)((pq * pp.gs + (int64_t)(y0c + yy) * a.pitch + x0c + 8 * k) * 2),
+                                lds_addr(stile + 64 * 8 * i));
+                }
+            }
             // top row of this CTU: 128 at y == 0, else the CTU above's bottom row (tagged line words)
             if (cy == 0) {
                 if (hl < ctb) rc[hq][0][1 + hl] = 128;
@@ -2394,7 +2437,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
 #if NH_CLOSED4_TL_INNER
                                         const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);
 #endif
-                                        closed_chain32_tf(a, pp.src(s2), pp.lvl(s2), pp.rec(s2), pp.tu(s2), x0c, y0c,
+                                        closed_chain32_tf(a, pp.src(s2), pp.stile ? pp.stile + s2 * 32 * 32 : nullptr,
+                                                          pp.lvl(s2), pp.rec(s2), pp.tu(s2), x0c, y0c,
                                                           rc[s2], t32, basis_s, cq[3], tl, wb);
                                     }
                                 } else {
@@ -2790,6 +2834,13 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
     static const int rec_ctu = NH_KNOB("NH_CLOSED4_REC_CTU", 1);
     a.rec_ctu = rec_ctu && !(set->pitch & 3) && !((set->base | set->plane_stride | set->group_stride) & 3) &&
                 !((uintptr_t)d_recon & 7);
+    // the pair kernel's LDS-DMA source tile: 16-B pieces of whole rows (width, pitch, offsets multiples of
+    // 8 samples, so no piece straddles a row's end) and 32-bit byte offsets within a group of planes;
+    // A/B knob NH_CLOSED4_SRCTILE = 0: the chains load their samples from global memory
+    static const int srctile = NH_KNOB("NH_CLOSED4_SRCTILE", 1);
+    a.srctile = srctile && !(set->width & 7) && !(set->pitch & 7) &&
+                !((set->base | set->plane_stride | set->group_stride) & 7) && !((uintptr_t)d_src & 15) &&
+                (3 * set->group_stride + (int64_t)set->height * set->pitch) * 2 < (1ll << 31);
     {   // tu_closed_batch_mma's per-lane bases and initial accumulators
         static PerDeviceOnce once_m;
         const int rcm = once_m.run([] {

@@ -170,6 +170,21 @@ __device__ __forceinline__ T lane_perm(T v) {
                    ((uint64_t)(uint32_t)lane_perm32<CTRL>((int32_t)(uint32_t)(u >> 32)) << 32));
     }
 }
+// DPP with a row mask: rows outside ROWMASK keep `old` (row_bcast:15 / :31 of the gfx9 wave reduction)
+template <int CTRL, int ROWMASK, class T>
+__device__ __forceinline__ T lane_perm_rows(T old, T v) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit lanes");
+    if constexpr (sizeof(T) == 4) {
+        return (T)__builtin_amdgcn_update_dpp((int32_t)old, (int32_t)v, CTRL, ROWMASK, 0xF, false);
+    } else {
+        const uint64_t u = (uint64_t)v, o = (uint64_t)old;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int32_t)(uint32_t)o, (int32_t)(uint32_t)u, CTRL,
+                                                                   ROWMASK, 0xF, false);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int32_t)(uint32_t)(o >> 32),
+                                                                   (int32_t)(uint32_t)(u >> 32), CTRL, ROWMASK, 0xF, false);
+        return (T)((uint64_t)lo | ((uint64_t)hi << 32));
+    }
+}
 template <class T>
 __device__ __forceinline__ T lane_read(T v, int l) {
     if constexpr (sizeof(T) == 4) {
@@ -187,8 +202,13 @@ __device__ __forceinline__ T grp_sum(T v) {
     if constexpr (N >= 4) v += lane_perm<0x4E>(v);    // quad_perm [2, 3, 0, 1]
     if constexpr (N >= 8) v += lane_perm<0x141>(v);   // row_half_mirror
     if constexpr (N >= 16) v += lane_perm<0x140>(v);  // row_mirror
-    if constexpr (N >= 32) v += lane_perm<-1>(v);     // ds_swizzle: lane ^ 16 inside 32
-    if constexpr (N >= 64) v = lane_read(v, 0) + lane_read(v, 32);
+    if constexpr (N == 32) v += lane_perm<-1>(v);     // ds_swizzle: lane ^ 16 inside 32
+    if constexpr (N >= 64) {   // every lane holds its row's total: row_bcast:15 then :31 leave the
+        // wave's total in lane 63 -- DPP only, no ds_swizzle round trip through the LDS unit
+        v += lane_perm_rows<0x142, 0xA>((T)0, v);
+        v += lane_perm_rows<0x143, 0xC>((T)0, v);
+        v = lane_read(v, 63);
+    }
     return v;
 }
 // The same reduction with min (unsigned / signed per T): every lane gets its group's minimum.
@@ -200,8 +220,12 @@ __device__ __forceinline__ T grp_min(T v) {
     if constexpr (N >= 4) v = mn(v, lane_perm<0x4E>(v));
     if constexpr (N >= 8) v = mn(v, lane_perm<0x141>(v));
     if constexpr (N >= 16) v = mn(v, lane_perm<0x140>(v));
-    if constexpr (N >= 32) v = mn(v, lane_perm<-1>(v));
-    if constexpr (N >= 64) v = mn(lane_read(v, 0), lane_read(v, 32));
+    if constexpr (N == 32) v = mn(v, lane_perm<-1>(v));
+    if constexpr (N >= 64) {   // as grp_sum: rows outside the mask keep their own value
+        v = mn(v, lane_perm_rows<0x142, 0xA>(v, v));
+        v = mn(v, lane_perm_rows<0x143, 0xC>(v, v));
+        v = lane_read(v, 63);
+    }
     return v;
 }
 // __shfl_up(v, 1, 64) by DPP wave_shr:1: lane i gets lane i - 1's value, lane 0 keeps its own
