@@ -1578,6 +1578,9 @@ __device__ __forceinline__ int entry_plane(int e, int cnt) {
 #ifndef NH_CLOSED4_MOSAIC   // 1: 16x16, 8x8 and luma 4x4 TUs on the f16 matrix cores (tu_closed_batch_mma); 2: + chroma 4x4
 #define NH_CLOSED4_MOSAIC 2
 #endif
+#ifndef NH_CLOSED4_DIRECT   // 1: launches of few CTU rows (REC = false) store the mosaics' outputs from registers
+#define NH_CLOSED4_DIRECT 1
+#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -1838,7 +1841,10 @@ __device__ __forceinline__ int32_t tu_sum(int32_t v) {
         return v + lane_perm<-1>(v);
     } else return grp_sum<64>(v);
 }
-template <int N, bool DST, int RP = 33>
+// DIRECT (the latency form: launches of few CTU rows): levels, recon and TU map leave straight from the
+// registers, one sample per lane and store (4 * NM + ...), none of the tile round trip on the chain;
+// otherwise (many rows, throughput) as N / 4 whole 16-B row pieces per lane through the tile
+template <int N, bool DST, int RP = 33, bool DIRECT = false>
 __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[RP][RP], int32_t* tile, const ChainQ& cq,
@@ -1965,8 +1971,16 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
         for (int q = 0; q < 2; ++q) {
             const int32_t L0 = quant_s(floor_i32(acc[m][2 * q]), cq.qs, cq.h_v, cq.hneg_v);
             const int32_t L1 = quant_s(floor_i32(acc[m][2 * q + 1]), cq.qs, cq.h_v, cq.hneg_v);
-            tl[(2 * q) * N] = L0;
-            tl[(2 * q + 1) * N] = L1;
+            if constexpr (DIRECT) {
+                if (onm[m] && !(NH_AB && (a.probe & 64))) {
+                    int32_t* lp = pp.lvl(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
+                    lp[0] = L0;
+                    lp[a.pitch] = L1;
+                }
+            } else {
+                tl[(2 * q) * N] = L0;
+                tl[(2 * q + 1) * N] = L1;
+            }
             const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
             const pk16 d2 = (l2 * dqs2 + dqr2) >> dqsh2;
             const _Float16 h0 = (_Float16)d2.x, h1 = (_Float16)d2.y;
@@ -2018,11 +2032,22 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
             if (onm[m]) {
                 rc[lym[m] + 1 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.x;
                 rc[lym[m] + 2 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.y;
+                if (DIRECT && !rec_later && !(NH_AB && (a.probe & 64))) {
+                    int16_t* rp = pp.rec(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
+                    rp[0] = (int16_t)rv.x;
+                    rp[a.pitch] = (int16_t)rv.y;
+                }
             }
         }
+        if (DIRECT && onm[m] && (t & 3) == 0 && !(NH_AB && (a.probe & 64)))   // the TU map: one byte per 4x4 unit
+            pp.tu(pm[m])[(int64_t)((y0c + lym[m] + yr0) / 4) * (a.w / 4) + (x0c + lxm[m] + t) / 4] = (uint8_t)L2;
     }
     pair_sync();
     phase(4);
+    if constexpr (DIRECT) {
+        phase(5);
+        return;
+    }
     // the levels (16-B row pieces from the tile), the recon (8-B row pieces from rc) and the TU map:
     // piece i = 4 samples of one TU row, N / 4 pieces per lane
     const bool st = !(NH_AB && (a.probe & 64));
@@ -2448,7 +2473,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             break;
 #define NH_MOSAIC_BATCH(NN, DST, Q)                                                                           \
                         for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 64 / NN)                    \
-                            tu_closed_batch_mma<NN, DST>(a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, Q, wb, ph, rec_flush);
+                            tu_closed_batch_mma<NN, DST, RP, !REC && NH_CLOSED4_DIRECT>(                               \
+                                a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, Q, wb, ph, rec_flush);
                         case 1:
                             if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(16, false, cq[2]) }
                             else { NH_PLAN_BATCH(16, false, cq[2]) }
