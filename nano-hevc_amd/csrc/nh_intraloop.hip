@@ -1542,13 +1542,10 @@ struct PairPlanes {
     int16_t* rec0;
     uint8_t* tu0;
     int64_t gs, ts;   // elements / TU-map bytes from one plane of the wave to the next
-    const int16_t* stile;   // the CTU's source samples in LDS ([plane][row][stp]), or null: read src
+    const __attribute__((address_space(3))) int16_t* stile;   // the CTU's source samples in LDS ([plane][row][stp]),
+                                                             // or null: read src
     int32_t stp;            // the tile's row pitch (CTB)
     __device__ const int16_t* src(int p) const { return src0 + p * gs; }
-    // source sample (y, x) of plane p: y / x relative to the CTU (cy0 / cx0 its origin) -- from the tile
-    __device__ int32_t sample(const Closed4Args& a, int p, int y, int x, int y0c, int x0c) const {
-        return stile ? (int32_t)stile[(p * stp + y) * stp + x] : (int32_t)src(p)[(int64_t)(y0c + y) * a.pitch + x0c + x];
-    }
     __device__ int32_t* lvl(int p) const { return lvl0 + p * gs; }
     __device__ int16_t* rec(int p) const { return rec0 + p * gs; }
     __device__ uint8_t* tu(int p) const { return tu0 + p * ts; }
@@ -1829,9 +1826,9 @@ inline void make_mosaic(MosaicLane (*out)[64]) {
         }
     }
 }
-__device__ __forceinline__ void mfma_result_ready4(f4_t& acc) {   // see mfma_result_ready (nh_f16mma.hpp)
-    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" : "+v"(acc));
-}
+// see mfma_result_ready (nh_f16mma.hpp): 8 wait states after a 16x16x16 MFMA -- what the compiler
+// itself inserts before a VALU read of such a result (tools/isa_check.py checks every such read)
+__device__ __forceinline__ void mfma_result_ready4(f4_t& acc) { asm volatile("s_nop 7" : "+v"(acc)); }
 // sum over the lanes of one TU of the mosaic (N = 4: 4 lanes; 8: 8 lanes + the 8 lanes 16 apart; 16: all 64)
 template <int N>
 __device__ __forceinline__ int32_t tu_sum(int32_t v) {
@@ -1881,7 +1878,7 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     if (pp.stile) {
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-            const int16_t* tp = pp.stile + (pm[m] * pp.stp + lym[m] + yr0) * pp.stp + lxm[m] + t;
+            const __attribute__((address_space(3))) int16_t* tp = pp.stile + (pm[m] * pp.stp + lym[m] + yr0) * pp.stp + lxm[m] + t;
 #pragma unroll
             for (int r = 0; r < 4; ++r) sv[m][r] = tp[r * pp.stp];
         }
@@ -2100,7 +2097,8 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
 // right column go into rc (the CTU's publish and slide read nothing else; the
 // next CTU's TUs rewrite the rest).  Same results as tu_closed_batch_pk2<32>.
 constexpr int kClOutP = 36, kClRecP = 24;   // int32 per tile row: levels, recon (48 halves; 16-B rows)
-__device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src, const int16_t* stl,
+__device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const int16_t* src,
+                                                  const __attribute__((address_space(3))) int16_t* stl,
                                                   int32_t* lvl, int16_t* rec,
                                                   uint8_t* tu, int x0c, int y0c, int16_t (*rc)[33], int32_t* ot,
                                                   const BasisHC& bs, const ChainQ& cq, const TfLane& tl, uint32_t& wb) {
@@ -2357,7 +2355,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
             pp.tu0 = a.tu + (int64_t)pl * a.tu_plane;
             pp.gs = a.group_stride;
             pp.ts = (int64_t)a.ppg * a.tu_plane;
-            pp.stile = a.srctile ? stile : nullptr;
+            pp.stile = a.srctile ? (const __attribute__((address_space(3))) int16_t*)(lds_void_t*)stile : nullptr;
             pp.stp = CTBM;
         }
         // plane hq's line words (lanes of planes past npl never touch them)
@@ -2462,7 +2460,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
 #if NH_CLOSED4_TL_INNER
                                         const TfLane tl = make_tf_lane(cq[3], basis_s, lane & 31);
 #endif
-                                        closed_chain32_tf(a, pp.src(s2), pp.stile ? pp.stile + s2 * 32 * 32 : nullptr,
+                                        closed_chain32_tf(a, pp.src(s2), pp.stile ? pp.stile + s2 * 32 * 32 : pp.stile,
                                                           pp.lvl(s2), pp.rec(s2), pp.tu(s2), x0c, y0c,
                                                           rc[s2], t32, basis_s, cq[3], tl, wb);
                                     }
