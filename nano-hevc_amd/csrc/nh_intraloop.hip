@@ -1578,6 +1578,9 @@ __device__ __forceinline__ int entry_plane(int e, int cnt) {
 #ifndef NH_CLOSED4_DIRECT   // 1: launches of few CTU rows (REC = false) store the mosaics' outputs from registers
 #define NH_CLOSED4_DIRECT 1
 #endif
+#ifndef NH_CLOSED4_MIX   // 1: a round's 8x8 and 4x4 TUs in one call when each fits one mosaic (tu_closed_batch_mix)
+#define NH_CLOSED4_MIX 1
+#endif
 #ifndef NH_CLOSED4_EARLYPOLL
 #define NH_CLOSED4_EARLYPOLL 0   // measured 2 % slower (profiles/r03/closed4/ab_libs_closed4_r03l.jsonl)
 #endif
@@ -1839,17 +1842,277 @@ __device__ __forceinline__ int32_t tu_sum(int32_t v) {
     } else return grp_sum<64>(v);
 }
 // DIRECT (the latency form: launches of few CTU rows): levels, recon and TU map leave straight from the
-// registers, one sample per lane and store (4 * NM + ...), none of the tile round trip on the chain;
-// otherwise (many rows, throughput) as N / 4 whole 16-B row pieces per lane through the tile
+// registers, one sample per lane and store, none of the tile round trip on the chain; otherwise (many
+// rows, throughput) as N / 4 whole 16-B row pieces per lane through the tile.
+//
+// MosaicSet<N, DST, NM>: NM mosaics of TUs of size N whose batch entries start at e0 of a round's
+// (entries, cnt per plane, total) list -- one phase of the chain per method, so a batch can run one set
+// (tu_closed_batch_mma) or two sets of different sizes interleaved (tu_closed_batch_mix: a round's
+// 8x8 and 4x4 TUs in one call, their latencies overlapped instead of added).
+template <int N, bool DST, int NM, int RP, bool DIRECT>
+struct MosaicSet {
+    static_assert(N == 4 || ((N == 8 || N == 16) && !DST), "mosaic kinds: DST4, DCT4, DCT8, DCT16");
+    static constexpr int L2 = Log2<N>::v, TS = 16 / N, TPM = TS * TS;
+    static constexpr int KIND = N == 4 ? (DST ? 0 : 3) : N == 8 ? 1 : 2;
+    static constexpr bool SPLIT = N == 4 && !DST;   // DCT4: the inverse pass 2 in two halves
+    int t, yr0, el;                                 // column in the TU, first row, TU slot of mosaic 0
+    int pm[NM], lxm[NM], lym[NM];
+    bool onm[NM];
+    uint4 mw0, mw1;
+    int32_t sv[NM][4];
+    uint32_t hx[NM][2], dq[NM][2];
+    pku16 pr2[NM][2];
+    f4_t acc[NM];
+
+    __device__ __forceinline__ void init(int lane, const uint8_t* ent, int cnt, int total, int e0) {
+        const int c = lane & 15, g = lane >> 4;
+        t = c % N;
+        yr0 = (4 * g) % N;
+        el = (4 * g) / N * TS + c / N;
+        mw0 = *(const uint4*)&c_mosaic[KIND][lane];
+        mw1 = *((const uint4*)&c_mosaic[KIND][lane] + 1);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            const int e = e0 + m * TPM + el;
+            onm[m] = e < total;
+            pm[m] = onm[m] ? entry_plane(e, cnt) : 0;
+            const int code = ent[onm[m] ? e - pm[m] * cnt : 0];   // idle lanes shadow plane 0's first TU
+            lxm[m] = (code & 7) * 4;
+            lym[m] = ((code >> 3) & 7) * 4;
+        }
+    }
+    // the TUs' source samples, every load issued before any use
+    __device__ __forceinline__ void load(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                         int16_t (*rc2)[RP][RP]) {
+        if (pp.stile) {
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const __attribute__((address_space(3))) int16_t* tp =
+                    pp.stile + (pm[m] * pp.stp + lym[m] + yr0) * pp.stp + lxm[m] + t;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) sv[m][r] = tp[r * pp.stp];
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                const int16_t* sp = pp.src(pm[m]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    sv[m][r] = (NH_AB && (a.probe & 32)) ? rc2[pm[m]][lym[m] + 1 + yr0 + r][lxm[m] + 1 + t]
+                                                         : sp[(int64_t)r * a.pitch];
+            }
+        }
+    }
+    __device__ __forceinline__ void predict(int16_t (*rc2)[RP][RP], uint32_t& wb) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) wb |= (uint32_t)sv[m][r];   // the stream's wide check
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            int16_t (*rc)[RP] = rc2[pm[m]];
+            const int lx = lxm[m], ly = lym[m];
+            const int32_t topt = rc[ly][lx + 1 + t], tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // __main__.py:168
+            // DC (intra.py:46-62): the TU's lanes of row group 0 add top[t], of row group 1 left[t] (N = 4: both)
+            int32_t sdc = N == 4 ? topt + rc[ly + 1 + t][lx] : yr0 == 0 ? topt : yr0 == 4 ? (int32_t)rc[ly + 1 + t][lx] : 0;
+            sdc = tu_sum<N>(sdc);
+            const int32_t dc = (sdc + N) >> (L2 + 1);
+            const pk16 dc2 = pk_splat(dc);
+            pk16 o2[2];
+            pku16 pl2[2];
+            {   // planar (intra.py:81-113) at (y, t): (N-1-t) left[y] + (t+1) tr + (N-1-y) top[t] + (y+1) bl + N >> L2+1
+                const int32_t b = (t + 1) * tr + (N - 1 - yr0) * topt + (yr0 + 1) * bl + N, st = bl - topt;
+                const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)}, sh = {L2 + 1, L2 + 1};
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const int y = yr0 + 2 * q;
+                    o2[q] = pk_pair(sv[m][2 * q], sv[m][2 * q + 1]);
+                    const pku16 lf = {(unsigned short)rc[ly + 1 + y][lx], (unsigned short)rc[ly + 2 + y][lx]};
+                    const pku16 bs = {(unsigned short)(b + 2 * q * st), (unsigned short)(b + (2 * q + 1) * st)};
+                    pl2[q] = (lf * wl + bs) >> sh;
+                }
+            }
+            int32_t ed = 0, ep = 0;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const pk16 d0 = o2[q] - dc2, d1 = o2[q] - __builtin_bit_cast(pk16, pl2[q]);
+                ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
+                ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
+            }
+            ed = tu_sum<N>(ed);
+            ep = tu_sum<N>(ep);
+            const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[q]);
+                const pku16 rr = __builtin_bit_cast(pku16, o2[q] - pr);   // residual, intra.py:65-67
+                hx[m][q] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of 768 + n
+                pr2[m][q] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
+            }
+        }
+    }
+    // forward passes (transform.py:179-194)
+    __device__ __forceinline__ void pass1() {
+        const h4_t bf = __builtin_bit_cast(h4_t, make_uint2(mw0.x, mw0.y));
+        const float c1 = __builtin_bit_cast(float, mw1.x);
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(hx[m][0], hx[m][1])), bf,
+                                                           (f4_t){c1, c1, c1, c1}, 0, 0, 0);
+    }
+    __device__ __forceinline__ void pass2() {
+        const h4_t bf = __builtin_bit_cast(h4_t, make_uint2(mw0.x, mw0.y));
+        const float c2 = __builtin_bit_cast(float, mw1.y);
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(acc[m][0], acc[m][1]), pk_trunc_h(acc[m][2], acc[m][3]))),
+                bf, (f4_t){c2, c2, c2, c2}, 0, 0, 0);
+    }
+    __device__ __forceinline__ void ready() {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) mfma_result_ready4(acc[m]);   // before floor_i32's inline-asm reads
+    }
+    // quantize_block (levels: straight out, or into the tile at TU slot tslot0 + ...) and
+    // dequantize_block in 16 bits
+    __device__ __forceinline__ void quant(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                          const ChainQ& cq, int32_t* tile) {
+        const pk16 dqs2 = pk_splat(cq.dqs), dqr2 = pk_splat((int32_t)cq.dqr_v), dqsh2 = pk_splat(cq.dqsh);
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            int32_t* tl = tile + ((m * TPM + el) * N + yr0) * N + t;
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const int32_t L0 = quant_s(floor_i32(acc[m][2 * q]), cq.qs, cq.h_v, cq.hneg_v);
+                const int32_t L1 = quant_s(floor_i32(acc[m][2 * q + 1]), cq.qs, cq.h_v, cq.hneg_v);
+                if constexpr (DIRECT) {
+                    if (onm[m] && !(NH_AB && (a.probe & 64))) {
+                        int32_t* lp = pp.lvl(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
+                        lp[0] = L0;
+                        lp[a.pitch] = L1;
+                    }
+                } else {
+                    tl[(2 * q) * N] = L0;
+                    tl[(2 * q + 1) * N] = L1;
+                }
+                const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
+                const pk16 d2 = (l2 * dqs2 + dqr2) >> dqsh2;
+                const _Float16 h0 = (_Float16)d2.x, h1 = (_Float16)d2.y;
+                dq[m][q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            }
+        }
+    }
+    // inverse passes (transform.py:221-236)
+    __device__ __forceinline__ void inv1() {
+        const h4_t bi = __builtin_bit_cast(h4_t, make_uint2(mw0.z, mw0.w));
+#pragma unroll
+        for (int m = 0; m < NM; ++m)
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(dq[m][0], dq[m][1])), bi,
+                                                           (f4_t){0.5f, 0.5f, 0.5f, 0.5f}, 0, 0, 0);
+    }
+    __device__ __forceinline__ void inv2() {
+        const h4_t bi = __builtin_bit_cast(h4_t, make_uint2(mw0.z, mw0.w));
+        if constexpr (SPLIT) {
+            const h4_t bi2 = __builtin_bit_cast(h4_t, make_uint2(mw1.z, mw1.w));
+#pragma unroll
+            for (int m = 0; m < NM; ++m) {
+                float hf[4], bf1[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const float f = __builtin_floorf(acc[m][r]);
+                    hf[r] = __builtin_floorf(acc[m][r] * 0.5f);   // floor(floor(x) / 2) = floor(x / 2)
+                    bf1[r] = __builtin_fmaf(-2.0f, hf[r], f);
+                }
+                const f4_t a4 = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                    __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(hf[0], hf[1]), pk_trunc_h(hf[2], hf[3]))), bi2,
+                    (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                    __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(bf1[0], bf1[1]), pk_trunc_h(bf1[2], bf1[3]))), bi, a4,
+                    0, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < NM; ++m)
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
+                    __builtin_bit_cast(h4_t,
+                                       make_uint2(pk_floor_h(acc[m][0], acc[m][1]), pk_floor_h(acc[m][2], acc[m][3]))),
+                    bi, (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
+        }
+    }
+    // reconstruct + clip (intra.py:70-78) into rc (no TU of the batch reads another's samples)
+    __device__ __forceinline__ void recon(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                          int16_t (*rc2)[RP][RP], bool rec_later) {
+#pragma unroll
+        for (int m = 0; m < NM; ++m) {
+            int16_t (*rc)[RP] = rc2[pm[m]];
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const float x0 = __builtin_amdgcn_fmed3f(acc[m][2 * q], 1280.0f, 1792.0f);
+                const float x1 = __builtin_amdgcn_fmed3f(acc[m][2 * q + 1], 1280.0f, 1792.0f);
+                const pku16 rv = __builtin_elementwise_min(
+                    __builtin_elementwise_sub_sat(__builtin_bit_cast(pku16, pk_trunc_h(x0, x1)), pr2[m][q]),
+                    (pku16){255, 255});
+                if (onm[m]) {
+                    rc[lym[m] + 1 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.x;
+                    rc[lym[m] + 2 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.y;
+                    if (DIRECT && !rec_later && !(NH_AB && (a.probe & 64))) {
+                        int16_t* rp = pp.rec(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
+                        rp[0] = (int16_t)rv.x;
+                        rp[a.pitch] = (int16_t)rv.y;
+                    }
+                }
+            }
+            if (DIRECT && onm[m] && (t & 3) == 0 && !(NH_AB && (a.probe & 64)))   // the TU map: a byte per 4x4 unit
+                pp.tu(pm[m])[(int64_t)((y0c + lym[m] + yr0) / 4) * (a.w / 4) + (x0c + lxm[m] + t) / 4] = (uint8_t)L2;
+        }
+    }
+    // the tile form's outputs (after the recon's sync): 16-B level rows from the tile, 8-B recon rows
+    // from rc, the TU map; piece i = 4 samples of one TU row, N / 4 pieces per lane for NM = N / 4
+    __device__ __forceinline__ void stores(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                           int16_t (*rc2)[RP][RP], const int32_t* tile, const uint8_t* ent, int cnt,
+                                           int total, int e0, bool rec_later, int lane) {
+        const bool st = !(NH_AB && (a.probe & 64));
+        constexpr int PIECES = NM * TPM * N * N / 4;   // the set's level pieces
+#pragma unroll
+        for (int i = 0; i < (PIECES + 63) / 64; ++i) {
+            const int pc = lane + 64 * i, tl = pc / (N * N / 4), row = (pc / (N / 4)) % N, c4 = pc % (N / 4);
+            const int e = e0 + tl;
+            if (pc < PIECES && e < total && st) {
+                const int p = entry_plane(e, cnt), code = ent[e - p * cnt];
+                const int lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4;
+                const int64_t o = (int64_t)(y0c + ly + row) * a.pitch + x0c + lx + 4 * c4;
+                const int4 lv = *(const int4*)&tile[(tl * N + row) * N + 4 * c4];
+                int32_t* lp = pp.lvl(p) + o;
+                lp[0] = lv.x;
+                lp[1] = lv.y;
+                lp[2] = lv.z;
+                lp[3] = lv.w;
+                if (!rec_later) {
+                    const int16_t* q4 = &rc2[p][ly + 1 + row][lx + 1 + 4 * c4];
+                    int16_t* rp = pp.rec(p) + o;
+                    rp[0] = q4[0];
+                    rp[1] = q4[1];
+                    rp[2] = q4[2];
+                    rp[3] = q4[3];
+                }
+                if (c4 == 0 && (row & 3) == 0) {
+                    uint8_t* tu = pp.tu(p);
+                    const int w4 = a.w / 4;
+#pragma unroll
+                    for (int jj = 0; jj < N / 4; ++jj)
+                        tu[(int64_t)((y0c + ly + row) / 4) * w4 + (x0c + lx) / 4 + jj] = (uint8_t)L2;
+                }
+            }
+        }
+    }
+};
+
 template <int N, bool DST, int RP = 33, bool DIRECT = false>
 __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[RP][RP], int32_t* tile, const ChainQ& cq,
                                                     uint32_t& wb, uint64_t* ph = nullptr, bool rec_later = false) {
-    static_assert(N == 4 || ((N == 8 || N == 16) && !DST), "mosaic kinds: DST4, DCT4, DCT8, DCT16");
-    constexpr int L2 = Log2<N>::v, NM = N / 4, TS = 16 / N, TPM = TS * TS;
-    constexpr int KIND = N == 4 ? (DST ? 0 : 3) : N == 8 ? 1 : 2;
-    constexpr bool SPLIT = N == 4 && !DST;   // DCT4: the inverse pass 2 in two halves
+    constexpr int L2 = Log2<N>::v;
     uint64_t ph_t = 0;
     auto phase = [&](int k) {   // A/B build, NH_CLOSED4_STAMPS (as tu_closed_batch_pk2)
         if (NH_AB && ph) {
@@ -1859,228 +2122,71 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
         }
     };
     phase(-1);
-    const int lane = opaque_lane64(), c = lane & 15, g = lane >> 4;
-    const int t = c % N, yr0 = (4 * g) % N, bc = c / N, br = (4 * g) / N;
-    const uint4 mw0 = *(const uint4*)&c_mosaic[KIND][lane], mw1 = *((const uint4*)&c_mosaic[KIND][lane] + 1);
-    int pm[NM], lxm[NM], lym[NM];
-    bool onm[NM];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-        const int e = c0 + m * TPM + br * TS + bc;
-        onm[m] = e < total;
-        pm[m] = onm[m] ? entry_plane(e, cnt) : 0;
-        const int code = ent[onm[m] ? e - pm[m] * cnt : 0];   // idle lanes shadow plane 0's first TU
-        lxm[m] = (code & 7) * 4;
-        lym[m] = ((code >> 3) & 7) * 4;
-    }
-    // the TUs' source samples, every load issued before any use
-    int32_t sv[NM][4];
-    if (pp.stile) {
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            const __attribute__((address_space(3))) int16_t* tp = pp.stile + (pm[m] * pp.stp + lym[m] + yr0) * pp.stp + lxm[m] + t;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) sv[m][r] = tp[r * pp.stp];
-        }
-    } else {
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            const int16_t* sp = pp.src(pm[m]) + (int64_t)(y0c + lym[m] + yr0) * a.pitch + x0c + lxm[m] + t;
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                sv[m][r] = (NH_AB && (a.probe & 32)) ? rc2[pm[m]][lym[m] + 1 + yr0 + r][lxm[m] + 1 + t]
-                                                     : sp[(int64_t)r * a.pitch];
-        }
-    }
+    const int lane = opaque_lane64();
+    MosaicSet<N, DST, N / 4, RP, DIRECT> ms;
+    ms.init(lane, ent, cnt, total, c0);
+    ms.load(a, pp, x0c, y0c, rc2);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int m = 0; m < NM; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wb |= (uint32_t)sv[m][r];   // the stream's wide check
-    uint32_t hx[NM][2];
-    pku16 pr2[NM][2];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-        int16_t (*rc)[RP] = rc2[pm[m]];
-        const int lx = lxm[m], ly = lym[m];
-        const int32_t topt = rc[ly][lx + 1 + t], tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // __main__.py:168
-        // DC (intra.py:46-62): the TU's lanes of row group 0 add top[t], of row group 1 left[t] (N = 4: both)
-        int32_t sdc = N == 4 ? topt + rc[ly + 1 + t][lx] : yr0 == 0 ? topt : yr0 == 4 ? (int32_t)rc[ly + 1 + t][lx] : 0;
-        sdc = tu_sum<N>(sdc);
-        const int32_t dc = (sdc + N) >> (L2 + 1);
-        const pk16 dc2 = pk_splat(dc);
-        pk16 o2[2];
-        pku16 pl2[2];
-        {   // planar (intra.py:81-113) at (y, t): (N-1-t) left[y] + (t+1) tr + (N-1-y) top[t] + (y+1) bl + N >> L2+1
-            const int32_t b = (t + 1) * tr + (N - 1 - yr0) * topt + (yr0 + 1) * bl + N, st = bl - topt;
-            const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)}, sh = {L2 + 1, L2 + 1};
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int y = yr0 + 2 * q;
-                o2[q] = pk_pair(sv[m][2 * q], sv[m][2 * q + 1]);
-                const pku16 lf = {(unsigned short)rc[ly + 1 + y][lx], (unsigned short)rc[ly + 2 + y][lx]};
-                const pku16 bs = {(unsigned short)(b + 2 * q * st), (unsigned short)(b + (2 * q + 1) * st)};
-                pl2[q] = (lf * wl + bs) >> sh;
-            }
-        }
-        int32_t ed = 0, ep = 0;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const pk16 d0 = o2[q] - dc2, d1 = o2[q] - __builtin_bit_cast(pk16, pl2[q]);
-            ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
-            ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
-        }
-        ed = tu_sum<N>(ed);
-        ep = tu_sum<N>(ep);
-        const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[q]);
-            const pku16 rr = __builtin_bit_cast(pku16, o2[q] - pr);   // residual, intra.py:65-67
-            hx[m][q] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of 768 + n
-            pr2[m][q] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
-        }
-    }
+    ms.predict(rc2, wb);
     phase(0);
-    const h4_t bf = __builtin_bit_cast(h4_t, make_uint2(mw0.x, mw0.y)), bi = __builtin_bit_cast(h4_t, make_uint2(mw0.z, mw0.w));
-    const float c1 = __builtin_bit_cast(float, mw1.x), c2 = __builtin_bit_cast(float, mw1.y);
-    // forward passes (transform.py:179-194)
-    f4_t acc[NM];
-#pragma unroll
-    for (int m = 0; m < NM; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(hx[m][0], hx[m][1])), bf,
-                                                       (f4_t){c1, c1, c1, c1}, 0, 0, 0);
-#pragma unroll
-    for (int m = 0; m < NM; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-            __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(acc[m][0], acc[m][1]), pk_trunc_h(acc[m][2], acc[m][3]))), bf,
-            (f4_t){c2, c2, c2, c2}, 0, 0, 0);
-#pragma unroll
-    for (int m = 0; m < NM; ++m) mfma_result_ready4(acc[m]);   // before floor_i32's inline-asm reads
+    ms.pass1();
+    ms.pass2();
+    ms.ready();
     phase(1);
-    // quantize_block (levels into the tile: TU e - c0, row, column) and dequantize_block in 16 bits
-    const pk16 dqs2 = pk_splat(cq.dqs), dqr2 = pk_splat((int32_t)cq.dqr_v), dqsh2 = pk_splat(cq.dqsh);
-    uint32_t dq[NM][2];
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-        int32_t* tl = tile + ((m * TPM + br * TS + bc) * N + yr0) * N + t;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int32_t L0 = quant_s(floor_i32(acc[m][2 * q]), cq.qs, cq.h_v, cq.hneg_v);
-            const int32_t L1 = quant_s(floor_i32(acc[m][2 * q + 1]), cq.qs, cq.h_v, cq.hneg_v);
-            if constexpr (DIRECT) {
-                if (onm[m] && !(NH_AB && (a.probe & 64))) {
-                    int32_t* lp = pp.lvl(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
-                    lp[0] = L0;
-                    lp[a.pitch] = L1;
-                }
-            } else {
-                tl[(2 * q) * N] = L0;
-                tl[(2 * q + 1) * N] = L1;
-            }
-            const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
-            const pk16 d2 = (l2 * dqs2 + dqr2) >> dqsh2;
-            const _Float16 h0 = (_Float16)d2.x, h1 = (_Float16)d2.y;
-            dq[m][q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-        }
-    }
+    ms.quant(a, pp, x0c, y0c, cq, tile);
     phase(2);
-    // inverse passes (transform.py:221-236)
-#pragma unroll
-    for (int m = 0; m < NM; ++m)
-        acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(dq[m][0], dq[m][1])), bi,
-                                                       (f4_t){0.5f, 0.5f, 0.5f, 0.5f}, 0, 0, 0);
-    if constexpr (SPLIT) {
-        const h4_t bi2 = __builtin_bit_cast(h4_t, make_uint2(mw1.z, mw1.w));
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            float hf[4], bf1[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float f = __builtin_floorf(acc[m][r]);
-                hf[r] = __builtin_floorf(acc[m][r] * 0.5f);   // floor(floor(x) / 2) = floor(x / 2)
-                bf1[r] = __builtin_fmaf(-2.0f, hf[r], f);
-            }
-            const f4_t a4 = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(hf[0], hf[1]), pk_trunc_h(hf[2], hf[3]))), bi2,
-                (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(bf1[0], bf1[1]), pk_trunc_h(bf1[2], bf1[3]))), bi, a4,
-                0, 0, 0);
-        }
-    } else {
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                __builtin_bit_cast(h4_t, make_uint2(pk_floor_h(acc[m][0], acc[m][1]), pk_floor_h(acc[m][2], acc[m][3]))),
-                bi, (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
-    }
+    ms.inv1();
+    ms.inv2();
     phase(3);
-    // reconstruct + clip (intra.py:70-78) into rc (no TU of this batch reads another's samples)
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
-        int16_t (*rc)[RP] = rc2[pm[m]];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const float x0 = __builtin_amdgcn_fmed3f(acc[m][2 * q], 1280.0f, 1792.0f);
-            const float x1 = __builtin_amdgcn_fmed3f(acc[m][2 * q + 1], 1280.0f, 1792.0f);
-            const pku16 rv = __builtin_elementwise_min(
-                __builtin_elementwise_sub_sat(__builtin_bit_cast(pku16, pk_trunc_h(x0, x1)), pr2[m][q]), (pku16){255, 255});
-            if (onm[m]) {
-                rc[lym[m] + 1 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.x;
-                rc[lym[m] + 2 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.y;
-                if (DIRECT && !rec_later && !(NH_AB && (a.probe & 64))) {
-                    int16_t* rp = pp.rec(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
-                    rp[0] = (int16_t)rv.x;
-                    rp[a.pitch] = (int16_t)rv.y;
-                }
-            }
-        }
-        if (DIRECT && onm[m] && (t & 3) == 0 && !(NH_AB && (a.probe & 64)))   // the TU map: one byte per 4x4 unit
-            pp.tu(pm[m])[(int64_t)((y0c + lym[m] + yr0) / 4) * (a.w / 4) + (x0c + lxm[m] + t) / 4] = (uint8_t)L2;
-    }
+    ms.recon(a, pp, x0c, y0c, rc2, rec_later);
     pair_sync();
     phase(4);
-    if constexpr (DIRECT) {
-        phase(5);
-        return;
+    if constexpr (!DIRECT) {
+        ms.stores(a, pp, x0c, y0c, rc2, tile, ent, cnt, total, c0, rec_later, lane);
+        pair_sync();   // the tile's and rc's reads before the next batch writes them
     }
-    // the levels (16-B row pieces from the tile), the recon (8-B row pieces from rc) and the TU map:
-    // piece i = 4 samples of one TU row, N / 4 pieces per lane
-    const bool st = !(NH_AB && (a.probe & 64));
-#pragma unroll
-    for (int i = 0; i < N / 4; ++i) {
-        const int pc = lane + 64 * i, el = pc / (N * N / 4), row = (pc / (N / 4)) % N, c4 = pc % (N / 4);
-        const int e = c0 + el;
-        if (e < total && st) {
-            const int p = entry_plane(e, cnt), code = ent[e - p * cnt];
-            const int lx = (code & 7) * 4, ly = ((code >> 3) & 7) * 4;
-            const int64_t o = (int64_t)(y0c + ly + row) * a.pitch + x0c + lx + 4 * c4;
-            const int4 lv = *(const int4*)&tile[(el * N + row) * N + 4 * c4];
-            int32_t* lp = pp.lvl(p) + o;
-            lp[0] = lv.x;
-            lp[1] = lv.y;
-            lp[2] = lv.z;
-            lp[3] = lv.w;
-            if (!rec_later) {
-                const int16_t* q4 = &rc2[p][ly + 1 + row][lx + 1 + 4 * c4];
-                int16_t* rp = pp.rec(p) + o;
-                rp[0] = q4[0];
-                rp[1] = q4[1];
-                rp[2] = q4[2];
-                rp[3] = q4[3];
-            }
-            if (c4 == 0 && (row & 3) == 0) {
-                uint8_t* tu = pp.tu(p);
-                const int w4 = a.w / 4;
-#pragma unroll
-                for (int jj = 0; jj < N / 4; ++jj)
-                    tu[(int64_t)((y0c + ly + row) / 4) * w4 + (x0c + lx) / 4 + jj] = (uint8_t)L2;
-            }
-        }
-    }
-    pair_sync();   // the tile's and rc's reads before the next batch writes them
     phase(5);
+}
+
+// A round's 8x8 TUs (tot8 <= 4: one mosaic) and 4x4 TUs (tot4 <= 16: one mosaic) in ONE call: the two
+// sets' chains interleaved phase by phase, so the round pays one chain's latency, not two
+template <bool DST4, int RP = 33, bool DIRECT = false>
+__device__ __forceinline__ void tu_closed_batch_mix(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
+                                                    int cnt8, const uint8_t* ent8, int cnt4, const uint8_t* ent4,
+                                                    int npl, int16_t (*rc2)[RP][RP], int32_t* tile,
+                                                    const ChainQ& cq8, const ChainQ& cq4, uint32_t& wb,
+                                                    bool rec_later) {
+    const int lane = opaque_lane64();
+    MosaicSet<8, false, 1, RP, DIRECT> s8;
+    MosaicSet<4, DST4, 1, RP, DIRECT> s4;
+    const int tot8 = cnt8 * npl, tot4 = cnt4 * npl;
+    s8.init(lane, ent8, cnt8, tot8, 0);
+    s4.init(lane, ent4, cnt4, tot4, 0);
+    s8.load(a, pp, x0c, y0c, rc2);
+    s4.load(a, pp, x0c, y0c, rc2);
+    __builtin_amdgcn_sched_barrier(0);
+    s8.predict(rc2, wb);
+    s4.predict(rc2, wb);
+    s8.pass1();
+    s4.pass1();
+    s8.pass2();
+    s4.pass2();
+    s8.ready();
+    s4.ready();
+    s8.quant(a, pp, x0c, y0c, cq8, tile);
+    s4.quant(a, pp, x0c, y0c, cq4, tile + 256);
+    s8.inv1();
+    s4.inv1();
+    s8.inv2();
+    s4.inv2();
+    s8.recon(a, pp, x0c, y0c, rc2, rec_later);
+    s4.recon(a, pp, x0c, y0c, rc2, rec_later);
+    pair_sync();
+    if constexpr (!DIRECT) {
+        s8.stores(a, pp, x0c, y0c, rc2, tile, ent8, cnt8, tot8, 0, rec_later, lane);
+        s4.stores(a, pp, x0c, y0c, rc2, tile + 256, ent4, cnt4, tot4, 0, rec_later, lane);
+        pair_sync();
+    }
 }
 
 // A 32x32 luma TU of the closed loop on the f16 matrix cores: the config-5
@@ -2478,6 +2584,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             else { NH_PLAN_BATCH(16, false, cq[2]) }
                             break;
                         case 2:
+                            if (NH_CLOSED4_MIX && NH_CLOSED4_MOSAIC >= 2 && (nz & (2ull << rs)) != 0) {
+                                // the round's 4x4 TUs follow: both sizes in one call when each fits a mosaic
+                                const int cnt4 = __builtin_amdgcn_readlane(cntv, rs + 1);
+                                if (tot <= 4 && cnt4 * npl <= 16 && !(NH_AB && (a.probe & 2))) {
+                                    if (a.is_luma)
+                                        tu_closed_batch_mix<true, RP, !REC && NH_CLOSED4_DIRECT>(
+                                            a, pp, x0c, y0c, cnt, ent, cnt4, ent + cnt, npl, rc, t32, cq[1], cq[0], wb,
+                                            rec_flush);
+                                    else
+                                        tu_closed_batch_mix<false, RP, !REC && NH_CLOSED4_DIRECT>(
+                                            a, pp, x0c, y0c, cnt, ent, cnt4, ent + cnt, npl, rc, t32, cq[1], cq[0], wb,
+                                            rec_flush);
+                                    nz &= ~(2ull << rs);   // the 4x4 entry is done
+                                    off += cnt4;
+                                    break;
+                                }
+                            }
                             if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(8, false, cq[1]) }
                             else { NH_PLAN_BATCH(8, false, cq[1]) }
                             break;
