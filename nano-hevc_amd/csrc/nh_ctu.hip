@@ -551,9 +551,8 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, 
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-    ed = grp_sum<64>(ed);
-    ep = grp_sum<64>(ep);
-    const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+    // DC wins ties (__main__.py:173): ed <= ep as ONE wave reduction of the difference (|.| < 2^27)
+    const bool use_dc = grp_sum<64>(ed - ep) <= 0;
     // residual (intra.py:65-67) + 1536 as f16 bits: 0x6600 + n for |n| < 512
     uint32_t hx[8];
 #pragma unroll
@@ -712,9 +711,8 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-    ed = grp_sum<64>(ed);
-    ep = grp_sum<64>(ep);
-    const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+    // DC wins ties (__main__.py:173): ed <= ep as ONE wave reduction of the difference (|.| < 2^27)
+    const bool use_dc = grp_sum<64>(ed - ep) <= 0;
     pku16 pr2[8];                   // 0x6600 (the f16 bits of 1536) - the chosen prediction
     uint32_t hx[8];
 #pragma unroll

@@ -1939,9 +1939,8 @@ struct MosaicSet {
                 ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
                 ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
             }
-            ed = tu_sum<N>(ed);
-            ep = tu_sum<N>(ep);
-            const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+            // DC wins ties (__main__.py:173): ed <= ep as ONE reduction of the difference
+            const bool use_dc = tu_sum<N>(ed - ep) <= 0;
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
                 const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[q]);
@@ -2107,7 +2106,7 @@ struct MosaicSet {
     }
 };
 
-template <int N, bool DST, int RP = 33, bool DIRECT = false>
+template <int N, bool DST, int RP = 33, bool DIRECT = false, int NMS = N / 4>
 __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                                     int cnt, int total, int c0, const uint8_t* ent,
                                                     int16_t (*rc2)[RP][RP], int32_t* tile, const ChainQ& cq,
@@ -2123,7 +2122,7 @@ __device__ __forceinline__ void tu_closed_batch_mma(const Closed4Args& a, const 
     };
     phase(-1);
     const int lane = opaque_lane64();
-    MosaicSet<N, DST, N / 4, RP, DIRECT> ms;
+    MosaicSet<N, DST, NMS, RP, DIRECT> ms;   // (4x4 rounds of more than 16 TUs: two mosaics in one call)
     ms.init(lane, ent, cnt, total, c0);
     ms.load(a, pp, x0c, y0c, rc2);
     __builtin_amdgcn_sched_barrier(0);
@@ -2258,9 +2257,8 @@ __device__ __forceinline__ void closed_chain32_tf(const Closed4Args& a, const in
         ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
         ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
     }
-    ed = grp_sum<64>(ed);
-    ep = grp_sum<64>(ep);
-    const bool use_dc = ed <= ep;   // DC wins ties (__main__.py:173)
+    // DC wins ties (__main__.py:173): ed <= ep as ONE wave reduction of the difference (|.| < 2^27)
+    const bool use_dc = grp_sum<64>(ed - ep) <= 0;
     uint32_t hx[8];
     pku16 pr2[8];
 #pragma unroll
@@ -2580,8 +2578,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             tu_closed_batch_mma<NN, DST, RP, !REC && NH_CLOSED4_DIRECT>(                               \
                                 a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, Q, wb, ph, rec_flush);
                         case 1:
-                            if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(16, false, cq[2]) }
-                            else { NH_PLAN_BATCH(16, false, cq[2]) }
+                            if (NH_CLOSED4_MOSAIC) {   // (a pair's one 16x16 TU each: two mosaics, not four)
+                                for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2)); c0 += 4) {
+                                    if (tot - c0 <= 2)
+                                        tu_closed_batch_mma<16, false, RP, !REC && NH_CLOSED4_DIRECT, 2>(
+                                            a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, cq[2], wb, ph, rec_flush);
+                                    else
+                                        tu_closed_batch_mma<16, false, RP, !REC && NH_CLOSED4_DIRECT, 4>(
+                                            a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, cq[2], wb, ph, rec_flush);
+                                }
+                            } else {
+                                NH_PLAN_BATCH(16, false, cq[2])
+                            }
                             break;
                         case 2:
                             if (NH_CLOSED4_MIX && NH_CLOSED4_MOSAIC >= 2 && (nz & (2ull << rs)) != 0) {
@@ -2604,14 +2612,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WAVES))
                             if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(8, false, cq[1]) }
                             else { NH_PLAN_BATCH(8, false, cq[1]) }
                             break;
+#define NH_MOSAIC4(DST)                                                                                       \
+                        for (int c0 = 0; c0 < tot && !(NH_AB && (a.probe & 2));) {                                \
+                            if (tot - c0 > 16) {                                                                  \
+                                tu_closed_batch_mma<4, DST, RP, !REC && NH_CLOSED4_DIRECT, 2>(                    \
+                                    a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, cq[0], wb, ph, rec_flush);       \
+                                c0 += 32;                                                                         \
+                            } else {                                                                              \
+                                tu_closed_batch_mma<4, DST, RP, !REC && NH_CLOSED4_DIRECT, 1>(                    \
+                                    a, pp, x0c, y0c, cnt, tot, c0, ent, rc, t32, cq[0], wb, ph, rec_flush);       \
+                                c0 += 16;                                                                         \
+                            }                                                                                     \
+                        }
                         default:
                             if (a.is_luma) {
-                                if (NH_CLOSED4_MOSAIC) { NH_MOSAIC_BATCH(4, true, cq[0]) }
+                                if (NH_CLOSED4_MOSAIC) { NH_MOSAIC4(true) }
                                 else { NH_PLAN_BATCH(4, true, cq[0]) }
                             } else {
-                                if (NH_CLOSED4_MOSAIC >= 2) { NH_MOSAIC_BATCH(4, false, cq[0]) }
+                                if (NH_CLOSED4_MOSAIC >= 2) { NH_MOSAIC4(false) }
                                 else { NH_PLAN_BATCH(4, false, cq[0]) }
                             }
+#undef NH_MOSAIC4
 #undef NH_PLAN_BATCH
 #undef NH_MOSAIC_BATCH
                     }
