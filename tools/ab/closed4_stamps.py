@@ -93,6 +93,25 @@ def main():
         calls = X[:, 1 + si].sum()
         if calls and ph[si].sum():
             out["batch_phases_cycles_per_call"][f"{nn}x{nn}"] = {k: float(v / calls) for k, v in zip(names_ph, ph[si])}
+    # where a wave's resident time goes (SQ_WAIT_ANY's structural part): per CTU row (ticket), the wait
+    # before its first CTU (the wavefront's ramp: a row starts once the row above is a CTU ahead), then
+    # per CTU the poll, the rounds and the publish / slide -- realtime (100 MHz) for the ramp, shader
+    # cycles for the rest, all in seconds
+    rt = buf[:n].reshape(-1, W16).astype(np.int64)
+    tk_of = np.arange(len(rt)) // ccols
+    ok = rt[:, 1] != 0
+    first = {}
+    for i in np.nonzero(ok)[0]:
+        k = tk_of[i]
+        if k not in first or rt[i, 5] < rt[first[k], 5]:
+            first[k] = i
+    fi = np.array(list(first.values()))
+    t0 = (rt[fi, 5] - (rt[fi, 4] - rt[fi, 1]) / (ghz * 10)).min()          # the first CTU's start (100 MHz ticks)
+    ramp = ((rt[fi, 5] - (rt[fi, 4] - rt[fi, 1]) / (ghz * 10)) - t0).sum() * 1e-8
+    cyc = 1.0 / (ghz * 1e9)
+    tot = ramp + float((r[:, 4] - r[:, 1]).sum()) * cyc
+    out["wave_time_split"] = {"ramp": ramp / tot, "poll": float(poll.sum()) * cyc / tot,
+                              "rounds": float(rounds.sum()) * cyc / tot, "tail": float(tail.sum()) * cyc / tot}
     out["note"] = "stamps in shader-clock cycles (s_memtime); medians per CTU unless mean_*"
     print(json.dumps(out))
 
