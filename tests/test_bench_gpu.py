@@ -63,9 +63,9 @@ def test_bench_config4_line():
     assert d["cpu_baseline"]["cores"] > 1 and d["cpu_baseline"]["value_1thread"] > 0
     assert d["config"]["source_fraction_rank0"] == 1.0
     if os.path.exists(os.path.join(ROOT, "profiles", "valu_roofline.json")):   # committed VALU roofline inputs
-        # the VALU view leads unless the committed counts describe other kernel sources (then the
-        # line says so and falls back to the HBM view)
-        assert d["roofline"]["bound"] == "valu" or d["roofline"].get("valu_profile_stale") is True
+        # the VALU view leads, from counts of THIS build's kernel sources (strict; the CPU
+        # suite's test_valu_profile_matches_the_tree fails first when the sources moved on)
+        assert d["roofline"]["bound"] == "valu" and not d["roofline"].get("valu_profile_stale"), d["roofline"]
     tu = d["config"]["tu_blocks_per_step"]
     # every sample of the two frames lies in exactly one TU
     area = sum(n * (4 << k) ** 2 for k, n in enumerate(tu[f"{4 << k}x{4 << k}"] for k in range(4)))

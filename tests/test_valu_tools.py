@@ -54,3 +54,23 @@ def test_committed_valu_roofline_is_self_consistent():
         # every kernel input the file cites is committed
         for src in e["source"].values():
             assert src is None or os.path.exists(os.path.join(ROOT, src)), (key, src)
+
+
+def test_valu_profile_matches_the_tree():
+    """The committed VALU roofline (profiles/valu_roofline.json) was measured on THESE kernel
+    sources: every config's recorded sha256 over its source files equals the tree's.
+    A kernel change must be re-profiled (TAG=x tools/gpu_run.sh valu_rate pmc_cal valu_kt
+    valu_pmc1 valu_pmc2 valu_pmc3 valu_pmc4; tools/pmc_valu.py --tag x --cal x --rates-tag x)."""
+    import json
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pmc_valu
+    d = json.load(open(os.path.join(ROOT, "profiles", "valu_roofline.json")))
+    keys = {v[0]: c for c, v in pmc_valu.CONFIGS.items()}
+    stale = {}
+    for key, ent in d["configs"].items():
+        src = ent["sources"]
+        assert src["files"] == pmc_valu.SOURCES[keys[key]], key
+        now = pmc_valu.sources_digest(src["files"])
+        if now != src["sha256"]:
+            stale[key] = (src["sha256"][:12], now[:12])
+    assert not stale, f"profiles/valu_roofline.json is stale for {stale}"

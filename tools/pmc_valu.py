@@ -47,7 +47,7 @@ CONFIGS = {
     "3": ("cfg3_1080p_yuv420", "k_intra_rdo8<1, true, 1>", 3.0),
     "closed": ("cfg3_closed_1080p_yuv420", "k_intra_rdo8_closed_tag<1, 1>", 1 / 64),
     "4b": ("cfg4_4k_yuv420", "k_ctu_open<32", 1 / 16),
-    "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair", 2 / 64),
+    "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair<3, true, 32", 1 / 64),   # (luma instance: one per launch set)
     "5b": ("cfg5_8k_yuv420", "k_tc32_hd<2", 2 / 8),
 }
 # the sources a config's kernels are compiled from: their digest goes into the
