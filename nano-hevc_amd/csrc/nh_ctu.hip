@@ -37,6 +37,8 @@
 #include "nh_mfma.hpp"
 #include "nh_f16mma.hpp"
 #include "nh_ldsdma.hpp"
+#define NH_MOSAIC_TABLE c_mosaic_ctu
+#include "nh_mosaic.hpp"
 // The open-loop CTU kernels keep the builtin's v_dot2c seeding (pdot_first,
 // nh_packed.hpp): the VOP3P form measured 1.3 % slower here (0.0390 vs 0.0385
 // ms per 4K frame, profiles/r03/cfg4/ab_libs_4b_pd.jsonl) and 2-4 % faster in
@@ -113,9 +115,10 @@ template <int CTB> struct Strip {
     // narrow workgroups: an int16 tile aliasing the int32 one, rows of TP int16
     // (an odd number of dwords: the pair reads of a row pass are conflict-free)
     static constexpr int TP = SW + 2;
-    // (CTB 32: room for the f16 transpose tile of ctu_chain32_h, 32 rows of QH = 40 halves)
-    static constexpr int QH = 40, T16 = CTB == 32 ? 32 * QH : CTB * TP;
-    static_assert((TP / 2) % 2 == 1 && T16 * 2 <= CF * 4, "int16 tile layout");
+    // (CTB 32: room for chain32_tf's level tile, 32 rows of 36 int32 -- round 5 -- which also
+    // holds ctu_chain32_h's f16 transpose tile, 32 rows of QH = 40 halves)
+    static constexpr int QH = 40, T16 = CTB == 32 ? 32 * 72 : CTB * TP;
+    static_assert((TP / 2) % 2 == 1 && (CTB == 32 || T16 * 2 <= CF * 4) && 32 * QH <= 32 * 72, "int16 tile layout");
 };
 
 // One batch of 64/N TUs of size N from the workgroup's size-N list: lane l
@@ -371,6 +374,85 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
     }
 }
 
+// The same batch on MFMA mosaics (round 5, nh_mosaic.hpp): the
+// closed loop's chain with the strip image as its source and neighbours (open
+// loop: every neighbour is a source sample).  OST: levels / recon into the LDS
+// output images (whole-row stores after the group); otherwise one sample per lane
+// and store straight to memory.  NM = N / 4 mosaics hold the batch's 64 / N TUs.
+template <int N, bool DST, int CTB, bool OST>
+__device__ __forceinline__ void ctu_batch_mma(const CtuArgs& a, const int16_t* s_img, const uint16_t* list, int cnt,
+                                              int b0, const int* s_org, int32_t* __restrict__ lvl,
+                                              int16_t* __restrict__ rec, int32_t* olvl, int16_t* orec) {
+    using G = Strip<CTB>;
+    constexpr int IP = G::IP, NM = N / 4;
+    using MC = MosaicCore<N, DST, NM>;
+    const ChainQ cq = make_chainq(a.q[MC::L2 - 2], a.dqs, a.dq_per);
+    MC mc;
+    mc.lane_init(opaque_lane());
+    const int16_t* pm[NM];   // pm[m][(1 + y) * IP + x]: sample (y, x) of the lane's TU; x = -1: left, y = -1: top
+    int swm[NM], lxm[NM], lym[NM];
+    bool onm[NM];
+    int32_t sv[NM][4];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        const int e = b0 + m * MC::TPM + mc.el;
+        onm[m] = e < cnt;
+        const int en = list[onm[m] ? e : b0], sw = en >> 6, u = en & 63;   // idle lanes shadow the batch's first TU
+        swm[m] = sw;
+        lxm[m] = 4 * (u % G::UW);
+        lym[m] = 4 * (u / G::UW);
+        pm[m] = s_img + sw * G::IMG + lym[m] * IP + 4 + lxm[m];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[m][r] = pm[m][(1 + mc.yr0 + r) * IP + mc.t];
+    }
+    struct Nb {
+        const int16_t* p[NM];   // (copies: a reference to the array kept it in memory)
+        int t;
+        __device__ int32_t top(int m) const { return p[m][t]; }
+        __device__ int32_t tr(int m) const { return p[m][N - 1]; }
+        __device__ int32_t bl(int m) const { return p[m][N * IP - 1]; }
+        __device__ int32_t dcl(int m) const { return p[m][(1 + t) * IP - 1]; }
+        __device__ pku16 left2(int m, int y) const {
+            return (pku16){(unsigned short)p[m][(1 + y) * IP - 1], (unsigned short)p[m][(2 + y) * IP - 1]};
+        }
+    };
+    Nb nb;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) nb.p[m] = pm[m];
+    nb.t = mc.t;
+    mc.predict(sv, nb);
+    mc.pass1();
+    mc.pass2();
+    mc.ready();
+    auto out_row = [&](int m, int q) { return lym[m] + mc.yr0 + 2 * q; };   // strip-local row of the pair
+    mc.quant(cq, [&](int m, int q, int32_t L0, int32_t L1) {
+        if (!onm[m]) return;
+        if constexpr (OST) {
+            int32_t* o = olvl + swm[m] * (CTB * G::SW) + out_row(m, q) * G::SW + lxm[m] + mc.t;
+            o[0] = L0;
+            o[G::SW] = L1;
+        } else {
+            int32_t* o = lvl + (int64_t)(s_org[2 * swm[m] + 1] + out_row(m, q)) * a.pitch + s_org[2 * swm[m]] + lxm[m] + mc.t;
+            o[0] = L0;
+            o[a.pitch] = L1;
+        }
+    });
+    mc.inv1();
+    mc.inv2();
+    mc.recon([&](int m, int q, pku16 rv) {
+        if (!onm[m]) return;
+        if constexpr (OST) {
+            int16_t* o = orec + swm[m] * (CTB * G::SW) + out_row(m, q) * G::SW + lxm[m] + mc.t;
+            o[0] = (int16_t)rv.x;
+            o[G::SW] = (int16_t)rv.y;
+        } else {
+            int16_t* o = rec + (int64_t)(s_org[2 * swm[m] + 1] + out_row(m, q)) * a.pitch + s_org[2 * swm[m]] + lxm[m] + mc.t;
+            o[0] = (int16_t)rv.x;
+            o[a.pitch] = (int16_t)rv.y;
+        }
+    });
+}
+
 // A 32x32 TU (a whole CTU of a CTB-32 strip) on the int8 matrix cores: the
 // chain of k_tc32_mfma (nh_tc32.hip) with the block, its
 // neighbours and the dequantized tile in the strip's LDS image / tile.
@@ -490,12 +572,30 @@ constexpr int kOutP = 36, kRecP = 24;   // int32 per row: level tile, recon tile
 // CTB-32 strip image (img[r * IP + c] = sample (r - 1, c), c = -1 the left
 // column); ImgDma: the LDS-DMA image of k_tc32_hd (the block body in 64-B rows,
 // the top row and left column side by side in a 64-sample edge array).
+// Config 4 open loop: narrow 32x32 luma TUs on the transposition-free chain (chain32_tf, round 5);
+// 0: round 4's ctu_chain32_h (LDS transpose after dequantization, bases in LDS)
+#ifndef NH_CTU_TF32
+#define NH_CTU_TF32 1
+#endif
+// Config 4 open loop, narrow 4..16 TUs on MFMA mosaics (ctu_batch_mma): 1 = the groups with LDS output
+// images (chroma), 2 = every group (luma's outputs then leave one sample per lane and store)
+#ifndef NH_CTU_MOSAIC
+#define NH_CTU_MOSAIC 1
+#endif
 struct ImgStrip {
     const int16_t* p;
     static constexpr int IP = Strip<32>::IP;
     __device__ __forceinline__ int32_t at(int y, int x) const { return p[(1 + y) * IP + x]; }
     __device__ __forceinline__ int32_t top(int x) const { return p[x]; }
     __device__ __forceinline__ int32_t left(int y) const { return p[(1 + y) * IP - 1]; }
+    // chain32_tf's reads (see ImgDma): rows of IP samples, 8-B aligned (sample (y, 0) at [1 + y][4])
+    static constexpr int RS = IP;
+    __device__ __forceinline__ const int16_t* trp(int L) const {
+        return p + (1 + 4 * (L >> 5) + ((L >> 2) & 3)) * IP + 16 * ((L >> 4) & 1) + 4 * (L & 3);
+    }
+    __device__ __forceinline__ pku16 left2(int y) const {   // (left[y], left[y + 1])
+        return (pku16){(unsigned short)left(y), (unsigned short)left(y + 1)};
+    }
 };
 struct ImgDma {
     const int16_t* body;   // [y][x], 32 x 32
@@ -513,6 +613,11 @@ struct ImgDma {
     // of its group's 16 columns.  EXEC must be all ones.
     __device__ __forceinline__ const int16_t* trp(int L) const {
         return body + (4 * (L >> 5) + ((L >> 2) & 3)) * 32 + 16 * ((L >> 4) & 1) + 4 * (L & 3);
+    }
+    // (left[y], left[y + 1]) for even y: one dword each, read as one pair
+    __device__ __forceinline__ pku16 left2(int y) const {
+        const uint2 lw = *(const uint2*)(edge + 32 + 2 * y);
+        return __builtin_bit_cast(pku16, __builtin_amdgcn_perm(lw.y, lw.x, 0x05040100u));
     }
 };
 template <bool TSTORE = false, class B = BasisH, class IMG = ImgStrip>
@@ -687,20 +792,17 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
         lds_v4s* tp = (lds_v4s*)(lds_void_t*)img.trp(l);
 #pragma unroll
         for (int t = 0; t < 4; ++t) {   // rows 8t + 4hh .. +3 of column r: o2[2t], o2[2t + 1]
-            const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(tp + 64 * t);
+            const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(tp + 2 * IMG::RS * t);
             o2[2 * t] = (pk16){v[0], v[1]};
             o2[2 * t + 1] = (pk16){v[2], v[3]};
         }
-        // left[y], left[y + 1]: one dword each (the 16-bit LDS-DMA's layout), read as one pair
-        const uint2* lft = (const uint2*)img.leftp(4 * hh);
         const pku16 wl = {(unsigned short)(31 - r), (unsigned short)(31 - r)}, sh = {6, 6};
         const int32_t d = bl - topr, b0 = (r + 1) * tr + (31 - 4 * hh) * topr + (4 * hh + 1) * bl + 32;
         const pku16 d2 = {(unsigned short)d, (unsigned short)d}, bb0 = {(unsigned short)b0, (unsigned short)(b0 + d)};
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
             const int c = 2 * (p & 1) + 8 * (p >> 1);   // y_p - 4 hh
-            const uint2 lw = lft[c / 2];   // (c is even: left[y_p] is dword 4 hh + c)
-            const pku16 lf = __builtin_bit_cast(pku16, __builtin_amdgcn_perm(lw.y, lw.x, 0x05040100u));
+            const pku16 lf = img.left2(4 * hh + c);   // (left[y_p], left[y_p + 1])
             pl2[p] = (lf * wl + (bb0 + (pku16){(unsigned short)c, (unsigned short)c} * d2)) >> sh;
         }
     }
@@ -960,7 +1062,8 @@ __device__ __forceinline__ void strip_writeout(const CtuArgs& a, int sx0, int sy
 // Returns with the workgroup's waves in the batch loop's exit (no barrier).
 template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, bool OST = false, class Prefetch>
 __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
-                                          CtuSmem<CTB, NARROW, NARROW && MFMA32, GS, OST>& sm, StripLoad<CTB>& ld,
+                                          CtuSmem<CTB, NARROW, NARROW && MFMA32 && !(NH_CTU_TF32 && !OST), GS, OST>& sm,
+                                          StripLoad<CTB>& ld,
                                           Prefetch&& prefetch) {
     using G = Strip<CTB>;
     constexpr int UW = G::UW;
@@ -1039,7 +1142,9 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
     const int n16 = CTB >= 16 ? (cnt[2] + 3) / 4 : 0, n8 = CTB >= 8 ? (cnt[1] + 7) / 8 : 0, n4 = (cnt[0] + 15) / 16;
     const int total = n32 + n16 + n8 + n4;
 #define NH_CHAIN(N, DST, L, B)                                                                              \
-    if constexpr (NARROW)                                                                                   \
+    if constexpr (NARROW && N <= 16 && (OST ? NH_CTU_MOSAIC >= 1 : NH_CTU_MOSAIC >= 2))                    \
+        ctu_batch_mma<N, DST, CTB, OST>(a, sm.img, sm.list[L], cnt[L], B, sm.org, lvl, rec, sm.olvl, sm.orec); \
+    else if constexpr (NARROW)                                                                              \
         ctu_chain_pk<N, DST, CTB, OST>(a, sm.img, (int16_t*)sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec, \
                                        sm.olvl, sm.orec);                                                   \
     else                                                                                                    \
@@ -1051,7 +1156,13 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
         if (item >= total) break;
         if constexpr (CTB == 32) {
             if (item < n32) {
-                if constexpr (NARROW && MFMA32) {   // one TU per wave on the f16 matrix cores
+                if constexpr (NARROW && MFMA32 && NH_CTU_TF32 && !OST) {   // the transposition-free chain (§4.5)
+                    const int e = sm.list[3][item], sw = e >> 6;
+                    const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
+                    const TfLane tl = make_tf_lane(cq, c_basis_hc, lane & 31);
+                    chain32_tf(a, ImgStrip{sm.img + sw * G::IMG + 4}, c_basis_hc, sm.org[2 * sw], sm.org[2 * sw + 1], lvl,
+                               rec, (int32_t*)((int16_t*)sm.tile + sw * G::T16), cq, tl);
+                } else if constexpr (NARROW && MFMA32) {   // one TU per wave on the f16 matrix cores
                     const int e = sm.list[3][item], sw = e >> 6;
                     if constexpr (OST)
                         ctu_chain32_h(a, ImgStrip{sm.img + sw * G::IMG + 4}, (uint16_t*)sm.tile + sw * G::T16, sm.basis, 0, 0,
@@ -1100,7 +1211,9 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
 // WAVES: the occupancy floor (waves/SIMD) the registers are allocated for.
 template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4, bool OST = false>
 __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
-    __shared__ CtuSmem<CTB, true, MFMA32, GS, OST> sm;
+    // (the transposition-free 32x32 chain reads its bases from the constant table: no LDS copy)
+    constexpr bool BAS = MFMA32 && !(NH_CTU_TF32 && !OST);
+    __shared__ CtuSmem<CTB, true, BAS, GS, OST> sm;
     if (NH_AB && (a.probe & 4)) return;   // A/B probe: the launch of the grid alone
     if constexpr (PERSIST == 0) {
         // the bases' loads issued with the strip's and written to LDS after the
@@ -1108,18 +1221,18 @@ __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WA
         static_assert(sizeof(BasisH) == 256 * 16 && GS >= 4, "one 16-byte piece per thread of the first 256");
         uint4 bq{};
         const bool bthr = threadIdx.x < 256;
-        if constexpr (MFMA32) {
+        if constexpr (BAS) {
             if (bthr) bq = ((const uint4*)&c_basis_h)[threadIdx.x];
         }
         StripLoad<CTB> ld;
         strip_issue<CTB, GS>(a, blockIdx.x, blockIdx.y, ld);
         ctu_group<CTB, LUMA, true, MFMA32, GS, OST>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
-            if constexpr (MFMA32) {
+            if constexpr (BAS) {
                 if (bthr) ((uint4*)&sm.basis)[threadIdx.x] = bq;
             }
         });
     } else {
-        if constexpr (MFMA32) copy_basis_h(sm.basis);   // ordered before use by ctu_group's barrier
+        if constexpr (BAS) copy_basis_h(sm.basis);   // ordered before use by ctu_group's barrier
         // PERSIST = 1: the next group's loads in flight under this group's chains;
         // PERSIST = 2: no prefetch (only the per-workgroup start-up amortised)
         StripLoad<CTB> ld;
@@ -1361,6 +1474,9 @@ static int ensure_basis_ctu() {
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_h), &bh, sizeof(bh)));
         const BasisHC bhc = make_basis_hc();
         NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_basis_hc), &bhc, sizeof(bhc)));
+        static MosaicLane mt[4][64];   // ctu_batch_mma's per-lane bases (this translation unit's copy)
+        make_mosaic(mt);
+        NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic_ctu), mt, sizeof(mt)));
         return (int)NH_OK;
     });
 }

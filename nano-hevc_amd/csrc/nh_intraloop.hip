@@ -17,6 +17,8 @@
 #include "nh_packed.hpp"
 #include "nh_f16mma.hpp"
 #include "nh_ldsdma.hpp"
+#define NH_MOSAIC_TABLE c_mosaic_cl
+#include "nh_mosaic.hpp"
 
 namespace nh {
 
@@ -1755,122 +1757,16 @@ __device__ __forceinline__ void tu_closed_batch_pk2(const Closed4Args& a, const 
 }
 
 // ---------------------------------------------------------------------------
-// Small closed-loop TUs on the f16 matrix cores: MOSAICS (round 5).  A batch of
-// 64 / N TUs of size N (4x4 DST, 8x8 and 16x16 DCT) is NM = N / 4 mosaics of
-// 16 x 16 samples -- 16 / N x 16 / N TUs each -- and every 1-D pass of every TU
-// of a mosaic is ONE v_mfma_f32_16x16x16_f16 against a block-diagonal basis:
-// lane l = (g = l / 16, c = l % 16) holds mosaic column c, rows 4g .. 4g + 3 (the
-// A operand of X^T), and each pass's accumulator IS the next pass's A operand
-// (it is the transposed product: D1 = temp^T, D2 = coeff, D3 = tmp^T, D4 = rres),
-// so the four passes need no transpose -- where the packed chain
-// (tu_closed_batch_pk2) moves every TU through the LDS tile three times.  The
-// basis enters scaled by 2^-S (exact in f16: |T| <= 90, S <= 9), so each
-// accumulator is the reference's sum / 2^S exactly (integer operands below 2048,
-// products exact in fp32, sums below 2^24 * 2^-S: tools/packed_bounds.py's
-// bounds), and the shift's rounding is the accumulator's
-// initial 0.5 then a floor:
-//  * the residual enters as the f16 of 768 + n (bits 0x6200 + 2n); the pass-1
-//    accumulator starts at 0.5 + 1536 - 768 rs / 2^S (rs = the lane's basis-row
-//    sum), so it holds temp + 1536 + frac in [1024, 2048): the truncating
-//    conversion to f16 is the floor;
-//  * pass 2 starts at 0.5 - 1536 rs / 2^S and floors to the coefficient;
-//  * the dequantized coefficients (<= 1024) enter as exact f16 integers, the
-//    inverse pass 1 floors to tmp (<= 1936, exact in f16);
-//  * the inverse pass 2 starts at 1536.5: clamped to [1280, 1792] its f16 bits
-//    are 0x6600 + R' (R' = R clamped to [-256, 256]), and bits - (0x6600 - pred)
-//    saturating at 0, then min 255, is the clip of pred + R.
-// DCT4 (chroma 4x4): its inverse pass 1 reaches 2223, beyond f16's integers, so
-// its inverse pass 2 is two MFMAs into one accumulator: tmp = 2h + b with h =
-// floor(tmp / 2) (<= 1112) against the basis * 2^-(S-1), b in {0, 1} against the
-// basis * 2^-S.  Same results as tu_closed_batch_pk2 on 8-bit streams.
-typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
-typedef float f4_t __attribute__((ext_vector_type(4)));
-struct MosaicLane {            // per (kind, lane): 32 B
-    uint32_t bf[2], bi[2];     // the B operands: Tb^T (passes 1, 2) and Tb (inverse passes), f16 * 2^-S
-    float c1, c2;              // the initial accumulators of passes 1 and 2
-    uint32_t bi2[2];           // DCT4: Tb * 2^-(S-1) (the inverse pass 2's h half)
-};
-__constant__ MosaicLane c_mosaic[4][64];   // kinds: 0 DST4, 1 DCT8, 2 DCT16, 3 DCT4
-constexpr int Log2Rt(int n) { return n == 4 ? 2 : n == 8 ? 3 : n == 16 ? 4 : 5; }
-inline uint16_t f16_bits_exact(int num, int sh) {   // num * 2^-sh as f16 bits (|num| < 2048, a normal result)
-    if (num == 0) return 0;
-    uint16_t s = num < 0 ? 0x8000 : 0;
-    unsigned m = (unsigned)(num < 0 ? -num : num);
-    int e = -sh;
-    while (m < 1024) { m <<= 1; --e; }   // m in [1024, 2048): value = m * 2^(e)
-    return (uint16_t)(s | (uint16_t)((e + 10 + 15) << 10) | (uint16_t)(m & 1023));
-}
-inline void make_mosaic(MosaicLane (*out)[64]) {
-    for (int kind = 0; kind < 4; ++kind) {
-        const int N = kind == 1 ? 8 : kind == 2 ? 16 : 4, S = Log2Rt(N) + 5;
-        auto T = [&](int k, int n) {
-            return kind == 0 ? dst4c(k, n) : kind == 1 ? dctc<8>(k, n) : kind == 2 ? dctc<16>(k, n) : dctc<4>(k, n);
-        };
-        for (int l = 0; l < 64; ++l) {
-            const int c = l & 15, g = l >> 4;
-            uint16_t bf[4], bi[4], bi2[4];
-            for (int r = 0; r < 4; ++r) {
-                const int k = 4 * g + r, same = k / N == c / N;
-                bf[r] = same ? f16_bits_exact(T(c % N, k % N), S) : 0;   // B1[k][j] = T[j][k]
-                bi[r] = same ? f16_bits_exact(T(k % N, c % N), S) : 0;   // B3[k][j] = T[k][j]
-                bi2[r] = same ? f16_bits_exact(T(k % N, c % N), S - 1) : 0;
-            }
-            int rs = 0;
-            for (int n = 0; n < N; ++n) rs += T(c % N, n);
-            MosaicLane& m = out[kind][l];
-            m.bf[0] = bf[0] | ((uint32_t)bf[1] << 16);
-            m.bf[1] = bf[2] | ((uint32_t)bf[3] << 16);
-            m.bi[0] = bi[0] | ((uint32_t)bi[1] << 16);
-            m.bi[1] = bi[2] | ((uint32_t)bi[3] << 16);
-            m.c1 = 0.5f + 1536.0f - 768.0f * (float)rs / (float)(1 << S);
-            m.c2 = 0.5f - 1536.0f * (float)rs / (float)(1 << S);
-            m.bi2[0] = bi2[0] | ((uint32_t)bi2[1] << 16);
-            m.bi2[1] = bi2[2] | ((uint32_t)bi2[3] << 16);
-        }
-    }
-}
-// see mfma_result_ready (nh_f16mma.hpp): 8 wait states after a 16x16x16 MFMA -- what the compiler
-// itself inserts before a VALU read of such a result (tools/isa_check.py checks every such read)
-__device__ __forceinline__ void mfma_result_ready4(f4_t& acc) { asm volatile("s_nop 7" : "+v"(acc)); }
-// sum over the lanes of one TU of the mosaic (N = 4: 4 lanes; 8: 8 lanes + the 8 lanes 16 apart; 16: all 64)
-template <int N>
-__device__ __forceinline__ int32_t tu_sum(int32_t v) {
-    if constexpr (N == 4) return grp_sum<4>(v);
-    else if constexpr (N == 8) {
-        v = grp_sum<8>(v);
-        return v + lane_perm<-1>(v);
-    } else return grp_sum<64>(v);
-}
-// DIRECT (the latency form: launches of few CTU rows): levels, recon and TU map leave straight from the
-// registers, one sample per lane and store, none of the tile round trip on the chain; otherwise (many
-// rows, throughput) as N / 4 whole 16-B row pieces per lane through the tile.
-//
-// MosaicSet<N, DST, NM>: NM mosaics of TUs of size N whose batch entries start at e0 of a round's
-// (entries, cnt per plane, total) list -- one phase of the chain per method, so a batch can run one set
-// (tu_closed_batch_mma) or two sets of different sizes interleaved (tu_closed_batch_mix: a round's
-// 8x8 and 4x4 TUs in one call, their latencies overlapped instead of added).
 template <int N, bool DST, int NM, int RP, bool DIRECT>
-struct MosaicSet {
-    static_assert(N == 4 || ((N == 8 || N == 16) && !DST), "mosaic kinds: DST4, DCT4, DCT8, DCT16");
-    static constexpr int L2 = Log2<N>::v, TS = 16 / N, TPM = TS * TS;
-    static constexpr int KIND = N == 4 ? (DST ? 0 : 3) : N == 8 ? 1 : 2;
-    static constexpr bool SPLIT = N == 4 && !DST;   // DCT4: the inverse pass 2 in two halves
-    int t, yr0, el;                                 // column in the TU, first row, TU slot of mosaic 0
+struct MosaicSet : MosaicCore<N, DST, NM> {
+    using C = MosaicCore<N, DST, NM>;
+    using C::t; using C::yr0; using C::el; using C::L2; using C::TPM;
     int pm[NM], lxm[NM], lym[NM];
     bool onm[NM];
-    uint4 mw0, mw1;
     int32_t sv[NM][4];
-    uint32_t hx[NM][2], dq[NM][2];
-    pku16 pr2[NM][2];
-    f4_t acc[NM];
 
     __device__ __forceinline__ void init(int lane, const uint8_t* ent, int cnt, int total, int e0) {
-        const int c = lane & 15, g = lane >> 4;
-        t = c % N;
-        yr0 = (4 * g) % N;
-        el = (4 * g) / N * TS + c / N;
-        mw0 = *(const uint4*)&c_mosaic[KIND][lane];
-        mw1 = *((const uint4*)&c_mosaic[KIND][lane] + 1);
+        C::lane_init(lane);
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
             const int e = e0 + m * TPM + el;
@@ -1903,167 +1799,60 @@ struct MosaicSet {
             }
         }
     }
+    // the neighbours from the pair's LDS reconstruction
+    struct Nb {
+        const MosaicSet& s;
+        int16_t (*rc2)[RP][RP];
+        __device__ int32_t top(int m) const { return rc2[s.pm[m]][s.lym[m]][s.lxm[m] + 1 + s.t]; }
+        __device__ int32_t tr(int m) const { return rc2[s.pm[m]][s.lym[m]][s.lxm[m] + N]; }
+        __device__ int32_t bl(int m) const { return rc2[s.pm[m]][s.lym[m] + N][s.lxm[m]]; }
+        __device__ int32_t dcl(int m) const { return rc2[s.pm[m]][s.lym[m] + 1 + s.t][s.lxm[m]]; }
+        __device__ pku16 left2(int m, int y) const {
+            return (pku16){(unsigned short)rc2[s.pm[m]][s.lym[m] + 1 + y][s.lxm[m]],
+                           (unsigned short)rc2[s.pm[m]][s.lym[m] + 2 + y][s.lxm[m]]};
+        }
+    };
     __device__ __forceinline__ void predict(int16_t (*rc2)[RP][RP], uint32_t& wb) {
 #pragma unroll
         for (int m = 0; m < NM; ++m)
 #pragma unroll
             for (int r = 0; r < 4; ++r) wb |= (uint32_t)sv[m][r];   // the stream's wide check
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            int16_t (*rc)[RP] = rc2[pm[m]];
-            const int lx = lxm[m], ly = lym[m];
-            const int32_t topt = rc[ly][lx + 1 + t], tr = rc[ly][lx + N], bl = rc[ly + N][lx];   // __main__.py:168
-            // DC (intra.py:46-62): the TU's lanes of row group 0 add top[t], of row group 1 left[t] (N = 4: both)
-            int32_t sdc = N == 4 ? topt + rc[ly + 1 + t][lx] : yr0 == 0 ? topt : yr0 == 4 ? (int32_t)rc[ly + 1 + t][lx] : 0;
-            sdc = tu_sum<N>(sdc);
-            const int32_t dc = (sdc + N) >> (L2 + 1);
-            const pk16 dc2 = pk_splat(dc);
-            pk16 o2[2];
-            pku16 pl2[2];
-            {   // planar (intra.py:81-113) at (y, t): (N-1-t) left[y] + (t+1) tr + (N-1-y) top[t] + (y+1) bl + N >> L2+1
-                const int32_t b = (t + 1) * tr + (N - 1 - yr0) * topt + (yr0 + 1) * bl + N, st = bl - topt;
-                const pku16 wl = {(unsigned short)(N - 1 - t), (unsigned short)(N - 1 - t)}, sh = {L2 + 1, L2 + 1};
-#pragma unroll
-                for (int q = 0; q < 2; ++q) {
-                    const int y = yr0 + 2 * q;
-                    o2[q] = pk_pair(sv[m][2 * q], sv[m][2 * q + 1]);
-                    const pku16 lf = {(unsigned short)rc[ly + 1 + y][lx], (unsigned short)rc[ly + 2 + y][lx]};
-                    const pku16 bs = {(unsigned short)(b + 2 * q * st), (unsigned short)(b + (2 * q + 1) * st)};
-                    pl2[q] = (lf * wl + bs) >> sh;
-                }
-            }
-            int32_t ed = 0, ep = 0;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const pk16 d0 = o2[q] - dc2, d1 = o2[q] - __builtin_bit_cast(pk16, pl2[q]);
-                ed = __builtin_amdgcn_sdot2(d0, d0, ed, false);
-                ep = __builtin_amdgcn_sdot2(d1, d1, ep, false);
-            }
-            // DC wins ties (__main__.py:173): ed <= ep as ONE reduction of the difference
-            const bool use_dc = tu_sum<N>(ed - ep) <= 0;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const pk16 pr = use_dc ? dc2 : __builtin_bit_cast(pk16, pl2[q]);
-                const pku16 rr = __builtin_bit_cast(pku16, o2[q] - pr);   // residual, intra.py:65-67
-                hx[m][q] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});   // f16 of 768 + n
-                pr2[m][q] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, pr);
-            }
-        }
+        C::predict(sv, Nb{*this, rc2});
     }
-    // forward passes (transform.py:179-194)
-    __device__ __forceinline__ void pass1() {
-        const h4_t bf = __builtin_bit_cast(h4_t, make_uint2(mw0.x, mw0.y));
-        const float c1 = __builtin_bit_cast(float, mw1.x);
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(hx[m][0], hx[m][1])), bf,
-                                                           (f4_t){c1, c1, c1, c1}, 0, 0, 0);
-    }
-    __device__ __forceinline__ void pass2() {
-        const h4_t bf = __builtin_bit_cast(h4_t, make_uint2(mw0.x, mw0.y));
-        const float c2 = __builtin_bit_cast(float, mw1.y);
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(acc[m][0], acc[m][1]), pk_trunc_h(acc[m][2], acc[m][3]))),
-                bf, (f4_t){c2, c2, c2, c2}, 0, 0, 0);
-    }
-    __device__ __forceinline__ void ready() {
-#pragma unroll
-        for (int m = 0; m < NM; ++m) mfma_result_ready4(acc[m]);   // before floor_i32's inline-asm reads
-    }
-    // quantize_block (levels: straight out, or into the tile at TU slot tslot0 + ...) and
-    // dequantize_block in 16 bits
+    // quantize_block (levels: straight out, or into the tile) and dequantize_block
     __device__ __forceinline__ void quant(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                           const ChainQ& cq, int32_t* tile) {
-        const pk16 dqs2 = pk_splat(cq.dqs), dqr2 = pk_splat((int32_t)cq.dqr_v), dqsh2 = pk_splat(cq.dqsh);
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            int32_t* tl = tile + ((m * TPM + el) * N + yr0) * N + t;
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const int32_t L0 = quant_s(floor_i32(acc[m][2 * q]), cq.qs, cq.h_v, cq.hneg_v);
-                const int32_t L1 = quant_s(floor_i32(acc[m][2 * q + 1]), cq.qs, cq.h_v, cq.hneg_v);
-                if constexpr (DIRECT) {
-                    if (onm[m] && !(NH_AB && (a.probe & 64))) {
-                        int32_t* lp = pp.lvl(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
-                        lp[0] = L0;
-                        lp[a.pitch] = L1;
-                    }
-                } else {
-                    tl[(2 * q) * N] = L0;
-                    tl[(2 * q + 1) * N] = L1;
+        C::quant(cq, [&](int m, int q, int32_t L0, int32_t L1) {
+            if constexpr (DIRECT) {
+                if (onm[m] && !(NH_AB && (a.probe & 64))) {
+                    int32_t* lp = pp.lvl(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
+                    lp[0] = L0;
+                    lp[a.pitch] = L1;
                 }
-                const pk16 l2 = __builtin_bit_cast(pk16, __builtin_amdgcn_perm((uint32_t)L1, (uint32_t)L0, 0x05040100u));
-                const pk16 d2 = (l2 * dqs2 + dqr2) >> dqsh2;
-                const _Float16 h0 = (_Float16)d2.x, h1 = (_Float16)d2.y;
-                dq[m][q] = (uint32_t)__builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            } else {
+                int32_t* tl = tile + ((m * TPM + el) * N + yr0) * N + t;
+                tl[(2 * q) * N] = L0;
+                tl[(2 * q + 1) * N] = L1;
             }
-        }
-    }
-    // inverse passes (transform.py:221-236)
-    __device__ __forceinline__ void inv1() {
-        const h4_t bi = __builtin_bit_cast(h4_t, make_uint2(mw0.z, mw0.w));
-#pragma unroll
-        for (int m = 0; m < NM; ++m)
-            acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4_t, make_uint2(dq[m][0], dq[m][1])), bi,
-                                                           (f4_t){0.5f, 0.5f, 0.5f, 0.5f}, 0, 0, 0);
-    }
-    __device__ __forceinline__ void inv2() {
-        const h4_t bi = __builtin_bit_cast(h4_t, make_uint2(mw0.z, mw0.w));
-        if constexpr (SPLIT) {
-            const h4_t bi2 = __builtin_bit_cast(h4_t, make_uint2(mw1.z, mw1.w));
-#pragma unroll
-            for (int m = 0; m < NM; ++m) {
-                float hf[4], bf1[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float f = __builtin_floorf(acc[m][r]);
-                    hf[r] = __builtin_floorf(acc[m][r] * 0.5f);   // floor(floor(x) / 2) = floor(x / 2)
-                    bf1[r] = __builtin_fmaf(-2.0f, hf[r], f);
-                }
-                const f4_t a4 = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                    __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(hf[0], hf[1]), pk_trunc_h(hf[2], hf[3]))), bi2,
-                    (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                    __builtin_bit_cast(h4_t, make_uint2(pk_trunc_h(bf1[0], bf1[1]), pk_trunc_h(bf1[2], bf1[3]))), bi, a4,
-                    0, 0, 0);
-            }
-        } else {
-#pragma unroll
-            for (int m = 0; m < NM; ++m)
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x16f16(
-                    __builtin_bit_cast(h4_t,
-                                       make_uint2(pk_floor_h(acc[m][0], acc[m][1]), pk_floor_h(acc[m][2], acc[m][3]))),
-                    bi, (f4_t){1536.5f, 1536.5f, 1536.5f, 1536.5f}, 0, 0, 0);
-        }
+        });
     }
     // reconstruct + clip (intra.py:70-78) into rc (no TU of the batch reads another's samples)
     __device__ __forceinline__ void recon(const Closed4Args& a, const PairPlanes& pp, int x0c, int y0c,
                                           int16_t (*rc2)[RP][RP], bool rec_later) {
-#pragma unroll
-        for (int m = 0; m < NM; ++m) {
-            int16_t (*rc)[RP] = rc2[pm[m]];
-#pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const float x0 = __builtin_amdgcn_fmed3f(acc[m][2 * q], 1280.0f, 1792.0f);
-                const float x1 = __builtin_amdgcn_fmed3f(acc[m][2 * q + 1], 1280.0f, 1792.0f);
-                const pku16 rv = __builtin_elementwise_min(
-                    __builtin_elementwise_sub_sat(__builtin_bit_cast(pku16, pk_trunc_h(x0, x1)), pr2[m][q]),
-                    (pku16){255, 255});
-                if (onm[m]) {
-                    rc[lym[m] + 1 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.x;
-                    rc[lym[m] + 2 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.y;
-                    if (DIRECT && !rec_later && !(NH_AB && (a.probe & 64))) {
-                        int16_t* rp = pp.rec(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
-                        rp[0] = (int16_t)rv.x;
-                        rp[a.pitch] = (int16_t)rv.y;
-                    }
+        C::recon([&](int m, int q, pku16 rv) {
+            if (onm[m]) {
+                int16_t (*rc)[RP] = rc2[pm[m]];
+                rc[lym[m] + 1 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.x;
+                rc[lym[m] + 2 + yr0 + 2 * q][lxm[m] + 1 + t] = (int16_t)rv.y;
+                if (DIRECT && !rec_later && !(NH_AB && (a.probe & 64))) {
+                    int16_t* rp = pp.rec(pm[m]) + (int64_t)(y0c + lym[m] + yr0 + 2 * q) * a.pitch + x0c + lxm[m] + t;
+                    rp[0] = (int16_t)rv.x;
+                    rp[a.pitch] = (int16_t)rv.y;
                 }
+                if (DIRECT && q == 1 && (t & 3) == 0 && !(NH_AB && (a.probe & 64)))   // the TU map: a byte per 4x4 unit
+                    pp.tu(pm[m])[(int64_t)((y0c + lym[m] + yr0) / 4) * (a.w / 4) + (x0c + lxm[m] + t) / 4] = (uint8_t)L2;
             }
-            if (DIRECT && onm[m] && (t & 3) == 0 && !(NH_AB && (a.probe & 64)))   // the TU map: a byte per 4x4 unit
-                pp.tu(pm[m])[(int64_t)((y0c + lym[m] + yr0) / 4) * (a.w / 4) + (x0c + lxm[m] + t) / 4] = (uint8_t)L2;
-        }
+        });
     }
     // the tile form's outputs (after the recon's sync): 16-B level rows from the tile, 8-B recon rows
     // from rc, the TU map; piece i = 4 samples of one TU row, N / 4 pieces per lane for NM = N / 4
@@ -3014,7 +2803,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
         const int rcm = once_m.run([] {
             static MosaicLane mt[4][64];
             make_mosaic(mt);
-            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic), mt, sizeof(mt)));
+            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic_cl), mt, sizeof(mt)));
             return (int)NH_OK;
         });
         if (rcm) return rcm;

@@ -53,7 +53,7 @@ CONFIGS = {
 # the sources a config's kernels are compiled from: their digest goes into the
 # entry, and bench.py / tools/bench_configs.py recompute it to tell whether the
 # committed instruction counts still describe the build they run
-_HDRS = ["nh_common.hpp", "nh_internal.hpp", "nh_packed.hpp", "nh_tree.hpp", "nh_mfma.hpp", "nh_f16mma.hpp",
+_HDRS = ["nh_common.hpp", "nh_internal.hpp", "nh_packed.hpp", "nh_tree.hpp", "nh_mfma.hpp", "nh_f16mma.hpp", "nh_mosaic.hpp",
          "nh_ldsdma.hpp"]
 SOURCES = {
     "3": ["nh_intraloop.hip"] + _HDRS,
