@@ -8,7 +8,10 @@ against the SHIPPED code object (tools/isa_check.py):
   constant is caught;
 * every inline-asm v_cvt_rpi / v_cvt_flr that reads an MFMA result directly has
   the 24 wait states of mfma_result_ready (nh_f16mma.hpp) after the MFMA;
-* the hot kernels use no scratch.
+* the hot kernels use no scratch, and config 4's open-loop kernels keep their
+  static LDS (a struct copy of the mosaic lane words once added 5 KB per
+  chroma workgroup);
+* no source bit_casts an ext-vector element (hipcc read element 0).
 """
 import os
 import sys
@@ -74,3 +77,26 @@ def test_hot_kernels_use_no_scratch(product):
     hot = {k: v for k, v in sizes.items() if any(h in k for h in HOT) and "ILi8ELi1ELb1ELi4E" not in k}
     assert len(hot) >= 20, sorted(hot)
     assert not {k: v for k, v in hot.items() if v}, "scratch in a hot kernel"
+
+
+def test_ctu_open_static_lds(product):
+    _, meta = product
+    lds = {k: v for k, v in ic.lds_sizes(meta).items() if "k_ctu_open" in k}
+    assert len(lds) >= 8, sorted(lds)
+    # CTB 4 / 8 / 16 groups: the strip images, lists, output images and tiles (45,568 B at most);
+    # CTB 32: 31,200 B
+    assert max(lds.values()) <= 45568, {k: v for k, v in lds.items() if v > 45568}
+
+
+def test_no_bitcast_of_a_vector_element():
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "nano-hevc_amd", "csrc", "*.hip")) + \
+        glob.glob(os.path.join(ROOT, "nano-hevc_amd", "csrc", "*.hpp"))
+    assert len(srcs) > 10
+    assert not ic.bitcast_element_uses(srcs)
+    with tempfile.TemporaryDirectory() as d:   # the lint itself
+        p = os.path.join(d, "x.hpp")
+        with open(p, "w") as f:
+            f.write("const float c2 = __builtin_bit_cast(float, mw1.y);\n"
+                    "const float ok = __uint_as_float((uint32_t)mw1.y);\n")
+        assert len(ic.bitcast_element_uses([p])) == 1

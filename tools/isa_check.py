@@ -497,6 +497,39 @@ def private_segment_sizes(meta: str) -> dict[str, int]:
     return out
 
 
+def lds_sizes(meta: str) -> dict[str, int]:
+    """Kernel name -> static LDS (.group_segment_fixed_size; listed before .name in each kernel's map)."""
+    out, pending = {}, None
+    for line in meta.splitlines():
+        m = re.search(r"\.group_segment_fixed_size:\s+(\d+)", line)
+        if m:
+            pending = int(m.group(1))
+        m = re.search(r"\.name:\s+(\S+)", line)
+        if m and pending is not None:
+            out[m.group(1)] = pending
+            pending = None
+    return out
+
+
+# ---------------------------------------------------------------------------
+# 4. source lint
+# ---------------------------------------------------------------------------
+# __builtin_bit_cast of an ext-vector ELEMENT (v.x / v.y / ...) read element 0 on hipcc 7.2 (round 5:
+# the mosaics' pass-2 initial accumulator silently became pass 1's); read the element as a value first
+BITCAST_ELEMENT = re.compile(r"__builtin_bit_cast\(\s*[\w:<> ]+,\s*[\w\[\]]+\.[xyzw]\s*\)")
+
+
+def bitcast_element_uses(paths) -> list[str]:
+    hits = []
+    for p in paths:
+        with open(p) as f:
+            for n, line in enumerate(f, 1):
+                code = line.split("//", 1)[0]
+                if BITCAST_ELEMENT.search(code):
+                    hits.append(f"{p}:{n}: {line.strip()}")
+    return hits
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=LIB)
