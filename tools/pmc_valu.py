@@ -236,6 +236,7 @@ def main():
                     continue
                 e["attainable_dynamic_lo"] = r["attainable_lo"]
                 e["attainable_dynamic_hi"] = r["attainable_hi"]
+                e["dynamic_counter_tol"] = r["tol"]   # the counters' agreement the LP needed (0.005 unless widened)
                 e["attainable_static"] = e.get("attainable_valu_winst_per_s")
                 e["attainable_valu_winst_per_s"] = r["attainable_hi"]   # the peak: the most the executed mix allows
                 e["valu_priced_measured_frac"] = r.get("valu_priced_measured_frac")
