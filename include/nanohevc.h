@@ -277,6 +277,17 @@ int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int qp, int32_t
  * the source layout.  Same per-plane results as nh_tc32_plane. */
 int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
                    int16_t* d_recon, int variant, void* stream);
+/* Config 5 with COMPACT levels (variant 1 only): levels of lvl_bytes = 2
+ * (int16) or 1 (int8) in the source layout.  Exact: an 8-bit block's 32x32
+ * levels satisfy |level| <= 51 at every QP (tools/packed_bounds.py).  A block
+ * that is not 8-bit writes its int32 levels into d_spill (int32, source
+ * layout, never read) and the marker -32768 / -128 at its compact origin;
+ * nh_tc32_levels_widen turns (d_lvl, d_spill) into the int32 levels
+ * nh_tc32_planes writes.  int8: base / pitch / strides multiples of 16. */
+int nh_tc32_planes_compact(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, void* d_lvl,
+                           int lvl_bytes, int32_t* d_spill, int16_t* d_recon, void* stream);
+int nh_tc32_levels_widen(const void* d_lvl, int lvl_bytes, const int32_t* d_spill, const nh_plane_set* sets,
+                         int nsets, int32_t* d_out, void* stream);
 /* Measurement / validation helper: D = A.B for row-major int8 32x32 A, B
  * (int32 D) with the lane maps the config-5 MFMA kernel assumes. */
 int nh_probe_mfma_i8(const int8_t* d_a, const int8_t* d_b, int32_t* d_d, void* stream);

@@ -46,7 +46,7 @@ __global__ void __launch_bounds__(256) k_fwd8x8_quant_h2(Fused8Args a) {
 // 2r and 2r+1 of the set's linear row numbering; a pair may straddle two
 // planes, block_offset handles that).  16 row loads in flight per lane; the
 // pattern probe of this shape streams ~4 % faster than the one-block form
-// (profiles/r01/ab_shapes.json).
+// (round-1 probe; its record was not kept).
 template <int POLICY, int WAVES>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_fwd8x8_quant_v2(Fused8Args a) {
     SetDev S;

@@ -817,7 +817,7 @@ __global__ void __launch_bounds__(256) k_srv(SrvReq* q, unsigned long long* hout
             if (threadIdx.x == 0) __hip_atomic_store(&q->exited, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
-        const SrvFn f = (SrvFn)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(fn >> 32)) << 32) |
+        const SrvFn f = (SrvFn)(((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(fn >> 32)) << 32) |
                                 (unsigned)__builtin_amdgcn_readfirstlane((unsigned)fn));
         f((const uint8_t*)(s_ci + kSrvCap / 8), s_w, (uint8_t*)hout, (const uint8_t*)s_ci, s_scr);
         __builtin_amdgcn_s_waitcnt(0);        // this wave's result stores acknowledged

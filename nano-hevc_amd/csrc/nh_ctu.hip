@@ -770,9 +770,20 @@ __device__ __forceinline__ void ctu_chain32_h(const CtuArgs& a, const IMG& img, 
 // product is exact in fp32 and every partial sum a multiple of 2^-10 below 2^13:
 // the accumulators hold the reference's integer sums exactly.
 constexpr int kRecH = 2 * kRecP;   // recon tile row pitch in int16
-template <class IMG>
+// LT: the level element type in HBM.  int32_t is the reference's dtype; int16_t /
+// int8_t are exact for 8-bit blocks (|level| <= 51 at every QP for N = 32:
+// tools/packed_bounds.py level_bounds, tests/test_range_proofs.py) and cut the
+// level rows to 4 / 2 store instructions of 16 / 32 whole rows (config 5's compact
+// levels; the wide blocks' int32 levels go to a spill plane).
+template <class LT> struct LvlTile {
+    static_assert(sizeof(LT) == 1 || sizeof(LT) == 2 || sizeof(LT) == 4, "level type");
+    // tile row pitch in LT elements (16-B aligned rows): int32 kOutP, int16 the recon tile's, int8 48 B
+    static constexpr int P = sizeof(LT) == 4 ? kOutP : sizeof(LT) == 2 ? kRecH : 48;
+    static constexpr int STORES = (int)sizeof(LT);   // level-row store instructions: 4 / 2 / 1
+};
+template <class IMG, class LT = int32_t>
 __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, const BasisHC& bs, int gx0, int gy0,
-                                           int32_t* __restrict__ lvl, int16_t* __restrict__ rec, int32_t* ot,
+                                           LT* __restrict__ lvl, int16_t* __restrict__ rec, int32_t* ot,
                                            const ChainQ& cq, const TfLane& tl) {
     const int64_t op = a.pitch;
     const int l = opaque_lane(), r = l & 31, hh = l >> 5;
@@ -827,13 +838,18 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
     // the passes; levels into the tile (row k, column l), out as whole rows between the passes
     char* lb = (char*)(lvl + (int64_t)gy0 * op + gx0);
     pku16 rec2[8];
-    tf_passes(hx, pr2, bs, cq, tl, r, hh, [&](int g, int32_t L) { ot[crow(g, hh) * kOutP + r] = L; },
+    constexpr int LP = LvlTile<LT>::P;
+    LT* lt = (LT*)ot;
+    tf_passes(hx, pr2, bs, cq, tl, r, hh, [&](int g, int32_t L) { lt[crow(g, hh) * LP + r] = (LT)L; },
               [&] {
                   wave_sync();
+                  // whole 16-B row pieces: 4 instructions of 8 128-B rows (int32), 2 of 16 64-B rows (int16),
+                  // 1 of 32 32-B rows (int8)
+                  constexpr int PER = 16 / (int)sizeof(LT), RPI = 64 / (32 / PER);   // elements per lane, rows per instr
 #pragma unroll
-                  for (int i = 0; i < 4; ++i) {   // 4 instructions of 8 whole 128-B level rows
-                      const int rr = (l >> 3) + 8 * i, c = 4 * (l & 7);
-                      *(int4*)(lb + vofs((rr * (int32_t)op + c) * 4)) = *(const int4*)&ot[rr * kOutP + c];
+                  for (int i = 0; i < 32 / RPI; ++i) {
+                      const int rr = l / (32 / PER) + RPI * i, c = PER * (l % (32 / PER));
+                      *(int4*)(lb + vofs((rr * (int32_t)op + c) * (int32_t)sizeof(LT))) = *(const int4*)&lt[rr * LP + c];
                   }
                   wave_sync();   // the tile's reads before the recon tile reuses it
               },
@@ -1359,9 +1375,6 @@ __global__ void __launch_bounds__(256) k_tc32_h(CtuArgs a, int nblk) {
 }
 #endif
 
-int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
-                       int dqs, int dq_per, hipStream_t s);
-
 // Config 5, 8-bit blocks, with the next block's image loaded under this one's
 // chain: a wave codes KB consecutive blocks; block k+1's
 // body (two 1-KiB LDS-DMA pieces: 16 B per lane, rows of 64 B), its top row and
@@ -1382,10 +1395,14 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
 #ifndef NH_TC32HD_STORES_WIDE
 #define NH_TC32HD_STORES_WIDE 2
 #endif
-constexpr int kTc32hdStoresNarrow = NH_TC32HD_STORES_NARROW;   // ctu_chain32_h<TSTORE>: 4 level-row + 2 recon-row stores
+constexpr int kTc32hdStoresNarrow = NH_TC32HD_STORES_NARROW;   // chain32_tf, int32 levels: 4 level-row + 2 recon-row stores
 constexpr int kTc32hdStoresWide = NH_TC32HD_STORES_WIDE;       // the wide mark and the wide flag (never null here)
-template <int KB>
+// LT: the level element type (LvlTile): int16 / int8 levels take 2 / 1 level-row stores instead of 4
+template <class LT> constexpr int tc32hd_stores_narrow() { return kTc32hdStoresNarrow - 4 + LvlTile<LT>::STORES; }
+template <int KB, class LT = int32_t>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_tc32_hd(CtuArgs a, int nblk) {
+    constexpr int kNarrow = tc32hd_stores_narrow<LT>();
+    static_assert(kNarrow > 0, "store count");   // (equal to the wide count: one wait serves both kinds)
     __shared__ __attribute__((aligned(16))) int16_t s_body[4][2][32 * 32];
     __shared__ __attribute__((aligned(16))) int16_t s_edge[4][2][96];
     __shared__ BasisHC s_basis;
@@ -1413,7 +1430,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
         if (lane < 32) glds2s(blk - (sx0 > 0 ? 1 : 0), o_left, lds_addr(&s_edge[wv][slot][32]));
     };
     issue(b0, 0);
-    int prev = 0;   // store instructions the previous block issued (0: none, kTc32hdStoresWide, kTc32hdStoresNarrow)
+    int prev = 0;   // store instructions the previous block issued (0: none, kTc32hdStoresWide, kNarrow)
     for (int k = 0; k < KB; ++k) {
         const int b = b0 + k;
         if (b >= nblk) break;
@@ -1425,11 +1442,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
         }
         // retire block b's DMA: it was issued before the previous block's stores and block b+1's DMA
         if (next) {
-            if (prev == kTc32hdStoresNarrow) wait_vm<4 + kTc32hdStoresNarrow>();
+            if (prev == kNarrow) wait_vm<4 + kNarrow>();
             else if (prev == kTc32hdStoresWide) wait_vm<4 + kTc32hdStoresWide>();
             else wait_vm<4>();
         } else {
-            if (prev == kTc32hdStoresNarrow) wait_vm<kTc32hdStoresNarrow>();
+            if (prev == kNarrow) wait_vm<kNarrow>();
             else if (prev == kTc32hdStoresWide) wait_vm<kTc32hdStoresWide>();
             else wait_vm<0>();
         }
@@ -1453,8 +1470,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
             }
             prev = kTc32hdStoresWide;
         } else {
-            chain32_tf(a, ImgDma{body, edge}, s_basis, sx0, sy0, a.lvl + poff, a.rec + poff, s_out[wv], cq, tl);
-            prev = kTc32hdStoresNarrow;
+            chain32_tf(a, ImgDma{body, edge}, s_basis, sx0, sy0, (LT*)a.lvl + poff, a.rec + poff, s_out[wv], cq, tl);
+            prev = kNarrow;
         }
         wave_sync();
     }
@@ -1614,14 +1631,16 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     return NH_OK;
 }
 
-// Config 5's narrow launch over one plane set (full 32x32 blocks only).
-int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
-                       int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s) {
+// Config 5's narrow launch over one plane set (full 32x32 blocks only); levels
+// of lvl_bytes = 4 / 2 / 1 bytes (int32, or the compact int16 / int8 levels).
+int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* rec, const nh_plane_set& S,
+                       const QuantParams& q, int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s) {
     const int rc = ensure_basis_ctu();
     if (rc) return rc;
+    if (lvl_bytes != 4 && lvl_bytes != 2 && lvl_bytes != 1) return NH_EARG;
     CtuArgs a{};
     a.src = src + S.base;
-    a.lvl = lvl + S.base;
+    a.lvl = (int32_t*)((char*)lvl + S.base * lvl_bytes);   // k_tc32_hd<KB, LT> reads it as LT*
     a.rec = rec + S.base;
     a.group_stride = S.group_stride;
     a.plane_stride = S.plane_stride;
@@ -1661,8 +1680,10 @@ int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_
         set_error("tc32: rows must be 16-byte aligned");
         return NH_EARG;
     }
-    if (!NH_AB || dma == 2) {
-        launch(k_tc32_hd<2>, 2);
+    if (!NH_AB || dma == 2 || lvl_bytes != 4) {
+        if (lvl_bytes == 4) launch(k_tc32_hd<2>, 2);
+        else if (lvl_bytes == 2) launch(k_tc32_hd<2, int16_t>, 2);
+        else launch(k_tc32_hd<2, int8_t>, 2);
         NH_HIP(hipGetLastError());
         return NH_OK;
     }

@@ -175,7 +175,7 @@ extern "C" int nh_fwd8x8_quant_planes(const int16_t* d_res, int16_t* d_lvl, cons
     // streamed once, kept out of L2/MALL -- and >= 5 waves/SIMD: 74 VGPRs -> 6
     // waves) with the XCD-aware workgroup order (XCD x streams the x-th
     // eighth of the launch): +5..10 % over variant 5 in the interleaved A/B
-    // (profiles/r01/ab_xcd_*.json).
+    // (profiles/r01/xcd/ab_xcd_*.json).
     return nh_fwd8x8_quant_planes_variant(d_res, d_lvl, sets, nsets, qp, is_intra, kDefaultVariant, stream);
 }
 

@@ -37,6 +37,14 @@ namespace nh {
 __constant__ Basis c_basis;
 
 constexpr int kOP = 40;  // LDS row pitch (elements) of the per-wave tiles: 16-B aligned rows
+// Compact levels: the marker at a wide block's origin (its levels are in the spill plane)
+constexpr int16_t kTc32SpillMark16 = (int16_t)0x8000;
+constexpr int8_t kTc32SpillMark8 = (int8_t)0x80;
+// k_tc32_hd addresses a block's rows as a wave-uniform 64-bit base (SGPRs) plus a
+// 32-bit per-lane byte offset (the saddr forms: glds16s / glds2s, vofs stores),
+// at most (31 * pitch + 28) * 4 bytes from the block's origin (int32 level rows),
+// computed in int32: pitches up to 2^24 samples keep it below 2^31.
+constexpr int kTc32MaxPitch = 1 << 24;
 
 // TREE (config 4's 32x32 TUs): block b walks the 32-aligned positions of the
 // band (rows from ta.y_base) of plane blockIdx.y of the batch, and a wave only
@@ -55,7 +63,8 @@ template <bool TREE, bool FIXUP>
 __device__ __forceinline__ void tc32_block(const int16_t* __restrict__ src, int w, int h, int pitch, int nbx, int b,
                                            QuantParams qp, int dq_scale, int dq_per, int32_t* lvl, int16_t* recon,
                                            TreeArgs ta, uint8_t* tu_log2, int16_t (*s_orig_w)[kOP],
-                                           int32_t (*s_dq_w)[kOP], int16_t* s_top_w, int16_t* s_left_w) {
+                                           int32_t (*s_dq_w)[kOP], int16_t* s_top_w, int16_t* s_left_w,
+                                           char* mark = nullptr, int mark_bytes = 0) {
     const int l = threadIdx.x & 63, r = l & 31, hh = l >> 5;
     const ChainQ cq = make_chainq(qp, dq_scale, dq_per);   // 32-bit quant/dequant (int16 residual)
     {   // this workgroup's plane of the batch (blockIdx.y; ta.ppg >= 1)
@@ -64,6 +73,7 @@ __device__ __forceinline__ void tc32_block(const int16_t* __restrict__ src, int 
         src += poff;
         lvl += poff;
         recon += poff;
+        if (mark) mark += poff * mark_bytes;
         if constexpr (TREE) {
             tu_log2 += (int64_t)pz * ta.tu_plane;
             ta.plane_id += cz;
@@ -72,6 +82,14 @@ __device__ __forceinline__ void tc32_block(const int16_t* __restrict__ src, int 
     const int x0 = (b % nbx) * 32, y0 = (b / nbx) * 32 + (TREE ? ta.y_base : 0);
     if constexpr (FIXUP) {
         if (recon[(int64_t)y0 * pitch + x0] != (int16_t)0x8000) return;
+        // compact levels (k_tc32_hd<KB, int16 / int8>): this block's int32 levels go to the spill
+        // plane (lvl) and its compact origin holds the marker, a value no 8-bit block's level takes
+        // (|level| <= 51, tools/packed_bounds.py level_bounds)
+        if (mark && l == 0) {
+            char* m = mark + ((int64_t)y0 * pitch + x0) * mark_bytes;
+            if (mark_bytes == 2) *(int16_t*)m = kTc32SpillMark16;
+            else *(int8_t*)m = kTc32SpillMark8;
+        }
     }
     if constexpr (TREE) {
         if (x0 + 32 > w || y0 + 32 > h || tu_leaf(w, h, ta.ctb, ta.plane_id, ta.seed, x0, y0) != 32) return;
@@ -178,7 +196,8 @@ template <bool TREE, bool FIXUP = false>
 __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                    int nbx, int nblk, QuantParams qp, int dq_scale, int dq_per,
                                                    int32_t* lvl, int16_t* recon, TreeArgs ta, uint8_t* tu_log2,
-                                                   const uint32_t* wide_flag = nullptr, uint32_t epoch = 0) {
+                                                   const uint32_t* wide_flag = nullptr, uint32_t epoch = 0,
+                                                   char* mark = nullptr, int mark_bytes = 0) {
     __shared__ int16_t s_orig[4][32][kOP];
     __shared__ int32_t s_dq[4][32][kOP];
     __shared__ int16_t s_top[4][32], s_left[4][32];
@@ -187,7 +206,7 @@ __global__ void __launch_bounds__(256) k_tc32_mfma(const int16_t* __restrict__ s
         if (*wide_flag != epoch) return;   // k_tc32_h left no block of this launch's planes to the fix-up
         for (int b = blockIdx.x * 4 + wv; b < nblk; b += gridDim.x * 4)   // wave-uniform walk
             tc32_block<TREE, true>(src, w, h, pitch, nbx, b, qp, dq_scale, dq_per, lvl, recon, ta, tu_log2, s_orig[wv],
-                                   s_dq[wv], s_top[wv], s_left[wv]);
+                                   s_dq[wv], s_top[wv], s_left[wv], mark, mark_bytes);
     } else {
         const int b = blockIdx.x * 4 + wv;
         if (b >= nblk) return;                       // whole wave exits together
@@ -225,8 +244,8 @@ using namespace nh;
 
 // butterfly variant lives in nh_intraloop.hip; the narrow f16 launch in nh_ctu.hip
 namespace nh {
-int tc32_narrow_launch(const int16_t* src, int32_t* lvl, int16_t* rec, const nh_plane_set& S, const QuantParams& q,
-                       int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s);
+int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* rec, const nh_plane_set& S,
+                       const QuantParams& q, int dqs, int dq_per, uint32_t* wide_flag, uint32_t epoch, hipStream_t s);
 
 // Config 5's wide flags: a ring of words per device, one per f16 launch (slot =
 // epoch mod kFlagRing), so concurrent launches on other streams use other
@@ -270,23 +289,42 @@ extern "C" int nh_tc32_plane(const int16_t* d_src, int w, int h, int pitch, int 
     nh_plane_set one{0, 0, 0, w, h, pitch, 1, 1, 0};
     return nh_tc32_planes(d_src, &one, 1, qp, d_lvl, d_recon, variant, stream);
 }
-extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
-                              int16_t* d_recon, int variant, void* stream) {
+// Config 5 over every plane of the sets.  lvl holds levels of lvl_bytes = 4
+// (int32, every variant) or 2 / 1 (the compact int16 / int8 levels, variant 1
+// only: 8-bit blocks store them directly; a wide block's int32 levels go to
+// `spill` -- same layout as src -- and its compact origin gets the marker, so
+// nh_tc32_levels_widen restores the reference's int32 levels exactly).
+static int tc32_planes_impl(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, void* d_lvl,
+                            int lvl_bytes, int32_t* d_spill, int16_t* d_recon, int variant, void* stream) {
     if (!d_src || !d_lvl || !d_recon || !sets || nsets < 0 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
-    if (((uintptr_t)d_src & 15) || ((uintptr_t)d_lvl & 15) || ((uintptr_t)d_recon & 15)) {
+    if (((uintptr_t)d_src & 15) || ((uintptr_t)d_lvl & 15) || ((uintptr_t)d_recon & 15) || ((uintptr_t)d_spill & 15)) {
         set_error("tc32_planes: buffers must be 16-byte aligned");
         return NH_EARG;
     }
+    if (lvl_bytes != 4 && !(variant == 1 && (lvl_bytes == 2 || lvl_bytes == 1) && d_spill)) {
+        set_error("tc32_planes: compact (int16 / int8) levels need variant 1 and a spill plane");
+        return NH_EARG;
+    }
+    // 16-B level row pieces: rows, planes and groups at 16-B aligned level offsets
+    const int lal = lvl_bytes == 1 ? 15 : 7;
     for (int k = 0; k < nsets; ++k) {
         const nh_plane_set& S = sets[k];
         const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
         if (S.width < 0 || S.height < 0 || S.pitch < S.width || S.planes_per_group < 1 || S.num_groups < 0 ||
-            planes > 65535 || ((S.base | S.plane_stride | S.group_stride | S.pitch) & 7)) {
-            set_error("tc32_planes: plane set must have pitch >= width, 8-element aligned base/pitch/strides");
+            planes > 65535 || ((S.base | S.plane_stride | S.group_stride | S.pitch) & lal)) {
+            set_error(lvl_bytes == 1 ? "tc32_planes: int8 levels need pitch >= width and 16-element aligned "
+                                       "base/pitch/strides"
+                                     : "tc32_planes: plane set must have pitch >= width, 8-element aligned "
+                                       "base/pitch/strides");
             return NH_EARG;
         }
     }
     if (variant < 0 || variant > 2) return NH_EARG;
+    for (int k = 0; k < nsets; ++k)
+        if (sets[k].pitch > kTc32MaxPitch) {
+            set_error("tc32_planes: pitch beyond 2^24 samples (32-bit per-lane offsets, DESIGN.md §4.5)");
+            return NH_EARG;
+        }
     hipStream_t s = as_stream(stream);
     int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
     const int per = q / 6, rem = q % 6;
@@ -298,6 +336,7 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
         int rc = ensure_basis(s);
         if (rc) return rc;
     }
+    int32_t* lvl32 = lvl_bytes == 4 ? (int32_t*)d_lvl : d_spill;   // where the int32 chains write
     for (int k = 0; k < nsets; ++k) {
         const nh_plane_set& S = sets[k];
         const int planes = S.planes_per_group * S.num_groups;
@@ -307,7 +346,7 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
             for (int pz = 0; pz < planes; ++pz) {
                 const int gz = pz / S.planes_per_group, cz = pz - gz * S.planes_per_group;
                 const int64_t off = S.base + (int64_t)gz * S.group_stride + (int64_t)cz * S.plane_stride;
-                int rc = tc32_butterfly(d_src + off, S.width, S.height, S.pitch, qp, d_lvl + off, d_recon + off, s);
+                int rc = tc32_butterfly(d_src + off, S.width, S.height, S.pitch, qp, lvl32 + off, d_recon + off, s);
                 if (rc) return rc;
             }
             continue;
@@ -322,19 +361,88 @@ extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, in
             uint32_t epoch = 0;
             int rc = wide_flag_slot(&flag, &epoch);
             if (rc) return rc;
-            rc = tc32_narrow_launch(d_src, d_lvl, d_recon, S, p, dequant_scale(rem), per, flag, epoch, s);
+            rc = tc32_narrow_launch(d_src, d_lvl, lvl_bytes, d_recon, S, p, dequant_scale(rem), per, flag, epoch, s);
             if (rc) return rc;
             int cus = 0;
             NH_TRY(device_cus(&cus));
             const dim3 gfix((unsigned)std::min<int64_t>((nblk + 3) / 4, 2 * cus), (unsigned)planes);
+            char* mark = lvl_bytes == 4 ? nullptr : (char*)d_lvl + S.base * lvl_bytes;
             k_tc32_mfma<false, true><<<gfix, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
-                                                          dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base,
-                                                          ta, nullptr, flag, epoch);
+                                                          dequant_scale(rem), per, lvl32 + S.base, d_recon + S.base,
+                                                          ta, nullptr, flag, epoch, mark, mark ? lvl_bytes : 0);
         } else {              // int8 matrix cores only (A/B)
             k_tc32_mfma<false><<<grid, 256, lds_cap(k_tc32_mfma<false>, NH_KNOB("NH_CAP_TC32", 0)), s>>>(d_src + S.base, S.width, S.height, S.pitch, nbx, nblk, p,
-                                                    dequant_scale(rem), per, d_lvl + S.base, d_recon + S.base, ta,
+                                                    dequant_scale(rem), per, lvl32 + S.base, d_recon + S.base, ta,
                                                     nullptr);
         }
+        NH_HIP(hipGetLastError());
+    }
+    return NH_OK;
+}
+extern "C" int nh_tc32_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, int32_t* d_lvl,
+                              int16_t* d_recon, int variant, void* stream) {
+    return tc32_planes_impl(d_src, sets, nsets, qp, d_lvl, 4, nullptr, d_recon, variant, stream);
+}
+extern "C" int nh_tc32_planes_compact(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp, void* d_lvl,
+                                      int lvl_bytes, int32_t* d_spill, int16_t* d_recon, void* stream) {
+    if (lvl_bytes != 2 && lvl_bytes != 1) return NH_EARG;
+    return tc32_planes_impl(d_src, sets, nsets, qp, d_lvl, lvl_bytes, d_spill, d_recon, 1, stream);
+}
+
+namespace nh {
+// Compact levels -> the reference's int32 levels: every sample of every full
+// 32x32 block (8 per thread), from the spill plane where the block's compact
+// origin holds the marker, else the compact value widened.  Samples outside
+// full blocks are not written (the int32 path leaves them untouched too).
+template <class LT>
+__global__ void __launch_bounds__(256) k_tc32_widen(const LT* __restrict__ lc, const int32_t* __restrict__ spill,
+                                                    int32_t* __restrict__ out, int64_t base, int64_t group_stride,
+                                                    int64_t plane_stride, int ppg, int fw8, int fh, int pitch) {
+    const LT mk = sizeof(LT) == 2 ? (LT)kTc32SpillMark16 : (LT)kTc32SpillMark8;
+    const int pz = blockIdx.y, gz = pz / ppg, cz = pz - gz * ppg;
+    const int64_t poff = base + (int64_t)gz * group_stride + (int64_t)cz * plane_stride;
+    const int64_t n = (int64_t)fw8 * fh;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int y = (int)(i / fw8), x = 8 * (int)(i - (int64_t)y * fw8);
+        const int64_t o = poff + (int64_t)y * pitch + x;
+        const bool sp = lc[poff + (int64_t)(y & ~31) * pitch + (x & ~31)] == mk;
+        int32_t v[8];
+        if (sp) {
+            const int4 a = *(const int4*)(spill + o), b = *(const int4*)(spill + o + 4);
+            v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = lc[o + e];
+        }
+        *(int4*)(out + o) = make_int4(v[0], v[1], v[2], v[3]);
+        *(int4*)(out + o + 4) = make_int4(v[4], v[5], v[6], v[7]);
+    }
+}
+}  // namespace nh
+
+extern "C" int nh_tc32_levels_widen(const void* d_lvl, int lvl_bytes, const int32_t* d_spill,
+                                    const nh_plane_set* sets, int nsets, int32_t* d_out, void* stream) {
+    if (!d_lvl || !d_spill || !d_out || !sets || nsets < 0 || nsets > NH_MAX_PLANE_SETS) return NH_EARG;
+    if ((lvl_bytes != 2 && lvl_bytes != 1) || (((uintptr_t)d_spill | (uintptr_t)d_out) & 15)) return NH_EARG;
+    hipStream_t s = as_stream(stream);
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& S = sets[k];
+        const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
+        if (S.width < 0 || S.height < 0 || S.pitch < S.width || S.planes_per_group < 1 || S.num_groups < 0 ||
+            planes > 65535 || ((S.base | S.plane_stride | S.group_stride | S.pitch) & 3)) {
+            set_error("tc32_levels_widen: plane set must have pitch >= width, 4-element aligned base/pitch/strides");
+            return NH_EARG;
+        }
+        const int fw8 = (S.width / 32) * 4, fh = (S.height / 32) * 32;
+        if (!fw8 || !fh || !planes) continue;
+        const int64_t items = (int64_t)fw8 * fh;
+        const dim3 grid((unsigned)std::min<int64_t>((items + 255) / 256, 4096), (unsigned)planes);
+        if (lvl_bytes == 2)
+            k_tc32_widen<int16_t><<<grid, 256, 0, s>>>((const int16_t*)d_lvl, d_spill, d_out, S.base, S.group_stride,
+                                                       S.plane_stride, S.planes_per_group, fw8, fh, S.pitch);
+        else
+            k_tc32_widen<int8_t><<<grid, 256, 0, s>>>((const int8_t*)d_lvl, d_spill, d_out, S.base, S.group_stride,
+                                                      S.plane_stride, S.planes_per_group, fw8, fh, S.pitch);
         NH_HIP(hipGetLastError());
     }
     return NH_OK;

@@ -11,6 +11,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
   tc32_plane          -- config 5: 32x32 chain, butterfly or matrix-core variants
   tc32_planes         -- config 5 over a frame stream (one MFMA launch per plane set)
+  tc32_planes_compact / tc32_levels_widen -- config 5 with exact int16 / int8 levels (+ int32 spill)
   tu_pipeline_closed  -- config 4 in closed loop (CTU-row wavefront, TUs in z-order)
   tu_pipeline_closed_yuv420 -- the same over a YUV420 stream, luma and chroma wavefronts concurrent
   widen_u8 / narrow_u8 -- frame I/O casts (YUV420p bytes <-> int16 planes)
@@ -507,6 +508,59 @@ def tc32_planes(src, sets, qp: int = 32, variant: int = 1, lvl=None, rec=None, s
     check(_lib.load().nh_tc32_planes(src.data_ptr(), arr, len(sets), int(qp), lvl.data_ptr(), rec.data_ptr(),
                                      int(variant), C.c_void_p(_stream(stream, src.device))), "tc32_planes")
     return lvl, rec
+
+
+def tc32_planes_compact(src, sets, qp: int = 32, level_dtype=None, lvl=None, rec=None, spill=None, stream=None):
+    """Config 5 (variant 1) with COMPACT levels: int16 (default) or int8 levels in
+    the source layout -- exact, an 8-bit block's 32x32 levels satisfy |level| <= 51
+    at every QP (tools/packed_bounds.py level_bounds) -- 6 / 5 bytes per sample of
+    traffic instead of 8.  A block that is not 8-bit writes its int32 levels into
+    ``spill`` (int32, source layout; allocated uninitialised when None) and the
+    marker -32768 / -128 at its compact origin.  Returns (lvl, rec, spill);
+    ``tc32_levels_widen(lvl, spill, sets)`` gives the int32 levels of
+    ``tc32_planes``."""
+    torch = _torch()
+    _need(src, torch.int16, "tc32_planes_compact(src)")
+    sets_fit(sets, src.numel(), "tc32_planes_compact")
+    dt = level_dtype if level_dtype is not None else (lvl.dtype if lvl is not None else torch.int16)
+    if dt not in (torch.int16, torch.int8):
+        raise TypeError("tc32_planes_compact: level_dtype must be torch.int16 or torch.int8")
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=dt, device=src.device)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    if spill is None:
+        spill = torch.empty(src.shape, dtype=torch.int32, device=src.device)
+    _need(lvl, dt, "tc32_planes_compact(lvl)")
+    _need(rec, torch.int16, "tc32_planes_compact(rec)")
+    _need(spill, torch.int32, "tc32_planes_compact(spill)")
+    if min(lvl.numel(), rec.numel(), spill.numel()) < src.numel():
+        raise ValueError("tc32_planes_compact: lvl / rec / spill smaller than src")
+    arr = (PlaneSet * len(sets))(*sets)
+    check(_lib.load().nh_tc32_planes_compact(src.data_ptr(), arr, len(sets), int(qp), lvl.data_ptr(),
+                                             lvl.element_size(), spill.data_ptr(), rec.data_ptr(),
+                                             C.c_void_p(_stream(stream, src.device))), "tc32_planes_compact")
+    return lvl, rec, spill
+
+
+def tc32_levels_widen(lvl, spill, sets, out=None, stream=None):
+    """(compact levels, spill) of ``tc32_planes_compact`` -> the reference's int32
+    levels at every sample of every full 32x32 block (other samples of ``out``
+    are left as they are: zeros by default, as ``tc32_planes``)."""
+    torch = _torch()
+    if not isinstance(lvl, torch.Tensor) or lvl.dtype not in (torch.int16, torch.int8):
+        raise TypeError("tc32_levels_widen: lvl must be an int16 / int8 device tensor")
+    _need(lvl, lvl.dtype, "tc32_levels_widen(lvl)")
+    _need(spill, torch.int32, "tc32_levels_widen(spill)")
+    if out is None:
+        out = torch.zeros(lvl.shape, dtype=torch.int32, device=lvl.device)
+    _need(out, torch.int32, "tc32_levels_widen(out)")
+    sets_fit(sets, min(lvl.numel(), spill.numel(), out.numel()), "tc32_levels_widen")
+    arr = (PlaneSet * len(sets))(*sets)
+    check(_lib.load().nh_tc32_levels_widen(lvl.data_ptr(), lvl.element_size(), spill.data_ptr(), arr, len(sets),
+                                           out.data_ptr(), C.c_void_p(_stream(stream, lvl.device))),
+          "tc32_levels_widen")
+    return out
 
 
 # ---------------------------------------------------------------------------

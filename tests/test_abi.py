@@ -99,3 +99,21 @@ def test_ab_library_exports_the_same_abi():
     for name in declared_functions():
         assert hasattr(L, name), name
     assert "getenv" in _undefined_symbols(_lib.LIB_AB_PATH)
+
+
+def test_tc32_layout_checks_precede_any_device_call():
+    """nh_tc32_planes / nh_tc32_planes_compact refuse, on the host and before any
+    HIP call, the layouts their kernels' address arithmetic does not cover: pitches
+    beyond 2^24 samples (k_tc32_hd's 32-bit per-lane offsets), int8 levels on rows
+    that are not 16-element aligned, compact levels without a spill plane."""
+    from nano_hevc import _lib
+    from nano_hevc._lib import PlaneSet
+    L = _lib.load()
+    fake = C.c_void_p(1 << 20)   # never dereferenced: the checks return first
+    big = PlaneSet(0, 0, 0, 64, 64, (1 << 24) + 8, 1, 1, 0)
+    assert L.nh_tc32_planes(fake, C.byref(big), 1, 30, fake, fake, 1, None) == _lib.NH_EARG
+    assert b"2^24" in L.nh_last_error()
+    odd = PlaneSet(0, 0, 0, 104, 64, 104, 1, 1, 0)   # 8- but not 16-element aligned rows
+    assert L.nh_tc32_planes_compact(fake, C.byref(odd), 1, 30, fake, 1, fake, fake, None) == _lib.NH_EARG
+    assert L.nh_tc32_planes_compact(fake, C.byref(odd), 1, 30, fake, 2, None, fake, None) == _lib.NH_EARG
+    assert L.nh_tc32_planes_compact(fake, C.byref(odd), 1, 30, fake, 4, fake, fake, None) == _lib.NH_EARG

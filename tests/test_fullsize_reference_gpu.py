@@ -139,6 +139,29 @@ def test_cfg5_8k_luma_equals_reference(ref, torch_dev, variant):
     assert sha(r.cpu().numpy()) == ref["cfg5_y"]["rec"]
 
 
+@pytest.mark.parametrize("ldt", ["int16", "int8"])
+def test_cfg5_8k_yuv420_compact_levels_equal_reference(ref, torch_dev, ldt):
+    """Config 5's compact levels (tc32_planes_compact: int16 / int8 levels, int32
+    spill for blocks that are not 8-bit) over the 8K YUV420 frame, widened back to
+    int32: every plane hashes to the reference's levels and recon."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = [FI.cfg5_plane()] + list(FI.cfg5_chroma())
+    h, w = planes[0].shape
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sets = gpu.yuv420_plane_sets(1, w, h)
+    lc, rec, spill = gpu.tc32_planes_compact(d, sets, FI.CFG5_QP, getattr(torch, ldt))
+    lvl = gpu.tc32_levels_widen(lc, spill, sets).cpu().numpy()
+    rec = rec.cpu().numpy()
+    off = 0
+    for name, p in zip("yuv", planes):
+        ph, pw = p.shape
+        assert sha(lvl[off:off + ph * pw].reshape(ph, pw)) == ref[f"cfg5_{name}"]["lvl"], name
+        assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == ref[f"cfg5_{name}"]["rec"], name
+        off += ph * pw
+
+
 @pytest.mark.parametrize("conc", [False, True])
 def test_cfg4_4k_closed_loop_equals_reference(ref, torch_dev, conc):
     """Config 4 in closed loop on the 4K YUV420 frame, luma and

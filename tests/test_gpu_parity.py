@@ -1092,3 +1092,80 @@ def test_tu_pipeline_closed_small_ctb_vs_oracle(nh, torch_dev, ctb):
     assert np.array_equal(lvl.cpu().numpy().reshape(h, w), el)
     assert np.array_equal(rec.cpu().numpy().reshape(h, w), er)
     assert np.array_equal(tu.cpu().numpy()[0], et)
+
+
+@pytest.mark.parametrize("ldt", ["int16", "int8"])
+def test_tc32_compact_levels_equal_int32_path(nh, torch_dev, ldt):
+    """Config 5 with compact levels (k_tc32_hd<2, int16 / int8>) over a ragged
+    YUV420 stream with wide frames: every 8-bit block's compact level equals the
+    int32 path's, every wide block carries the spill marker at its origin with its
+    int32 levels in the spill plane, and the widened levels equal tc32_planes' (and
+    the oracle's) everywhere; recon identical; outside full blocks untouched."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    dt = getattr(torch, ldt)
+    rng = np.random.default_rng(66)
+    nf, w, h = 3, 224, 136                       # chroma pitch 112: 16-element aligned (int8 rows)
+    sets = gpu.yuv420_plane_sets(nf, w, h)
+    fe = gpu.yuv420_frame_elems(w, h)
+    buf = rng.integers(0, 256, size=nf * fe).astype(np.int16)
+    buf[fe:2 * fe] = rng.integers(-32768, 32768, size=fe)   # frame 1: every block wide
+    buf[2 * fe + 5 * w + 40] = 300                          # frame 2: one wide luma block
+    buf[2 * fe + w * h + 3 * (w // 2) + 70] = -1            # ... and one wide U block
+    d = torch.from_numpy(buf).cuda()
+    for qp in (0, 4, 30, 51):
+        lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+        rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+        gpu.tc32_planes(d, sets, qp, 1, lvl=lvl, rec=rec)
+        lc = torch.full(d.shape, 5, dtype=dt, device="cuda")
+        rc = torch.full(d.shape, -7, dtype=torch.int16, device="cuda")
+        lc, rc, spill = gpu.tc32_planes_compact(d, sets, qp, dt, lvl=lc, rec=rc)
+        out = torch.full(d.shape, -9, dtype=torch.int32, device="cuda")
+        wide = gpu.tc32_levels_widen(lc, spill, sets, out=out)
+        lv, rv, cv, wv, wr = (lvl.cpu().numpy(), rec.cpu().numpy(), lc.cpu().numpy(), wide.cpu().numpy(),
+                              rc.cpu().numpy())
+        mark = -32768 if ldt == "int16" else -128
+        for f in range(nf):
+            off = f * fe
+            for (ph, pw) in ((h, w), (h // 2, w // 2), (h // 2, w // 2)):
+                fh, fw = ph // 32 * 32, pw // 32 * 32
+                src = buf[off:off + ph * pw].reshape(ph, pw)
+                L, R = lv[off:off + ph * pw].reshape(ph, pw), rv[off:off + ph * pw].reshape(ph, pw)
+                Cc, Wd = cv[off:off + ph * pw].reshape(ph, pw), wv[off:off + ph * pw].reshape(ph, pw)
+                Rc = wr[off:off + ph * pw].reshape(ph, pw)
+                assert np.array_equal(Wd[:fh, :fw], L[:fh, :fw]), (qp, f, ph)
+                assert np.array_equal(Rc[:fh, :fw], R[:fh, :fw]), (qp, f, ph)
+                assert (Wd[fh:, :] == -9).all() and (Wd[:, fw:] == -9).all()
+                assert (Cc[fh:, :] == 5).all() and (Cc[:, fw:] == 5).all()
+                for by in range(0, fh, 32):
+                    for bx in range(0, fw, 32):
+                        parts = [src[by:by + 32, bx:bx + 32].ravel()]   # the block, the row above, the column left
+                        if by:
+                            parts.append(src[by - 1, bx:bx + 32])
+                        if bx:
+                            parts.append(src[by:by + 32, bx - 1])
+                        blk = np.concatenate(parts)
+                        narrow = blk.min() >= 0 and blk.max() <= 255
+                        if narrow:
+                            assert np.array_equal(Cc[by:by + 32, bx:bx + 32], L[by:by + 32, bx:bx + 32]), (qp, f, by, bx)
+                            assert np.abs(L[by:by + 32, bx:bx + 32]).max() <= 51
+                        else:
+                            assert Cc[by, bx] == mark, (qp, f, by, bx)
+                if f == 2 and ph == h:
+                    el, er = O.tc32_plane(src, qp)
+                    assert np.array_equal(Wd[:fh, :fw], el[:fh, :fw]) and np.array_equal(Rc[:fh, :fw], er[:fh, :fw])
+                off += ph * pw
+
+
+def test_tc32_compact_levels_refuse_bad_layouts(nh, torch_dev):
+    """int8 levels need 16-element aligned rows and planes; only variant 1 has
+    compact levels (tc32_planes keeps int32)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    d = torch.zeros(3 * gpu.yuv420_frame_elems(208, 136), dtype=torch.int16, device="cuda")
+    sets = gpu.yuv420_plane_sets(3, 208, 136)     # chroma pitch 104: 8- but not 16-element aligned
+    with pytest.raises(ValueError):
+        gpu.tc32_planes_compact(d, sets, 30, torch.int8)
+    gpu.tc32_planes_compact(d, sets, 30, torch.int16)
+    with pytest.raises(TypeError):
+        gpu.tc32_planes_compact(d, sets, 30, torch.int32)

@@ -34,25 +34,30 @@ def product():
     return ic.load(ic.LIB)
 
 
-def test_tc32hd_dma_waits_match_the_code(product):
+@pytest.mark.parametrize("levels", sorted(ic.TC32HD_LEVELS))
+def test_tc32hd_dma_waits_match_the_code(product, levels):
+    """Every level type's instance (int32, and the compact int16 / int8 levels)."""
     funcs, _ = product
-    s = ic.check_dma_waits(funcs[ic.TC32HD])
+    name, narrow = ic.TC32HD_LEVELS[levels]
+    s = ic.check_dma_waits(funcs[name])
     # both block kinds reached a wait, with exactly the counted stores behind them
-    assert s["stores_per_segment"] == [2, 6], s
+    assert s["stores_per_segment"] == [2, narrow], s
     assert {0, 4}.issubset(s["wait_imms"]) and s["block_waits"] >= 3, s
 
 
 @pytest.mark.parametrize("define", ["NH_TC32HD_STORES_NARROW=7", "NH_TC32HD_STORES_NARROW=5",
                                     "NH_TC32HD_STORES_WIDE=1"])
 def test_tc32hd_miscounted_constant_is_caught(define):
-    """The same kernel built with a wrong store count (UNSAFE for an over-count:
-    the wait leaves the block's DMA in flight; LOOSE for an under-count)."""
+    """The same kernels built with a wrong store count (UNSAFE for an over-count:
+    the wait leaves the block's DMA in flight; LOOSE for an under-count) -- every
+    level type's instance."""
     src = os.path.join(ROOT, "nano-hevc_amd", "csrc", "nh_ctu.hip")
     with tempfile.TemporaryDirectory() as d:
         elf = ic.compile_device(src, os.path.join(d, "ctu.o"), [define])
         funcs = ic.disassemble(elf)
-    with pytest.raises(ic.DmaModelError):
-        ic.check_dma_waits(funcs[ic.TC32HD])
+    for name, _ in ic.TC32HD_LEVELS.values():
+        with pytest.raises(ic.DmaModelError):
+            ic.check_dma_waits(funcs[name])
 
 
 def test_mfma_results_read_by_inline_asm_wait(product):
@@ -100,3 +105,19 @@ def test_no_bitcast_of_a_vector_element():
             f.write("const float c2 = __builtin_bit_cast(float, mw1.y);\n"
                     "const float ok = __uint_as_float((uint32_t)mw1.y);\n")
         assert len(ic.bitcast_element_uses([p])) == 1
+
+
+def test_no_readfirstlane_widened_to_64_bits():
+    """readfirstlane returns int: (uint64_t)readfirstlane(lo) sign-extends an address
+    word with bit 31 set (the round-5 illegal address in k_tc32_hd's SGPR-base
+    pointers).  Every such widening goes through uint32_t."""
+    import glob
+    srcs = glob.glob(os.path.join(ROOT, "nano-hevc_amd", "csrc", "*.hip")) + \
+        glob.glob(os.path.join(ROOT, "nano-hevc_amd", "csrc", "*.hpp"))
+    assert not ic.readfirstlane_widen_uses(srcs)
+    with tempfile.TemporaryDirectory() as d:   # the lint itself
+        p = os.path.join(d, "x.hpp")
+        with open(p, "w") as f:
+            f.write("return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)v) | hi;\n"
+                    "return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v) | hi;\n")
+        assert len(ic.readfirstlane_widen_uses([p])) == 1

@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--cfg5-frames", type=int, default=8, help="frames of the batched cfg5 stream")
+    ap.add_argument("--cfg5-levels", default="int32,int16,int8", help="5b: level dtypes (int16 / int8: compact levels)")
     ap.add_argument("--closed4-frames", type=int, default=64, help="frames of the closed-loop cfg4 stream")
     ap.add_argument("--closed4-seq", action="store_true", help="closed4: luma then chroma (default: concurrent wavefronts)")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
@@ -265,19 +266,37 @@ def main():
         stream5 = torch.cat([torch.cat([synth_plane(H, W, 7 + 3 * f).flatten(), synth_plane(H // 2, W // 2, 8 + 3 * f).flatten(),
                                         synth_plane(H // 2, W // 2, 9 + 3 * f).flatten()]) for f in range(nf)])
         sets5 = gpu.yuv420_plane_sets(nf, W, H)
-        lv5 = torch.zeros_like(stream5, dtype=torch.int32)
         rc5 = torch.zeros_like(stream5)
-        ms = timed(lambda: gpu.tc32_planes(stream5, sets5, args.qp5, 1, lvl=lv5, rec=rc5), args.reps)
         nblk = nf * sum((h // 32) * (w // 32) for w, h in ((W, H), (W // 2, H // 2), (W // 2, H // 2)))
-        print(json.dumps({"config": "cfg5 batched: 8K YUV420 frame stream, f16 MFMA launch + int8 fix-up per plane set",
-                          "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "blocks_per_s": nblk / ms * 1e3,
-                          "samples_per_s": nf * fe / ms * 1e3, "bytes_per_sample": 8,
-                          "achieved_GBps": nf * fe * 8 / ms / 1e6, "psnr_y_frame0": psnr_dev(stream5[:W * H], rc5[:W * H]),
-                          "knobs": knobs, "roofline": valu_roofline("cfg5_8k_yuv420", ms / nf),
-                          "out_digest": [int(lv5.to(torch.int64).sum().item()), int(rc5.to(torch.int64).sum().item()),
-                                         int((lv5.to(torch.int64) * torch.arange(lv5.numel(), device="cuda") % 1000003)
-                                             .sum().item())]}),
-              flush=True)
+        spill = None
+        for ldt in args.cfg5_levels.split(","):
+            # int32: the reference's level dtype; int16 / int8: the exact compact levels (|level| <= 51 for an
+            # 8-bit 32x32 block) plus the int32 spill plane, widened afterwards for the digest
+            dt = getattr(torch, ldt)
+            lv = torch.zeros_like(stream5, dtype=dt)
+            if ldt == "int32":
+                ms = timed(lambda: gpu.tc32_planes(stream5, sets5, args.qp5, 1, lvl=lv, rec=rc5), args.reps)
+                lv5 = lv
+            else:
+                if spill is None:
+                    spill = torch.empty_like(stream5, dtype=torch.int32)
+                ms = timed(lambda: gpu.tc32_planes_compact(stream5, sets5, args.qp5, dt, lvl=lv, rec=rc5, spill=spill),
+                           args.reps)
+                lv5 = gpu.tc32_levels_widen(lv, spill, sets5)
+            bps = 4 + lv.element_size()
+            key = "cfg5_8k_yuv420" if ldt == "int32" else "cfg5_8k_yuv420_" + ldt
+            print(json.dumps({"config": "cfg5 batched: 8K YUV420 frame stream, f16 MFMA launch + int8 fix-up per plane set",
+                              "levels": ldt, "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
+                              "blocks_per_s": nblk / ms * 1e3,
+                              "samples_per_s": nf * fe / ms * 1e3, "bytes_per_sample": bps,
+                              "achieved_GBps": nf * fe * bps / ms / 1e6,
+                              "psnr_y_frame0": psnr_dev(stream5[:W * H], rc5[:W * H]),
+                              "knobs": knobs, "roofline": valu_roofline(key, ms / nf),
+                              "out_digest": [int(lv5.to(torch.int64).sum().item()), int(rc5.to(torch.int64).sum().item()),
+                                             int((lv5.to(torch.int64) * torch.arange(lv5.numel(), device="cuda") % 1000003)
+                                                 .sum().item())]}),
+                  flush=True)
+            del lv, lv5
 
     if 5 in cfgs:
         W, H = 7680, 4320

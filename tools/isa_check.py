@@ -45,7 +45,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "nano-hevc_amd", "nano_hevc", "libnanohevc.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 TRIPLE = "hipv4-amdgcn-amd-amdhsa--gfx950"
-TC32HD = "_ZN2nh9k_tc32_hdILi2EEEvNS_7CtuArgsEi"
+TC32HD = "_ZN2nh9k_tc32_hdILi2EiEEvNS_7CtuArgsEi"          # k_tc32_hd<2, int32_t>: int32 levels
+# the three level types and the store instructions a narrow block issues (4 / 2 / 1 level rows + 2 recon)
+TC32HD_LEVELS = {"int32": (TC32HD, 6), "int16": ("_ZN2nh9k_tc32_hdILi2EsEEvNS_7CtuArgsEi", 4),
+                 "int8": ("_ZN2nh9k_tc32_hdILi2EaEEvNS_7CtuArgsEi", 3)}
 
 
 # ---------------------------------------------------------------------------
@@ -530,13 +533,33 @@ def bitcast_element_uses(paths) -> list[str]:
     return hits
 
 
+# readfirstlane returns int: widening its result straight to 64 bits sign-extends a low address word
+# with bit 31 set, so a pointer rebuilt from two readfirstlanes (sgpr_ptr, nh_ldsdma.hpp) got an all-ones
+# high word -- the round-5 hipErrorIllegalAddress in k_tc32_hd, seen only for buffers whose address had
+# bit 31 set; widen through uint32_t
+RFL_WIDEN = re.compile(r"\(\s*(?:u?int64_t|uintptr_t|intptr_t|size_t|(?:unsigned\s+)?long(?:\s+long)?)\s*\)"
+                       r"\s*__builtin_amdgcn_readfirstlane\b")
+
+
+def readfirstlane_widen_uses(paths) -> list[str]:
+    hits = []
+    for p in paths:
+        with open(p) as f:
+            for n, line in enumerate(f, 1):
+                code = line.split("//", 1)[0]
+                if RFL_WIDEN.search(code):
+                    hits.append(f"{p}:{n}: {line.strip()}")
+    return hits
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=LIB)
     a = ap.parse_args()
     funcs, meta = load(a.lib)
-    s = check_dma_waits(funcs[TC32HD])
-    print("k_tc32_hd<2>:", s)
+    for lv, (name, narrow) in sorted(TC32HD_LEVELS.items()):
+        s = check_dma_waits(funcs[name])
+        print(f"k_tc32_hd<2, {lv}> (narrow block: {narrow} stores):", s)
     print("MFMA results read by inline asm, checked:", check_mfma_hazard(funcs))
     ps = private_segment_sizes(meta)
     print("scratch:", {k: v for k, v in ps.items() if v}, "of", len(ps), "kernels")

@@ -106,6 +106,7 @@ def main():
     assert max(ops.values()) < 2048 and max(sums.values()) < 2 ** 24
     assert all(int(r) == 0 for r in rs[1:]) and int(rs[0]) == 2048
     mosaic_bounds()
+    level_bounds()
 
 
 def mosaic_bounds():
@@ -114,8 +115,13 @@ def mosaic_bounds():
     stay below 2^24 (exact fp32), every f16 operand an exact integer: the residual as
     768 + n (|n| <= 255, binade [512, 1024)), the pass-1 output as 1536 + t in
     [1024, 2048) (|t| <= 511: truncation = floor), the dequantized coefficients and
-    the inverse-pass-1 output below 2048.  DCT4 (chroma 4x4) is printed to show why
-    it stays on the packed chain."""
+    the inverse-pass-1 output below 2048 -- except DCT4 (chroma 4x4), whose inverse
+    pass 1 reaches 2223: its inverse pass 2 runs split (nh_mosaic.hpp MosaicCore::
+    SPLIT), tmp = 2h + b with h = floor(tmp / 2) against the basis * 2^-(S-1) and
+    b in {0, 1} against the basis * 2^-S, two MFMAs into one accumulator that starts
+    at 1536.5.  Its bounds: |h| <= 1112 (an exact f16 integer), every partial sum of
+    the two MFMAs (units 2^-S) <= (|tmp| + 1) * colL1 + 1536.5 * 2^S < 2^24, and the
+    16-bit dequantization l * dqs + dqr < 2^15."""
     print("mosaic    pass1-out  pass2 op  coeff   dq  inv1-out  |sum| max (units 2^-S)  ok")
     for n, dst in ((4, True), (8, False), (16, False), (4, False)):
         T = mat(n, dst)
@@ -135,16 +141,43 @@ def mosaic_bounds():
                 rl1 * (1536 + f1) + int(c2 * 2 ** s),
                 dq * cl1 + 2 ** (s - 1),
                 i1 * cl1 + int(1536.5 * 2 ** s)]
-        ok = f1 <= 511 and 1536 + f1 < 2048 and dq < 2048 and i1 <= 2048 and max(sums) < 2 ** 24
-        print("%-8s %9d %9d %6d %4d %9d %23d  %s" % (("DST" if dst else "DCT") + str(n), f1, 1536 + f1, c, dq, i1,
-                                                      max(sums), ok))
+        split = (n, dst) == (4, False)
+        if split:   # inverse pass 2 on (h, b): tmp = 2h + b, so 2|h| <= |tmp| + 1
+            h = (i1 + 1) // 2
+            sums[3] = (i1 + 1) * cl1 + int(1536.5 * 2 ** s)
+            inv_ok = h <= 2048 and 2 * h + 1 >= i1   # h exact in f16; tmp's range covered
+        else:
+            inv_ok = i1 <= 2048
+        ok = f1 <= 511 and 1536 + f1 < 2048 and dq < 2048 and inv_ok and max(sums) < 2 ** 24
+        print("%-8s %9d %9d %6d %4d %9d %23d  %s%s" % (("DST" if dst else "DCT") + str(n), f1, 1536 + f1, c, dq, i1,
+                                                        max(sums), ok, "  (split: |h| <= %d)" % h if split else ""))
         # dequantize in 16-bit lanes: (l * dqs + dqr) >> dqsh with dqs = DQ << max(per - 4, 0)
         ldq = max(quant(c, qp, l2, intra) * (DQ[qp % 6] << max(qp // 6 - 4, 0)) + (1 << 3)
                   for qp in range(52) for intra in (True, False))
         ok = ok and ldq < 2 ** 15
-        if (n, dst) != (4, False):
-            assert ok, (n, dst, ldq)
+        assert ok, (n, dst, ldq)
         assert i2 < 1 << 15
+
+
+def level_bounds():
+    """The largest |level| quantize_block gives an 8-bit block (residual in
+    [-255, 255]) of every kind, over QP 0..51 and both rounding offsets.  Config
+    5's compact levels (k_tc32_hd<KB, int16 / int8>) rest on the
+    32x32 bound: <= 51, so int8 holds every 8-bit block's level, and the marker
+    values -128 / -32768 (a wide block's levels are in the spill plane) never
+    occur as a level.  Returns {kind: bound}."""
+    out = {}
+    for n, dst in ((4, True), (4, False), (8, False), (16, False), (32, False)):
+        T = mat(n, dst)
+        l2 = int(np.log2(n))
+        s = l2 + 5
+        rl1 = int(np.abs(T).sum(1).max())
+        c = shift_bound(shift_bound(255 * rl1, s) * rl1, s)
+        out[("DST" if dst else "DCT") + str(n)] = max(quant(c, qp, l2, intra) for qp in range(52)
+                                                      for intra in (True, False))
+    print("largest |level| of an 8-bit block:", out)
+    assert out["DCT32"] <= 51 < 127
+    return out
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Static instruction mix of the product kernels, and their attainable VALU rate.
 
-    python tools/valu_mix.py [--rates profiles/r03/valu_rate.jsonl] [--json out.json] [--kernels REGEX]
+    python tools/valu_mix.py [--rates profiles/r05/valu/valu_rate_r05w.jsonl] [--json out.json] [--kernels REGEX]
 
 1. Compiles every nano-hevc_amd/csrc/*.hip for gfx950 with the product flags
    (device code only, unbundled ELF) and disassembles it (llvm-objdump).
