@@ -171,6 +171,15 @@ def cpu_model() -> str:
     return "unknown"
 
 
+# The reference's own numpy path (quantize_block(forward_transform(block), 32) per 8x8 block), timed
+# by the survey in the BUILD container: the reference cannot travel to the
+# GPU box, so this is a different host's figure, reported beside the box's own C-port legs.
+REFERENCE_NUMPY_CFG2 = {"value": 3102.0, "unit": "blocks/s", "cores": 1, "kind": "reference",
+                        "host": "build container (8-vCPU Xeon), not the GPU box",
+                        "sample": "reference nano_hevc.transform.forward_transform + quant.quantize_block, "
+                                  "322 us per 8x8 block at QP 32 (SURVEY.md §6)"}
+
+
 def cpu_baseline(gpu_out, res, fe: int, frames: int, qp: int, budget_s: float):
     """Time the oracle (CPU restatement) on whole 4K YUV420 frames: first 1
     thread, then all of the job's host threads, each for
@@ -206,7 +215,8 @@ def cpu_baseline(gpu_out, res, fe: int, frames: int, qp: int, budget_s: float):
                       f"fwd8x8_quant_plane_mt on {nthr} threads ({tn:.1f} s); single thread: {f1} frames, "
                       f"{b1} blocks, {t1:.1f} s",
             "value_1thread": v1, "cpu_model": cpu_model(), "nproc_machine": os.cpu_count(),
-            "gpu_levels_bit_exact_on_sample": exact}
+            "gpu_levels_bit_exact_on_sample": exact,
+            "reference_numpy": REFERENCE_NUMPY_CFG2}
 
 
 def load_traffic(cfg_key: str):
@@ -383,7 +393,9 @@ def run_cfg2(args, dist, world, rank, dev):
         gpu.fwd8x8_quant(res, sets, args.qp, True, out=outs[slot], variant=args.variant, stream=stream)
 
     elapsed, kern_ms = timed_steps(lambda: step_into(0), args.steps, args.warmup, dist, stream)
-    (elapsed, kern_ms), (blocks_all,) = reduce_max_sum(dist, dev, (elapsed, kern_ms), (nblk,))
+    # compute only: each rank's blocks over its own device time, summed over ranks
+    (elapsed, kern_ms), (blocks_all, rate_sum) = reduce_max_sum(dist, dev, (elapsed, kern_ms),
+                                                                (nblk, nblk / (kern_ms * 1e-3)))
     value = blocks_all * args.steps / elapsed
 
     gather = None
@@ -436,6 +448,9 @@ def run_cfg2(args, dist, world, rank, dev):
                                     "input bytes into its output buffer (read + write counted)",
                      "torch_copy_GBps": torch_copy_gbs},
         "cpu_baseline": None,
+        "compute_only_sum_blocks_per_s": rate_sum,
+        "compute_only_note": "sum over ranks of blocks per step / that rank's mean HIP-event time per step "
+                             "(device time only: no barrier, no gather); `value` is the wall-clock whole-job rate",
     }
     if gather:
         line["gather_inclusive"] = gather
@@ -578,8 +593,9 @@ def run_cfg4(args, dist, world, rank, dev):
 
     elapsed, kern_ms = timed_steps(lambda: step_into(0), args.steps, args.warmup, dist, stream)
     my_samples = me.packed_elems
-    (elapsed, kern_ms), sums = reduce_max_sum(dist, dev, (elapsed, kern_ms), [my_samples] + me.tu_counts())
-    samples_all, tu_all = sums[0], sums[1:]
+    (elapsed, kern_ms), sums = reduce_max_sum(dist, dev, (elapsed, kern_ms),
+                                              [my_samples, my_samples / (kern_ms * 1e-3)] + me.tu_counts())
+    samples_all, rate_sum, tu_all = sums[0], sums[1], sums[2:]
     value = samples_all * args.steps / elapsed
 
     sizes = [shard.cfg4_packed_elems(r, world, nf, W, H) for r in range(world)]
@@ -628,6 +644,9 @@ def run_cfg4(args, dist, world, rank, dev):
                    "tu_blocks_per_s": {f"{4 << k}x{4 << k}": tu_all[k] * args.steps / elapsed for k in range(4)}},
         "roofline": cfg4_roofline(my_samples, kern_ms, args.frames, world),
         "cpu_baseline": None,
+        "compute_only_sum_samples_per_s": rate_sum,
+        "compute_only_note": "sum over ranks of samples per step / that rank's mean HIP-event time per step "
+                             "(device time only: no barrier, no gather); `value` is the wall-clock whole-job rate",
     }
     if gather:
         line["gather_inclusive"] = gather

@@ -1399,18 +1399,23 @@ constexpr int kTc32hdStoresNarrow = NH_TC32HD_STORES_NARROW;   // chain32_tf, in
 constexpr int kTc32hdStoresWide = NH_TC32HD_STORES_WIDE;       // the wide mark and the wide flag (never null here)
 // LT: the level element type (LvlTile): int16 / int8 levels take 2 / 1 level-row stores instead of 4
 template <class LT> constexpr int tc32hd_stores_narrow() { return kTc32hdStoresNarrow - 4 + LvlTile<LT>::STORES; }
-template <int KB, class LT = int32_t>
+// ILV: wave w of workgroup g codes blocks 4 KB g + w + 4 k (k < KB), so the 4 waves work on 4
+// horizontally adjacent blocks at a time (their row pieces form 4x longer contiguous runs in HBM);
+// otherwise blocks KB (4 g + w) + k.
+template <int KB, class LT = int32_t, bool ILV = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_tc32_hd(CtuArgs a, int nblk) {
     constexpr int kNarrow = tc32hd_stores_narrow<LT>();
     static_assert(kNarrow > 0, "store count");   // (equal to the wide count: one wait serves both kinds)
     __shared__ __attribute__((aligned(16))) int16_t s_body[4][2][32 * 32];
     __shared__ __attribute__((aligned(16))) int16_t s_edge[4][2][96];
     __shared__ BasisHC s_basis;
-    __shared__ __attribute__((aligned(16))) int32_t s_out[4][32 * kOutP];
+    // the level / recon tile: int32 level rows (kOutP), else the recon tile's kRecP (compact levels fit in it)
+    __shared__ __attribute__((aligned(16))) int32_t s_out[4][32 * (sizeof(LT) == 4 ? kOutP : kRecP)];
     // the wave index in an SGPR: block index, `next` and the loop are scalar
     // branches, so one wave never runs both sides of a block's wait selection
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int b0 = ((int)blockIdx.x * 4 + wv) * KB, pz = (int)blockIdx.y;
+    constexpr int BS = ILV ? 4 : 1;   // block stride of a wave
+    const int b0 = ILV ? (int)blockIdx.x * 4 * KB + wv : ((int)blockIdx.x * 4 + wv) * KB, pz = (int)blockIdx.y;
     const int64_t poff = plane_off(a, pz);
     const int16_t* src = a.src + poff;
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
@@ -1432,13 +1437,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     issue(b0, 0);
     int prev = 0;   // store instructions the previous block issued (0: none, kTc32hdStoresWide, kNarrow)
     for (int k = 0; k < KB; ++k) {
-        const int b = b0 + k;
+        const int b = b0 + BS * k;
         if (b >= nblk) break;
         const int slot = k & 1;
-        const bool next = k + 1 < KB && b + 1 < nblk;
+        const bool next = k + 1 < KB && b + BS < nblk;
         if (next) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // WAR on the slot block k+1 overwrites
-            issue(b + 1, slot ^ 1);
+            issue(b + BS, slot ^ 1);
         }
         // retire block b's DMA: it was issued before the previous block's stores and block b+1's DMA
         if (next) {
@@ -1666,9 +1671,11 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
     // NH_TC32H_CAP = workgroups per CU, NH_TC32H_K = k_tc32_h blocks per wave (2 / 4),
     // NH_TC32H_FORM = 1 XCD-ordered grid, 3 the same with whole-row stores,
     // 4 row-piece stores from registers (the round-2 form), NH_TC32H_BREG = bases in registers.
-    static const int cap = NH_KNOB("NH_TC32H_CAP", 3);
-    auto launch = [&](auto kern, int K) {
-        kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, cap), s>>>(a, nblk);
+    static const int cap = NH_KNOB("NH_TC32H_CAP", 3), cap_c = NH_KNOB("NH_TC32H_CAP_C", 3);
+    static const int ilv = NH_KNOB("NH_TC32H_ILV", 0);   // A/B: 1 = interleaved block order (k_tc32_hd ILV)
+    (void)ilv;
+    auto launch = [&](auto kern, int K, int wgs) {
+        kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, wgs), s>>>(a, nblk);
     };
     // two blocks per wave, the second's image by LDS-DMA under the first's chain (k_tc32_hd<2>):
     // 0.0966-0.0976 vs 0.0982-0.0983 ms per 8K YUV420 frame for one block per wave loading its
@@ -1681,25 +1688,47 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
         return NH_EARG;
     }
     if (!NH_AB || dma == 2 || lvl_bytes != 4) {
-        if (lvl_bytes == 4) launch(k_tc32_hd<2>, 2);
-        else if (lvl_bytes == 2) launch(k_tc32_hd<2, int16_t>, 2);
-        else launch(k_tc32_hd<2, int8_t>, 2);
+        // compact levels: a 3-KB tile per wave (34 KB per workgroup), so the A/B knob NH_TC32H_CAP_C
+        // may also allow 4 resident workgroups per CU
+        bool done = false;
+#if NH_AB
+        {
+          if (ilv || dma == 4) {   // A/B: interleaved order and / or 4 blocks per wave
+            done = true;
+            auto by_lt = [&](auto kb_c, auto ilv_c) {
+                constexpr int K = decltype(kb_c)::value;
+                constexpr bool I = decltype(ilv_c)::value;
+                if (lvl_bytes == 4) launch(k_tc32_hd<K, int32_t, I>, K, cap);
+                else if (lvl_bytes == 2) launch(k_tc32_hd<K, int16_t, I>, K, cap_c);
+                else launch(k_tc32_hd<K, int8_t, I>, K, cap_c);
+            };
+            using K2 = std::integral_constant<int, 2>;
+            using K4 = std::integral_constant<int, 4>;
+            if (dma == 4) ilv ? by_lt(K4{}, std::true_type{}) : by_lt(K4{}, std::false_type{});
+            else by_lt(K2{}, std::true_type{});
+          }
+        }
+#endif
+        if (done) {
+        } else if (lvl_bytes == 4) launch(k_tc32_hd<2>, 2, cap);
+        else if (lvl_bytes == 2) launch(k_tc32_hd<2, int16_t>, 2, cap_c);
+        else launch(k_tc32_hd<2, int8_t>, 2, cap_c);
         NH_HIP(hipGetLastError());
         return NH_OK;
     }
 #if NH_AB
     static const int kk = NH_KNOB("NH_TC32H_K", 1), form = NH_KNOB("NH_TC32H_FORM", 0);
-    if (dma == 4) launch(k_tc32_hd<4>, 4);
-    else if (dma == 8) launch(k_tc32_hd<8>, 8);
-    else if (kk == 2) launch(k_tc32_h<2, false, true>, 2);
-    else if (kk == 4) launch(k_tc32_h<4, false, true>, 4);
-    else if (form == 1) launch(k_tc32_h<1, true, false>, 1);
-    else if (form == 4) launch(k_tc32_h<1, false, false>, 1);
-    else if (form == 3) launch(k_tc32_h<1, true, true>, 1);
+    if (dma == 4) launch(k_tc32_hd<4>, 4, cap);
+    else if (dma == 8) launch(k_tc32_hd<8>, 8, cap);
+    else if (kk == 2) launch(k_tc32_h<2, false, true>, 2, cap);
+    else if (kk == 4) launch(k_tc32_h<4, false, true>, 4, cap);
+    else if (form == 1) launch(k_tc32_h<1, true, false>, 1, cap);
+    else if (form == 4) launch(k_tc32_h<1, false, false>, 1, cap);
+    else if (form == 3) launch(k_tc32_h<1, true, true>, 1, cap);
     // whole-row output stores: 0.106 vs 0.125 ms per 8K YUV420 frame (forms 2 vs 0 of
     // profiles/r03/cfg5/ab_tc32h_forms.jsonl; the XCD-ordered grid is slower, 0.132)
-    else if (NH_KNOB("NH_TC32H_BREG", 0)) launch(k_tc32_h<1, false, true, true>, 1);
-    else launch(k_tc32_h<1, false, true>, 1);
+    else if (NH_KNOB("NH_TC32H_BREG", 0)) launch(k_tc32_h<1, false, true, true>, 1, cap);
+    else launch(k_tc32_h<1, false, true>, 1, cap);
 #endif
     NH_HIP(hipGetLastError());
     return NH_OK;

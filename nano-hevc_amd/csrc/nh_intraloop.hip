@@ -8,6 +8,7 @@
 // (the test-side CPU restatement, oh_intra_rdo_plane / oh_tu_pipeline_plane) and the golden
 // planes generated from the reference functions pin them.
 #include <hip/hip_runtime.h>
+#include <mutex>
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -3013,14 +3014,49 @@ extern "C" int nh_intra_rdo_planes_closed(const int16_t* d_src, const nh_plane_s
     return NH_OK;
 }
 
+// The status word lands in a pinned host slot: a direct DMA, not the staged copy of a pageable
+// destination (the call sits inside every timed closed-loop launch set).  One process-wide pinned
+// page of kStatusSlots slots, allocated once and kept for the process (a per-thread
+// allocation was never freed); a call holds one slot for its copy + synchronize; when every slot is
+// held by a concurrent call it copies into pageable memory instead (same result, slower).
+namespace {
+constexpr int kStatusSlots = 64;
+std::mutex g_status_mu;
+int32_t* g_status_page = nullptr;
+uint64_t g_status_used = 0;
+int status_slot_acquire() {
+    std::lock_guard<std::mutex> lk(g_status_mu);
+    if (!g_status_page && hipHostMalloc((void**)&g_status_page, kStatusSlots * 64, hipHostMallocDefault) != hipSuccess) {
+        g_status_page = nullptr;
+        return -1;
+    }
+    if (g_status_used == ~0ull) return -1;
+    const int k = __builtin_ctzll(~g_status_used);
+    g_status_used |= 1ull << k;
+    return k;
+}
+void status_slot_release(int k) {
+    std::lock_guard<std::mutex> lk(g_status_mu);
+    g_status_used &= ~(1ull << k);
+}
+}  // namespace
+
 extern "C" int nh_intra_rdo_closed_status(const void* d_work, int* status, void* stream) {
     if (!d_work || !status) return NH_EARG;
-    // the word lands in a per-thread pinned slot: a direct DMA, not the staged copy of a pageable
-    // destination (the call sits inside every timed closed-loop launch set)
-    static thread_local int32_t* pinned = nullptr;
-    if (!pinned) NH_HIP(hipHostMalloc((void**)&pinned, 64, hipHostMallocDefault));
-    NH_HIP(hipMemcpyAsync(pinned, (const int32_t*)d_work + 1, 4, hipMemcpyDeviceToHost, as_stream(stream)));
-    NH_HIP(hipStreamSynchronize(as_stream(stream)));
-    *status = *(volatile int32_t*)pinned;
+    hipStream_t s = as_stream(stream);
+    const int k = status_slot_acquire();
+    if (k < 0) {   // no free pinned slot: a pageable copy (hipMemcpyAsync then synchronizes the stream)
+        int32_t v = 0;
+        NH_HIP(hipMemcpyAsync(&v, (const int32_t*)d_work + 1, 4, hipMemcpyDeviceToHost, s));
+        NH_HIP(hipStreamSynchronize(s));
+        *status = v;
+        return NH_OK;
+    }
+    int32_t* pinned = g_status_page + 16 * k;   // 64-B slots
+    hipError_t e = hipMemcpyAsync(pinned, (const int32_t*)d_work + 1, 4, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) *status = *(volatile int32_t*)pinned;
+    status_slot_release(k);
+    NH_HIP(e);
     return NH_OK;
 }

@@ -646,13 +646,14 @@ def encode_intra_planes(src, sets: Sequence[PlaneSet], block_sizes: Sequence[int
     bsz = (C.c_int32 * len(sets))(*[int(b) for b in block_sizes])
     wide = src.dtype == torch.int16 and any(int(b) & (int(b) - 1) or int(b) < 4 or int(b) > 64 for b in block_sizes)
     status = torch.zeros(1, dtype=torch.int32, device=src.device) if wide else None
+    strm = stream if stream is not None else torch.cuda.current_stream(src.device)
     check(_lib.load().nh_encode_intra_planes(
         src.data_ptr(), int(src.dtype == torch.uint8), arr, len(sets), bsz,
         recon.data_ptr() if recon is not None else None, recon_u8.data_ptr() if recon_u8 is not None else None,
         stats.data_ptr(), status.data_ptr() if status is not None else None,
-        C.c_void_p(_stream(stream, src.device))))
+        C.c_void_p(_stream(strm, src.device))))
     if status is not None:
-        torch.cuda.synchronize(src.device)          # the launch may be on another stream than torch's current one
+        strm.synchronize()   # the launch's stream only (it may not be torch's current one), not the whole device
     if status is not None and int(status.item()):
         raise OverflowError("encode_intra_planes: planar prediction out of bounds for int16 (intra.py:111)")
     return stats

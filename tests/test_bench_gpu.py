@@ -54,6 +54,11 @@ def test_bench_headline_line():
     assert abs(rf["frac_of_achievable_copy"] - rf["achieved"] / rf["stream_copy_GBps"]) < 1e-9
     # value is the whole job's blocks over the timed wall clock
     assert abs(d["value"] * d["ms_per_step"] / 1e3 - 2 * 194400) / (2 * 194400) < 1e-6
+    # device-time-only rate (one rank: blocks / HIP-event time) beside it, and the reference's numpy
+    # figure, labelled as another host's
+    assert abs(d["compute_only_sum_blocks_per_s"] - 2 * 194400 / (rf["kernel_ms_avg"] * 1e-3)) < 1e-3 * d["value"]
+    rn = d["cpu_baseline"]["reference_numpy"]
+    assert rn["kind"] == "reference" and rn["value"] > 0 and "not the GPU box" in rn["host"]
 
 
 def test_bench_config4_line():
@@ -62,6 +67,7 @@ def test_bench_config4_line():
     assert d["unit"] == "samples/s" and d["cpu_baseline"]["gpu_outputs_bit_exact_on_sample"] is True
     assert d["cpu_baseline"]["cores"] > 1 and d["cpu_baseline"]["value_1thread"] > 0
     assert d["config"]["source_fraction_rank0"] == 1.0
+    assert d["compute_only_sum_samples_per_s"] >= d["value"] * 0.95
     if os.path.exists(os.path.join(ROOT, "profiles", "valu_roofline.json")):   # committed VALU roofline inputs
         # the VALU view leads, from counts of THIS build's kernel sources (strict; the CPU
         # suite's test_valu_profile_matches_the_tree fails first when the sources moved on)

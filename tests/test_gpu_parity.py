@@ -985,23 +985,32 @@ def test_tu_pipeline_closed_pairs_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
             off += ph * pw
 
 
-@pytest.mark.parametrize("where", ["last", "first"])
-def test_tu_pipeline_closed_pairs_late_wide_sample(nh, torch_dev, where):
+@pytest.mark.parametrize("where,F", [("last", 4), ("first", 4), ("chroma_v_last", 3), ("chroma_u_neg", 3),
+                                     ("luma_lone_last", 3)])
+def test_tu_pipeline_closed_pairs_late_wide_sample(nh, torch_dev, where, F):
     """The pair kernel checks the source samples its chains load (round 5; no scan
     before the launch): ONE 9-bit sample in the last CTU of the last frame's luma --
     found after every other row is coded -- or in the first CTU of the first frame
     sends the whole set to the 32-bit form behind it (its own tickets and line-word
-    tags); every plane equals the sequential oracle."""
+    tags); every plane equals the sequential oracle.  Also the chroma instance (4
+    planes per wave; F = 3: the last group holds 2 planes) with the wide sample only
+    in the last V plane or a negative one in a U plane, and a lone last luma plane
+    (F = 3: npl = 1) holding it."""
     torch = torch_dev
     from nano_hevc import gpu
-    F, W, H, qp = 4, 104, 72, 27
+    W, H, qp = 104, 72, 27
     rng = np.random.default_rng(404)
     fe = gpu.yuv420_frame_elems(W, H)
+    cw, ch = W // 2, H // 2
     buf = np.clip(100 + rng.integers(-90, 91, F * fe), 0, 255).astype(np.int16)
-    if where == "last":
+    if where in ("last", "luma_lone_last"):
         buf[(F - 1) * fe + (H - 3) * W + W - 5] = 300   # inside the bottom-right whole CTU's TUs
-    else:
+    elif where == "first":
         buf[7 * W + 3] = -4
+    elif where == "chroma_v_last":                      # the last frame's V plane, bottom-right CTU
+        buf[(F - 1) * fe + W * H + cw * ch + (ch - 2) * cw + cw - 3] = 511
+    else:                                               # frame 1's U plane, an inner CTU
+        buf[fe + W * H + 20 * cw + 21] = -1
     d = torch.from_numpy(buf).cuda()
     sy, suv = gpu.yuv420_plane_sets(F, W, H)
     lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")

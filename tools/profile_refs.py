@@ -23,8 +23,10 @@ SOURCES = ["DESIGN.md", "README.md", "INTEGRATION.md", "bench.py", "profiles/val
            "profiles/pmc_traffic.json"]
 SOURCE_DIRS = [("tools", (".py", ".sh")), ("tests", (".py",)), ("nano-hevc_amd/csrc", (".hip", ".hpp"))]
 FULL = re.compile(r"profiles/[A-Za-z0-9_./*{},-]+")
-# bare names: a round tag r0N plus letters, as a file name, stem or glob
-BARE = re.compile(r"(?<![/A-Za-z0-9])_?[A-Za-z0-9_]*_r0\d[a-z0-9]*[A-Za-z0-9_*.]*")
+# bare names: a round tag r0N plus letters, as a file name, stem or glob; or any file name with a
+# record's extension (e.g. `ab_variants*.json`, `not_kept_srclds.diff`)
+BARE = re.compile(r"(?<![/A-Za-z0-9])_?[A-Za-z0-9_]*_r0\d[a-z0-9]*[A-Za-z0-9_*.]*"
+                  r"|(?<![/A-Za-z0-9])[A-Za-z0-9_*{},-]+\.(?:jsonl|json|csv|diff|log)\b")
 
 
 def source_files():
@@ -57,7 +59,7 @@ def citations():
             for m in BARE.finditer(txt):
                 t = m.group(0).rstrip(".,);:")
                 if len(t) >= 6:
-                    bare.add(t)
+                    bare.update(expand_braces(t))
     return sorted(full), sorted(bare)
 
 
