@@ -72,6 +72,9 @@ struct CtuArgs {
                                      // 4 = return at once, 8 = no TU-map stores (wrong outputs)
     uint32_t* wide_flag;             // config 5: set to `epoch` when a block is left to the int8 fix-up
     uint32_t epoch;
+    const uint8_t* plan;             // config 4: the groups' TU plans (k_ctu_plan; null: classified in the kernel)
+    uint8_t* plan_w;                 // k_ctu_plan's output (the same buffer)
+    int32_t ngroups;                 // groups of the band (records per plane id)
 };
 
 __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
@@ -1061,6 +1064,56 @@ __device__ __forceinline__ void strip_writeout(const CtuArgs& a, int sx0, int sy
     }
 }
 
+// A group's TU plan (k_ctu_plan, one record per (plane id, group) of a launch's band): the TU
+// byte of every (strip, unit) (0xFF: outside the plane), the pooled TU counts per size and the
+// entries (strip << 6 | unit) of every size, back to back in size order.  The seeded quadtree
+// depends on (plane id, position) only, so every frame of a plane set shares its records:
+// k_ctu_open reads them instead of hashing and pooling per group (one barrier less).
+constexpr int kCtuPlanCnt = 256, kCtuPlanEnt = 272, kCtuPlanBytes = 1024;
+template <int CTB, int GS>
+__global__ void __launch_bounds__(64 * GS) k_ctu_plan(CtuArgs a) {
+    static_assert(GS * 64 <= kCtuPlanCnt && kCtuPlanEnt + 2 * 64 * GS <= kCtuPlanBytes, "plan record layout");
+    using G = Strip<CTB>;
+    constexpr int UW = G::UW;
+    __shared__ int cnt_s[GS][4];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63, grp = blockIdx.x, c = blockIdx.y;
+    int sx0, sy0;
+    const bool valid = strip_of<CTB, GS>(a, grp, wv, sx0, sy0);
+    uint8_t* pr = a.plan_w + ((int64_t)c * a.ngroups + grp) * kCtuPlanBytes;
+    bool org = false, in = false;
+    int ls = 0;
+    if (valid) {   // as ctu_group's classification
+        const uint64_t split = strip_splits<CTB>(a.seed, a.plane_id + c, sx0, sy0, a.w, a.h);
+        const int ux = lane % UW, uy = lane / UW, x = sx0 + 4 * ux, y = sy0 + 4 * uy;
+        in = x < a.w && y < a.h;
+        int cx, cy;
+        ls = unit_leaf<CTB>(split, ux, uy, sx0, sy0, cx, cy);
+        org = in && cx == x && cy == y;
+    }
+    pr[wv * 64 + lane] = in ? (uint8_t)ls : (uint8_t)0xFF;
+    uint64_t m[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[k] = __ballot(org && ls == k + 2);
+        if (lane == 0) cnt_s[wv][k] = __popcll(m[k]);
+    }
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < GS; ++q) {
+            off += q < wv ? cnt_s[q][k] : 0;
+            tot += cnt_s[q][k];
+        }
+        if (org && ls == k + 2)
+            ((uint16_t*)(pr + kCtuPlanEnt))[base + off + __popcll(m[k] & ((1ull << lane) - 1))] = (uint16_t)(wv << 6 | lane);
+        if (threadIdx.x == k) ((int*)(pr + kCtuPlanCnt))[k] = tot;
+        base += tot;
+    }
+}
+
 // MFMA32: the 32x32 TUs on the matrix cores, one per batch (narrow: f16,
 // ctu_chain32_h; wide: int8, ctu_chain32 -- A/B forms); otherwise two per
 // batch on 32-point butterflies.
@@ -1076,7 +1129,7 @@ __device__ __forceinline__ void strip_writeout(const CtuArgs& a, int sx0, int sy
 // the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
 // !NARROW: the 32-bit chain, any int16 input.
 // Returns with the workgroup's waves in the batch loop's exit (no barrier).
-template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, bool OST = false, class Prefetch>
+template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, bool OST = false, bool PLAN = false, class Prefetch>
 __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
                                           CtuSmem<CTB, NARROW, NARROW && MFMA32 && !(NH_CTU_TF32 && !OST), GS, OST>& sm,
                                           StripLoad<CTB>& ld,
@@ -1097,21 +1150,43 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
     bool org = false;
     int ls = 0;
     const int64_t tu_org = (int64_t)pz * a.tu_plane + (int64_t)(sy0 >> 2) * (w >> 2) + (sx0 >> 2);
-    if (valid) {
-        const uint64_t split = strip_splits<CTB>(a.seed, pid, sx0, sy0, w, h);
-        const int ux = lane % UW, uy = lane / UW, x = sx0 + 4 * ux, y = sy0 + 4 * uy;
-        const bool in = x < w && y < h;
-        int cx, cy;
-        ls = unit_leaf<CTB>(split, ux, uy, sx0, sy0, cx, cy);
-        if (in && (!NH_AB || (a.probe & 8) == 0))
-            a.tu[(int64_t)pz * a.tu_plane + (int64_t)(y >> 2) * (w >> 2) + (x >> 2)] = (uint8_t)ls;
-        org = in && cx == x && cy == y;
-    }
     uint64_t m[4];
+    int pcnt[4];   // PLAN: the group's TU counts per size
+    if constexpr (PLAN) {
+        // the group's TUs from its plan (k_ctu_plan: same for every plane of this plane id): this
+        // unit's TU byte, and the group's pooled entries straight into the per-size lists
+        const uint8_t* pr = a.plan + ((int64_t)(pz % a.ppg) * a.ngroups + grp) * kCtuPlanBytes;
+        const int4 cn = *(const int4*)(pr + kCtuPlanCnt);
+        pcnt[0] = cn.x; pcnt[1] = cn.y; pcnt[2] = cn.z; pcnt[3] = cn.w;
+        const int tub = pr[wv * 64 + lane];
+        const int pe = wv * 64 + lane, b1 = cn.x, b2 = b1 + cn.y, b3 = b2 + cn.z, te = b3 + cn.w;
+        const int ent = pe < te ? ((const uint16_t*)(pr + kCtuPlanEnt))[pe] : 0;
+        ls = tub;
+        if (valid && tub != 0xFF && (!NH_AB || (a.probe & 8) == 0)) {
+            const int x = sx0 + 4 * (lane % UW), y = sy0 + 4 * (lane / UW);
+            a.tu[(int64_t)pz * a.tu_plane + (int64_t)(y >> 2) * (w >> 2) + (x >> 2)] = (uint8_t)tub;
+        }
+        if (pe < te) {
+            const int k = (pe >= b1) + (pe >= b2) + (pe >= b3);
+            const int base = k == 0 ? 0 : k == 1 ? b1 : k == 2 ? b2 : b3;
+            sm.list[k][pe - base] = (uint16_t)ent;
+        }
+    } else {
+        if (valid) {
+            const uint64_t split = strip_splits<CTB>(a.seed, pid, sx0, sy0, w, h);
+            const int ux = lane % UW, uy = lane / UW, x = sx0 + 4 * ux, y = sy0 + 4 * uy;
+            const bool in = x < w && y < h;
+            int cx, cy;
+            ls = unit_leaf<CTB>(split, ux, uy, sx0, sy0, cx, cy);
+            if (in && (!NH_AB || (a.probe & 8) == 0))
+                a.tu[(int64_t)pz * a.tu_plane + (int64_t)(y >> 2) * (w >> 2) + (x >> 2)] = (uint8_t)ls;
+            org = in && cx == x && cy == y;
+        }
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        m[k] = __ballot(org && ls == k + 2);
-        if (lane == 0) sm.cnt[wv][k] = __popcll(m[k]);
+        for (int k = 0; k < 4; ++k) {
+            m[k] = __ballot(org && ls == k + 2);
+            if (lane == 0) sm.cnt[wv][k] = __popcll(m[k]);
+        }
     }
     // ---- 2. the strip image: its samples, the row above and the column left, into LDS ----
     {
@@ -1137,20 +1212,25 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
             return;
         }
     }
-    // pool the strips' TUs per size: entry = strip << 6 | unit
+    // pool the strips' TUs per size: entry = strip << 6 | unit (PLAN: pooled by k_ctu_plan, stored above)
     int cnt[4];
+    if constexpr (PLAN) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        int off = 0;
-        cnt[k] = 0;
+        for (int k = 0; k < 4; ++k) cnt[k] = pcnt[k];
+    } else {
 #pragma unroll
-        for (int q = 0; q < GS; ++q) {
-            off += q < wv ? sm.cnt[q][k] : 0;
-            cnt[k] += sm.cnt[q][k];
+        for (int k = 0; k < 4; ++k) {
+            int off = 0;
+            cnt[k] = 0;
+#pragma unroll
+            for (int q = 0; q < GS; ++q) {
+                off += q < wv ? sm.cnt[q][k] : 0;
+                cnt[k] += sm.cnt[q][k];
+            }
+            if (org && ls == k + 2) sm.list[k][off + __popcll(m[k] & ((1ull << lane) - 1))] = (uint16_t)(wv << 6 | lane);
         }
-        if (org && ls == k + 2) sm.list[k][off + __popcll(m[k] & ((1ull << lane) - 1))] = (uint16_t)(wv << 6 | lane);
+        __syncthreads();
     }
-    __syncthreads();
 
     // ---- 3. batches, claimed in descending cost: 32x32 chains, then 16, 8, 4 ----
     if (NH_AB && (a.probe & 1)) return;
@@ -1225,8 +1305,11 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
 // resident workgroups walking the (group, plane) items with stride gridDim.x,
 // each group's loads issued during the previous group's chains.
 // WAVES: the occupancy floor (waves/SIMD) the registers are allocated for.
-template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4, bool OST = false>
+// PLAN: the groups' TUs from k_ctu_plan's records (a.plan) instead of classified per group.
+template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4, bool OST = false,
+          bool PLAN = false>
 __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
+    static_assert(!PLAN || (GS == 4 && PERSIST == 0), "plan records: groups of 4 strips, one group per workgroup");
     // (the transposition-free 32x32 chain reads its bases from the constant table: no LDS copy)
     constexpr bool BAS = MFMA32 && !(NH_CTU_TF32 && !OST);
     __shared__ CtuSmem<CTB, true, BAS, GS, OST> sm;
@@ -1242,7 +1325,7 @@ __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WA
         }
         StripLoad<CTB> ld;
         strip_issue<CTB, GS>(a, blockIdx.x, blockIdx.y, ld);
-        ctu_group<CTB, LUMA, true, MFMA32, GS, OST>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
+        ctu_group<CTB, LUMA, true, MFMA32, GS, OST, PLAN>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
             if constexpr (BAS) {
                 if (bthr) ((uint4*)&sm.basis)[threadIdx.x] = bq;
             }
@@ -1564,6 +1647,27 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
     // A/B build: NH_CTU_OST = bit 1 luma / bit 2 chroma with whole-row output stores (LDS output images)
     static const int ost_knob = NH_KNOB("NH_CTU_OST", 0);
     (void)ost_knob;
+    // A/B build only, NH_CTU_PLAN = 1: the groups' TU plans (k_ctu_plan, one 1-KB record per (plane
+    // id, group)) in stream-ordered memory, built by a prologue launch and read by k_ctu_open instead
+    // of classifying every group: 0.0342-0.0344 vs 0.0341-0.0346 ms per 4K frame, not kept
+    // (profiles/r06/cfg4/ab_NH_CTU_PLAN_4b_r06f.jsonl; the classification runs under the strip loads)
+    static const int plan_knob = NH_KNOB("NH_CTU_PLAN", 0);
+    const bool plan_on = NH_AB && plan_knob != 0 && gs_knob == 4 && persist == 0;
+    a.ngroups = (int)groups;
+    void* plan_buf = nullptr;
+    if (plan_on) {
+        NH_HIP(hipMallocAsync(&plan_buf, (size_t)groups * a.ppg * kCtuPlanBytes, s));
+        a.plan = (const uint8_t*)plan_buf;
+        a.plan_w = (uint8_t*)plan_buf;
+    }
+    auto launch_plan = [&](auto ctb_c) {
+#if NH_AB
+        constexpr int C = decltype(ctb_c)::value;
+        if (plan_buf) k_ctu_plan<C, 4><<<dim3((unsigned)groups, (unsigned)a.ppg), 256, 0, s>>>(a);
+#else
+        (void)ctb_c;
+#endif
+    };
     auto launch_open = [&](auto kern, auto gs_c) -> int {
         constexpr int GSZ = decltype(gs_c)::value;
         const int64_t ngrp = (strips + GSZ - 1) / GSZ;
@@ -1589,6 +1693,7 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         constexpr bool L = decltype(luma_c)::value;
         constexpr bool M32 = C == 32 && L;
         int rc3;
+        launch_plan(ctb_c);
         using G4 = std::integral_constant<int, 4>;
         if constexpr (NH_AB != 0) {
             const bool m = M32 && t32 != 0;
@@ -1597,12 +1702,17 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
                          : persist == 2 ? launch_open(k_ctu_open<C, L, M32, 2>, G4{})
                          : gs_knob == 6 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 6>, std::integral_constant<int, 6>{})
                          : gs_knob == 8 ? launch_open(k_ctu_open<C, L, M32, 0, 5, 8>, std::integral_constant<int, 8>{})
-                         : ost_on       ? launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true>, G4{})
+                         : ost_on       ? (plan_on ? launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true, true>, G4{})
+                                                   : launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true>, G4{}))
+                         : plan_on      ? launch_open(k_ctu_open<C, L, M32, 0, 3, 4, false, true>, G4{})
                                         : launch_open(k_ctu_open<C, L, M32, 0, 3, 4>, G4{});
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>, G4{})
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>, G4{})
                        : gs_knob == 6 ? launch_open(k_ctu_open<C, L, false, 0, 5, 6>, std::integral_constant<int, 6>{})
                        : gs_knob == 8 ? launch_open(k_ctu_open<C, L, false, 0, 5, 8>, std::integral_constant<int, 8>{})
+                       : plan_on && ost_on ? launch_open(k_ctu_open<C, L, false, 0, 3, 4, true, true>, G4{})
+                       : ost_on       ? launch_open(k_ctu_open<C, L, false, 0, 3, 4, true>, G4{})
+                       : plan_on      ? launch_open(k_ctu_open<C, L, false, 0, 3, 4, false, true>, G4{})
                                       : launch_open(k_ctu_open<C, L, false, 0, 3, 4>, G4{});
             if (C == 32 && t32 == 1) k_ctu_wide<C, L, C == 32><<<grid_wide, 256, 0, s>>>(a);
             else k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
@@ -1629,8 +1739,9 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
                                : launch_ctb(integral_constant<int, 16>{}, std::false_type{}); break;
         case 32: rc2 = is_luma ? launch_ctb(integral_constant<int, 32>{}, std::true_type{})
                                : launch_ctb(integral_constant<int, 32>{}, std::false_type{}); break;
-        default: return NH_EVALUE;
+        default: rc2 = NH_EVALUE;
     }
+    if (plan_buf) NH_HIP(hipFreeAsync(plan_buf, s));   // (stream-ordered: after the kernels that read it)
     if (rc2) return rc2;
     NH_HIP(hipGetLastError());
     return NH_OK;
@@ -1672,7 +1783,7 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
     // NH_TC32H_FORM = 1 XCD-ordered grid, 3 the same with whole-row stores,
     // 4 row-piece stores from registers (the round-2 form), NH_TC32H_BREG = bases in registers.
     static const int cap = NH_KNOB("NH_TC32H_CAP", 3), cap_c = NH_KNOB("NH_TC32H_CAP_C", 3);
-    static const int ilv = NH_KNOB("NH_TC32H_ILV", 0);   // A/B: 1 = interleaved block order (k_tc32_hd ILV)
+    static const int ilv = NH_KNOB("NH_TC32H_ILV", 0);   // A/B: 2 = the round-5 block order (k_tc32_hd !ILV)
     (void)ilv;
     auto launch = [&](auto kern, int K, int wgs) {
         kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, wgs), s>>>(a, nblk);
@@ -1693,7 +1804,7 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
         bool done = false;
 #if NH_AB
         {
-          if (ilv || dma == 4) {   // A/B: interleaved order and / or 4 blocks per wave
+          if (ilv == 2 || dma == 4) {   // A/B: the round-5 order and / or 4 blocks per wave
             done = true;
             auto by_lt = [&](auto kb_c, auto ilv_c) {
                 constexpr int K = decltype(kb_c)::value;
@@ -1704,15 +1815,18 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
             };
             using K2 = std::integral_constant<int, 2>;
             using K4 = std::integral_constant<int, 4>;
-            if (dma == 4) ilv ? by_lt(K4{}, std::true_type{}) : by_lt(K4{}, std::false_type{});
-            else by_lt(K2{}, std::true_type{});
+            if (dma == 4) ilv == 1 ? by_lt(K4{}, std::true_type{}) : by_lt(K4{}, std::false_type{});
+            else by_lt(K2{}, std::false_type{});   // NH_TC32H_ILV=2: the round-5 order (blocks 2w, 2w + 1)
           }
         }
 #endif
+        // the 4 waves of a workgroup on 4 horizontally adjacent blocks at a time (ILV): 0.078 vs
+        // 0.088-0.090 ms per 8K YUV420 frame (int32 levels), 0.067 vs 0.074 (int16), 0.063 vs 0.065
+        // (int8) -- profiles/r06/cfg5/ab_tc32_r06e.jsonl
         if (done) {
-        } else if (lvl_bytes == 4) launch(k_tc32_hd<2>, 2, cap);
-        else if (lvl_bytes == 2) launch(k_tc32_hd<2, int16_t>, 2, cap_c);
-        else launch(k_tc32_hd<2, int8_t>, 2, cap_c);
+        } else if (lvl_bytes == 4) launch(k_tc32_hd<2, int32_t, true>, 2, cap);
+        else if (lvl_bytes == 2) launch(k_tc32_hd<2, int16_t, true>, 2, cap_c);
+        else launch(k_tc32_hd<2, int8_t, true>, 2, cap_c);
         NH_HIP(hipGetLastError());
         return NH_OK;
     }
