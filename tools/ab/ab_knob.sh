@@ -1,15 +1,9 @@
-#!/bin/bash
-# Generic A/B of one NH_* knob of the A/B library over a bench_configs config,
-# alternating processes, REPS rounds:   KNOB=NH_TC32H_K VALUES="1 2" CFG=5b TAG=x tools/ab/ab_knob.sh
-# (EXTRA: more environment assignments for every run, e.g. EXTRA="NH_TC32H_CAP=2")
+# A/B of one A/B-library knob on one bench_configs config, alternating processes:
+#   TAG=x KNOB=NH_CTU_PLAN VALS="0 1" CFG=4b FIX="NH_CTU_OST=2" bash tools/ab/ab_knob.sh
 set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
-TAG=${TAG:-ab}
-REPS=${REPS:-2}
-OUT=gpurun_out/ab_${KNOB}_${CFG}_${TAG}.jsonl
-for rep in $(seq $REPS); do
-  for v in $VALUES; do
-    env $EXTRA $KNOB=$v timeout -k 10 120 python tools/bench_configs.py --ab --configs $CFG --reps 20 >> $OUT || exit 1
-  done
-done
-cat $OUT
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
+OUT=gpurun_out/ab_${KNOB}_${CFG}_${TAG:-x}.jsonl
+for rep in $(seq 1 ${REPS:-2}); do for v in $VALS; do
+  echo "{\"knob\": \"$KNOB\", \"val\": \"$v\", \"rep\": $rep, \"fixed\": \"$FIX\"}" >> $OUT
+  env $FIX $KNOB=$v timeout -k 10 200 python tools/bench_configs.py --ab --configs $CFG --reps ${BREPS:-20} $BARGS >> $OUT 2>> ${OUT%.jsonl}.err || exit 1
+done; done
