@@ -784,7 +784,8 @@ template <class LT> struct LvlTile {
     static constexpr int P = sizeof(LT) == 4 ? kOutP : sizeof(LT) == 2 ? kRecH : 48;
     static constexpr int STORES = (int)sizeof(LT);   // level-row store instructions: 4 / 2 / 1
 };
-template <class IMG, class LT = int32_t>
+// NT: nontemporal level / recon stores (A/B form)
+template <class IMG, class LT = int32_t, bool NT = false>
 __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, const BasisHC& bs, int gx0, int gy0,
                                            LT* __restrict__ lvl, int16_t* __restrict__ rec, int32_t* ot,
                                            const ChainQ& cq, const TfLane& tl) {
@@ -852,7 +853,9 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
 #pragma unroll
                   for (int i = 0; i < 32 / RPI; ++i) {
                       const int rr = l / (32 / PER) + RPI * i, c = PER * (l % (32 / PER));
-                      *(int4*)(lb + vofs((rr * (int32_t)op + c) * (int32_t)sizeof(LT))) = *(const int4*)&lt[rr * LP + c];
+                      int4* dst = (int4*)(lb + vofs((rr * (int32_t)op + c) * (int32_t)sizeof(LT)));
+                      if constexpr (NT) __builtin_nontemporal_store(*(const v4i_t*)&lt[rr * LP + c], (v4i_t*)dst);
+                      else *dst = *(const int4*)&lt[rr * LP + c];
                   }
                   wave_sync();   // the tile's reads before the recon tile reuses it
               },
@@ -870,7 +873,9 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
 #pragma unroll
     for (int i = 0; i < 2; ++i) {   // 2 instructions of 16 whole 64-B recon rows
         const int rr = (l >> 2) + 16 * i, c = 4 * (l & 3);
-        *(uint4*)(rb + vofs((rr * (int32_t)op + 2 * c) * 2)) = *(const uint4*)&ot[rr * kRecP + c];
+        uint4* dst = (uint4*)(rb + vofs((rr * (int32_t)op + 2 * c) * 2));
+        if constexpr (NT) __builtin_nontemporal_store(*(const v4i_t*)&ot[rr * kRecP + c], (v4i_t*)dst);
+        else *dst = *(const uint4*)&ot[rr * kRecP + c];
     }
 }
 
@@ -1485,20 +1490,21 @@ template <class LT> constexpr int tc32hd_stores_narrow() { return kTc32hdStoresN
 // ILV: wave w of workgroup g codes blocks 4 KB g + w + 4 k (k < KB), so the 4 waves work on 4
 // horizontally adjacent blocks at a time (their row pieces form 4x longer contiguous runs in HBM);
 // otherwise blocks KB (4 g + w) + k.
-template <int KB, class LT = int32_t, bool ILV = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_tc32_hd(CtuArgs a, int nblk) {
+// W: waves per workgroup (A/B: 8); NT: nontemporal output stores (A/B)
+template <int KB, class LT = int32_t, bool ILV = false, int W = 4, bool NT = false>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(3))) k_tc32_hd(CtuArgs a, int nblk) {
     constexpr int kNarrow = tc32hd_stores_narrow<LT>();
     static_assert(kNarrow > 0, "store count");   // (equal to the wide count: one wait serves both kinds)
-    __shared__ __attribute__((aligned(16))) int16_t s_body[4][2][32 * 32];
-    __shared__ __attribute__((aligned(16))) int16_t s_edge[4][2][96];
+    __shared__ __attribute__((aligned(16))) int16_t s_body[W][2][32 * 32];
+    __shared__ __attribute__((aligned(16))) int16_t s_edge[W][2][96];
     __shared__ BasisHC s_basis;
     // the level / recon tile: int32 level rows (kOutP), else the recon tile's kRecP (compact levels fit in it)
-    __shared__ __attribute__((aligned(16))) int32_t s_out[4][32 * (sizeof(LT) == 4 ? kOutP : kRecP)];
+    __shared__ __attribute__((aligned(16))) int32_t s_out[W][32 * (sizeof(LT) == 4 ? kOutP : kRecP)];
     // the wave index in an SGPR: block index, `next` and the loop are scalar
     // branches, so one wave never runs both sides of a block's wait selection
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    constexpr int BS = ILV ? 4 : 1;   // block stride of a wave
-    const int b0 = ILV ? (int)blockIdx.x * 4 * KB + wv : ((int)blockIdx.x * 4 + wv) * KB, pz = (int)blockIdx.y;
+    constexpr int BS = ILV ? W : 1;   // block stride of a wave
+    const int b0 = ILV ? (int)blockIdx.x * W * KB + wv : ((int)blockIdx.x * W + wv) * KB, pz = (int)blockIdx.y;
     const int64_t poff = plane_off(a, pz);
     const int16_t* src = a.src + poff;
     const ChainQ cq = make_chainq(a.q[3], a.dqs, a.dq_per);
@@ -1558,7 +1564,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
             }
             prev = kTc32hdStoresWide;
         } else {
-            chain32_tf(a, ImgDma{body, edge}, s_basis, sx0, sy0, (LT*)a.lvl + poff, a.rec + poff, s_out[wv], cq, tl);
+            chain32_tf<ImgDma, LT, NT>(a, ImgDma{body, edge}, s_basis, sx0, sy0, (LT*)a.lvl + poff, a.rec + poff, s_out[wv], cq, tl);
             prev = kNarrow;
         }
         wave_sync();
@@ -1785,8 +1791,9 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
     static const int cap = NH_KNOB("NH_TC32H_CAP", 3), cap_c = NH_KNOB("NH_TC32H_CAP_C", 3);
     static const int ilv = NH_KNOB("NH_TC32H_ILV", 0);   // A/B: 2 = the round-5 block order (k_tc32_hd !ILV)
     (void)ilv;
-    auto launch = [&](auto kern, int K, int wgs) {
-        kern<<<dim3((unsigned)((nblk + 4 * K - 1) / (4 * K)), (unsigned)planes), 256, lds_cap(kern, wgs), s>>>(a, nblk);
+    auto launch = [&](auto kern, int K, int wgs, int W = 4) {
+        kern<<<dim3((unsigned)((nblk + W * K - 1) / (W * K)), (unsigned)planes), 64 * W, lds_cap(kern, wgs), s>>>(a,
+                                                                                                            nblk);
     };
     // two blocks per wave, the second's image by LDS-DMA under the first's chain (k_tc32_hd<2>):
     // 0.0966-0.0976 vs 0.0982-0.0983 ms per 8K YUV420 frame for one block per wave loading its
@@ -1804,19 +1811,28 @@ int tc32_narrow_launch(const int16_t* src, void* lvl, int lvl_bytes, int16_t* re
         bool done = false;
 #if NH_AB
         {
-          if (ilv == 2 || dma == 4) {   // A/B: the round-5 order and / or 4 blocks per wave
+          // A/B: the round-5 order (NH_TC32H_ILV=2), 4 blocks per wave (NH_TC32H_DMA=4), 8-wave
+          // workgroups (NH_TC32H_W=8), nontemporal output stores (NH_TC32H_NT=1)
+          static const int wk = NH_KNOB("NH_TC32H_W", 4), nt = NH_KNOB("NH_TC32H_NT", 0);
+          if (ilv == 2 || dma == 4 || wk == 8 || nt) {
             done = true;
-            auto by_lt = [&](auto kb_c, auto ilv_c) {
-                constexpr int K = decltype(kb_c)::value;
-                constexpr bool I = decltype(ilv_c)::value;
-                if (lvl_bytes == 4) launch(k_tc32_hd<K, int32_t, I>, K, cap);
-                else if (lvl_bytes == 2) launch(k_tc32_hd<K, int16_t, I>, K, cap_c);
-                else launch(k_tc32_hd<K, int8_t, I>, K, cap_c);
+            auto by_lt = [&](auto kb_c, auto ilv_c, auto w_c, auto nt_c) {
+                constexpr int K = decltype(kb_c)::value, WW = decltype(w_c)::value;
+                constexpr bool I = decltype(ilv_c)::value, N = decltype(nt_c)::value;
+                if (lvl_bytes == 4) launch(k_tc32_hd<K, int32_t, I, WW, N>, K, cap, WW);
+                else if (lvl_bytes == 2) launch(k_tc32_hd<K, int16_t, I, WW, N>, K, cap_c, WW);
+                else launch(k_tc32_hd<K, int8_t, I, WW, N>, K, cap_c, WW);
             };
             using K2 = std::integral_constant<int, 2>;
             using K4 = std::integral_constant<int, 4>;
-            if (dma == 4) ilv == 1 ? by_lt(K4{}, std::true_type{}) : by_lt(K4{}, std::false_type{});
-            else by_lt(K2{}, std::false_type{});   // NH_TC32H_ILV=2: the round-5 order (blocks 2w, 2w + 1)
+            using W4 = std::integral_constant<int, 4>;
+            using W8 = std::integral_constant<int, 8>;
+            using T = std::true_type;
+            using F = std::false_type;
+            if (dma == 4) ilv == 2 ? by_lt(K4{}, F{}, W4{}, F{}) : by_lt(K4{}, T{}, W4{}, F{});
+            else if (ilv == 2) by_lt(K2{}, F{}, W4{}, F{});   // the round-5 order (blocks 2w, 2w + 1)
+            else if (wk == 8) nt ? by_lt(K2{}, T{}, W8{}, T{}) : by_lt(K2{}, T{}, W8{}, F{});
+            else by_lt(K2{}, T{}, W4{}, T{});
           }
         }
 #endif

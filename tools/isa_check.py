@@ -45,10 +45,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "nano-hevc_amd", "nano_hevc", "libnanohevc.so")
 LLVM = "/opt/rocm/lib/llvm/bin"
 TRIPLE = "hipv4-amdgcn-amd-amdhsa--gfx950"
-TC32HD = "_ZN2nh9k_tc32_hdILi2EiLb1EEEvNS_7CtuArgsEi"      # k_tc32_hd<2, int32_t, ILV>: int32 levels
+TC32HD = "_ZN2nh9k_tc32_hdILi2EiLb1ELi4ELb0EEEvNS_7CtuArgsEi"   # k_tc32_hd<2, int32_t, ILV, 4, !NT>: int32 levels
 # the three level types and the store instructions a narrow block issues (4 / 2 / 1 level rows + 2 recon)
-TC32HD_LEVELS = {"int32": (TC32HD, 6), "int16": ("_ZN2nh9k_tc32_hdILi2EsLb1EEEvNS_7CtuArgsEi", 4),
-                 "int8": ("_ZN2nh9k_tc32_hdILi2EaLb1EEEvNS_7CtuArgsEi", 3)}
+TC32HD_LEVELS = {"int32": (TC32HD, 6), "int16": ("_ZN2nh9k_tc32_hdILi2EsLb1ELi4ELb0EEEvNS_7CtuArgsEi", 4),
+                 "int8": ("_ZN2nh9k_tc32_hdILi2EaLb1ELi4ELb0EEEvNS_7CtuArgsEi", 3)}
 
 
 # ---------------------------------------------------------------------------
