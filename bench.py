@@ -71,7 +71,8 @@ METRIC = "transform-blocks/sec (8×8 DCT+quant, 4K YUV420) at 1/2/4/8 MI355X; % 
 METRIC_CFG4 = "samples/sec (4K YUV420, mixed 4/8/16/32 TUs per 32x32 CTU: pred+DCT+quant+dequant+IDCT+recon)"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BYTES_PER_BLOCK = 256          # 64 x int16 in + 64 x int16 out
-BYTES_PER_SAMPLE_CFG4 = 2 + 4 + 2 + 1 / 16
+BYTES_PER_SAMPLE_CFG4 = 2 + 4 + 2 + 1 / 16   # int16 in, int32 levels + int16 recon out, 1 TU-map byte per 4x4
+BYTES_PER_SAMPLE_CFG4_COMPACT = 2 + 2 + 2 + 1 / 16   # --levels int16: the exact compact levels
 W4K, H4K = 3840, 2160
 
 
@@ -84,6 +85,10 @@ def parse_args(argv=None):
     ap.add_argument("--frames", type=int, default=None,
                     help="4K YUV420 frames per GPU per step (default 128 for config 2, 16 for config 4)")
     ap.add_argument("--qp", type=int, default=32)
+    ap.add_argument("--levels", default="int16", choices=("int16", "int32"),
+                    help="config 4: level dtype on the device -- int16 = the exact compact levels (|level| <= 408 "
+                         "for an 8-bit TU; int32 spill for the rest, nh_tu_pipeline_planes_compact), int32 = the "
+                         "reference's dtype")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--variant", type=int, default=4341, help="config 2 launch variant (nanohevc.h); 4341 = default")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline budget (1-thread + all-threads legs)")
@@ -531,14 +536,35 @@ class Cfg4Rank:
         src = torch.zeros(max(1, self.total), dtype=torch.int16, device=self.dev)
         return self.lay.fill_from_stream(stream, src)
 
-    def new_lvl(self):
+    def new_lvl(self, compact=False):
+        """The level buffer: int32, or the int16 compact levels plus their int32 spill plane (self.spill)."""
+        if compact:
+            self.spill = torch.empty(max(1, self.total), dtype=torch.int32, device=self.dev)
+            return torch.zeros(max(1, self.total), dtype=torch.int16, device=self.dev)
+        self.spill = None
         return torch.zeros(max(1, self.total), dtype=torch.int32, device=self.dev)
+
+    def widen(self, lvl):
+        """int32 levels of the compact ones (outside the timed region: the CPU check)."""
+        if lvl.dtype == torch.int32:
+            return lvl
+        out = torch.zeros(lvl.shape, dtype=torch.int32, device=self.dev)
+        for sy, suv, r0, r1, _, _ in self.work:
+            self.gpu.tu_levels_widen(lvl, self.spill, sy, 32, r0, r1, out=out)
+            self.gpu.tu_levels_widen(lvl, self.spill, suv, 16, r0, r1, out=out)
+        return out
 
     def new_rec(self):
         return torch.zeros(max(1, self.total), dtype=torch.int16, device=self.dev)
 
     def run(self, src, qp, lvl, rec, stream):
         for sy, suv, r0, r1, tuy, tuc in self.work:
+            if lvl.dtype == torch.int16:   # the exact compact levels (int32 spill for strips that are not 8-bit)
+                self.gpu.tu_pipeline_planes_compact(src, sy, 32, 0, self.seed, qp, True, r0, r1, lvl=lvl, rec=rec,
+                                                    tu=tuy, spill=self.spill, stream=stream)
+                self.gpu.tu_pipeline_planes_compact(src, suv, 16, 1, self.seed, qp, False, r0, r1, lvl=lvl, rec=rec,
+                                                    tu=tuc, spill=self.spill, stream=stream)
+                continue
             self.gpu.tu_pipeline_planes(src, sy, 32, 0, self.seed, qp, True, r0, r1, lvl=lvl, rec=rec, tu=tuy,
                                         stream=stream)
             self.gpu.tu_pipeline_planes(src, suv, 16, 1, self.seed, qp, False, r0, r1, lvl=lvl, rec=rec, tu=tuc,
@@ -584,7 +610,8 @@ def run_cfg4(args, dist, world, rank, dev):
     nf = args.frames * world
     me = Cfg4Rank(rank, world, nf, W, H, dev, args.seed)
     src = me.synth_source()          # only this rank's bands + one halo row each
-    lvl = me.new_lvl()
+    compact = args.levels == "int16"
+    lvl = me.new_lvl(compact)
     recs = [me.new_rec()]
     stream = torch.cuda.current_stream(dev)
 
@@ -628,7 +655,6 @@ def run_cfg4(args, dist, world, rank, dev):
 
     if rank != 0:
         return None
-    achieved = my_samples * BYTES_PER_SAMPLE_CFG4 / (kern_ms * 1e-3) / 1e9
     line = {
         "metric": METRIC_CFG4, "value": value, "unit": "samples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -641,8 +667,12 @@ def run_cfg4(args, dist, world, rank, dev):
                    "source_bytes_rank0": 2 * me.total, "source_bytes_stream": 2 * nf * fe,
                    "source_fraction_rank0": me.total / (nf * fe),
                    "tu_blocks_per_step": {f"{4 << k}x{4 << k}": int(tu_all[k]) for k in range(4)},
-                   "tu_blocks_per_s": {f"{4 << k}x{4 << k}": tu_all[k] * args.steps / elapsed for k in range(4)}},
-        "roofline": cfg4_roofline(my_samples, kern_ms, args.frames, world),
+                   "tu_blocks_per_s": {f"{4 << k}x{4 << k}": tu_all[k] * args.steps / elapsed for k in range(4)},
+                   "levels": ("int16 on the device: the exact compact levels (|level| <= 408 for an 8-bit TU), "
+                              "int32 spill + strip markers for the rest, widened to the reference's int32 by "
+                              "nh_tu_levels_widen (outside the timed region, for the CPU check)" if compact else
+                              "int32 (the reference's dtype)")},
+        "roofline": cfg4_roofline(my_samples, kern_ms, args.frames, world, compact),
         "cpu_baseline": None,
         "compute_only_sum_samples_per_s": rate_sum,
         "compute_only_note": "sum over ranks of samples per step / that rank's mean HIP-event time per step "
@@ -653,7 +683,7 @@ def run_cfg4(args, dist, world, rank, dev):
     if check is not None:
         line["gathered_recon_equals_unsharded"] = check
     if world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline_cfg4(me, src, lvl, recs[0], args, fe)
+        line["cpu_baseline"] = cpu_baseline_cfg4(me, src, me.widen(lvl), recs[0], args, fe)
     return line
 
 
@@ -688,21 +718,22 @@ def load_valu(cfg_key: str):
         return None
 
 
-def cfg4_roofline(samples, kern_ms, frames, world):
+def cfg4_roofline(samples, kern_ms, frames, world, compact=False):
     """Config 4 is VALU-issue-bound: the roofline is the VALU
     issue rate.  achieved = the step's VALU wave-instructions (PMC, per kernel of
     the step, from profiles/valu_roofline.json) / the step's HIP-event time
     measured here; peak = the attainable rate of the step's instruction mix
     (harmonic combination of each kernel's attainable rate, weighted by its
-    instructions).  The HBM view (8 B/sample) rides along as ``hbm``."""
-    gbs = samples * BYTES_PER_SAMPLE_CFG4 / (kern_ms * 1e-3) / 1e9
+    instructions).  The HBM view (8 B/sample; 6 with compact levels) rides along as ``hbm``."""
+    bps = BYTES_PER_SAMPLE_CFG4_COMPACT if compact else BYTES_PER_SAMPLE_CFG4
+    gbs = samples * bps / (kern_ms * 1e-3) / 1e9
     hbm = {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS,
-           "traffic": load_traffic(f"cfg4_4k_yuv420_f{frames}_n{world}"),
+           "traffic": load_traffic(f"cfg4_4k_yuv420_f{frames}_n{world}" + ("_int16" if compact else "")),
            "traffic_note": "PMC bytes per step (all 4 launches): reads as the 64-B request tally (a lower bound for "
                            "8-B/lane row reads, <= 2x that if every request were 128 B), writes exact; "
                            "profiles/pmc_traffic.json",
-           "bytes_per_sample": BYTES_PER_SAMPLE_CFG4}
-    v = load_valu("cfg4_4k_yuv420")
+           "bytes_per_sample": bps}
+    v = load_valu("cfg4_4k_yuv420_int16" if compact else "cfg4_4k_yuv420")
     if not v:
         return dict(hbm, kernel_ms_avg=kern_ms)
     if not valu_sources_match(v):   # the committed counts describe another build: the HBM view leads

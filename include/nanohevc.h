@@ -262,6 +262,21 @@ int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane_set* set, 
                                  uint32_t seed, int qp, int is_luma, int32_t* d_lvl, int16_t* d_recon,
                                  uint8_t* d_tu, void* d_work, void* stream);
 
+/* Config 4 with COMPACT levels: int16 levels in the source layout (exact: an
+ * 8-bit TU's level satisfies |level| <= 408 at every QP and size,
+ * tools/packed_bounds.py).  Groups of strips with a sample outside [0, 255]
+ * (k_ctu_wide's 32-bit chain) write their int32 levels into d_spill (int32,
+ * source layout, only those strips touched) and -32768 at each of their strip
+ * origins in d_lvl (strips: CTB rows x 1024/CTB columns); nh_tu_levels_widen
+ * turns (d_lvl, d_spill) into the int32 levels nh_tu_pipeline_planes writes.
+ * CTB 16 or 32; pitch, base and strides multiples of 8; level buffers 16-B
+ * aligned. */
+int nh_tu_pipeline_planes_compact(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
+                                  uint32_t seed, int qp, int is_luma, int row0, int row1, int16_t* d_lvl,
+                                  int32_t* d_spill, int16_t* d_recon, uint8_t* d_tu, void* stream);
+int nh_tu_levels_widen(const int16_t* d_lvl, const int32_t* d_spill, const nh_plane_set* set, int ctb, int row0,
+                       int row1, int32_t* d_out, void* stream);
+
 /* Config 5: every full 32x32 block of an int16 source plane through the
  * config-4 chain at N=32.  variant 0 = butterfly
  * (k_tu_process<32>), 1 = matrix cores: blocks whose samples and neighbours

@@ -72,6 +72,8 @@ struct CtuArgs {
                                      // 4 = return at once, 8 = no TU-map stores (wrong outputs)
     uint32_t* wide_flag;             // config 5: set to `epoch` when a block is left to the int8 fix-up
     uint32_t epoch;
+    int32_t* spill;                  // config 4 compact levels: k_ctu_wide's int32 levels (null: int32 levels)
+    int16_t* lvl_c;                  // config 4 compact levels: the int16 level plane (k_ctu_wide's strip markers)
     const uint8_t* plan;             // config 4: the groups' TU plans (k_ctu_plan; null: classified in the kernel)
     uint8_t* plan_w;                 // k_ctu_plan's output (the same buffer)
     int32_t ngroups;                 // groups of the band (records per plane id)
@@ -83,6 +85,15 @@ __device__ __forceinline__ void wave_sync() { __builtin_amdgcn_wave_barrier(); }
 // rows are never re-read here) took 127 vs 39 us per 4K YUV420 frame: 8-16 B
 // pieces of scattered rows (profiles/r02/session5/nt_ab.jsonl).
 __device__ __forceinline__ void st_lvl4(int32_t* p, int4 v) { *(int4*)p = v; }
+// 4 consecutive levels in the level type LT: one 16-B (int32) or 8-B (int16, compact) store
+__device__ __forceinline__ void st_lvl4t(int32_t* p, const int32_t (&L)[4]) { st_lvl4(p, make_int4(L[0], L[1], L[2], L[3])); }
+__device__ __forceinline__ void st_lvl4t(int16_t* p, const int32_t (&L)[4]) {
+    *(uint2*)p = make_uint2(((uint32_t)L[0] & 0xffffu) | ((uint32_t)L[1] << 16), ((uint32_t)L[2] & 0xffffu) | ((uint32_t)L[3] << 16));
+}
+// Config 4 compact levels: the marker k_ctu_wide leaves at the origin of every strip it codes (its
+// int32 levels are in the spill plane); an 8-bit TU's level never takes it (|level| <= 408,
+// tools/packed_bounds.py level_bounds)
+constexpr int16_t kCtuSpillMark = (int16_t)0x8000;
 __device__ __forceinline__ void st_rec4(int16_t* p, uint2 v) { *(uint2*)p = v; }
 
 // The lane id.  With NH_OPAQUE_LANE (A/B builds) it is opaque to the compiler
@@ -248,10 +259,10 @@ __device__ __forceinline__ void ctu_chain(const CtuArgs& a, int16_t* s_img, int3
 // OST: levels and recon go to the group's LDS output images (olvl / orec: strip
 // sw's rows of SW at sw * CTB * SW), written out in whole rows after the
 // group's batches (strip_writeout).
-template <int N, bool DST, int CTB, bool OST = false>
+template <int N, bool DST, int CTB, bool OST = false, class LT = int32_t>
 __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_img, int16_t* s_t16, const uint16_t* list,
-                                             int cnt, int b0, const int* s_org, int32_t* __restrict__ lvl,
-                                             int16_t* __restrict__ rec, int32_t* olvl = nullptr,
+                                             int cnt, int b0, const int* s_org, LT* __restrict__ lvl,
+                                             int16_t* __restrict__ rec, LT* olvl = nullptr,
                                              int16_t* orec = nullptr) {
     using G = Strip<CTB>;
     constexpr int L2 = Log2<N>::v, S = L2 + 5, IP = G::IP, TP = G::TP, H = N / 2;
@@ -321,7 +332,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
         fwd1d_pk<N, DST>(P, y, BIAS);
     }
     if (on) {
-        int32_t* lrow = OST ? olvl + sw * (CTB * G::SW) + (ly + t) * G::SW + lx : lvl + (int64_t)(gy0 + t) * a.pitch + gx0;
+        LT* lrow = OST ? olvl + sw * (CTB * G::SW) + (ly + t) * G::SW + lx : lvl + (int64_t)(gy0 + t) * a.pitch + gx0;
 #pragma unroll
         for (int k0 = 0; k0 < N; k0 += 4) {
             int32_t L4[4];
@@ -330,7 +341,7 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
                 L4[q] = quant_s(y[k0 + q] >> S, cq.qs, cq.h_v, cq.hneg_v);
                 tl[(k0 + q) * TP + st] = (int16_t)dequant_s(L4[q], cq);
             }
-            st_lvl4(lrow + k0, make_int4(L4[0], L4[1], L4[2], L4[3]));
+            st_lvl4t(lrow + k0, L4);
         }
     }
     wave_sync();
@@ -382,10 +393,10 @@ __device__ __forceinline__ void ctu_chain_pk(const CtuArgs& a, const int16_t* s_
 // loop: every neighbour is a source sample).  OST: levels / recon into the LDS
 // output images (whole-row stores after the group); otherwise one sample per lane
 // and store straight to memory.  NM = N / 4 mosaics hold the batch's 64 / N TUs.
-template <int N, bool DST, int CTB, bool OST>
+template <int N, bool DST, int CTB, bool OST, class LT = int32_t>
 __device__ __forceinline__ void ctu_batch_mma(const CtuArgs& a, const int16_t* s_img, const uint16_t* list, int cnt,
-                                              int b0, const int* s_org, int32_t* __restrict__ lvl,
-                                              int16_t* __restrict__ rec, int32_t* olvl, int16_t* orec) {
+                                              int b0, const int* s_org, LT* __restrict__ lvl,
+                                              int16_t* __restrict__ rec, LT* olvl, int16_t* orec) {
     using G = Strip<CTB>;
     constexpr int IP = G::IP, NM = N / 4;
     using MC = MosaicCore<N, DST, NM>;
@@ -431,13 +442,13 @@ __device__ __forceinline__ void ctu_batch_mma(const CtuArgs& a, const int16_t* s
     mc.quant(cq, [&](int m, int q, int32_t L0, int32_t L1) {
         if (!onm[m]) return;
         if constexpr (OST) {
-            int32_t* o = olvl + swm[m] * (CTB * G::SW) + out_row(m, q) * G::SW + lxm[m] + mc.t;
-            o[0] = L0;
-            o[G::SW] = L1;
+            LT* o = olvl + swm[m] * (CTB * G::SW) + out_row(m, q) * G::SW + lxm[m] + mc.t;
+            o[0] = (LT)L0;
+            o[G::SW] = (LT)L1;
         } else {
-            int32_t* o = lvl + (int64_t)(s_org[2 * swm[m] + 1] + out_row(m, q)) * a.pitch + s_org[2 * swm[m]] + lxm[m] + mc.t;
-            o[0] = L0;
-            o[a.pitch] = L1;
+            LT* o = lvl + (int64_t)(s_org[2 * swm[m] + 1] + out_row(m, q)) * a.pitch + s_org[2 * swm[m]] + lxm[m] + mc.t;
+            o[0] = (LT)L0;
+            o[a.pitch] = (LT)L1;
         }
     });
     mc.inv1();
@@ -881,7 +892,7 @@ __device__ __forceinline__ void chain32_tf(const CtuArgs& a, const IMG& img, con
 
 // Shared memory of one workgroup = GS strips (a group).  Narrow kernels keep
 // the coefficient tile in int16 (half the LDS: more workgroups per CU).
-template <int CTB, bool NARROW, bool BASIS = false, int GS = 4, bool OST = false> struct CtuSmem {
+template <int CTB, bool NARROW, bool BASIS = false, int GS = 4, bool OST = false, class LT = int32_t> struct CtuSmem {
     using G = Strip<CTB>;
     struct Empty {};
     static constexpr int TILE32 = NARROW ? (GS * G::T16 + 1) / 2 : GS * G::CF;
@@ -891,7 +902,7 @@ template <int CTB, bool NARROW, bool BASIS = false, int GS = 4, bool OST = false
     int cnt[GS][4], org[2 * GS], next, wide[GS];
     std::conditional_t<BASIS, BasisH, Empty> basis;   // ctu_chain32_h's f16 bases
     // OST: the group's level / recon images, strip-major rows of SW (whole-row stores at the end)
-    __attribute__((aligned(16))) int32_t olvl[OST ? GS * CTB * G::SW : 4];
+    __attribute__((aligned(16))) LT olvl[OST ? GS * CTB * G::SW : 8];
     __attribute__((aligned(16))) int16_t orec[OST ? GS * CTB * G::SW : 8];
 };
 
@@ -1046,16 +1057,29 @@ __device__ __forceinline__ bool strip_store(const StripLoad<CTB>& ld, int16_t* i
 // OST: a strip's level / recon rows from the group's LDS images to the plane in
 // whole rows -- a wave instruction writes 1 KiB of contiguous row segments
 // (16 B per lane) instead of 16-128 B pieces of N rows.
-template <int CTB>
-__device__ __forceinline__ void strip_writeout(const CtuArgs& a, int sx0, int sy0, const int32_t* ol, const int16_t* orr,
-                                               int32_t* lvl, int16_t* rec) {
+template <int CTB, class LT = int32_t>
+__device__ __forceinline__ void strip_writeout(const CtuArgs& a, int sx0, int sy0, const LT* ol, const int16_t* orr,
+                                               LT* lvl, int16_t* rec) {
     constexpr int SW = Strip<CTB>::SW;
     const int lane = threadIdx.x & 63, w = a.w, h = a.h;
     const int64_t pitch = a.pitch;
+    if constexpr (sizeof(LT) == 4) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {   // CTB * SW int32 = 256 pieces of 16 B
-        const int c = 64 * i + lane, r = c / (SW / 4), x = 4 * (c % (SW / 4));
-        if (sy0 + r < h && sx0 + x < w) st_lvl4(lvl + (int64_t)(sy0 + r) * pitch + sx0 + x, *(const int4*)&ol[r * SW + x]);
+        for (int i = 0; i < 4; ++i) {   // CTB * SW int32 = 256 pieces of 16 B
+            const int c = 64 * i + lane, r = c / (SW / 4), x = 4 * (c % (SW / 4));
+            if (sy0 + r < h && sx0 + x < w) st_lvl4(lvl + (int64_t)(sy0 + r) * pitch + sx0 + x, *(const int4*)&ol[r * SW + x]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {   // CTB * SW int16 (compact levels) = 128 pieces of 16 B
+            const int c = 64 * i + lane, r = c / (SW / 8), x = 8 * (c % (SW / 8));
+            if (sy0 + r < h && sx0 + x < w) {
+                const uint4 v = *(const uint4*)&ol[r * SW + x];
+                LT* p = lvl + (int64_t)(sy0 + r) * pitch + sx0 + x;
+                if (sx0 + x + 8 <= w) *(uint4*)p = v;
+                else *(uint2*)p = make_uint2(v.x, v.y);   // w % 4 == 0: the last 4 levels of a row
+            }
+        }
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {   // CTB * SW int16 = 128 pieces of 16 B
@@ -1134,9 +1158,11 @@ __global__ void __launch_bounds__(64 * GS) k_ctu_plan(CtuArgs a) {
 // the TU map (bit 7 of each strip's origin byte) for k_ctu_wide.
 // !NARROW: the 32-bit chain, any int16 input.
 // Returns with the workgroup's waves in the batch loop's exit (no barrier).
-template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, bool OST = false, bool PLAN = false, class Prefetch>
+// LT: the level type (int16_t: config 4's compact levels, narrow groups only).
+template <int CTB, bool LUMA, bool NARROW, bool MFMA32, int GS, bool OST = false, bool PLAN = false,
+          class LT = int32_t, class Prefetch>
 __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
-                                          CtuSmem<CTB, NARROW, NARROW && MFMA32 && !(NH_CTU_TF32 && !OST), GS, OST>& sm,
+                                          CtuSmem<CTB, NARROW, NARROW && MFMA32 && !(NH_CTU_TF32 && !OST), GS, OST, LT>& sm,
                                           StripLoad<CTB>& ld,
                                           Prefetch&& prefetch) {
     using G = Strip<CTB>;
@@ -1144,8 +1170,9 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
     const int wv = threadIdx.x >> 6, lane = opaque_lane();
     int sx0, sy0;
     const bool valid = strip_of<CTB, GS>(a, grp, wv, sx0, sy0);
+    static_assert(NARROW || sizeof(LT) == 4, "the 32-bit chain writes int32 levels");
     const int64_t poff = plane_off(a, pz);
-    int32_t* lvl = a.lvl + poff;
+    LT* lvl = (LT*)a.lvl + poff;
     int16_t* rec = a.rec + poff;
     const int pid = a.plane_id + (pz % a.ppg);
     const int w = a.w, h = a.h;
@@ -1244,9 +1271,9 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
     const int total = n32 + n16 + n8 + n4;
 #define NH_CHAIN(N, DST, L, B)                                                                              \
     if constexpr (NARROW && N <= 16 && (OST ? NH_CTU_MOSAIC >= 1 : NH_CTU_MOSAIC >= 2))                    \
-        ctu_batch_mma<N, DST, CTB, OST>(a, sm.img, sm.list[L], cnt[L], B, sm.org, lvl, rec, sm.olvl, sm.orec); \
+        ctu_batch_mma<N, DST, CTB, OST, LT>(a, sm.img, sm.list[L], cnt[L], B, sm.org, lvl, rec, sm.olvl, sm.orec); \
     else if constexpr (NARROW)                                                                              \
-        ctu_chain_pk<N, DST, CTB, OST>(a, sm.img, (int16_t*)sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec, \
+        ctu_chain_pk<N, DST, CTB, OST, LT>(a, sm.img, (int16_t*)sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec, \
                                        sm.olvl, sm.orec);                                                   \
     else                                                                                                    \
         ctu_chain<N, DST, CTB>(a, sm.img, sm.tile, sm.list[L], cnt[L], B, sm.org, lvl, rec);
@@ -1301,7 +1328,7 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
 #undef NH_CHAIN
     if constexpr (OST) {   // every TU of the group is coded: each wave writes its strip out in whole rows
         __syncthreads();
-        if (valid) strip_writeout<CTB>(a, sx0, sy0, sm.olvl + wv * (CTB * G::SW), sm.orec + wv * (CTB * G::SW), lvl, rec);
+        if (valid) strip_writeout<CTB, LT>(a, sx0, sy0, sm.olvl + wv * (CTB * G::SW), sm.orec + wv * (CTB * G::SW), lvl, rec);
     }
 }
 
@@ -1312,12 +1339,12 @@ __device__ __forceinline__ void ctu_group(const CtuArgs& a, int grp, int pz,
 // WAVES: the occupancy floor (waves/SIMD) the registers are allocated for.
 // PLAN: the groups' TUs from k_ctu_plan's records (a.plan) instead of classified per group.
 template <int CTB, bool LUMA, bool MFMA32 = false, int PERSIST = 0, int WAVES = 5, int GS = 4, bool OST = false,
-          bool PLAN = false>
+          bool PLAN = false, class LT = int32_t>
 __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WAVES))) k_ctu_open(CtuArgs a, int items) {
     static_assert(!PLAN || (GS == 4 && PERSIST == 0), "plan records: groups of 4 strips, one group per workgroup");
     // (the transposition-free 32x32 chain reads its bases from the constant table: no LDS copy)
     constexpr bool BAS = MFMA32 && !(NH_CTU_TF32 && !OST);
-    __shared__ CtuSmem<CTB, true, BAS, GS, OST> sm;
+    __shared__ CtuSmem<CTB, true, BAS, GS, OST, LT> sm;
     if (NH_AB && (a.probe & 4)) return;   // A/B probe: the launch of the grid alone
     if constexpr (PERSIST == 0) {
         // the bases' loads issued with the strip's and written to LDS after the
@@ -1330,7 +1357,7 @@ __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WA
         }
         StripLoad<CTB> ld;
         strip_issue<CTB, GS>(a, blockIdx.x, blockIdx.y, ld);
-        ctu_group<CTB, LUMA, true, MFMA32, GS, OST, PLAN>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
+        ctu_group<CTB, LUMA, true, MFMA32, GS, OST, PLAN, LT>(a, blockIdx.x, blockIdx.y, sm, ld, [&] {
             if constexpr (BAS) {
                 if (bthr) ((uint4*)&sm.basis)[threadIdx.x] = bq;
             }
@@ -1346,7 +1373,7 @@ __global__ void __launch_bounds__(64 * GS) __attribute__((amdgpu_waves_per_eu(WA
         for (; it < items; it += gridDim.x) {
             const int nx = it + gridDim.x;
             if constexpr (PERSIST == 2) strip_issue<CTB, GS>(a, it % gcount, it / gcount, ld);
-            ctu_group<CTB, LUMA, true, MFMA32, GS, OST>(a, it % gcount, it / gcount, sm, ld, [&] {
+            ctu_group<CTB, LUMA, true, MFMA32, GS, OST, false, LT>(a, it % gcount, it / gcount, sm, ld, [&] {
                 if (PERSIST == 1 && nx < items) strip_issue<CTB, GS>(a, nx % gcount, nx / gcount, ld);
             });
             __syncthreads();   // every wave done with this group's LDS
@@ -1385,7 +1412,16 @@ __global__ void __launch_bounds__(256) k_ctu_wide(CtuArgs a) {
         mask &= mask - 1;
         StripLoad<CTB> ld;
         strip_issue<CTB>(a, g0 + b, pz, ld);
-        ctu_group<CTB, LUMA, false, MFMA32, 4>(a, g0 + b, pz, sm, ld, [] {});
+        if (a.spill) {   // compact levels: int32 levels into the spill plane, a marker at every strip origin
+            CtuArgs aw = a;
+            aw.lvl = a.spill;
+            ctu_group<CTB, LUMA, false, MFMA32, 4>(aw, g0 + b, pz, sm, ld, [] {});
+            int sx0, sy0;
+            if (strip_of<CTB>(a, g0 + b, threadIdx.x >> 6, sx0, sy0) && (threadIdx.x & 63) == 0)
+                a.lvl_c[plane_off(a, pz) + (int64_t)sy0 * a.pitch + sx0] = kCtuSpillMark;
+        } else {
+            ctu_group<CTB, LUMA, false, MFMA32, 4>(a, g0 + b, pz, sm, ld, [] {});
+        }
         __syncthreads();
     }
 }
@@ -1595,18 +1631,30 @@ static int ensure_basis_ctu() {
 // Launches k_ctu_open over CTU rows [row0, row1) of every plane of the set.
 // Returns NH_EVALUE when the layout does not allow the kernel's vector accesses
 // (8-B rows / 16-B level rows): the caller then takes the per-size path.
-int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu, const nh_plane_set* set, int ctb,
+// lvl_bytes = 2: config 4's compact levels (int16 level plane `lvl`, int32 `spill` for the wide groups
+// k_ctu_wide codes, a marker at each of their strip origins; CTB 16 / 32 only, 16-B aligned rows).
+int ctu_open_launch(const int16_t* src, void* lvl, int16_t* rec, uint8_t* tu, const nh_plane_set* set, int ctb,
                     int plane_id, uint32_t seed, int is_luma, int row0, int row1, const QuantParams* q, int dqs,
-                    int dq_per, hipStream_t s) {
+                    int dq_per, hipStream_t s, int lvl_bytes, int32_t* spill) {
     const int64_t planes = (int64_t)set->planes_per_group * set->num_groups;
     if ((set->pitch & 3) || ((set->base | set->plane_stride | set->group_stride) & 3) ||
         (((uintptr_t)src | (uintptr_t)rec) & 7) || ((uintptr_t)lvl & 15))
+        return NH_EVALUE;
+    const bool compact = lvl_bytes == 2;
+    if (compact && ((ctb != 16 && ctb != 32) || (set->pitch & 7) || ((set->base | set->plane_stride | set->group_stride) & 7) ||
+                    !spill || ((uintptr_t)spill & 15)))
         return NH_EVALUE;
     const int rc = ensure_basis_ctu();
     if (rc) return rc;
     CtuArgs a{};
     a.src = src + set->base;
-    a.lvl = lvl + set->base;
+    if (compact) {
+        a.lvl = (int32_t*)((int16_t*)lvl + set->base);   // k_ctu_open<.., int16_t> reads it as int16_t*
+        a.lvl_c = (int16_t*)lvl + set->base;
+        a.spill = spill + set->base;
+    } else {
+        a.lvl = (int32_t*)lvl + set->base;
+    }
     a.rec = rec + set->base;
     a.tu = tu;
     a.group_stride = set->group_stride;
@@ -1701,7 +1749,12 @@ int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu,
         int rc3;
         launch_plan(ctb_c);
         using G4 = std::integral_constant<int, 4>;
-        if constexpr (NH_AB != 0) {
+        if (compact) {   // (CTB 16 / 32: the configurations' CTB sizes)
+            if constexpr (C == 32) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4, false, false, int16_t>, G4{});
+            else if constexpr (C == 16) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true, false, int16_t>, G4{});
+            else rc3 = NH_EVALUE;
+            k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
+        } else if constexpr (NH_AB != 0) {
             const bool m = M32 && t32 != 0;
             const bool ost_on = (ost_knob & (L ? 1 : 2)) != 0;
             if (m) rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, M32, 1>, G4{})

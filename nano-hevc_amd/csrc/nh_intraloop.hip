@@ -2587,9 +2587,9 @@ extern "C" int64_t nh_tu_workspace_bytes(int w, int h, int ctb) {
 
 namespace nh {
 // nh_ctu.hip: config 4 as one CTU-granular launch (NH_EVALUE: layout needs the per-size path)
-int ctu_open_launch(const int16_t* src, int32_t* lvl, int16_t* rec, uint8_t* tu, const nh_plane_set* set, int ctb,
+int ctu_open_launch(const int16_t* src, void* lvl, int16_t* rec, uint8_t* tu, const nh_plane_set* set, int ctb,
                     int plane_id, uint32_t seed, int is_luma, int row0, int row1, const QuantParams* q, int dqs,
-                    int dq_per, hipStream_t s);
+                    int dq_per, hipStream_t s, int lvl_bytes = 4, int32_t* spill = nullptr);
 // nh_tc32.hip: config 4's 32x32 TUs on the int8 matrix cores
 int tc32_mfma_tree(const int16_t* src, int w, int h, int pitch, const QuantParams& qp, int dq_scale, int dq_per,
                    int32_t* lvl, int16_t* rec, uint8_t* tu, int bw, int n, const TreeArgs& ta, unsigned planes,
@@ -2664,6 +2664,91 @@ extern "C" int nh_tu_pipeline_planes(const int16_t* d_src, const nh_plane_set* s
     // (A/B: forking the four size launches onto side streams with events was
     // slower -- 0.066 -> 0.068-0.071 ms per frame batched, 0.157 -> 0.275 one
     // plane at a time: profiles/r01/cfg4/cfg4_streams_*.jsonl)
+    NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+// Config 4 with COMPACT levels (include/nanohevc.h): the CTU-granular launch only.
+extern "C" int nh_tu_pipeline_planes_compact(const int16_t* d_src, const nh_plane_set* set, int ctb, int plane_id,
+                                             uint32_t seed, int qp, int is_luma, int row0, int row1, int16_t* d_lvl,
+                                             int32_t* d_spill, int16_t* d_recon, uint8_t* d_tu, void* stream) {
+    if (!d_src || !set || !d_lvl || !d_spill || !d_recon || !d_tu) return NH_EARG;
+    const int w = set->width, h = set->height, pitch = set->pitch;
+    const int64_t planes = (int64_t)set->planes_per_group * set->num_groups;
+    if (pitch < w || w <= 0 || h <= 0 || set->planes_per_group < 1 || planes < 0 || planes > 65535) return NH_EARG;
+    if ((w & 3) || (h & 3) || w > 65535 || h > 65535) return NH_EARG;
+    if (ctb != 16 && ctb != 32) {
+        set_error("tu_pipeline_planes_compact: CTB 16 or 32");
+        return NH_EARG;
+    }
+    if ((pitch & 7) || ((set->base | set->plane_stride | set->group_stride) & 7) ||
+        (((uintptr_t)d_lvl | (uintptr_t)d_spill) & 15) || (((uintptr_t)d_src | (uintptr_t)d_recon) & 7)) {
+        set_error("tu_pipeline_planes_compact: 8-sample aligned pitch / base / strides, 16-B aligned level buffers");
+        return NH_EARG;
+    }
+    if (!planes) return NH_OK;
+    hipStream_t s = as_stream(stream);
+    const int rows = (h + ctb - 1) / ctb;
+    if (row0 < 0) row0 = 0;
+    if (row1 > rows) row1 = rows;
+    if (row1 <= row0) return NH_OK;
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    QuantParams q4[4];
+    for (int k = 0; k < 4; ++k) q4[k] = qparams(qp, k + 2, true);
+    const int rc = ctu_open_launch(d_src, d_lvl, d_recon, d_tu, set, ctb, plane_id, seed, is_luma, row0, row1, q4,
+                                   dequant_scale(rem), per, s, 2, d_spill);
+    if (rc == NH_EVALUE) {
+        set_error("tu_pipeline_planes_compact: layout outside the CTU-granular launch's");
+        return NH_EARG;
+    }
+    return rc;
+}
+
+// Config 4 compact levels -> the reference's int32 levels, rows [row0 * ctb, row1 * ctb): from the
+// spill plane where the sample's strip (CTB rows x 1024 / CTB columns) holds the marker at its
+// origin, else the int16 level widened.  4 samples per thread (w % 4 == 0).
+__global__ void __launch_bounds__(256) k_tu_widen(const int16_t* __restrict__ lc, const int32_t* __restrict__ spill,
+                                                  int32_t* __restrict__ out, int64_t base, int64_t group_stride,
+                                                  int64_t plane_stride, int ppg, int w4, int y0, int ny, int pitch,
+                                                  int ctb, int sw) {
+    const int pz = blockIdx.y, gz = pz / ppg, cz = pz - gz * ppg;
+    const int64_t poff = base + (int64_t)gz * group_stride + (int64_t)cz * plane_stride;
+    const int64_t n = (int64_t)w4 * ny;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int yy = (int)(i / w4), x = 4 * (int)(i - (int64_t)yy * w4), y = y0 + yy;
+        const int64_t o = poff + (int64_t)y * pitch + x;
+        const bool sp = lc[poff + (int64_t)(y - y % ctb) * pitch + (x - x % sw)] == (int16_t)0x8000;
+        int4 v;
+        if (sp) {
+            v = *(const int4*)(spill + o);
+        } else {
+            const uint2 q = *(const uint2*)(lc + o);
+            v = make_int4((int16_t)(q.x & 0xffffu), (int16_t)(q.x >> 16), (int16_t)(q.y & 0xffffu), (int16_t)(q.y >> 16));
+        }
+        *(int4*)(out + o) = v;
+    }
+}
+
+extern "C" int nh_tu_levels_widen(const int16_t* d_lvl, const int32_t* d_spill, const nh_plane_set* set, int ctb,
+                                  int row0, int row1, int32_t* d_out, void* stream) {
+    if (!d_lvl || !d_spill || !d_out || !set) return NH_EARG;
+    const int w = set->width, h = set->height, pitch = set->pitch;
+    const int64_t planes = (int64_t)set->planes_per_group * set->num_groups;
+    if (pitch < w || w <= 0 || h <= 0 || set->planes_per_group < 1 || planes < 0 || planes > 65535 || (w & 3) ||
+        (pitch & 3) || ((set->base | set->plane_stride | set->group_stride) & 3) || (ctb != 16 && ctb != 32) ||
+        (((uintptr_t)d_spill | (uintptr_t)d_out) & 15) || ((uintptr_t)d_lvl & 7))
+        return NH_EARG;
+    const int rows = (h + ctb - 1) / ctb;
+    if (row0 < 0) row0 = 0;
+    if (row1 > rows) row1 = rows;
+    if (row1 <= row0 || !planes) return NH_OK;
+    const int y0 = row0 * ctb, ny = std::min(h, row1 * ctb) - y0;
+    const int64_t items = (int64_t)(w / 4) * ny;
+    const dim3 grid((unsigned)std::min<int64_t>((items + 255) / 256, 4096), (unsigned)planes);
+    k_tu_widen<<<grid, 256, 0, as_stream(stream)>>>(d_lvl, d_spill, d_out, set->base, set->group_stride,
+                                                   set->plane_stride, set->planes_per_group, w / 4, y0, ny, pitch, ctb,
+                                                   1024 / ctb);
     NH_HIP(hipGetLastError());
     return NH_OK;
 }

@@ -78,6 +78,8 @@ SIGNATURES = {
     "nh_tu_workspace_bytes": ([I32, I32, I32], I64),
     "nh_tu_pipeline_plane": ([P, I32, I32, I32, I32, I32, U32, I32, I32, I32, I32, P, P, P, P, VP], I32),
     "nh_tu_pipeline_planes": ([P, C.POINTER(PlaneSet), I32, I32, U32, I32, I32, I32, I32, P, P, P, VP], I32),
+    "nh_tu_pipeline_planes_compact": ([P, C.POINTER(PlaneSet), I32, I32, U32, I32, I32, I32, I32, P, P, P, P, VP], I32),
+    "nh_tu_levels_widen": ([P, P, C.POINTER(PlaneSet), I32, I32, I32, P, VP], I32),
     "nh_tc32_plane": ([P, I32, I32, I32, I32, P, P, I32, VP], I32),
     "nh_tc32_planes": ([P, C.POINTER(PlaneSet), I32, I32, P, P, I32, VP], I32),
     "nh_tc32_planes_compact": ([P, C.POINTER(PlaneSet), I32, I32, P, I32, P, P, VP], I32),

@@ -9,6 +9,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
   intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
+  tu_pipeline_planes_compact / tu_levels_widen -- config 4 with exact int16 levels (+ int32 spill)
   tc32_plane          -- config 5: 32x32 chain, butterfly or matrix-core variants
   tc32_planes         -- config 5 over a frame stream (one MFMA launch per plane set)
   tc32_planes_compact / tc32_levels_widen -- config 5 with exact int16 / int8 levels (+ int32 spill)
@@ -355,6 +356,59 @@ def tu_pipeline_planes(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, 
                                             int(qp), int(bool(is_luma)), int(row0), int(min(row1, 1 << 30)),
                                             lvl.data_ptr(), rec.data_ptr(), tu.data_ptr(), C.c_void_p(_stream(stream, src.device))))
     return lvl, rec, tu
+
+
+def tu_pipeline_planes_compact(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int = 32,
+                               is_luma: bool = True, row0: int = 0, row1: int = 1 << 30, lvl=None, rec=None, tu=None,
+                               spill=None, stream=None):
+    """``tu_pipeline_planes`` with COMPACT levels: int16 levels in the source
+    layout (exact: |level| <= 408 for an 8-bit TU at every QP and size,
+    tools/packed_bounds.py level_bounds) -- 6 instead of 8 bytes per sample.
+    Strips with a sample outside [0, 255] (the 32-bit chain) write their int32
+    levels into ``spill`` (int32, source layout; allocated uninitialised when
+    None) and -32768 at each strip origin.  CTB 16 / 32.  Returns (lvl int16, rec,
+    tu, spill); ``tu_levels_widen`` gives the int32 levels of ``tu_pipeline_planes``."""
+    torch = _torch()
+    _need(src, torch.int16, "tu_pipeline_planes_compact(src)")
+    sets_fit_rows([pset], src.numel(), int(row0) * ctb - 1, min(int(row1), 1 << 30) * ctb, "tu_pipeline_planes_compact")
+    planes = pset.planes_per_group * pset.num_groups
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=src.device)
+    if tu is None:
+        tu = torch.zeros((planes, pset.height // 4, pset.width // 4), dtype=torch.uint8, device=src.device)
+    if spill is None:
+        spill = torch.empty(src.shape, dtype=torch.int32, device=src.device)
+    _need(lvl, torch.int16, "tu_pipeline_planes_compact(lvl)")
+    _need(rec, torch.int16, "tu_pipeline_planes_compact(rec)")
+    _need(tu, torch.uint8, "tu_pipeline_planes_compact(tu)")
+    _need(spill, torch.int32, "tu_pipeline_planes_compact(spill)")
+    if min(lvl.numel(), rec.numel(), spill.numel()) < src.numel() or \
+            tu.numel() < planes * (pset.height // 4) * (pset.width // 4):
+        raise ValueError("tu_pipeline_planes_compact: output too small")
+    check(_lib.load().nh_tu_pipeline_planes_compact(
+        src.data_ptr(), C.byref(pset), int(ctb), int(plane_id), int(seed) & 0xffffffff, int(qp), int(bool(is_luma)),
+        int(row0), int(min(row1, 1 << 30)), lvl.data_ptr(), spill.data_ptr(), rec.data_ptr(), tu.data_ptr(),
+        C.c_void_p(_stream(stream, src.device))), "tu_pipeline_planes_compact")
+    return lvl, rec, tu, spill
+
+
+def tu_levels_widen(lvl, spill, pset: PlaneSet, ctb: int, row0: int = 0, row1: int = 1 << 30, out=None, stream=None):
+    """(int16 levels, spill) of ``tu_pipeline_planes_compact`` -> the reference's
+    int32 levels of CTU rows [row0, row1) of every plane of ``pset``."""
+    torch = _torch()
+    _need(lvl, torch.int16, "tu_levels_widen(lvl)")
+    _need(spill, torch.int32, "tu_levels_widen(spill)")
+    if out is None:
+        out = torch.zeros(lvl.shape, dtype=torch.int32, device=lvl.device)
+    _need(out, torch.int32, "tu_levels_widen(out)")
+    sets_fit_rows([pset], min(lvl.numel(), spill.numel(), out.numel()), int(row0) * ctb,
+                  min(int(row1), 1 << 30) * ctb, "tu_levels_widen")
+    check(_lib.load().nh_tu_levels_widen(lvl.data_ptr(), spill.data_ptr(), C.byref(pset), int(ctb), int(row0),
+                                         int(min(row1, 1 << 30)), out.data_ptr(), C.c_void_p(_stream(stream, lvl.device))),
+          "tu_levels_widen")
+    return out
 
 
 def _tu_closed_launch(src, pset: PlaneSet, ctb: int, plane_id: int, seed: int, qp: int, is_luma: bool,

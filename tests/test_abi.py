@@ -117,3 +117,19 @@ def test_tc32_layout_checks_precede_any_device_call():
     assert L.nh_tc32_planes_compact(fake, C.byref(odd), 1, 30, fake, 1, fake, fake, None) == _lib.NH_EARG
     assert L.nh_tc32_planes_compact(fake, C.byref(odd), 1, 30, fake, 2, None, fake, None) == _lib.NH_EARG
     assert L.nh_tc32_planes_compact(fake, C.byref(odd), 1, 30, fake, 4, fake, fake, None) == _lib.NH_EARG
+
+
+def test_tu_compact_layout_checks_precede_any_device_call():
+    """nh_tu_pipeline_planes_compact refuses CTB sizes other than 16 / 32 and rows
+    that are not 8-sample aligned on the host, before any HIP call."""
+    from nano_hevc import _lib
+    from nano_hevc._lib import PlaneSet
+    L = _lib.load()
+    fake = C.c_void_p(1 << 20)
+    ok = PlaneSet(0, 0, 0, 64, 64, 64, 1, 1, 0)
+    assert L.nh_tu_pipeline_planes_compact(fake, C.byref(ok), 8, 0, 1, 30, 1, 0, 99, fake, fake, fake, fake,
+                                           None) == _lib.NH_EARG
+    odd = PlaneSet(0, 0, 0, 100, 64, 100, 1, 1, 0)
+    assert L.nh_tu_pipeline_planes_compact(fake, C.byref(odd), 32, 0, 1, 30, 1, 0, 99, fake, fake, fake, fake,
+                                           None) == _lib.NH_EARG
+    assert L.nh_tu_levels_widen(fake, fake, C.byref(ok), 8, 0, 99, fake, None) == _lib.NH_EARG

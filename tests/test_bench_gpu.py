@@ -68,6 +68,9 @@ def test_bench_config4_line():
     assert d["cpu_baseline"]["cores"] > 1 and d["cpu_baseline"]["value_1thread"] > 0
     assert d["config"]["source_fraction_rank0"] == 1.0
     assert d["compute_only_sum_samples_per_s"] >= d["value"] * 0.95
+    # the default: exact compact int16 levels on the device (widened for the CPU check above)
+    rf = d["roofline"]
+    assert d["config"]["levels"].startswith("int16") and rf.get("hbm", rf)["bytes_per_sample"] == 6.0625
     if os.path.exists(os.path.join(ROOT, "profiles", "valu_roofline.json")):   # committed VALU roofline inputs
         # the VALU view leads, from counts of THIS build's kernel sources (strict; the CPU
         # suite's test_valu_profile_matches_the_tree fails first when the sources moved on)

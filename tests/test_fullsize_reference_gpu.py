@@ -101,6 +101,37 @@ def test_cfg4_4k_equals_reference(ref, torch_dev):
         off += ph * pw
 
 
+def test_cfg4_4k_compact_levels_equal_reference(ref, torch_dev):
+    """Config 4 with compact int16 levels (tu_pipeline_planes_compact), widened back
+    to int32: every plane of the 4K frame hashes to the reference's levels, recon
+    and TU map."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = FI.cfg4_frame()
+    h, w = planes[0].shape
+    buf = np.concatenate([p.reshape(-1) for p in planes])
+    d = torch.from_numpy(buf).cuda()
+    sy, suv = gpu.yuv420_plane_sets(1, w, h)
+    lc = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+    spill = torch.empty(d.shape, dtype=torch.int32, device="cuda")
+    _, _, tuy, _ = gpu.tu_pipeline_planes_compact(d, sy, 32, 0, FI.CFG4_SEED, FI.CFG4_QP, True, lvl=lc, rec=rec,
+                                                  spill=spill)
+    _, _, tuc, _ = gpu.tu_pipeline_planes_compact(d, suv, 16, 1, FI.CFG4_SEED, FI.CFG4_QP, False, lvl=lc, rec=rec,
+                                                  spill=spill)
+    lvl = gpu.tu_levels_widen(lc, spill, sy, 32)
+    lvl = gpu.tu_levels_widen(lc, spill, suv, 16, out=lvl)
+    lvl, rec, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    off = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        e = ref[f"cfg4_p{k}"]
+        assert sha(lvl[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], k
+        assert sha(rec[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
+        assert sha(tuy[0] if k == 0 else tuc[k - 1]) == e["tu"], k
+        off += ph * pw
+
+
 def test_cfg2_4k_yuv420_equals_reference(ref, torch_dev):
     """The metric's own workload: every 8x8 block of a 4K YUV420 residual frame
     through forward_transform + quantize_block (transform.py:154-196,

@@ -1178,3 +1178,66 @@ def test_tc32_compact_levels_refuse_bad_layouts(nh, torch_dev):
     gpu.tc32_planes_compact(d, sets, 30, torch.int16)
     with pytest.raises(TypeError):
         gpu.tc32_planes_compact(d, sets, 30, torch.int32)
+
+
+@pytest.mark.parametrize("qp", [0, 22, 51])
+def test_tu_compact_levels_equal_int32_path(nh, torch_dev, qp):
+    """Config 4 with compact int16 levels over a ragged YUV420 stream with a wide
+    frame (int16 extremes: every group on the 32-bit chain) and a frame with one
+    9-bit luma sample and one negative chroma sample (one wide group each among 8-bit
+    ones): the widened levels, recon and TU maps equal tu_pipeline_planes' (int32);
+    every 8-bit strip's int16 levels are the int32 ones (|level| <= 408), every wide
+    strip has the marker at its origin; a CTU-row band (row0, row1) widens alone;
+    the oracle checks the mixed frame's luma."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(70 + qp)
+    nf, w, h = 3, 208, 136                              # ragged CTUs; chroma pitch 104: 8-sample aligned
+    sets = gpu.yuv420_plane_sets(nf, w, h)
+    fe = gpu.yuv420_frame_elems(w, h)
+    buf = np.clip(100 + rng.integers(-100, 101, size=nf * fe), 0, 255).astype(np.int16)
+    buf[fe:2 * fe] = rng.integers(-32768, 32768, size=fe)   # frame 1: wide everywhere
+    buf[2 * fe + 70 * w + 150] = 300                         # frame 2: one wide luma strip
+    buf[2 * fe + w * h + 10 * (w // 2) + 5] = -3             # ... and one wide U strip
+    d = torch.from_numpy(buf).cuda()
+    for (ps, ctb, pid, luma) in ((sets[0], 32, 0, True), (sets[1], 16, 1, False)):
+        lvl = torch.zeros(d.shape, dtype=torch.int32, device="cuda")
+        rec = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+        _, _, tu = gpu.tu_pipeline_planes(d, ps, ctb, pid, 99, qp, luma, lvl=lvl, rec=rec)
+        lc = torch.full(d.shape, 7, dtype=torch.int16, device="cuda")
+        rc = torch.zeros(d.shape, dtype=torch.int16, device="cuda")
+        _, _, tuc, spill = gpu.tu_pipeline_planes_compact(d, ps, ctb, pid, 99, qp, luma, lvl=lc, rec=rc)
+        wide = gpu.tu_levels_widen(lc, spill, ps, ctb)
+        assert torch.equal(tu, tuc) and torch.equal(rec, rc)
+        lv, wv, cv = lvl.cpu().numpy(), wide.cpu().numpy(), lc.cpu().numpy()
+        sw = 1024 // ctb
+        for p_ in range(ps.planes_per_group * ps.num_groups):
+            g, c = divmod(p_, ps.planes_per_group)
+            off = ps.base + g * ps.group_stride + c * ps.plane_stride
+            L = lv[off:off + ps.height * ps.pitch].reshape(ps.height, ps.pitch)[:, :ps.width]
+            W = wv[off:off + ps.height * ps.pitch].reshape(ps.height, ps.pitch)[:, :ps.width]
+            Cc = cv[off:off + ps.height * ps.pitch].reshape(ps.height, ps.pitch)[:, :ps.width]
+            S = buf[off:off + ps.height * ps.pitch].reshape(ps.height, ps.pitch)[:, :ps.width]
+            assert np.array_equal(W, L), (ctb, p_)
+            for sy0 in range(0, ps.height, ctb):          # strips in groups of 4 share the narrow decision
+                for sx0 in range(0, ps.width, sw):
+                    blk = Cc[sy0:sy0 + ctb, sx0:sx0 + sw]
+                    if blk[0, 0] == -32768:
+                        continue
+                    assert np.array_equal(blk, L[sy0:sy0 + ctb, sx0:sx0 + sw]) and np.abs(blk).max() <= 408
+            if p_ == 0 and luma:                          # frame 0 is 8-bit: no marker anywhere
+                assert not (Cc[::ctb, ::sw] == -32768).any()
+            if p_ == 1 and luma:                          # frame 1: every strip marked
+                assert (Cc[::ctb, ::sw] == -32768).all()
+            if p_ == 2 and luma:
+                el, er, et = O.tu_pipeline_plane(S.copy(), 32, 0, 99, qp, True)
+                assert np.array_equal(W, el)
+        # a band of CTU rows widens alone
+        band = gpu.tu_levels_widen(lc, spill, ps, ctb, 1, 3)
+        bv = band.cpu().numpy()
+        for p_ in range(ps.planes_per_group * ps.num_groups):
+            g, c = divmod(p_, ps.planes_per_group)
+            off = ps.base + g * ps.group_stride + c * ps.plane_stride
+            B = bv[off:off + ps.height * ps.pitch].reshape(ps.height, ps.pitch)[:, :ps.width]
+            L = lv[off:off + ps.height * ps.pitch].reshape(ps.height, ps.pitch)[:, :ps.width]
+            assert np.array_equal(B[ctb:3 * ctb], L[ctb:3 * ctb]) and not B[:ctb].any() and not B[3 * ctb:].any()

@@ -109,7 +109,10 @@ def main():
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--cfg5-frames", type=int, default=8, help="frames of the batched cfg5 stream")
-    ap.add_argument("--cfg5-levels", default="int32,int16,int8", help="5b: level dtypes (int16 / int8: compact levels)")
+    ap.add_argument("--cfg5-levels", default=None,
+                    help="5b: level dtypes (default from the configs: 5b int32, 5bc int16, 5bc8 int8 compact levels)")
+    ap.add_argument("--cfg4-levels", default=None,
+                    help="4b: level dtypes (default from the configs: 4b int32, 4bc int16 compact levels)")
     ap.add_argument("--closed4-frames", type=int, default=64, help="frames of the closed-loop cfg4 stream")
     ap.add_argument("--closed4-seq", action="store_true", help="closed4: luma then chroma (default: concurrent wavefronts)")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
@@ -132,6 +135,16 @@ def main():
     knobs = {k: v for k, v in os.environ.items() if k.startswith("NH_")}
     torch.cuda.set_device(0)
     cfgs = {int(c) if c.isdigit() else c for c in args.configs.split(",")}
+    # the batched configs 4 and 5 by level type: 4b / 5b the reference's int32 levels, 4bc / 5bc the exact
+    # int16 compact levels, 5bc8 int8 (each its own kernel instance: one profiler run per config name)
+    if args.cfg4_levels is None:
+        args.cfg4_levels = ",".join([n for c, n in (("4b", "int32"), ("4bc", "int16")) if c in cfgs])
+    if args.cfg5_levels is None:
+        args.cfg5_levels = ",".join([n for c, n in (("5b", "int32"), ("5bc", "int16"), ("5bc8", "int8")) if c in cfgs])
+    if args.cfg4_levels:
+        cfgs.add("4b")
+    if args.cfg5_levels:
+        cfgs.add("5b")
 
     if 3 in cfgs:
         W, H = 1920, 1080
@@ -182,20 +195,42 @@ def main():
         tuy = torch.zeros((nf, H // 4, W // 4), dtype=torch.uint8, device="cuda")
         tuc = torch.zeros((2 * nf, H // 8, W // 8), dtype=torch.uint8, device="cuda")
 
-        def run4b():
-            gpu.tu_pipeline_planes(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy)
-            gpu.tu_pipeline_planes(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc)
-        ms = timed(run4b, args.reps)
-        samples = stream.numel()
-        print(json.dumps({"config": "cfg4 batched: 16 x 4K YUV420 frames, mixed 4/8/16/32 TUs per CTU, 8 launches",
-                          "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf, "frames_per_s": nf / ms * 1e3,
-                          "samples_per_s": samples / ms * 1e3,
-                          "bytes_per_sample": 8, "achieved_GBps": samples * 8 / ms / 1e6,
-                          "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H]), "knobs": knobs,
-                          "roofline": valu_roofline("cfg4_4k_yuv420", ms / nf),
-                          "out_digest": [int(lv.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item()),
-                                         int((lv.to(torch.int64) * torch.arange(lv.numel(), device="cuda") % 1000003)
-                                             .sum().item())]}), flush=True)
+        spill = None
+        for ldt in args.cfg4_levels.split(","):
+            # int32: the reference's level dtype; int16: the exact compact levels (|level| <= 408 for an
+            # 8-bit TU) plus the int32 spill plane, widened afterwards for the digest
+            if ldt == "int32":
+                lvx = lv
+
+                def run4b():
+                    gpu.tu_pipeline_planes(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy)
+                    gpu.tu_pipeline_planes(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc)
+            else:
+                lc = torch.zeros(stream.shape, dtype=torch.int16, device="cuda")
+                if spill is None:
+                    spill = torch.empty(stream.shape, dtype=torch.int32, device="cuda")
+
+                def run4b():
+                    gpu.tu_pipeline_planes_compact(stream, sy, 32, 0, 1234, args.qp, True, lvl=lc, rec=rc, tu=tuy,
+                                                   spill=spill)
+                    gpu.tu_pipeline_planes_compact(stream, suv, 16, 1, 1234, args.qp, False, lvl=lc, rec=rc, tu=tuc,
+                                                   spill=spill)
+            ms = timed(run4b, args.reps)
+            if ldt != "int32":
+                lvx = gpu.tu_levels_widen(lc, spill, sy, 32)
+                lvx = gpu.tu_levels_widen(lc, spill, suv, 16, out=lvx)
+            samples = stream.numel()
+            bps = 8 if ldt == "int32" else 6
+            key = "cfg4_4k_yuv420" if ldt == "int32" else "cfg4_4k_yuv420_" + ldt
+            print(json.dumps({"config": "cfg4 batched: 16 x 4K YUV420 frames, mixed 4/8/16/32 TUs per CTU, 8 launches",
+                              "levels": ldt, "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
+                              "frames_per_s": nf / ms * 1e3, "samples_per_s": samples / ms * 1e3,
+                              "bytes_per_sample": bps, "achieved_GBps": samples * bps / ms / 1e6,
+                              "psnr_y_frame0": psnr_dev(stream[:W * H], rc[:W * H]), "knobs": knobs,
+                              "roofline": valu_roofline(key, ms / nf),
+                              "out_digest": [int(lvx.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item()),
+                                             int((lvx.to(torch.int64) * torch.arange(lvx.numel(), device="cuda") % 1000003)
+                                                 .sum().item())]}), flush=True)
 
     if "closed4" in cfgs:   # config 4 in closed loop: 64 4K YUV420 frames, 2 concurrent launches (CTU-row wavefronts)
         W, H, nf = 3840, 2160, args.closed4_frames

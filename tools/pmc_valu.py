@@ -49,6 +49,9 @@ CONFIGS = {
     "4b": ("cfg4_4k_yuv420", "k_ctu_open<32", 1 / 16),
     "closed4": ("cfg4_closed_4k_yuv420", "k_tu_closed_pair<3, true, 32", 1 / 64),   # (luma instance: one per launch set)
     "5b": ("cfg5_8k_yuv420", "k_tc32_hd<2", 2 / 8),
+    # round 6: the compact-level instances (int16 levels, int32 spill; one profiler run each)
+    "4bc": ("cfg4_4k_yuv420_int16", "k_ctu_open<32", 1 / 16),
+    "5bc": ("cfg5_8k_yuv420_int16", "k_tc32_hd<2", 2 / 8),
 }
 # the sources a config's kernels are compiled from: their digest goes into the
 # entry, and bench.py / tools/bench_configs.py recompute it to tell whether the
@@ -61,6 +64,8 @@ SOURCES = {
     "4b": ["nh_ctu.hip"] + _HDRS,
     "closed4": ["nh_intraloop.hip"] + _HDRS,
     "5b": ["nh_ctu.hip", "nh_tc32.hip"] + _HDRS,
+    "4bc": ["nh_ctu.hip"] + _HDRS,
+    "5bc": ["nh_ctu.hip", "nh_tc32.hip"] + _HDRS,
 }
 
 
