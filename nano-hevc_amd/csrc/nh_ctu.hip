@@ -1706,6 +1706,8 @@ int ctu_open_launch(const int16_t* src, void* lvl, int16_t* rec, uint8_t* tu, co
     // of classifying every group: 0.0342-0.0344 vs 0.0341-0.0346 ms per 4K frame, not kept
     // (profiles/r06/cfg4/ab_NH_CTU_PLAN_4b_r06f.jsonl; the classification runs under the strip loads)
     static const int plan_knob = NH_KNOB("NH_CTU_PLAN", 0);
+    static const int w4_knob = NH_KNOB("NH_CTU_W4", 0);   // A/B: int32 levels with registers for 4 waves/SIMD
+    (void)w4_knob;
     const bool plan_on = NH_AB && plan_knob != 0 && gs_knob == 4 && persist == 0;
     a.ngroups = (int)groups;
     void* plan_buf = nullptr;
@@ -1722,13 +1724,13 @@ int ctu_open_launch(const int16_t* src, void* lvl, int16_t* rec, uint8_t* tu, co
         (void)ctb_c;
 #endif
     };
-    auto launch_open = [&](auto kern, auto gs_c) -> int {
+    auto launch_open = [&](auto kern, auto gs_c, int cap_default = 0) -> int {
         constexpr int GSZ = decltype(gs_c)::value;
         const int64_t ngrp = (strips + GSZ - 1) / GSZ;
         if (ngrp * planes > INT32_MAX) return NH_EARG;
         const int items = (int)(ngrp * planes);
         const dim3 grid((unsigned)ngrp, (unsigned)planes);
-        const int cap_wgs = cap_knob > 0 ? cap_knob : GSZ == 4 ? 3 : 2;   // (CTB <= 16: the LDS allows 3 anyway)
+        const int cap_wgs = cap_knob > 0 ? cap_knob : cap_default > 0 ? cap_default : GSZ == 4 ? 3 : 2;   // (CTB <= 16: the LDS allows 3 anyway)
         if (NH_AB != 0 && persist) {
             int cus = 0, per_cu = 0;
             NH_TRY(device_cus(&cus));
@@ -1750,8 +1752,11 @@ int ctu_open_launch(const int16_t* src, void* lvl, int16_t* rec, uint8_t* tu, co
         launch_plan(ctb_c);
         using G4 = std::integral_constant<int, 4>;
         if (compact) {   // (CTB 16 / 32: the configurations' CTB sizes)
-            if constexpr (C == 32) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4, false, false, int16_t>, G4{});
-            else if constexpr (C == 16) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true, false, int16_t>, G4{});
+            // registers for 4 waves per SIMD, residency left to registers and LDS (chroma's output images
+            // are half the size: 36.8 KB, 4 workgroups per CU): 29.1-29.5 vs 32.5-32.6 us per 4K frame
+            // capped at 3 workgroups (profiles/r06/cfg4/ab_env_4bc_r06k.jsonl)
+            if constexpr (C == 32) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 4, 4, false, false, int16_t>, G4{}, 5);
+            else if constexpr (C == 16) rc3 = launch_open(k_ctu_open<C, L, M32, 0, 4, 4, true, false, int16_t>, G4{}, 5);
             else rc3 = NH_EVALUE;
             k_ctu_wide<C, L, false><<<grid_wide, 256, 0, s>>>(a);
         } else if constexpr (NH_AB != 0) {
@@ -1764,11 +1769,13 @@ int ctu_open_launch(const int16_t* src, void* lvl, int16_t* rec, uint8_t* tu, co
                          : ost_on       ? (plan_on ? launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true, true>, G4{})
                                                    : launch_open(k_ctu_open<C, L, M32, 0, 3, 4, true>, G4{}))
                          : plan_on      ? launch_open(k_ctu_open<C, L, M32, 0, 3, 4, false, true>, G4{})
+                         : w4_knob      ? launch_open(k_ctu_open<C, L, M32, 0, 4, 4>, G4{})
                                         : launch_open(k_ctu_open<C, L, M32, 0, 3, 4>, G4{});
             else rc3 = persist == 1   ? launch_open(k_ctu_open<C, L, false, 1>, G4{})
                        : persist == 2 ? launch_open(k_ctu_open<C, L, false, 2>, G4{})
                        : gs_knob == 6 ? launch_open(k_ctu_open<C, L, false, 0, 5, 6>, std::integral_constant<int, 6>{})
                        : gs_knob == 8 ? launch_open(k_ctu_open<C, L, false, 0, 5, 8>, std::integral_constant<int, 8>{})
+                       : w4_knob && ost_on ? launch_open(k_ctu_open<C, L, false, 0, 4, 4, true>, G4{})
                        : plan_on && ost_on ? launch_open(k_ctu_open<C, L, false, 0, 3, 4, true, true>, G4{})
                        : ost_on       ? launch_open(k_ctu_open<C, L, false, 0, 3, 4, true>, G4{})
                        : plan_on      ? launch_open(k_ctu_open<C, L, false, 0, 3, 4, false, true>, G4{})
