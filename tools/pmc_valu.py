@@ -40,7 +40,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # kernels of the measuring harness, not of a config (bench_configs' PSNR reduction)
-HARNESS = ("k_sse_i16",)
+HARNESS = ("k_sse_i16", "k_tc32_widen", "k_tu_widen")   # (+ the compact levels' widen, run once for the digest)
 
 # bench_configs config -> (profile key, anchor kernel, anchor dispatches per frame)
 CONFIGS = {
