@@ -592,6 +592,280 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     if (sse_out && t == 0) atomicAdd(sse_out, wg_sse);   // after the last barrier
 }
 
+#if NH_AB   // the mosaic forms of config 3 (A/B build only: not faster, see nh_intra_rdo_plane)
+// ---------------------------------------------------------------------------
+// Config 3 on f16 MFMA MOSAICS (round 6): the same 35 chains per 8x8 block, but
+// a chain is no longer one lane's registers.  Each 8x8 TU (block, mode) is a
+// quarter of a 16x16 mosaic (MosaicCore<8, false, 2>, nh_mosaic.hpp: the
+// closed loop's exact f16 chain) -- lane (g, c) holds column
+// c % 8, rows 4g % 8 .. +3 of one TU -- so each 1-D pass of 4 TUs is one
+// v_mfma_f32_16x16x16_f16, and a lane's VALU work is its 4 samples'
+// prediction, conversions, quantizer and reconstruction instead of a TU's
+// butterflies.  Phases per group of 7 blocks (8-bit only: a group with a wide
+// block is left to the general fallback launch, as k_intra_rdo8<.., 1>):
+//   A. lane (slot, mode) builds its mode's angular reference pairs in LDS
+//      (_build_ref_array, intra.py:159-188; as rdo8_predict);
+//   B. the waves walk the 245 TUs 8 at a time (two mosaics per call): each lane
+//      predicts its 4 samples (intra.py:46-207 through the same pair/dot2 path
+//      as rdo8_predict), the chain runs, the TU's SSE of orig - recon
+//      (residual_energy(residual_block(orig, recon))) is reduced over its 16
+//      lanes and (sse << 6 | mode) goes to the block's LDS minimum: lowest SSE,
+//      lowest mode on ties (__main__.py:97);
+//   C. wave 0 runs the 7 winning TUs again with their levels, recon and mode
+//      map written out (1 extra call per 245 TUs), and the group adds the
+//      winners' SSE to the plane's total once.
+// Same outputs as k_intra_rdo8 (every operand exact: tools/packed_bounds.py
+// mosaic_bounds, DCT8 row).
+// REF16: the reference as 25 int16 samples (13 words per TU: LDS for 8 waves per SIMD), a pair read as
+// two samples; else as 25 (r[i], r[i + 1]) pairs
+template <bool REF16>
+__device__ __forceinline__ void rdo8_build_refs(const RdoSlotLds& L, int mode, uint32_t* refp) {
+    const int angle = intra_angle_alu(mode);
+    const bool vert = mode >= 18;
+    const int16_t* pri = vert ? L.topA : L.leftA;
+    const int16_t* sec = vert ? L.leftA : L.topA;
+    const int np = vert ? L.ntA : L.nlA, ns = vert ? L.nlA : L.ntA;
+    int32_t r[25];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = 0;
+    r[8] = pri[0];
+#pragma unroll
+    for (int i = 1; i <= 16; ++i) r[8 + i] = pri[i < np ? i : np - 1];
+    if (angle < 0) {
+        const int inv = inv_angle_alu(angle), next = (8 * angle) >> 5;
+#pragma unroll
+        for (int i = -1; i >= -8; --i) {
+            const int proj = ((i + 1) * inv + 128) >> 8;
+            if (i >= next && proj < ns) r[8 + i] = sec[proj];
+        }
+    }
+    if constexpr (REF16) {
+#pragma unroll
+        for (int i = 0; i < 12; ++i) refp[i] = pack16(r[2 * i], r[2 * i + 1]);
+        refp[12] = (uint32_t)r[24] & 0xffffu;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 24; ++i) refp[i] = pack16(r[i], r[i + 1]);
+        refp[24] = (uint32_t)r[24] & 0xffffu;
+    }
+}
+template <bool REF16>
+__device__ __forceinline__ uint32_t rdo8_ref_pair(const uint32_t* refp, int i) {   // (r[i], r[i + 1])
+    if constexpr (REF16) {
+        const int16_t* q = (const int16_t*)refp;
+        return pack16(q[i], q[i + 1]);
+    } else {
+        return refp[i];
+    }
+}
+// The prediction of rows y0 .. y0 + 3 of column x for mode `mode` (rdo8_predict's Q / P)
+template <bool REF16>
+__device__ __forceinline__ void rdo8_pred_col4(const RdoSlotLds& L, const uint32_t* refp, int mode, int y0, int x,
+                                               int32_t (&pr)[4]) {
+    if (mode < 2) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[r] = mode == 0 ? (int16_t)L.planar[8 * (y0 + r) + x] : (int16_t)L.dcv[0];
+        return;
+    }
+    const int angle = intra_angle_alu(mode);
+    if (mode >= 18) {   // vertical: P = Q, scan line = row
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int proj = (y0 + r + 1) * angle, f = proj & 31;
+            const int tt = dot2_16(rdo8_ref_pair<REF16>(refp, 9 + x + (proj >> 5)), (uint32_t)(32 - f) | ((uint32_t)f << 16));
+            pr[r] = __builtin_amdgcn_sbfe(tt, 5u, f ? 11u : 27u);
+        }
+    } else {            // horizontal: P = Q^T (intra.py:153-156), scan line = column: one weight pair
+        const int proj = (x + 1) * angle, f = proj & 31;
+        const uint32_t wf = (uint32_t)(32 - f) | ((uint32_t)f << 16), wd = f ? 11u : 27u;
+        const int i0 = 9 + y0 + (proj >> 5);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pr[r] = __builtin_amdgcn_sbfe(dot2_16(rdo8_ref_pair<REF16>(refp, i0 + r), wf), 5u, wd);
+    }
+}
+// One call: two mosaics = 8 TUs; tu_of(k) gives TU k's (slot, mode) or slot < 0 (idle).
+// keep(m, q, L0, L1, rv...) hooks: OUT = true writes levels / recon / mode (the winners).
+template <bool OUT, int NM, bool REF16, class TuOf>
+__device__ __forceinline__ void rdo8_mma_call(const RdoSlotLds* S, const uint32_t* refs, int rstride, const ChainQ& rq,
+                                              TuOf&& tu_of, uint32_t* best, int b0, int bw, int pitch, int32_t* lvl,
+                                              int16_t* recon, uint8_t* modes) {
+    using MC = MosaicCore<8, false, NM>;
+    MC mc;
+    mc.lane_init(threadIdx.x & 63);
+    int slot[NM], mode[NM];
+    int32_t sv[NM][4];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        tu_of(4 * m + mc.el, slot[m], mode[m]);
+        const int sl = slot[m] < 0 ? 0 : slot[m], md = slot[m] < 0 ? 1 : mode[m];   // idle: block 0's DC
+        const RdoSlotLds& L = S[sl];
+        int32_t pr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sv[m][r] = L.orig[8 * (mc.yr0 + r) + mc.t];
+        rdo8_pred_col4<REF16>(L, refs + (sl * kModes + md) * rstride, md, mc.yr0, mc.t, pr);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {   // as MosaicCore::predict: residual + 768 as f16, 0x6600 - pred
+            const pk16 o2 = pk_pair(sv[m][2 * q], sv[m][2 * q + 1]), p2 = pk_pair(pr[2 * q], pr[2 * q + 1]);
+            const pku16 rr = __builtin_bit_cast(pku16, o2 - p2);   // residual_block, intra.py:65-67
+            mc.hx[m][q] = __builtin_bit_cast(uint32_t, rr * (pku16){2, 2} + (pku16){0x6200, 0x6200});
+            mc.pr2[m][q] = (pku16){0x6600, 0x6600} - __builtin_bit_cast(pku16, p2);
+        }
+    }
+    mc.pass1();
+    mc.pass2();
+    mc.ready();
+    auto bpos = [&](int m, int row) -> int64_t {   // sample offset of (row, column t) of TU m's block
+        const int b = b0 + slot[m], by = b / bw, bx = b - by * bw;
+        return (int64_t)(by * 8 + row) * pitch + bx * 8 + mc.t;
+    };
+    mc.quant(rq, [&](int m, int q, int32_t L0, int32_t L1) {
+        if constexpr (OUT) {
+            if (slot[m] < 0) return;
+            const int64_t o = bpos(m, mc.yr0 + 2 * q);
+            lvl[o] = L0;
+            lvl[o + pitch] = L1;
+        }
+    });
+    mc.inv1();
+    mc.inv2();
+    int32_t e[NM];
+#pragma unroll
+    for (int m = 0; m < NM; ++m) e[m] = 0;
+    mc.recon([&](int m, int q, pku16 rv) {
+        const pk16 d = pk_pair(sv[m][2 * q], sv[m][2 * q + 1]) - __builtin_bit_cast(pk16, rv);   // |d| <= 255
+        e[m] = __builtin_amdgcn_sdot2(d, d, e[m], false);
+        if constexpr (OUT) {
+            if (slot[m] < 0) return;
+            const int64_t o = bpos(m, mc.yr0 + 2 * q);
+            recon[o] = (int16_t)rv.x;
+            recon[o + pitch] = (int16_t)rv.y;
+        }
+    });
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+        const int32_t sse = tu_sum<8>(e[m]);   // the TU's 64 squared differences (< 2^22)
+        if (slot[m] >= 0 && mc.t == 0 && mc.yr0 == 0) {
+            if constexpr (OUT) {
+                modes[b0 + slot[m]] = (uint8_t)mode[m];
+            } else {
+                atomicMin(&best[slot[m]], ((uint32_t)sse << 6) | (uint32_t)mode[m]);
+            }
+        }
+    }
+}
+
+// NMS: mosaics per call in phase B (2: 8 TUs, 4: 16 TUs); REF16: int16 reference arrays
+template <int WAVES, int NMS = 2, bool REF16 = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)))
+k_intra_rdo8_mma(const int16_t* __restrict__ src, int w, int h, int pitch, QuantParams qp, int dq_scale, int dq_per,
+                 uint8_t* modes, int32_t* lvl, int16_t* recon, unsigned long long* sse_out) {
+    __shared__ RdoSlotLds S[kRdoSlots];
+    constexpr int RS = REF16 ? 13 : kRefStride;   // words per TU's reference (odd: conflict-free)
+    __shared__ uint32_t refs[kRdoSlots * kModes * RS];
+    __shared__ uint32_t best[kRdoSlots];
+    const int bw = w / 8, bh = h / 8;
+    const int nblk = bw * bh;
+    const int t = threadIdx.x, wv = t >> 6;
+    const int b0 = (int)blockIdx.x * kRdoSlots;
+    // ---- the 7 blocks' samples and neighbours (as k_intra_rdo8) ----
+    int16_t vo0 = 0, vo1 = 0, vn = 128, vtl = 128;
+    auto orig_at = [&](int e) -> const int16_t* {
+        const int b = b0 + e / 64, k = e % 64;
+        const int by = b / bw, bx = b - by * bw;
+        return src + (int64_t)(by * 8 + k / 8) * pitch + bx * 8 + (k % 8);
+    };
+    const bool o0 = b0 + t / 64 < nblk;
+    const bool o1 = t + 256 < kRdoSlots * 64 && b0 + (t + 256) / 64 < nblk;
+    if (o0) vo0 = *orig_at(t);
+    if (o1) vo1 = *orig_at(t + 256);
+    const int nsl = t / 32, nk = t % 32;
+    const bool nv = t < kRdoSlots * 32 && b0 + nsl < nblk;
+    if (nv) {
+        const int b = b0 + nsl, nby = b / bw, nbx = b - nby * bw;
+        const int x = nbx * 8, y = nby * 8;
+        const bool top = nk < 16;   // top row x..x+15 (block.py:38-43) / left column y..y+15 (block.py:45-50)
+        const int kk = nk - 16;
+        const bool in = top ? (y > 0 && x + nk < w) : (x > 0 && y + kk < h);
+        const int ry = top ? y - 1 : y + kk, rx = top ? x + nk : x - 1;
+        if (in) vn = src[(int64_t)ry * pitch + rx];
+    }
+    const bool tv = t < kRdoSlots && b0 + t < nblk;
+    int tby = 0, tbx = 0;
+    if (tv) {
+        tby = (b0 + t) / bw;
+        tbx = b0 + t - tby * bw;
+        if (tby > 0 && tbx > 0) vtl = src[(int64_t)(tby * 8 - 1) * pitch + tbx * 8 - 1];
+    }
+    if (o0) S[t / 64].orig[t % 64] = vo0;
+    if (o1) S[(t + 256) / 64].orig[(t + 256) % 64] = vo1;
+    if (nv) {
+        if (nk < 16) {
+            S[nsl].topA[1 + nk] = vn;
+            if (nk < 8) S[nsl].topN[nk] = vn;
+        } else {
+            S[nsl].leftA[1 + nk - 16] = vn;
+            if (nk < 24) S[nsl].leftN[nk - 16] = vn;
+        }
+    }
+    if (t < kRdoSlots) {
+        S[t].valid = tv;
+        if (tv) {
+            const int x = tbx * 8, y = tby * 8;
+            S[t].topA[0] = vtl;
+            S[t].leftA[0] = vtl;
+            S[t].ntA = 1 + (y == 0 ? 16 : min(16, w - x));
+            S[t].nlA = 1 + (x == 0 ? 16 : min(16, h - y));
+        }
+        S[t].wide = 0;
+        best[t] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    for (int e = t; e < kRdoSlots * 64; e += 256)
+        if (S[e / 64].valid) rdo8_block_prep(S[e / 64], e % 64);
+    __syncthreads();
+    {   // a wide block in the group: leave the group to the fallback launch (k_intra_rdo8<.., 2>)
+        bool any_wide = false;
+#pragma unroll
+        for (int k = 0; k < kRdoSlots; ++k) any_wide |= S[k].valid && S[k].wide;
+        if (any_wide) {
+            if (t < kRdoSlots && S[t].valid) modes[b0 + t] = 0xFF;
+            return;   // uniform over the workgroup
+        }
+    }
+    // ---- A. the angular reference pairs of every (block, mode) ----
+    {
+        const int slot = t / kModes, mode = t - slot * kModes;
+        if (slot < kRdoSlots && S[slot].valid && mode >= 2) rdo8_build_refs<REF16>(S[slot], mode, refs + t * RS);
+    }
+    __syncthreads();
+    // ---- B. the 245 chains, 8 TUs a call ----
+    const ChainQ rq = make_chainq(qp, dq_scale, dq_per);
+    constexpr int kTus = kRdoSlots * kModes, TPC = 4 * NMS;   // TUs per call
+    for (int c0 = TPC * wv; c0 < kTus; c0 += 4 * TPC) {
+        rdo8_mma_call<false, NMS, REF16>(S, refs, RS, rq, [&](int k, int& sl, int& md) {
+            const int e = c0 + k;
+            sl = e < kTus ? e / kModes : -1;
+            md = e - (sl < 0 ? 0 : sl) * kModes;
+            if (sl >= 0 && !S[sl].valid) sl = -1;
+        }, best, b0, bw, pitch, lvl, recon, modes);
+    }
+    __syncthreads();
+    // ---- C. the winners again, with their outputs; the group's SSE once ----
+    if (wv == 0) {
+        rdo8_mma_call<true, 2, REF16>(S, refs, RS, rq, [&](int k, int& sl, int& md) {
+            sl = k < kRdoSlots && S[k].valid ? k : -1;
+            md = (int)(best[k < kRdoSlots ? k : 0] & 63u);
+        }, best, b0, bw, pitch, lvl, recon, modes);
+    } else if (wv == 1 && sse_out) {
+        unsigned long long s = 0;
+        if (t - 64 < kRdoSlots && S[t - 64].valid) s = best[t - 64] >> 6;
+        s = grp_sum<64>(s);
+        if (t == 64 && s) atomicAdd(sse_out, s);
+    }
+}
+
+#endif  // NH_AB
+
 // ===========================================================================
 // Config 3, closed loop: blocks in raster order, neighbours
 // from the reconstruction.  Wavefront schedule: one wave per block row; rows
@@ -2557,6 +2831,27 @@ int tc32_butterfly(const int16_t* d_src, int w, int h, int pitch, int qp, int32_
 
 using namespace nh;
 
+namespace nh {
+// The mosaics' per-lane bases and initial accumulators (c_mosaic_cl), once per device
+// (host-synchronous upload: every later kernel on any stream reads them)
+int ensure_mosaic_cl() {
+    static PerDeviceOnce once_m;
+    return once_m.run([] {
+        static MosaicLane mt[4][64];
+        make_mosaic(mt);
+        NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic_cl), mt, sizeof(mt)));
+        return (int)NH_OK;
+    });
+}
+// Config 3's product kernel: 0 = k_intra_rdo8<1, true, 1> (lane per mode); the mosaic forms
+// (k_intra_rdo8_mma, A/B build only) measured 201.5-208 vs 200.4-201.8 us per 1080p frame with
+// 1.17x the VALU wave-instructions (profiles/r06/cfg3/): not kept
+#ifndef NH_RDO_MMA_DEFAULT
+#define NH_RDO_MMA_DEFAULT 0
+#endif
+constexpr int kRdoMmaDefault = NH_RDO_MMA_DEFAULT;
+}  // namespace nh
+
 extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch, int qp, uint8_t* d_modes,
                                   int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse, void* stream) {
     if (!d_src || !d_modes || !d_lvl || !d_recon || w < 0 || h < 0 || pitch < w) return NH_EARG;
@@ -2571,6 +2866,30 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
     {   // the packed-chain-only launch (3 waves/SIMD), then the fallback for groups with wide blocks
         // A/B build: NH_CAP_RDO = resident workgroups per CU (LDS reservation, lds_cap)
         static const int cap_rdo = NH_KNOB("NH_CAP_RDO", 0);
+        // A/B build: NH_RDO_MMA = 0 the lane-per-mode packed chains, 3 / 4 the f16 MFMA mosaics at that many
+        // waves per SIMD (k_intra_rdo8_mma)
+        static const int rdo_mma = NH_KNOB("NH_RDO_MMA", kRdoMmaDefault);
+#if NH_AB
+        if (rdo_mma) {
+            const int rcm = ensure_mosaic_cl();
+            if (rcm) return rcm;
+        }
+        if (rdo_mma == 4)
+            k_intra_rdo8_mma<3, 4><<<ngroups, 256, lds_cap(k_intra_rdo8_mma<3, 4>, cap_rdo), s>>>(
+                d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse);
+        else if (rdo_mma == 5)
+            k_intra_rdo8_mma<3, 2, true><<<ngroups, 256, lds_cap(k_intra_rdo8_mma<3, 2, true>, cap_rdo), s>>>(
+                d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse);
+        else if (rdo_mma == 6)
+            k_intra_rdo8_mma<6, 2, true><<<ngroups, 256, lds_cap(k_intra_rdo8_mma<6, 2, true>, cap_rdo), s>>>(
+                d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse);
+        else if (rdo_mma)
+            k_intra_rdo8_mma<3><<<ngroups, 256, lds_cap(k_intra_rdo8_mma<3>, cap_rdo), s>>>(
+                d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse);
+        else
+#else
+        (void)rdo_mma;
+#endif
         k_intra_rdo8<1, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
             d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups);
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
@@ -2885,13 +3204,7 @@ extern "C" int nh_tu_pipeline_planes_closed(const int16_t* d_src, const nh_plane
                 !((set->base | set->plane_stride | set->group_stride) & 7) && !((uintptr_t)d_src & 15) &&
                 (3 * set->group_stride + (int64_t)set->height * set->pitch) * 2 < (1ll << 31);
     {   // tu_closed_batch_mma's per-lane bases and initial accumulators
-        static PerDeviceOnce once_m;
-        const int rcm = once_m.run([] {
-            static MosaicLane mt[4][64];
-            make_mosaic(mt);
-            NH_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_mosaic_cl), mt, sizeof(mt)));
-            return (int)NH_OK;
-        });
+        const int rcm = ensure_mosaic_cl();
         if (rcm) return rcm;
     }
     if (a.mfma32) {

@@ -151,10 +151,16 @@ def main():
         planes = [synth_plane(H, W, 1), synth_plane(H // 2, W // 2, 2), synth_plane(H // 2, W // 2, 3)]
         nblk = sum((p.shape[0] // 8) * (p.shape[1] // 8) for p in planes)
         ms = timed(lambda: [gpu.intra_rdo_plane(p, args.qp) for p in planes], args.reps)
+        outs = [gpu.intra_rdo_plane(p, args.qp) for p in planes]
+        dig = [int(sum(int(o[0].to(torch.int64).sum().item()) for o in outs)),
+               int(sum(int(o[1].to(torch.int64).sum().item()) for o in outs)),
+               int(sum(int(o[2].to(torch.int64).sum().item()) for o in outs)),
+               int(sum(int(o[3].item()) for o in outs))]
         print(json.dumps({"config": "cfg3 1080p YUV420 35-mode RDO per 8x8 (pred+res+DCT+Q+DQ+IDCT+recon+SSE)",
                           "ms_per_frame": ms, "frames_per_s": 1e3 / ms, "blocks_per_frame": nblk,
-                          "blocks_per_s": nblk / ms * 1e3, "mode_evals_per_s": 35 * nblk / ms * 1e3,
-                          "roofline": valu_roofline("cfg3_1080p_yuv420", ms)}), flush=True)
+                          "blocks_per_s": nblk / ms * 1e3, "mode_evals_per_s": 35 * nblk / ms * 1e3, "knobs": knobs,
+                          "roofline": valu_roofline("cfg3_1080p_yuv420", ms),
+                          "out_digest": dig}), flush=True)
 
     if 4 in cfgs:
         W, H = 3840, 2160

@@ -11,6 +11,7 @@
 #   rehearse4  the same for --config 4, with the gathered-recon check
 #   prof       rocprofv3 --kernel-trace --stats of bench.py
 #   pmc        the FETCH_SIZE and WRITE_SIZE passes of bench.py (MI355X_MICROARCH.md §HBM)
+#   pmc4       the same passes of bench.py --config 4 (BENCH_ARGS: e.g. --levels int32)
 #   configs    tools/bench_configs.py (configs 3/4/5 + frame driver)
 #   percall    tools/percall.py (drop-in per-call cost); percall_ab: the same over tools/_ab/ (older build)
 #   pmc_sq     SQ wave-state pass (issue / wait fractions) of bench.py; CONFIG=4 for the config-4 bench
@@ -70,6 +71,10 @@ run_step() {
       echo "== rocprof pmc FETCH_SIZE / WRITE_SIZE"
       timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_${TAG} -o run -- python3 bench.py --steps 5 --warmup 2 --frames $FRAMES --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc_fetch_${TAG}.log 2>&1 && \
       timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_${TAG} -o run -- python3 bench.py --steps 5 --warmup 2 --frames $FRAMES --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc_write_${TAG}.log 2>&1 ;;
+    pmc4)
+      echo "== rocprof pmc FETCH_SIZE / WRITE_SIZE of bench.py --config 4 $BENCH_ARGS"
+      timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc4_fetch_${TAG} -o run -- python3 bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc4_fetch_${TAG}.log 2>&1 && \
+      timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc4_write_${TAG} -o run -- python3 bench.py --config 4 --steps 5 --warmup 2 --no-cpu-baseline $BENCH_ARGS > gpurun_out/pmc4_write_${TAG}.log 2>&1 ;;
     configs)
       echo "== bench_configs"
       timeout -k 10 400 python tools/bench_configs.py $CONFIGS_ARGS > gpurun_out/configs_${TAG}.jsonl 2> gpurun_out/configs_${TAG}.err; rc=$?
