@@ -252,3 +252,32 @@ def test_cfg4_4k_closed_loop_64_frames_equals_reference(ref, torch_dev):
         assert sha(r0[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
         assert sha(tuy if k == 0 else tuc[k - 1]) == e["tu"], k
         off += ph * pw
+
+
+def test_cfg4_4k_closed_loop_stream_equals_reference(ref, torch_dev):
+    """8 copies of the 4K YUV420 frame through tu_pipeline_closed_yuv420_stream in
+    batches of 3 frames over 3 stream pairs (batches in flight together, a
+    ragged last batch): frame 0 equals the reference's hashes and every other
+    frame equals frame 0."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F = 8
+    planes = FI.cfg4_frame()
+    h, w = planes[0].shape
+    one = np.concatenate([p.reshape(-1) for p in planes])
+    fe = one.size
+    d = torch.from_numpy(one).cuda().repeat(F)
+    lvl, rec, tuy, tuc = gpu.tu_pipeline_closed_yuv420_stream(d, w, h, F, FI.CFG4_SEED, FI.CFG4_QP, batch_frames=3,
+                                                              depth=3)
+    lvl, rec = lvl.view(F, fe), rec.view(F, fe)
+    assert bool((lvl == lvl[:1]).all()) and bool((rec == rec[:1]).all())
+    assert bool((tuy == tuy[:1]).all()) and bool((tuc.view(F, 2, -1) == tuc.view(F, 2, -1)[:1]).all())
+    l0, r0, tuy, tuc = lvl[0].cpu().numpy(), rec[0].cpu().numpy(), tuy[0].cpu().numpy(), tuc[:2].cpu().numpy()
+    off = 0
+    for k, p in enumerate(planes):
+        ph, pw = p.shape
+        e = ref[f"closed4_p{k}"]
+        assert sha(l0[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], k
+        assert sha(r0[off:off + ph * pw].reshape(ph, pw)) == e["rec"], k
+        assert sha(tuy if k == 0 else tuc[k - 1]) == e["tu"], k
+        off += ph * pw

@@ -941,6 +941,46 @@ def test_tu_pipeline_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp, conc):
             off += ph * pw
 
 
+@pytest.mark.parametrize("batch,depth,pad", [(3, 2, 0), (3, 3, 0), (2, 4, 24), (1, 3, 8), (8, 3, 0)])
+def test_tu_pipeline_closed_batches_vs_oracle(nh, torch_dev, batch, depth, pad):
+    """tu_pipeline_closed_yuv420_stream: a 7-frame YUV420 stream in batches of
+    ``batch`` frames over ``depth`` stream pairs (batches in flight together, a
+    ragged last batch, a frame stride with ``pad`` spare samples and a base
+    offset), one 9-bit frame (its batch alone takes the 32-bit form); every
+    plane equals the sequential oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H, qp, base = 7, 136, 104, 27, 40
+    rng = np.random.default_rng(7000 + batch * 10 + depth)
+    fe = gpu.yuv420_frame_elems(W, H)
+    fs = fe + pad
+    buf = np.zeros(base + F * fs, np.int16)
+    for f in range(F):
+        off = base + f * fs
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            p = np.clip(60 + (3 * xx + 2 * yy + 13 * f) % 150 + rng.integers(-25, 26, (ph, pw)), 0, 255)
+            if f == 4:
+                p[ph // 2, pw // 3] = 300
+            buf[off:off + ph * pw] = p.reshape(-1)
+            off += ph * pw
+    d = torch.from_numpy(buf).cuda()
+    lvl, rec, tuy, tuc = gpu.tu_pipeline_closed_yuv420_stream(d, W, H, F, 555, qp, batch_frames=batch, depth=depth,
+                                                              frame_stride=fs, base=base)
+    lv, rv, tuy, tuc = lvl.cpu().numpy(), rec.cpu().numpy(), tuy.cpu().numpy(), tuc.cpu().numpy()
+    assert tuy.shape == (F, H // 4, W // 4) and tuc.shape == (2 * F, H // 8, W // 8)
+    for f in range(F):
+        off = base + f * fs
+        for k, (pw, ph) in enumerate(((W, H), (W // 2, H // 2), (W // 2, H // 2))):
+            src = buf[off:off + ph * pw].reshape(ph, pw)
+            el, er, et = O.tu_pipeline_plane_closed(src, 32 if k == 0 else 16, k, 555, qp, k == 0)
+            assert np.array_equal(lv[off:off + ph * pw].reshape(ph, pw), el), (f, k)
+            assert np.array_equal(rv[off:off + ph * pw].reshape(ph, pw), er), (f, k)
+            assert np.array_equal(tuy[f] if k == 0 else tuc[2 * f + k - 1], et), (f, k)
+            off += ph * pw
+        assert not lv[off:base + (f + 1) * fs].any() and not rv[off:base + (f + 1) * fs].any()   # the pad untouched
+
+
 @pytest.mark.parametrize("conc", [False, True])
 @pytest.mark.parametrize("F,W,H,qp", [(1, 104, 72, 32), (2, 136, 104, 22), (3, 104, 72, 32), (5, 72, 40, 0), (2, 136, 104, 4),
                                       (4, 136, 104, 51)])

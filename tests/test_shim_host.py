@@ -138,3 +138,18 @@ def test_estimate_bits_extended_precision_is_refused():
         estimate_bits(np.array([1.5, -3.0], np.longdouble))
     with pytest.raises(NotImplementedError):
         estimate_bits(np.array([1 + 2j], np.clongdouble))
+
+
+def test_closed_stream_argument_checks():
+    """tu_pipeline_closed_yuv420_stream refuses bad batch / depth / stride / size
+    arguments on the host, before any device call."""
+    import torch
+    W, H, F = 64, 32, 3
+    src = torch.zeros(F * gpu.yuv420_frame_elems(W, H), dtype=torch.int16)
+    for kw in ({"batch_frames": 0}, {"depth": 0}, {"frame_stride": gpu.yuv420_frame_elems(W, H) - 1}):
+        with pytest.raises(ValueError):
+            gpu.tu_pipeline_closed_yuv420_stream(src, W, H, F, 1, 32, **kw)
+    with pytest.raises(ValueError):   # one frame more than the buffer holds
+        gpu.tu_pipeline_closed_yuv420_stream(src, W, H, F + 1, 1, 32)
+    with pytest.raises(ValueError):   # the base pushes the last frame out
+        gpu.tu_pipeline_closed_yuv420_stream(src, W, H, F, 1, 32, base=1)

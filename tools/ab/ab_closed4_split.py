@@ -30,6 +30,12 @@ def main():
     ap.add_argument("--frames", type=int, default=64)
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--qp", type=int, default=32)
+    ap.add_argument("--pipe", type=int, default=0,
+                    help="also time K back-to-back launch sets over two stream pairs (two output copies), "
+                         "one status check at the end (form pipeK)")
+    ap.add_argument("--depth", type=int, default=2, help="stream pairs / output copies of --pipe")
+    ap.add_argument("--only-pipe", action="store_true")
+    ap.add_argument("--one-stream", action="store_true", help="--pipe: a set's luma then chroma on ONE stream")
     args = ap.parse_args()
     from nano_hevc import gpu, _lib
     from bench_configs import synth_plane
@@ -68,6 +74,36 @@ def main():
         join.record(side)
         main.wait_event(join)
 
+    pipe_bufs = []
+    if args.pipe:   # a second copy of the frames and outputs: consecutive sets alternate between the copies
+        pipe_bufs = [(stream, lv, rc, tuy, tuc)] + [
+            (stream.clone(), torch.zeros_like(lv), torch.zeros_like(rc), torch.zeros_like(tuy), torch.zeros_like(tuc))
+            for _ in range(args.depth - 1)]
+        pipe_streams = [(torch.cuda.Stream(), torch.cuda.Stream()) for _ in range(args.depth)]
+
+    def pipe():   # K launch sets, set k on stream pair k % depth, no host round trip between sets
+        main = torch.cuda.current_stream()
+        fork = torch.cuda.Event()
+        fork.record(main)
+        for pr in pipe_streams:
+            for s_ in pr:
+                s_.wait_event(fork)
+        works = []
+        for k in range(args.pipe):
+            src_, lv_, rc_, ty_, tc_ = pipe_bufs[k % args.depth]
+            ls, cs = pipe_streams[k % args.depth]
+            if args.one_stream:
+                cs = ls
+            works.append(gpu._tu_closed_launch(src_, sy, 32, 0, 1234, args.qp, True, lv_, rc_, ty_, ls)[3])
+            works.append(gpu._tu_closed_launch(src_, suv, 16, 1, 1234, args.qp, False, lv_, rc_, tc_, cs)[3])
+        for pr in pipe_streams:
+            for s_ in pr:
+                j = torch.cuda.Event()
+                j.record(s_)
+                main.wait_event(j)
+        for w_ in works:
+            gpu._tu_closed_status(w_, int(main.cuda_stream), "pipe")
+
     forms = {
         "luma": lambda: gpu.tu_pipeline_closed(stream, sy, 32, 0, 1234, args.qp, True, lvl=lv, rec=rc, tu=tuy),
         "chroma": lambda: gpu.tu_pipeline_closed(stream, suv, 16, 1, 1234, args.qp, False, lvl=lv, rec=rc, tu=tuc),
@@ -75,6 +111,10 @@ def main():
                                                             tu_luma=tuy, tu_chroma=tuc),
         "luma_first": luma_first,
     }
+    if args.only_pipe:
+        forms = {}
+    if args.pipe:
+        forms[f"pipe{args.pipe}d{args.depth}" + ("s" if args.one_stream else "")] = pipe
     out = {"lib": args.lib or ("ab" if args.ab else "product"),
            "knobs": {k: v for k, v in os.environ.items() if k.startswith("NH_")}, "frames": nf}
     for name, fn in forms.items():
@@ -89,8 +129,9 @@ def main():
             e1.record()
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
+        per = nf * (args.pipe if name.startswith("pipe") else 1)
         out[name] = {"median_ms": statistics.median(ts), "min_ms": min(ts),
-                     "median_ms_per_frame": statistics.median(ts) / nf}
+                     "median_ms_per_frame": statistics.median(ts) / per}
     out["out_digest"] = [int(lv.to(torch.int64).sum().item()), int(rc.to(torch.int64).sum().item())]
     print(json.dumps(out), flush=True)
 

@@ -21,5 +21,5 @@ python3 - "$OUT" <<'EOF'
 import json, sys
 for l in open(sys.argv[1]):
     d = json.loads(l)
-    print(d["lib"], d["knobs"], *(f"{k} {d[k]['median_ms_per_frame']:.4f}" for k in ("luma", "chroma", "concurrent", "luma_first") if k in d), d["out_digest"])
+    print(d["lib"], d["knobs"], *(f"{k} {d[k]['median_ms_per_frame']:.4f}" for k in d if isinstance(d[k], dict) and "median_ms_per_frame" in d[k]), d["out_digest"])
 EOF

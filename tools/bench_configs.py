@@ -13,6 +13,8 @@
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
   closed4 config 4 in CLOSED loop over a 4K YUV420 stream (TUs in z-order, CTU-row
         wavefront; with --check, frame 0's luma against the oracle).
+  closed4s  config 4 closed loop over a 384-frame stream in batches of --closed4s-batch
+        frames, --closed4-depth of them in flight (tu_pipeline_closed_yuv420_stream)
   closed4mix  config 4 closed loop on an 8-bit stream vs the same stream with one
         9-bit sample (the stream-wide packed / 32-bit form choice)
   closed  config 3 in CLOSED loop (neighbours from the reconstruction, wavefront
@@ -115,6 +117,9 @@ def main():
                     help="4b: level dtypes (default from the configs: 4b int32, 4bc int16 compact levels)")
     ap.add_argument("--closed4-frames", type=int, default=64, help="frames of the closed-loop cfg4 stream")
     ap.add_argument("--closed4-seq", action="store_true", help="closed4: luma then chroma (default: concurrent wavefronts)")
+    ap.add_argument("--closed4s-batch", default="64,128", help="closed4s: frames per batch (one line each)")
+    ap.add_argument("--closed4s-frames", type=int, default=384, help="closed4s: frames in the stream")
+    ap.add_argument("--closed4-depth", type=int, default=3, help="closed4s: batches in flight")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
     ap.add_argument("--configs", default="3,4,4b,5,closed,closed4,enc,io")
     ap.add_argument("--enc-frames", type=int, default=64)
@@ -275,6 +280,43 @@ def main():
                     np.array_equal(er, rc[f * fe:f * fe + W * H].view(H, W).cpu().numpy()) and
                     np.array_equal(el, lv[f * fe:f * fe + W * H].view(H, W).cpu().numpy()))
         print(json.dumps(line), flush=True)
+
+    if "closed4s" in cfgs:   # config 4 closed loop over a frame stream: batches of frames, `depth` of them in flight
+        W, H, nf = 3840, 2160, args.closed4s_frames
+        depth = args.closed4_depth
+        batches = [int(x) for x in args.closed4s_batch.split(",")]
+        nd = max(batches)   # distinct frames; the stream repeats them (disjoint outputs per frame)
+        planes = []
+        for f in range(nd):
+            planes += [synth_plane(H, W, 40 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 41 + 3 * f).reshape(-1),
+                       synth_plane(H // 2, W // 2, 42 + 3 * f).reshape(-1)]
+        one = torch.cat(planes)
+        del planes
+        assert nf % nd == 0
+        stream = one.repeat(nf // nd)
+        del one
+        fe = gpu.yuv420_frame_elems(W, H)
+        lv = torch.zeros(stream.shape, dtype=torch.int32, device="cuda")
+        rc = torch.zeros(stream.shape, dtype=torch.int16, device="cuda")
+        tuy = torch.zeros((nf, H // 4, W // 4), dtype=torch.uint8, device="cuda")
+        tuc = torch.zeros((2 * nf, H // 8, W // 8), dtype=torch.uint8, device="cuda")
+        for bf in batches:
+            run4s = lambda: gpu.tu_pipeline_closed_yuv420_stream(stream, W, H, nf, 1234, args.qp, batch_frames=bf,
+                                                                   depth=depth, lvl=lv, rec=rc, tu_luma=tuy, tu_chroma=tuc)
+            ms = timed(run4s, max(3, args.reps // 5))
+            rep = nf // nd
+            print(json.dumps({"config": "cfg4 closed loop over a frame stream: 4K YUV420, batches of frames coded as "
+                                        "concurrent luma + chroma CTU-row wavefronts, `depth` batches in flight "
+                                        "(tu_pipeline_closed_yuv420_stream)",
+                              "frames": nf, "batch_frames": bf, "depth": depth, "ms_per_stream": ms,
+                              "ms_per_frame": ms / nf, "frames_per_s": nf / ms * 1e3,
+                              "samples_per_s": stream.numel() / ms * 1e3, "knobs": knobs,
+                              "roofline": valu_roofline("cfg4_closed_4k_yuv420", ms / nf),
+                              "repeats_equal": bool((lv.view(rep, -1) == lv.view(rep, -1)[:1]).all() and
+                                                    (rc.view(rep, -1) == rc.view(rep, -1)[:1]).all()),
+                              "out_digest": [int(lv[:64 * fe].to(torch.int64).sum().item()),
+                                             int(rc[:64 * fe].to(torch.int64).sum().item())]}), flush=True)
+        del stream, lv, rc, tuy, tuc
 
     if "closed4mix" in cfgs:   # the stream-wide wide flag: one 9-bit sample in the last frame
         W, H, nf = 3840, 2160, args.closed4_frames
