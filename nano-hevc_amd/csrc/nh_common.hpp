@@ -222,6 +222,18 @@ __device__ __forceinline__ int32_t quant_s(int32_t c, const QuantS& q, uint32_t 
         : "vcc");
     return r;
 }
+// quant_s with the sign-dependent rounding offset chosen by a bit-field insert
+// instead of a compare + VCC select: sgn = (any value with c's sign) >> 31, the
+// offset = v_bfi_b32(sgn, hneg, h).  Two full-rate-class VALU (the shifts) and two
+// half-rate-class (bfi, mad) instead of one and three, and no VCC chain between
+// neighbouring coefficients.  Same results as quant_s.
+__device__ __forceinline__ int32_t quant_sb(int32_t c, int32_t sgn, const QuantS& q, uint32_t h_v) {
+    uint32_t hs;
+    int32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(hs) : "v"(sgn), "s"(q.hneg), "v"(h_v));
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(r) : "v"(c), "s"(q.mh), "v"(hs));
+    return r >> q.sh;
+}
 // General int32 form (64-bit product), abs wrapping at int32 min like np.abs.
 __device__ __forceinline__ int32_t quant_i32(int32_t c, const QuantParams& q) {
     int64_t a = (c == INT32_MIN) ? (int64_t)c : (int64_t)(c < 0 ? -(int64_t)c : (int64_t)c);

@@ -159,6 +159,9 @@ __device__ __forceinline__ unsigned long long rdo8_recon_sse(uint32_t (&X)[8][8]
 // precomputed prediction through the same path (f = 0).  P = Q for vertical
 // modes and planar/DC, P = Q^T for horizontal modes (intra.py:153-156).
 // Prediction of one mode into Rpk (int16 pairs along columns, row-major).
+// NARROW: the block's neighbours are 8-bit (wide == 0), so every prediction sample is in
+// [0, 255] before the >> 5: an arithmetic shift instead of the 11 / 27-bit extract
+template <bool NARROW = false>
 __device__ __forceinline__ void rdo8_predict(const RdoSlotLds& L, int mode, uint32_t* refp, uint32_t (&Rpk)[32]) {
     const uint32_t* rowp[8];
     uint32_t wf[8], wd[8];
@@ -207,7 +210,7 @@ __device__ __forceinline__ void rdo8_predict(const RdoSlotLds& L, int mode, uint
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
             const int t = dot2_16(rowp[s][b], wf[s]);
-            Q[s][b] = __builtin_amdgcn_sbfe(t, 5u, wd[s]);
+            Q[s][b] = NARROW ? t >> 5 : __builtin_amdgcn_sbfe(t, 5u, wd[s]);
         }
 #pragma unroll
     for (int y = 0; y < 8; ++y)
@@ -227,7 +230,7 @@ __device__ __forceinline__ unsigned long long rdo8_chain_n(const RdoSlotLds& L, 
 template <bool NARROW_ONLY = false>
 __device__ __forceinline__ unsigned long long rdo8_chain(const RdoSlotLds& L, int mode, uint32_t* refp,
                                                          const ChainQ& q, uint32_t (&Rpk)[32], uint32_t (&Lpk)[32]) {
-    rdo8_predict(L, mode, refp, Rpk);
+    rdo8_predict<NARROW_ONLY>(L, mode, refp, Rpk);
     if (NARROW_ONLY || !L.wide) return rdo8_chain_n(L, q, Rpk, Lpk);   // 8-bit block and neighbours: packed 16-bit chain
     uint32_t X[8][8];
     const uint32_t* opk = (const uint32_t*)L.orig;
@@ -403,15 +406,18 @@ __device__ __forceinline__ unsigned long long rdo8_chain_n(const RdoSlotLds& L, 
         int32_t la[8], lb[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            la[j] = quant_s(za[j] >> 8, q.qs, q.h_v, q.hneg_v);
-            lb[j] = quant_s(zb[j] >> 8, q.qs, q.h_v, q.hneg_v);
+            la[j] = quant_sb(za[j] >> 8, za[j] >> 31, q.qs, q.h_v);
+            lb[j] = quant_sb(zb[j] >> 8, zb[j] >> 31, q.qs, q.h_v);
         }
+        // dequantize_block on the level pairs (v_pk_mad + v_pk_ashr): l * dqs + dqr stays within
+        // int16 for 8-bit 8x8 blocks at every QP (tools/packed_bounds.py rdo8_dequant_bounds)
+        const pk16 dqs2 = pk_splat(q.dqs), dqr2 = pk_splat((int32_t)q.dqr_v), dqsh2 = pk_splat(q.dqsh);
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             Lpk[(2 * i) * 4 + m] = pack16(la[2 * m], la[2 * m + 1]);
             Lpk[(2 * i + 1) * 4 + m] = pack16(lb[2 * m], lb[2 * m + 1]);
-            D[2 * i][m] = pack16(dequant_s(la[2 * m], q), dequant_s(la[2 * m + 1], q));          // (col 2m, 2m+1) pairs
-            D[2 * i + 1][m] = pack16(dequant_s(lb[2 * m], q), dequant_s(lb[2 * m + 1], q));
+            D[2 * i][m] = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(pk16, Lpk[(2 * i) * 4 + m]) * dqs2 + dqr2) >> dqsh2);
+            D[2 * i + 1][m] = __builtin_bit_cast(uint32_t, (__builtin_bit_cast(pk16, Lpk[(2 * i + 1) * 4 + m]) * dqs2 + dqr2) >> dqsh2);
         }
     }
 #pragma unroll
@@ -459,7 +465,7 @@ template <int WAVES, bool ONESHOT, int CHAIN = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
                                                     int32_t* lvl, int16_t* recon, unsigned long long* sse_out,
-                                                    uint32_t ngroups) {
+                                                    uint32_t ngroups, int vec_out) {
     __shared__ RdoSlotLds S[kRdoSlots];
     __shared__ uint32_t refs[kRdoSlots * kModes][kRefStride];
     __shared__ unsigned long long wg_sse;
@@ -571,14 +577,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
         // (A/B: handing the block to the workgroup through LDS for wave-wide
         // stores measured 0.225 vs 0.222 ms/frame -- the winners' stores overlap
         // the other wave's chain here; kept in the closed loop, where they do not)
+        if (vec_out) {   // 16-B aligned rows (the launch checks pitch and bases): 3 stores a row, not 16
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
-            int16_t* rrow = recon + (int64_t)(by * 8 + i) * pitch + bx * 8;
+            for (int i = 0; i < 8; ++i) {
+                int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
+                int16_t* rrow = recon + (int64_t)(by * 8 + i) * pitch + bx * 8;
+                *(uint4*)rrow = make_uint4(P[i * 4], P[i * 4 + 1], P[i * 4 + 2], P[i * 4 + 3]);
+                int32_t lv[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                lrow[j] = (int32_t)(int16_t)(Lv[i * 4 + j / 2] >> (16 * (j & 1)));
-                rrow[j] = (int16_t)(P[i * 4 + j / 2] >> (16 * (j & 1)));
+                for (int m = 0; m < 4; ++m) {
+                    lv[2 * m] = __builtin_amdgcn_sbfe((int32_t)Lv[i * 4 + m], 0u, 16u);
+                    lv[2 * m + 1] = (int32_t)Lv[i * 4 + m] >> 16;
+                }
+                *(int4*)lrow = make_int4(lv[0], lv[1], lv[2], lv[3]);
+                *(int4*)(lrow + 4) = make_int4(lv[4], lv[5], lv[6], lv[7]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                int32_t* lrow = lvl + (int64_t)(by * 8 + i) * pitch + bx * 8;
+                int16_t* rrow = recon + (int64_t)(by * 8 + i) * pitch + bx * 8;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    lrow[j] = (int32_t)(int16_t)(Lv[i * 4 + j / 2] >> (16 * (j & 1)));
+                    rrow[j] = (int16_t)(P[i * 4 + j / 2] >> (16 * (j & 1)));
+                }
             }
         }
     }
@@ -2850,6 +2873,9 @@ int ensure_mosaic_cl() {
 #define NH_RDO_MMA_DEFAULT 0
 #endif
 constexpr int kRdoMmaDefault = NH_RDO_MMA_DEFAULT;
+#ifndef NH_RDO_VEC_OUT   // the winners' rows as 16-B stores (when aligned)
+#define NH_RDO_VEC_OUT 1
+#endif
 }  // namespace nh
 
 extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch, int qp, uint8_t* d_modes,
@@ -2890,10 +2916,12 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
 #else
         (void)rdo_mma;
 #endif
+        // the winners' rows as 16-B stores when every row start is 16-B aligned
+        const int vec_out = NH_RDO_VEC_OUT && !(pitch & 7) && !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 15);
         k_intra_rdo8<1, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
-            d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups);
+            d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups, vec_out);
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
-                                                        d_recon, sse, ngroups);
+                                                        d_recon, sse, ngroups, vec_out);
     }
     NH_HIP(hipGetLastError());
     return NH_OK;

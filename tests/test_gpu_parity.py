@@ -356,11 +356,13 @@ def test_intra_rdo_golden(nh, torch_dev, golden):
         assert int(sse.item()) == int(g[f"{k}_sse"]), k
 
 
-@pytest.mark.parametrize("h,w,kind", [(64, 96, "natural"), (48, 40, "noise"), (72, 64, "int16"), (56, 72, "mixed")])
+@pytest.mark.parametrize("h,w,kind", [(64, 96, "natural"), (48, 40, "noise"), (72, 64, "int16"), (56, 72, "mixed"),
+                                      (40, 60, "noise")])
 def test_intra_rdo_vs_oracle(nh, torch_dev, h, w, kind):
     """noise: the packed 16-bit chain at its extremes (residuals +-255); int16:
     the 32-bit chain; mixed: 8-bit blocks whose left / top neighbours are not
-    8-bit (wide = 2: the 32-bit chain with the 32-bit SSE)."""
+    8-bit (wide = 2: the 32-bit chain with the 32-bit SSE); width 60: rows not
+    16-B aligned (the winners' per-sample stores instead of 16-B rows)."""
     torch = torch_dev
     from nano_hevc import gpu
     rng = np.random.default_rng(h * w)
@@ -382,6 +384,29 @@ def test_intra_rdo_vs_oracle(nh, torch_dev, h, w, kind):
         assert np.array_equal(l.cpu().numpy(), el), (kind, qp)
         assert np.array_equal(r.cpu().numpy(), er), (kind, qp)
         assert int(sse.item()) == esse
+
+
+def test_intra_rdo_every_qp_vs_oracle(nh, torch_dev):
+    """The packed chain at every QP 0..51 on 8-bit extremes (0 / 255 checkerboards and
+    noise: the largest coefficients and levels, where the packed dequantization's
+    int16 bound is tightest, tools/packed_bounds.py rdo8_dequant_bounds)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    rng = np.random.default_rng(52)
+    h, w = 32, 64
+    yy, xx = np.mgrid[0:h, 0:w]
+    src = rng.integers(0, 256, size=(h, w))
+    src[:, :24] = 255 * ((xx[:, :24] + yy[:, :24]) % 2)          # checkerboards
+    src[:16, 24:40] = 255 * ((xx[:16, 24:40] // 2 + yy[:16, 24:40]) % 2)
+    src = src.astype(np.int16)
+    d = torch.from_numpy(src).cuda()
+    for qp in range(52):
+        m, l, r, sse = gpu.intra_rdo_plane(d, qp)
+        em, el, er, esse = O.intra_rdo_plane(src, qp)
+        assert np.array_equal(m.cpu().numpy(), em), qp
+        assert np.array_equal(l.cpu().numpy(), el), qp
+        assert np.array_equal(r.cpu().numpy(), er), qp
+        assert int(sse.item()) == esse, qp
 
 
 def test_tu_pipeline_golden(nh, torch_dev, golden):

@@ -37,3 +37,10 @@ def test_compact_level_bound_for_config5():
     int16 / int8 compact levels are exact, and the spill markers never collide."""
     b = packed_bounds.level_bounds()
     assert b["DCT32"] == 51 and max(b.values()) < 2 ** 15
+
+
+def test_config3_packed_dequant_bound():
+    """rdo8_chain_n dequantizes level pairs in int16 lanes: l * dqs + dqr fits int16
+    at every QP for an 8-bit 8x8 block (and the shift gives dequantize_block's value)."""
+    w = packed_bounds.rdo8_dequant_bounds()
+    assert len(w) == 52 and max(w.values()) <= 32767

@@ -107,6 +107,7 @@ def main():
     assert all(int(r) == 0 for r in rs[1:]) and int(rs[0]) == 2048
     mosaic_bounds()
     level_bounds()
+    rdo8_dequant_bounds()
 
 
 def mosaic_bounds():
@@ -180,5 +181,31 @@ def level_bounds():
     return out
 
 
+def rdo8_dequant_bounds():
+    """Config 3's packed chain (rdo8_chain_n) dequantizes level PAIRS
+    with v_pk_mad + v_pk_ashr: l * dqs + dqr (dqs = scale << max(per - 4, 0), dqr =
+    2^(3 - per) for per < 4) must stay within int16 for every level an 8-bit 8x8 block
+    can produce (intra rounding, the coefficient bound of the DCT8 row), every QP.
+    Returns the largest |l * dqs + dqr| per QP."""
+    T = mat(8, False)
+    rl1 = int(np.abs(T).sum(1).max())
+    c = shift_bound(shift_bound(255 * rl1, 8) * rl1, 8)
+    worst = {}
+    for qp in range(52):
+        per, rem = qp // 6, qp % 6
+        lmax = quant(c, qp, 3, True)
+        dqs = DQ[rem] << max(per - 4, 0)
+        dqr = (1 << (3 - per)) if per < 4 else 0
+        v = max(lmax * dqs + dqr, lmax * dqs)
+        assert v <= 32767 and -lmax * dqs + dqr >= -32768, (qp, lmax, dqs)
+        assert (v >> (4 - per if per < 4 else 0)) == dequant(lmax, qp)
+        worst[qp] = v
+    print("config-3 packed dequant: |coeff| <= %d, max |l * dqs + dqr| %d (QP %d; limit 32767)"
+          % (c, max(worst.values()), max(worst, key=worst.get)))
+    return worst
+
+
+
 if __name__ == "__main__":
     main()
+
