@@ -8,6 +8,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   yuv420_plane_sets   -- nh_plane_set descriptors for a stream of YUV420 frames
   fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
   intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
+  intra_rdo_closed    -- config 3 in closed loop (row wavefront); _yuv420_stream: in batches, several in flight
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
   tu_pipeline_planes_compact / tu_levels_widen -- config 4 with exact int16 levels (+ int32 spill)
   tc32_plane          -- config 5: 32x32 chain, butterfly or matrix-core variants
@@ -305,6 +306,95 @@ def intra_rdo_closed(src, sets: Sequence[PlaneSet], qp: int = 32, lvl=None, rec=
     if status.value:
         raise RuntimeError("intra_rdo_closed: the wavefront stalled (device status word set)")
     return modes[:nmodes], lvl, rec, sse[:nplanes]
+
+
+def intra_rdo_closed_yuv420_stream(src, width: int, height: int, num_frames: int, qp: int = 32,
+                                   batch_frames: int = 64, depth: int = 3, lvl=None, rec=None, stream=None,
+                                   frame_stride: int | None = None, base: int = 0):
+    """``intra_rdo_closed`` over a stream of YUV420 frames laid out back to back
+    (``yuv420_plane_sets``), in batches of ``batch_frames`` frames whose launches
+    rotate over ``depth`` streams with no host round trip between them, so a
+    batch's block rows fill what the previous batch's wavefront leaves idle while
+    it ramps down (1080p: 0.214 vs 0.233 ms per frame for one
+    64-frame call).  Same outputs, in the same layout, as one ``intra_rdo_closed``
+    call over ``yuv420_plane_sets(num_frames, ...)``: modes and sse of the Y
+    planes, then of the U, V planes; lvl / rec in the source layout."""
+    torch = _torch()
+    if batch_frames < 1 or depth < 1 or num_frames < 0:
+        raise ValueError("intra_rdo_closed_yuv420_stream: batch_frames, depth >= 1 and num_frames >= 0")
+    fs = frame_stride or yuv420_frame_elems(width, height)
+    if fs < yuv420_frame_elems(width, height):
+        raise ValueError("intra_rdo_closed_yuv420_stream: frame_stride shorter than a frame")
+    all_sets = yuv420_plane_sets(num_frames, width, height, fs, base)
+    sets_fit(all_sets, src.numel(), "intra_rdo_closed_yuv420_stream")
+    _need(src, torch.int16, "intra_rdo_closed_yuv420_stream(src)")
+    dev = src.device
+    main = stream if stream is not None else torch.cuda.current_stream(dev)
+    if main.device != dev:
+        raise ValueError(f"intra_rdo_closed_yuv420_stream: stream on {main.device} but src on {dev}")
+    ny = (width // 8) * (height // 8)          # modes per Y plane
+    nc = (width // 16) * (height // 16)        # per U / V plane
+    with torch.cuda.device(dev), torch.cuda.stream(main):
+        if lvl is None:
+            lvl = torch.zeros(src.shape, dtype=torch.int32, device=dev)
+        if rec is None:
+            rec = torch.zeros(src.shape, dtype=torch.int16, device=dev)
+        modes = torch.zeros(max(1, num_frames * (ny + 2 * nc)), dtype=torch.uint8, device=dev)
+        sse = torch.zeros(max(1, 3 * num_frames), dtype=torch.int64, device=dev)
+    _need(lvl, torch.int32, "intra_rdo_closed_yuv420_stream(lvl)")
+    _need(rec, torch.int16, "intra_rdo_closed_yuv420_stream(rec)")
+    if lvl.numel() < src.numel() or rec.numel() < src.numel():
+        raise ValueError("intra_rdo_closed_yuv420_stream: lvl / rec smaller than src")
+    if num_frames == 0:
+        return modes[:0], lvl, rec, sse[:0]
+    L = _lib.load()
+    pool = _PIPE_STREAMS3.setdefault(dev.index, [])
+    while len(pool) < depth:
+        pool.append(torch.cuda.Stream(device=dev))
+    fork = torch.cuda.Event()
+    fork.record(main)
+    for s_ in pool[:depth]:
+        s_.wait_event(fork)
+    works, keep = [], []
+    for b, f0 in enumerate(range(0, num_frames, batch_frames)):
+        nb = min(batch_frames, num_frames - f0)
+        sets = yuv420_plane_sets(nb, width, height, fs, base + f0 * fs)
+        arr = (PlaneSet * 2)(*sets)
+        wb = int(L.nh_intra_rdo_closed_workspace_bytes(arr, 2))
+        if wb < 0:
+            raise ValueError("intra_rdo_closed_yuv420_stream: bad frame size")
+        s_ = pool[b % depth]
+        with torch.cuda.stream(s_):
+            md = torch.empty(nb * (ny + 2 * nc), dtype=torch.uint8, device=dev)
+            ss = torch.zeros(3 * nb, dtype=torch.int64, device=dev)   # the kernels add into it
+            w_ = torch.empty((wb + 3) // 4, dtype=torch.int32, device=dev)
+            check(L.nh_intra_rdo_planes_closed(src.data_ptr(), arr, 2, int(qp), md.data_ptr(), lvl.data_ptr(),
+                                               rec.data_ptr(), ss.data_ptr(), w_.data_ptr(), C.c_void_p(s_.cuda_stream)))
+            # the batch's modes / sse into the whole stream's layout (Y planes, then U, V planes)
+            modes[f0 * ny:(f0 + nb) * ny].copy_(md[:nb * ny])
+            modes[num_frames * ny + 2 * f0 * nc:num_frames * ny + 2 * (f0 + nb) * nc].copy_(md[nb * ny:])
+            sse[f0:f0 + nb].copy_(ss[:nb])
+            sse[num_frames + 2 * f0:num_frames + 2 * (f0 + nb)].copy_(ss[nb:])
+        works.append(w_)
+        keep += [md, ss]
+    for s_ in pool[:depth]:
+        join = torch.cuda.Event()
+        join.record(s_)
+        main.wait_event(join)
+    for t in works + keep:
+        t.record_stream(main)
+    with torch.cuda.device(dev), torch.cuda.stream(main):   # every status word ORed: one host round trip
+        both = works[0][:2].clone()
+        for w_ in works[1:]:
+            both.bitwise_or_(w_[:2])
+    status = C.c_int(0)
+    check(L.nh_intra_rdo_closed_status(both.data_ptr(), C.byref(status), C.c_void_p(main.cuda_stream)))
+    if status.value:
+        raise RuntimeError("intra_rdo_closed_yuv420_stream: the wavefront stalled (device status word set)")
+    return modes[:num_frames * (ny + 2 * nc)], lvl, rec, sse[:3 * num_frames]
+
+
+_PIPE_STREAMS3 = {}
 
 
 def tu_pipeline_plane(src, ctb: int, plane_id: int, seed: int, qp: int = 32, is_luma: bool = True,

@@ -776,6 +776,40 @@ def test_intra_rdo_closed_stream_vs_oracle(nh, torch_dev, F, W, H, qp):
     assert not np.array_equal(ro, rec[:planes[0].size].reshape(planes[0].shape))
 
 
+@pytest.mark.parametrize("batch,depth,pad", [(3, 2, 0), (2, 3, 16), (1, 4, 0), (9, 3, 8)])
+def test_intra_rdo_closed_batches_equal_one_call(nh, torch_dev, batch, depth, pad):
+    """intra_rdo_closed_yuv420_stream: a 7-frame stream in batches over rotating
+    streams (a ragged last batch, a padded frame stride, a base offset, one frame
+    with a 9-bit sample: its batch alone takes the 32-bit form) gives the outputs,
+    in the same layout, of one intra_rdo_closed call; frame 0's Y plane equals
+    the oracle."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    F, W, H, qp, base = 7, 72, 48, 27, 24
+    rng = np.random.default_rng(900 + batch * 10 + depth)
+    fe = gpu.yuv420_frame_elems(W, H)
+    fs = fe + pad
+    buf = np.zeros(base + F * fs, np.int16)
+    for f in range(F):
+        off = base + f * fs
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            p = np.clip(50 + (2 * xx + 3 * yy + 11 * f) % 160 + rng.integers(-20, 21, (ph, pw)), 0, 255)
+            if f == 5:
+                p[ph // 3, pw // 2] = 300
+            buf[off:off + ph * pw] = p.reshape(-1)
+            off += ph * pw
+    d = torch.from_numpy(buf).cuda()
+    m1, l1, r1, s1 = gpu.intra_rdo_closed_yuv420_stream(d, W, H, F, qp, batch_frames=batch, depth=depth,
+                                                        frame_stride=fs, base=base)
+    m0, l0, r0, s0 = gpu.intra_rdo_closed(d, gpu.yuv420_plane_sets(F, W, H, fs, base), qp)
+    assert torch.equal(m1, m0) and torch.equal(l1, l0) and torch.equal(r1, r0) and torch.equal(s1, s0)
+    y0 = buf[base:base + W * H].reshape(H, W)
+    em, el, er, es = O.intra_rdo_plane(y0, qp, closed=True)
+    assert np.array_equal(m1[:(H // 8) * (W // 8)].cpu().numpy().reshape(H // 8, W // 8), em)
+    assert np.array_equal(r1[base:base + W * H].cpu().numpy().reshape(H, W), er) and int(s1[0]) == es
+
+
 def test_intra_rdo_closed_ragged_and_int16(nh, torch_dev):
     """Partial blocks (recon 0 there, and read as 0 by the top-right references)
     and full-range int16 sources."""

@@ -153,3 +153,18 @@ def test_closed_stream_argument_checks():
         gpu.tu_pipeline_closed_yuv420_stream(src, W, H, F + 1, 1, 32)
     with pytest.raises(ValueError):   # the base pushes the last frame out
         gpu.tu_pipeline_closed_yuv420_stream(src, W, H, F, 1, 32, base=1)
+
+
+def test_closed3_stream_argument_checks():
+    """intra_rdo_closed_yuv420_stream refuses bad batch / depth / stride / size
+    arguments on the host, before any device call."""
+    import torch
+    W, H, F = 64, 32, 3
+    src = torch.zeros(F * gpu.yuv420_frame_elems(W, H), dtype=torch.int16)
+    for kw in ({"batch_frames": 0}, {"depth": 0}, {"frame_stride": gpu.yuv420_frame_elems(W, H) - 1}):
+        with pytest.raises(ValueError):
+            gpu.intra_rdo_closed_yuv420_stream(src, W, H, F, 32, **kw)
+    with pytest.raises(ValueError):
+        gpu.intra_rdo_closed_yuv420_stream(src, W, H, F + 1, 32)
+    with pytest.raises(TypeError):   # a host tensor: the device entry points take device memory only
+        gpu.intra_rdo_closed_yuv420_stream(src, W, H, F, 32)

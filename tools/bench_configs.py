@@ -118,6 +118,8 @@ def main():
     ap.add_argument("--closed4-frames", type=int, default=64, help="frames of the closed-loop cfg4 stream")
     ap.add_argument("--closed4-seq", action="store_true", help="closed4: luma then chroma (default: concurrent wavefronts)")
     ap.add_argument("--closed4s-batch", default="64,128", help="closed4s: frames per batch (one line each)")
+    ap.add_argument("--closed-stream-batches", type=int, default=4,
+                    help="closed: also code the frames this many times as a pipelined stream (0: off)")
     ap.add_argument("--closed4s-frames", type=int, default=384, help="closed4s: frames in the stream")
     ap.add_argument("--closed4-depth", type=int, default=3, help="closed4s: batches in flight")
     ap.add_argument("--check", action="store_true", help="oracle PSNR on the cfg5 luma plane (slow, CPU)")
@@ -511,6 +513,23 @@ def main():
             line["luma0_matches_oracle"] = bool(np.array_equal(rec[:W * H].view(H, W).cpu().numpy(), er)
                                                 and int(sse[0].item()) == es)
         print(json.dumps(line), flush=True)
+        if args.closed_stream_batches:   # the same frames, coded `batches` times as a stream of 64-frame batches
+            nb_ = args.closed_stream_batches
+            big = stream.repeat(nb_)
+            lvl2 = torch.zeros(big.shape, dtype=torch.int32, device="cuda")
+            rec2 = torch.zeros(big.shape, dtype=torch.int16, device="cuda")
+            run = lambda: gpu.intra_rdo_closed_yuv420_stream(big, W, H, nf * nb_, args.qp, batch_frames=nf,
+                                                               depth=args.closed4_depth, lvl=lvl2, rec=rec2)
+            ms2 = timed(run, max(2, args.reps // 4))
+            _, _, rec2, sse2 = run()
+            print(json.dumps({"config": "cfg3 closed loop over a frame stream: batches of 1080p YUV420 frames, "
+                                        "`depth` in flight (intra_rdo_closed_yuv420_stream)",
+                              "frames": nf * nb_, "batch_frames": nf, "depth": args.closed4_depth,
+                              "ms_per_stream": ms2, "ms_per_frame": ms2 / (nf * nb_),
+                              "roofline": valu_roofline("cfg3_closed_1080p_yuv420", ms2 / (nf * nb_)),
+                              "repeats_equal_single_call": bool((rec2.view(nb_, -1) == rec.view(1, -1)).all()) and
+                              int(sse2[0].item()) == int(sse[0].item())}), flush=True)
+            del big, lvl2, rec2
 
 
 if __name__ == "__main__":
