@@ -2895,6 +2895,8 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
         // A/B build: NH_RDO_MMA = 0 the lane-per-mode packed chains, 3 / 4 the f16 MFMA mosaics at that many
         // waves per SIMD (k_intra_rdo8_mma)
         static const int rdo_mma = NH_KNOB("NH_RDO_MMA", kRdoMmaDefault);
+        // the winners' rows as 16-B stores when every row start is 16-B aligned
+        const int vec_out = NH_RDO_VEC_OUT && !(pitch & 7) && !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 15);
 #if NH_AB
         if (rdo_mma) {
             const int rcm = ensure_mosaic_cl();
@@ -2916,8 +2918,6 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
 #else
         (void)rdo_mma;
 #endif
-        // the winners' rows as 16-B stores when every row start is 16-B aligned
-        const int vec_out = NH_RDO_VEC_OUT && !(pitch & 7) && !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 15);
         k_intra_rdo8<1, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
             d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups, vec_out);
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
