@@ -74,6 +74,17 @@ def main():
         join.record(side)
         main.wait_event(join)
 
+    def chroma_first():   # the same two launches, chroma submitted first (its waves take their slots first)
+        main = torch.cuda.current_stream()
+        fork = torch.cuda.Event()
+        fork.record(main)
+        side.wait_event(fork)
+        gpu._tu_closed_launch(stream, suv, 16, 1, 1234, args.qp, False, lv, rc, tuc, side)
+        gpu._tu_closed_launch(stream, sy, 32, 0, 1234, args.qp, True, lv, rc, tuy, main)
+        join = torch.cuda.Event()
+        join.record(side)
+        main.wait_event(join)
+
     pipe_bufs = []
     if args.pipe:   # a second copy of the frames and outputs: consecutive sets alternate between the copies
         pipe_bufs = [(stream, lv, rc, tuy, tuc)] + [
@@ -110,6 +121,7 @@ def main():
         "concurrent": lambda: gpu.tu_pipeline_closed_yuv420(stream, sy, suv, 1234, args.qp, lvl=lv, rec=rc,
                                                             tu_luma=tuy, tu_chroma=tuc),
         "luma_first": luma_first,
+        "chroma_first": chroma_first,
     }
     if args.only_pipe:
         forms = {}
