@@ -83,7 +83,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=(2, 4), help="2: headline 8x8 DCT+quant; 4: mixed-TU chain")
     ap.add_argument("--frames", type=int, default=None,
-                    help="4K YUV420 frames per GPU per step (default 128 for config 2, 16 for config 4)")
+                    help="4K YUV420 frames per GPU per step (default 128 for config 2, 64 for config 4)")
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--levels", default="int16", choices=("int16", "int32"),
                     help="config 4: level dtype on the device -- int16 = the exact compact levels (|level| <= 408 "
@@ -105,7 +105,7 @@ def parse_args(argv=None):
     ap.add_argument("--launcher-selftest", action="store_true", help=argparse.SUPPRESS)
     a = ap.parse_args(argv)
     if a.frames is None:
-        a.frames = 128 if a.config == 2 else 16
+        a.frames = 128 if a.config == 2 else 64
     if a.gpus < 1:
         ap.error("--gpus must be >= 1")
     return a
