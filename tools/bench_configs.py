@@ -9,7 +9,7 @@
   enc   encode_frame_intra (__main__.py:142-189, DC vs planar per block, 8x8 luma /
         4x4 chroma) over a stream of 4K YUV420p byte frames -> int16 recon + stats;
         HBM roofline at 3 B/sample (1 B source read + 2 B recon write).
-  4b    config 4 batched: 16 4K YUV420 frames in one launch per TU size and plane set.
+  4b    config 4 batched: --cfg4-frames 4K YUV420 frames in one launch per plane set.
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
   closed4 config 4 in CLOSED loop over a 4K YUV420 stream (TUs in z-order, CTU-row
         wavefront; with --check, frame 0's luma against the oracle).
@@ -110,7 +110,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--qp", type=int, default=32)
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
-    ap.add_argument("--cfg5-frames", type=int, default=8, help="frames of the batched cfg5 stream")
+    ap.add_argument("--cfg5-frames", type=int, default=32,
+                    help="frames of the batched cfg5 stream (8 until late in round 6: 32 amortise the launch tails)")
+    ap.add_argument("--cfg4-frames", type=int, default=64,
+                    help="frames of the batched cfg4 stream (16 until late in round 6)")
     ap.add_argument("--cfg5-levels", default=None,
                     help="5b: level dtypes (default from the configs: 5b int32, 5bc int16, 5bc8 int8 compact levels)")
     ap.add_argument("--cfg4-levels", default=None,
@@ -196,7 +199,7 @@ def main():
                           "samples_by_tu_size": hist, "psnr_y": psnr_dev(planes[0][0], bufs[0][1])}), flush=True)
 
     if "4b" in cfgs:   # config 4 batched: the whole stream in 2 plane sets x 4 TU sizes = 8 launches
-        W, H, nf = 3840, 2160, 16
+        W, H, nf = 3840, 2160, args.cfg4_frames
         planes = []
         for f in range(nf):
             planes += [synth_plane(H, W, 40 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 41 + 3 * f).reshape(-1),
@@ -235,7 +238,7 @@ def main():
             samples = stream.numel()
             bps = 8 if ldt == "int32" else 6
             key = "cfg4_4k_yuv420" if ldt == "int32" else "cfg4_4k_yuv420_" + ldt
-            print(json.dumps({"config": "cfg4 batched: 16 x 4K YUV420 frames, mixed 4/8/16/32 TUs per CTU, 8 launches",
+            print(json.dumps({"config": f"cfg4 batched: {nf} x 4K YUV420 frames, mixed 4/8/16/32 TUs per CTU, 8 launches",
                               "levels": ldt, "frames": nf, "ms_per_launch_set": ms, "ms_per_frame": ms / nf,
                               "frames_per_s": nf / ms * 1e3, "samples_per_s": samples / ms * 1e3,
                               "bytes_per_sample": bps, "achieved_GBps": samples * bps / ms / 1e6,
