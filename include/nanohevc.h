@@ -228,6 +228,16 @@ int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch, int qp,
                        uint8_t* d_modes, int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse,
                        void* stream);
 
+/* Config 3 over every plane of nsets plane sets in one launch pair per set
+ * (frame streams: no launch per plane).  d_modes: the planes' mode maps back
+ * to back in set order ((h/8)*(w/8) each); d_sse (optional): one int64 per
+ * plane, in the same order, the chosen SSEs added to it; d_lvl / d_recon in the
+ * source layout (each plane at its set's offsets, pitch).  Same results as
+ * nh_intra_rdo_plane plane by plane. */
+int nh_intra_rdo_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp,
+                        uint8_t* d_modes, int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse,
+                        void* stream);
+
 /* Config 4: mixed 4/8/16/32 TU pipeline on one plane over CTU rows
  * [row0, row1): seeded quadtree per CTB (ctb 32 luma / 16
  * chroma), per TU the __main__.py:165-178 DC-vs-planar choice then the full

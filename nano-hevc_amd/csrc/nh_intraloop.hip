@@ -33,6 +33,10 @@ namespace nh {
 // ===========================================================================
 constexpr int kRdoSlots = 7;
 constexpr int kModes = 35;
+struct RdoPlanes {   // k_intra_rdo8 over gridDim.y planes of one size: plane z = (group z / ppg, plane z % ppg)
+    int64_t group_stride, plane_stride;
+    int32_t ppg;
+};
 
 struct RdoSlotLds {
     int16_t orig[64];
@@ -465,7 +469,7 @@ template <int WAVES, bool ONESHOT, int CHAIN = 0>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES))) k_intra_rdo8(const int16_t* __restrict__ src, int w, int h, int pitch,
                                                     QuantParams qp, int dq_scale, int dq_per, uint8_t* modes,
                                                     int32_t* lvl, int16_t* recon, unsigned long long* sse_out,
-                                                    uint32_t ngroups, int vec_out) {
+                                                    uint32_t ngroups, int vec_out, RdoPlanes pg) {
     __shared__ RdoSlotLds S[kRdoSlots];
     __shared__ uint32_t refs[kRdoSlots * kModes][kRefStride];
     __shared__ unsigned long long wg_sse;
@@ -474,6 +478,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES)
     const int t = threadIdx.x;
     const int slot = t / kModes, mode = t - slot * kModes;
     const bool lane_on = slot < kRdoSlots;
+    {   // plane blockIdx.y of the set (nh_intra_rdo_planes): its samples, levels and recon at the plane's
+        // offset, its modes after the previous planes' and its own SSE word
+        const int pz = (int)blockIdx.y, gz = pz / pg.ppg;
+        const int64_t poff = (int64_t)gz * pg.group_stride + (int64_t)(pz - gz * pg.ppg) * pg.plane_stride;
+        src += poff;
+        lvl += poff;
+        recon += poff;
+        modes += (int64_t)pz * nblk;
+        if (sse_out) sse_out += pz;
+    }
     // A workgroup adds its SSE to *sse_out ONCE (one 64-bit word takes ~90
     // atomic adds/us: an atomic per block serialised the whole launch).
     // ONESHOT: one group of 7 blocks per workgroup; else persistent, groups
@@ -2919,11 +2933,59 @@ extern "C" int nh_intra_rdo_plane(const int16_t* d_src, int w, int h, int pitch,
         (void)rdo_mma;
 #endif
         k_intra_rdo8<1, true, 1><<<ngroups, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
-            d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups, vec_out);
+            d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl, d_recon, sse, ngroups, vec_out,
+            RdoPlanes{0, 0, 1});
         k_intra_rdo8<1, true, 2><<<ngroups, 256, 0, s>>>(d_src, w, h, pitch, q, dequant_scale(rem), per, d_modes, d_lvl,
-                                                        d_recon, sse, ngroups, vec_out);
+                                                        d_recon, sse, ngroups, vec_out, RdoPlanes{0, 0, 1});
     }
     NH_HIP(hipGetLastError());
+    return NH_OK;
+}
+
+// Config 3 over every plane of plane sets (include/nanohevc.h): one launch pair per set, plane z of the
+// set in grid row z -- no launch per plane, and the sets' planes share the chip instead of each
+// plane's last workgroups running alone.  Modes and SSE per plane in set order; levels / recon in
+// the source layout.
+extern "C" int nh_intra_rdo_planes(const int16_t* d_src, const nh_plane_set* sets, int nsets, int qp,
+                                   uint8_t* d_modes, int32_t* d_lvl, int16_t* d_recon, int64_t* d_sse, void* stream) {
+    if (!d_src || !sets || nsets < 0 || !d_modes || !d_lvl || !d_recon) return NH_EARG;
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& S = sets[k];
+        const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
+        if (S.width < 0 || S.height < 0 || S.pitch < S.width || S.planes_per_group < 1 || S.num_groups < 0 ||
+            planes > 65535 || S.base < 0 || S.plane_stride < 0 || S.group_stride < 0) {
+            set_error("nh_intra_rdo_planes: bad plane set");
+            return NH_EARG;
+        }
+    }
+    int per, rem;
+    qp_split(qp, &per, &rem);
+    const hipStream_t s = as_stream(stream);
+    const QuantParams q = qparams(qp, 3, true);
+    static const int cap_rdo = NH_KNOB("NH_CAP_RDO", 0);
+    int64_t moff = 0, soff = 0;
+    for (int k = 0; k < nsets; ++k) {
+        const nh_plane_set& S = sets[k];
+        const int64_t planes = (int64_t)S.planes_per_group * S.num_groups;
+        const int nblk = (S.width / 8) * (S.height / 8);
+        if (nblk && planes) {
+            const uint32_t ngroups = (uint32_t)((nblk + kRdoSlots - 1) / kRdoSlots);
+            const int vec_out = NH_RDO_VEC_OUT && !(S.pitch & 7) && !((S.base | S.plane_stride | S.group_stride) & 7) &&
+                                !((uintptr_t)d_lvl & 15) && !((uintptr_t)d_recon & 15);
+            const RdoPlanes pg{S.group_stride, S.plane_stride, S.planes_per_group};
+            unsigned long long* sse = d_sse ? (unsigned long long*)(d_sse + soff) : nullptr;
+            const dim3 grid(ngroups, (unsigned)planes);
+            k_intra_rdo8<1, true, 1><<<grid, 256, lds_cap(k_intra_rdo8<1, true, 1>, cap_rdo), s>>>(
+                d_src + S.base, S.width, S.height, S.pitch, q, dequant_scale(rem), per, d_modes + moff, d_lvl + S.base,
+                d_recon + S.base, sse, ngroups, vec_out, pg);
+            k_intra_rdo8<1, true, 2><<<grid, 256, 0, s>>>(d_src + S.base, S.width, S.height, S.pitch, q,
+                                                         dequant_scale(rem), per, d_modes + moff, d_lvl + S.base,
+                                                         d_recon + S.base, sse, ngroups, vec_out, pg);
+            NH_HIP(hipGetLastError());
+        }
+        moff += planes * nblk;
+        soff += planes;
+    }
     return NH_OK;
 }
 

@@ -75,6 +75,7 @@ SIGNATURES = {
     "nh_quant_batch": ([P, P, I64, I32, I32, I32, VP], I32),
     "nh_dequant_batch": ([P, P, I64, I32, VP], I32),
     "nh_intra_rdo_plane": ([P, I32, I32, I32, I32, P, P, P, P, VP], I32),
+    "nh_intra_rdo_planes": ([P, C.POINTER(PlaneSet), I32, I32, P, P, P, P, VP], I32),
     "nh_tu_workspace_bytes": ([I32, I32, I32], I64),
     "nh_tu_pipeline_plane": ([P, I32, I32, I32, I32, I32, U32, I32, I32, I32, I32, P, P, P, P, VP], I32),
     "nh_tu_pipeline_planes": ([P, C.POINTER(PlaneSet), I32, I32, U32, I32, I32, I32, I32, P, P, P, VP], I32),

@@ -7,7 +7,7 @@ launch the gfx950 kernels through the C ABI on the tensor's current stream.
   fwd8x8_quant        -- the hot path: fused 8x8 DCT + quant over plane sets
   yuv420_plane_sets   -- nh_plane_set descriptors for a stream of YUV420 frames
   fwd_transform_batch / inv_transform_batch / quant_batch / dequant_batch
-  intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane
+  intra_rdo_plane     -- config 3: 35-mode RDO per 8x8 block of a plane; intra_rdo_planes: over plane sets
   intra_rdo_closed    -- config 3 in closed loop (row wavefront); _yuv420_stream: in batches, several in flight
   tu_pipeline_plane   -- config 4: mixed 4..32 TU reconstruction chain on a plane
   tu_pipeline_planes_compact / tu_levels_widen -- config 4 with exact int16 levels (+ int32 spill)
@@ -266,6 +266,35 @@ def intra_rdo_plane(src, qp: int = 32, pitch: int | None = None, stream=None):
     check(_lib.load().nh_intra_rdo_plane(src.data_ptr(), w, h, pitch or w, int(qp), modes.data_ptr(), lvl.data_ptr(),
                                          rec.data_ptr(), sse.data_ptr(), C.c_void_p(_stream(stream, src.device))), "intra_rdo_plane")
     return modes, lvl, rec, sse
+
+
+def intra_rdo_planes(src, sets: Sequence[PlaneSet], qp: int = 32, lvl=None, rec=None, stream=None):
+    """Config 3 over every plane of ``sets`` -- a frame stream
+    in one launch pair per set instead of a launch per plane.  Returns (modes
+    uint8 [sum of per-plane (h/8)*(w/8), set order], lvl int32, recon int16
+    (source layout), sse int64 per plane); the same results as ``intra_rdo_plane``
+    plane by plane."""
+    torch = _torch()
+    _need(src, torch.int16, "intra_rdo_planes(src)")
+    sets_fit(sets, src.numel(), "intra_rdo_planes")
+    nmodes = sum((s.width // 8) * (s.height // 8) * s.planes_per_group * s.num_groups for s in sets)
+    nplanes = sum(s.planes_per_group * s.num_groups for s in sets)
+    dev = src.device
+    if lvl is None:
+        lvl = torch.zeros(src.shape, dtype=torch.int32, device=dev)
+    if rec is None:
+        rec = torch.zeros(src.shape, dtype=torch.int16, device=dev)
+    _need(lvl, torch.int32, "intra_rdo_planes(lvl)")
+    _need(rec, torch.int16, "intra_rdo_planes(rec)")
+    if lvl.numel() < src.numel() or rec.numel() < src.numel():
+        raise ValueError("intra_rdo_planes: lvl / rec smaller than src")
+    modes = torch.zeros(max(1, nmodes), dtype=torch.uint8, device=dev)
+    sse = torch.zeros(max(1, nplanes), dtype=torch.int64, device=dev)
+    arr = (PlaneSet * len(sets))(*sets)
+    check(_lib.load().nh_intra_rdo_planes(src.data_ptr(), arr, len(sets), int(qp), modes.data_ptr(), lvl.data_ptr(),
+                                          rec.data_ptr(), sse.data_ptr(), C.c_void_p(_stream(stream, dev))),
+          "intra_rdo_planes")
+    return modes[:nmodes], lvl, rec, sse[:nplanes]
 
 
 def intra_rdo_closed(src, sets: Sequence[PlaneSet], qp: int = 32, lvl=None, rec=None, stream=None):

@@ -56,6 +56,34 @@ def test_cfg3_1080p_open_loop_equals_reference(ref, torch_dev):
         assert int(s.item()) == e["sse"], k
 
 
+def test_cfg3_1080p_planes_equals_reference(ref, torch_dev):
+    """Config 3 through the plane-set launch (intra_rdo_planes): 3 copies of the
+    1080p YUV420 frame in one launch pair per set; every copy's planes equal the
+    reference's hashes."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    planes = FI.cfg3_frame()
+    h, w = planes[0].shape
+    one = np.concatenate([p.reshape(-1) for p in planes])
+    F, fe = 3, one.size
+    d = torch.from_numpy(one).cuda().repeat(F)
+    m, l, r, s = gpu.intra_rdo_planes(d, gpu.yuv420_plane_sets(F, w, h), FI.CFG3_QP)
+    m, l, r, s = m.cpu().numpy(), l.cpu().numpy(), r.cpu().numpy(), s.cpu().numpy()
+    ny, nc = (h // 8) * (w // 8), (h // 16) * (w // 16)
+    for f in range(F):
+        off = f * fe
+        for k, p in enumerate(planes):
+            ph, pw = p.shape
+            e = ref[f"cfg3_p{k}"]
+            mo = f * ny if k == 0 else F * ny + (2 * f + k - 1) * nc
+            n = (ph // 8) * (pw // 8)
+            assert sha(m[mo:mo + n].reshape(ph // 8, pw // 8)) == e["modes"], (f, k)
+            assert sha(l[off:off + ph * pw].reshape(ph, pw)) == e["lvl"], (f, k)
+            assert sha(r[off:off + ph * pw].reshape(ph, pw)) == e["rec"], (f, k)
+            assert int(s[f if k == 0 else F + 2 * f + k - 1]) == e["sse"], (f, k)
+            off += ph * pw
+
+
 def test_cfg3_1080p_closed_loop_equals_reference(ref, torch_dev):
     torch = torch_dev
     from nano_hevc import gpu

@@ -386,6 +386,46 @@ def test_intra_rdo_vs_oracle(nh, torch_dev, h, w, kind):
         assert int(sse.item()) == esse
 
 
+@pytest.mark.parametrize("qp,pad", [(32, 0), (7, 24), (51, 8)])
+def test_intra_rdo_planes_equal_per_plane(nh, torch_dev, qp, pad):
+    """intra_rdo_planes (plane sets, one launch pair per set) equals intra_rdo_plane
+    plane by plane: a 3-frame YUV420 stream with a padded frame stride and a base
+    offset, partial blocks at the right / bottom edges, one int16-extreme frame
+    (its groups go to the general fallback launch)."""
+    torch = torch_dev
+    from nano_hevc import gpu
+    W, H, F, base = 104, 76, 3, 16
+    rng = np.random.default_rng(qp * 10 + pad)
+    fe = gpu.yuv420_frame_elems(W, H)
+    fs = fe + pad
+    buf = np.zeros(base + F * fs, np.int16)
+    planes = []
+    for f in range(F):
+        off = base + f * fs
+        for pw, ph in ((W, H), (W // 2, H // 2), (W // 2, H // 2)):
+            yy, xx = np.mgrid[0:ph, 0:pw]
+            p = np.clip(40 + (3 * xx + 2 * yy + 9 * f) % 170 + rng.integers(-15, 16, (ph, pw)), 0, 255)
+            if f == 1:
+                p = rng.integers(-32768, 32768, (ph, pw))
+            buf[off:off + ph * pw] = p.reshape(-1)
+            planes.append((off, ph, pw))
+            off += ph * pw
+    d = torch.from_numpy(buf).cuda()
+    m, l, r, s = gpu.intra_rdo_planes(d, gpu.yuv420_plane_sets(F, W, H, fs, base), qp)
+    m, l, r, s = m.cpu().numpy(), l.cpu().numpy(), r.cpu().numpy(), s.cpu().numpy()
+    order = [3 * f for f in range(F)] + [3 * f + c for f in range(F) for c in (1, 2)]
+    mo = 0
+    for k, pi in enumerate(order):
+        off, ph, pw = planes[pi]
+        em, el, er, es = gpu.intra_rdo_plane(d[off:off + ph * pw].view(ph, pw), qp)
+        n = (ph // 8) * (pw // 8)
+        assert np.array_equal(m[mo:mo + n], em.cpu().numpy().reshape(-1)), (k, pi)
+        mo += n
+        assert np.array_equal(l[off:off + ph * pw].reshape(ph, pw), el.cpu().numpy()), (k, pi)
+        assert np.array_equal(r[off:off + ph * pw].reshape(ph, pw), er.cpu().numpy()), (k, pi)
+        assert int(s[k]) == int(es.item()), (k, pi)
+
+
 def test_intra_rdo_every_qp_vs_oracle(nh, torch_dev):
     """The packed chain at every QP 0..51 on 8-bit extremes (0 / 255 checkerboards and
     noise: the largest coefficients and levels, where the packed dequantization's

@@ -13,6 +13,7 @@
   io    frame I/O casts: YUV420p bytes -> int16 planes and back (3 B/sample each).
   closed4 config 4 in CLOSED loop over a 4K YUV420 stream (TUs in z-order, CTU-row
         wavefront; with --check, frame 0's luma against the oracle).
+  3s    config 3 over a --cfg3-frames 1080p YUV420 stream, one launch pair per plane set (intra_rdo_planes)
   closed4s  config 4 closed loop over a 384-frame stream in batches of --closed4s-batch
         frames, --closed4-depth of them in flight (tu_pipeline_closed_yuv420_stream)
   closed4mix  config 4 closed loop on an 8-bit stream vs the same stream with one
@@ -112,6 +113,7 @@ def main():
     ap.add_argument("--qp5", type=int, default=4, help="cfg5 QP (D1 scaling leaves every 32x32 level 0 at QP 32)")
     ap.add_argument("--cfg5-frames", type=int, default=32,
                     help="frames of the batched cfg5 stream (8 until late in round 6: 32 amortise the launch tails)")
+    ap.add_argument("--cfg3-frames", type=int, default=16, help="frames of the cfg3 plane-set stream line")
     ap.add_argument("--cfg4-frames", type=int, default=64,
                     help="frames of the batched cfg4 stream (16 until late in round 6)")
     ap.add_argument("--cfg5-levels", default=None,
@@ -171,6 +173,23 @@ def main():
                           "blocks_per_s": nblk / ms * 1e3, "mode_evals_per_s": 35 * nblk / ms * 1e3, "knobs": knobs,
                           "roofline": valu_roofline("cfg3_1080p_yuv420", ms),
                           "out_digest": dig}), flush=True)
+    if "3s" in cfgs:   # config 3 over a frame stream through the plane-set launch (one launch pair per set)
+        W, H = 1920, 1080
+        nblk = sum(((h // 8) * (w // 8)) for w, h in ((W, H), (W // 2, H // 2), (W // 2, H // 2)))
+        nf3 = args.cfg3_frames
+        stream3 = torch.cat([torch.cat([synth_plane(H, W, 1 + 3 * f).reshape(-1), synth_plane(H // 2, W // 2, 2 + 3 * f).reshape(-1),
+                                        synth_plane(H // 2, W // 2, 3 + 3 * f).reshape(-1)]) for f in range(nf3)])
+        sets3 = gpu.yuv420_plane_sets(nf3, W, H)
+        lv3 = torch.zeros(stream3.shape, dtype=torch.int32, device="cuda")
+        rc3 = torch.zeros(stream3.shape, dtype=torch.int16, device="cuda")
+        ms3 = timed(lambda: gpu.intra_rdo_planes(stream3, sets3, args.qp, lvl=lv3, rec=rc3), args.reps)
+        m3, _, _, s3 = gpu.intra_rdo_planes(stream3, sets3, args.qp, lvl=lv3, rec=rc3)
+        print(json.dumps({"config": "cfg3 over a 1080p YUV420 frame stream: one launch pair per plane set "
+                                    "(intra_rdo_planes)", "frames": nf3, "ms_per_frame": ms3 / nf3,
+                          "frames_per_s": nf3 / ms3 * 1e3, "blocks_per_s": nf3 * nblk / ms3 * 1e3,
+                          "roofline": valu_roofline("cfg3_1080p_yuv420", ms3 / nf3),
+                          "sse_frame0": [int(s3[0].item()), int(s3[nf3].item()), int(s3[nf3 + 1].item())]}), flush=True)
+        del stream3, lv3, rc3
 
     if 4 in cfgs:
         W, H = 3840, 2160
